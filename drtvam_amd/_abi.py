@@ -1,0 +1,148 @@
+"""ctypes binding of libtvam.so (include/tvam.h).
+
+The GPU path has no fallback: if the HIP library is missing or fails to load,
+every call raises.  ``TvamDesc`` mirrors ``struct tvam_desc`` field for field.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libtvam.so")
+
+ABI_VERSION = 1
+
+TVAM_OK = 0
+TVAM_ERR_INVALID = -1
+TVAM_ERR_UNSUPPORTED = -2
+TVAM_ERR_HIP = -3
+TVAM_ERR_TOO_LARGE = -4
+
+PROJECTOR_COLLIMATED = 0
+VIAL_INDEX_MATCHED = 0
+VIAL_CYLINDRICAL = 1
+SENSOR_DDA = 0
+
+FLAG_NO_ZERO_SKIP = 1
+
+
+class TvamDesc(ctypes.Structure):
+    _fields_ = [
+        ("abi_version", ctypes.c_int32),
+        ("projector_type", ctypes.c_int32),
+        ("n_patterns", ctypes.c_int32),
+        ("res_x", ctypes.c_int32),
+        ("res_y", ctypes.c_int32),
+        ("crop_x", ctypes.c_int32),
+        ("crop_y", ctypes.c_int32),
+        ("crop_offset_x", ctypes.c_int32),
+        ("crop_offset_y", ctypes.c_int32),
+        ("pixel_size_x", ctypes.c_float),
+        ("pixel_size_y", ctypes.c_float),
+        ("distance", ctypes.c_float),
+        ("clockwise", ctypes.c_int32),
+        ("sensor_type", ctypes.c_int32),
+        ("bbox_min", ctypes.c_float * 3),
+        ("bbox_max", ctypes.c_float * 3),
+        ("film_res", ctypes.c_int32 * 3),
+        ("film_channels", ctypes.c_int32),
+        ("vial_type", ctypes.c_int32),
+        ("vial_r", ctypes.c_float),
+        ("vial_r_ext", ctypes.c_float),
+        ("vial_height", ctypes.c_float),
+        ("vial_ior", ctypes.c_float),
+        ("medium_ior", ctypes.c_float),
+        ("sigma_t", ctypes.c_float),
+        ("albedo", ctypes.c_float),
+        ("print_time", ctypes.c_float),
+        ("regular_sampling", ctypes.c_int32),
+        ("sample_time", ctypes.c_int32),
+        ("max_depth", ctypes.c_int32),
+        ("rr_depth", ctypes.c_int32),
+        ("transmission_only", ctypes.c_int32),
+        ("angle_begin", ctypes.c_int32),
+        ("angle_end", ctypes.c_int32),
+        ("tile", ctypes.c_int32),
+        ("flags", ctypes.c_int32),
+    ]
+
+    def copy(self) -> "TvamDesc":
+        d = TvamDesc()
+        ctypes.pointer(d)[0] = self
+        return d
+
+    def as_dict(self) -> dict:
+        out = {}
+        for name, _ in self._fields_:
+            v = getattr(self, name)
+            out[name] = list(v) if isinstance(v, ctypes.Array) else v
+        return out
+
+
+# Entry points declared in include/tvam.h, with their ctypes signatures.
+_P = ctypes.c_void_p
+EXPORTS = {
+    "tvam_desc_init": (None, [ctypes.POINTER(TvamDesc)]),
+    "tvam_plan_create": (ctypes.c_int, [ctypes.POINTER(TvamDesc), ctypes.c_int, ctypes.POINTER(_P)]),
+    "tvam_plan_destroy": (None, [_P]),
+    "tvam_forward": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _P, _P]),
+    "tvam_adjoint": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _P, _P]),
+    "tvam_count_visits": (ctypes.c_int, [_P, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]),
+    "tvam_loss_threshold": (
+        ctypes.c_int,
+        [_P, _P, ctypes.c_float, _P, ctypes.c_uint64, ctypes.c_int32, ctypes.c_float, ctypes.c_float,
+         ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, _P, _P],
+    ),
+    "tvam_last_error": (ctypes.c_char_p, []),
+    "tvam_abi_version": (ctypes.c_int, []),
+}
+
+_lib = None
+_lock = threading.Lock()
+
+
+class TvamError(RuntimeError):
+    pass
+
+
+def load_library(path: str | None = None) -> ctypes.CDLL:
+    """Load libtvam.so (no fallback: raises if it is absent)."""
+    global _lib
+    with _lock:
+        if _lib is not None and path is None:
+            return _lib
+        p = path or LIB_PATH
+        if not os.path.exists(p):
+            raise TvamError(
+                f"libtvam.so not found at {p}: build it with `python -c 'import __graft_entry__ as g; g.build()'` "
+                "or drtvam_amd/csrc/build.sh (there is no CPU fallback)"
+            )
+        lib = ctypes.CDLL(p)
+        for name, (res, args) in EXPORTS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        if lib.tvam_abi_version() != ABI_VERSION:
+            raise TvamError("libtvam.so ABI version mismatch; rebuild it")
+        if path is None:
+            _lib = lib
+        return lib
+
+
+def check(rc: int) -> None:
+    if rc == TVAM_OK:
+        return
+    msg = load_library().tvam_last_error().decode(errors="replace")
+    if rc in (TVAM_ERR_INVALID, TVAM_ERR_UNSUPPORTED):
+        raise ValueError(msg)
+    if rc == TVAM_ERR_TOO_LARGE:
+        raise Exception(msg)
+    raise TvamError(msg)
+
+
+def default_desc() -> TvamDesc:
+    d = TvamDesc()
+    load_library().tvam_desc_init(ctypes.byref(d))
+    return d

@@ -1,0 +1,66 @@
+"""Workload configurations of BASELINE.json, as drtvam JSON-style config dicts.
+
+config 1 / 2: index-matched "Benchy" scene (README.md:118-123: 10 mm print,
+25 um pixels at N=400), N^3 voxels, N angles, N x N DMD, 1 ray/pixel,
+regular sampling.  benchy.ply is not in the reference
+snapshot (.MISSING_LARGE_BLOBS), so the target is analytic; the target only
+enters the loss, never the projection.
+"""
+from __future__ import annotations
+
+import copy
+
+from . import _abi
+
+
+def benchy_index_matched(N: int = 400, angles: int | None = None, size_mm: float = 10.0, r: float = 8.0,
+                         sigma_t: float = 0.03, spp: int = 1, regular_sampling: bool = True, n_steps: int = 40):
+    A = N if angles is None else angles
+    pix = size_mm / N
+    return {
+        "vial": {"type": "index_matched", "r": r, "height": 40.0,
+                 "medium": {"ior": 1.0, "extinction": sigma_t, "albedo": 0.0}},
+        "projector": {"type": "collimated", "n_patterns": A, "resx": N, "resy": N, "pixel_size": pix,
+                      "motion": "circular", "distance": 20.0},
+        "sensor": {"type": "dda", "scalex": size_mm, "scaley": size_mm, "scalez": size_mm,
+                   "film": {"type": "vfilm", "resx": N, "resy": N, "resz": N}},
+        "target": {"analytic": "box_hole"},
+        "loss": {"type": "threshold", "tl": 0.9, "tu": 0.95},
+        "spp": spp,
+        "regular_sampling": regular_sampling,
+        "n_steps": n_steps,
+        "time": 1.0,
+    }
+
+
+# tests/files/box_hole_index_matched.json of the reference (data, restated)
+BOX_HOLE_INDEX_MATCHED = {
+    "vial": {"type": "index_matched", "r": 2.9,
+             "medium": {"ior": 1.347, "phase": {"type": "rayleigh"}, "extinction": 0.03, "albedo": 0.0}},
+    "projector": {"type": "collimated", "n_patterns": 200, "resx": 200, "resy": 20, "pixel_size": 50e-3,
+                  "motion": "circular", "distance": 20},
+    "sensor": {"type": "dda", "scalex": 5, "scaley": 5, "scalez": 1.25,
+               "film": {"type": "vfilm", "resx": 100, "resy": 100, "resz": 50}},
+    "target": {"filename": "tests/files/box_hole.ply", "size": 4.0},
+    "loss": {"type": "threshold", "tl": 0.85, "tu": 0.95},
+    "progressive": True,
+    "n_steps": 30,
+}
+
+
+def desc_from_config(config, angle_range=None, tile: int = 0) -> _abi.TvamDesc:
+    """tvam_desc of a config through the plugin classes (no GPU needed)."""
+    from .optimize import load_scene
+    from .scene import load_dict
+    from .integrators import VolumeIntegrator
+
+    cfg = copy.deepcopy(config)
+    cfg["projector"]["device"] = "cpu"
+    if "filename" in cfg.get("target", {}):
+        cfg["target"] = {"analytic": "box_hole"}
+    scene = load_dict(load_scene(cfg))
+    integ = VolumeIntegrator({
+        "max_depth": cfg.get("max_depth", 6), "rr_depth": cfg.get("rr_depth", 6), "print_time": cfg.get("time", 1.0),
+        "transmission_only": cfg.get("transmission_only", True),
+        "regular_sampling": cfg.get("regular_sampling", False), "angle_range": angle_range, "tile": tile})
+    return integ.desc(scene, scene.sensor_by_id("sensor"))

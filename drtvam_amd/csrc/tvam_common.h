@@ -1,0 +1,234 @@
+// tvam_common.h — scene constants and the per-ray fp32 geometry shared by the
+// host-side plan builder and the gfx950 kernels.
+//
+// Every function here follows one reference routine op for op (fp32, no
+// implicit FMA: the library is built with -ffp-contract=off and FMAs are
+// written out where Mitsuba/Dr.Jit form them):
+//   tvam_ray_camera    integrators/common.py:81-108 + projector.py:184-188
+//                      (collimated get_ray through sample_to_camera)
+//   tvam_ray_world     projector.py:160-162 + motion.py:26-36 (look_at)
+//   tvam_segment_im    geometry.py:75-96 index-matched vial: null-BSDF open
+//                      cylinder entry, spawn_ray offset, exit (volume.py:191,
+//                      :237, :247) -> the one medium segment of the ray
+//   tvam_dda_init      sensor.py:327-365 (box clip, start/end voxel, dtmax,
+//                      tstep) restricted to planar rays (d.z == 0)
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include <math.h>
+
+#define TVAM_HD __host__ __device__ __forceinline__
+
+#define TVAM_RAY_EPS (1500.0f * 5.9604644775390625e-08f)  // math::RayEpsilon<float>
+#define TVAM_TWO_PI 6.2831855f                            // float(2*pi), motion.py:28
+#define TVAM_INF __builtin_huge_valf()
+
+struct TvamConsts {
+    // film / sensor (sensor.py:14-19, film.py:9-14)
+    float bmin[3], bmax[3], h[3];
+    int32_t res[3];
+    float inv_vol;       // volume.py:41-42 (fp32, like the reference)
+    // projector (projector.py:73-99, :171-182)
+    int32_t res_x, res_y, crop_x, crop_y, crop_off_x, crop_off_y;
+    int32_t n_patterns;  // A
+    int32_t a0, a1;      // angle shard
+    int64_t shard_base;  // a0 * crop_y * crop_x: first dense index of the shard
+    float ex, ey;        // emitter size W*a_x, H*a_y
+    float inv_w, inv_h;  // rcp(ScalarVector2f(w, h)) (common.py:98)
+    float dist_m_zc;     // distance - 0.005 (camera-space z of ray origins)
+    int32_t clockwise, regular, sample_time;
+    int32_t skip_zero;   // forward: rays with pattern value 0 add exactly 0 -> skipped
+    // container (geometry.py:75-96)
+    float vial_r, vial_half_h;
+    // medium / weights
+    float nsig2;         // -sigma_t * log2(e): exp(-st t) == exp2(nsig2 t)
+    float wscale;        // inv_pdf/n_samples * print_time * sa/st (projector.py:164-165,187; common.py:111; sensor.py:404)
+};
+
+// --------------------------------------------------------------------------
+// Sampler: TEA-scrambled PCG32 (Mitsuba 'independent' sampler, restated)
+// --------------------------------------------------------------------------
+struct TvamPcg {
+    uint64_t state, inc;
+    TVAM_HD uint32_t next() {
+        uint64_t old = state;
+        state = old * 0x5851f42d4c957f2dULL + inc;
+        uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+        uint32_t rot = (uint32_t)(old >> 59u);
+        return (xs >> rot) | (xs << ((~rot + 1u) & 31u));
+    }
+    TVAM_HD float next_float() {
+        uint32_t bits = (next() >> 9) | 0x3f800000u;
+        return __builtin_bit_cast(float, bits) - 1.0f;
+    }
+    TVAM_HD void seed(uint32_t seed_value, uint64_t wave_index) {
+        uint32_t v0 = seed_value, v1 = (uint32_t)wave_index, sum = 0;
+        for (int i = 0; i < 4; ++i) {
+            sum += 0x9e3779b9u;
+            v0 += ((v1 << 4) + 0xa341316cu) ^ (v1 + sum) ^ ((v1 >> 5) + 0xc8013ea4u);
+            v1 += ((v0 << 4) + 0xad90777du) ^ (v0 + sum) ^ ((v0 >> 5) + 0x7e95761eu);
+        }
+        state = 0u;
+        inc = ((uint64_t)v1 << 1u) | 1u;
+        (void)next();
+        state += (uint64_t)v0;
+        (void)next();
+    }
+};
+
+// --------------------------------------------------------------------------
+// Ray generation
+// --------------------------------------------------------------------------
+// Camera-space origin of the collimated ray through (col + jx, row + jy).
+TVAM_HD void tvam_ray_camera(const TvamConsts& k, int col, int row, float jx, float jy,
+                             float& xc, float& yc) {
+    float u = ((float)col + jx) * k.inv_w;
+    float v = ((float)row + jy) * k.inv_h;
+    xc = (0.5f - u) * k.ex;
+    yc = (0.5f - v) * k.ey;
+}
+
+// World-space ray for rotation (c, s): o = look_at(dist*(c,s,0) -> 0, up z) @ (xc, yc, 0.005)
+TVAM_HD void tvam_ray_world(const TvamConsts& k, float c, float s, float xc, float yc,
+                            float& ox, float& oy, float& oz, float& dx, float& dy) {
+    ox = c * k.dist_m_zc + s * xc;
+    oy = s * k.dist_m_zc - c * xc;
+    oz = yc;
+    dx = -c;
+    dy = -s;
+}
+
+// Mitsuba math::solve_quadratic (stable form).
+TVAM_HD bool tvam_quadratic(float a, float b, float c, float& x0, float& x1) {
+    float disc = b * b - 4.0f * a * c;
+    if (!(disc >= 0.0f)) return false;
+    float sq = sqrtf(disc);
+    float temp = -0.5f * (b + copysignf(sq, b));
+    float r0 = temp / a, r1 = c / temp;
+    x0 = fminf(r0, r1);
+    x1 = fmaxf(r0, r1);
+    return true;
+}
+
+TVAM_HD bool tvam_cyl_roots(float ox, float oy, float dx, float dy, float r, float& t0, float& t1) {
+    float A = dx * dx + dy * dy;
+    float B = 2.0f * (dx * ox + dy * oy);
+    float C = ox * ox + oy * oy - r * r;
+    return tvam_quadratic(A, B, C, t0, t1);
+}
+
+// Index-matched vial: the medium segment (o2, maxt) of a projector ray.
+TVAM_HD bool tvam_segment_im(const TvamConsts& k, float ox, float oy, float oz, float dx, float dy,
+                             float& o2x, float& o2y, float& maxt) {
+    if (!(oz >= -k.vial_half_h && oz <= k.vial_half_h)) return false;
+    float t0, t1;
+    if (!tvam_cyl_roots(ox, oy, dx, dy, k.vial_r, t0, t1)) return false;
+    if (!(t0 >= 0.0f)) return false;
+    float px = fmaf(dx, t0, ox), py = fmaf(dy, t0, oy), pz = oz;
+    float rp = sqrtf(px * px + py * py);
+    float nx = px / rp, ny = py / rp;
+    float m = fmaxf(fmaxf(fabsf(px), fabsf(py)), fabsf(pz));
+    float mag = (1.0f + m) * TVAM_RAY_EPS;
+    float ndd = nx * dx + ny * dy + 0.0f;  // n.z * d.z == +0
+    if (__builtin_signbit(ndd)) mag = -mag;
+    o2x = fmaf(mag, nx, px);
+    o2y = fmaf(mag, ny, py);
+    float u0, u1;
+    if (!tvam_cyl_roots(o2x, o2y, dx, dy, k.vial_r, u0, u1)) return false;
+    if (!(u1 > 0.0f)) return false;
+    maxt = u1;
+    return true;
+}
+
+// z slice of a planar ray with origin height oz: the DDA's start voxel z
+// (sensor.py:345) when the box clip admits the ray, else -1.  For d.z == +0
+// the z slab test (bmin.z - oz)/0 admits exactly bmin.z < oz < bmax.z.
+TVAM_HD int tvam_slice_of(const TvamConsts& k, float oz) {
+    if (!(oz > k.bmin[2] && oz < k.bmax[2])) return -1;
+    int sv = (int)((oz - k.bmin[2]) / k.h[2]);
+    sv = sv < 0 ? 0 : (sv > k.res[2] - 1 ? k.res[2] - 1 : sv);
+    return sv;
+}
+
+// In-plane DDA initialisation of the medium segment (o, d, [0, maxt]) of a
+// planar ray.  Times are kept relative to t_start.
+struct TvamDda {
+    float t_start, tau_end;   // tau_end = t_end - t_start
+    float dtm0[2], ts[2];     // dtmax at t_start, tstep (inf on invalid axes)
+    int32_t sv[2], ev[2], step[2];
+};
+
+TVAM_HD bool tvam_dda_init(const TvamConsts& k, float ox, float oy, float dx, float dy, float maxt,
+                           TvamDda& q) {
+    float o[2] = {ox, oy}, d[2] = {dx, dy};
+    float lo[2], hi[2];
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+        float tb0 = (k.bmin[a] - o[a]) / d[a];
+        float tb1 = (k.bmax[a] - o[a]) / d[a];
+        lo[a] = fminf(tb0, tb1);
+        hi[a] = fmaxf(tb0, tb1);
+    }
+    // z axis: admitted (-inf, +inf) once tvam_slice_of() >= 0
+    float mint_box = fmaxf(fmaxf(fmaxf(lo[0], lo[1]), -TVAM_INF), 0.0f);
+    float maxt_box = fminf(fminf(hi[0], hi[1]), TVAM_INF);
+    float t_start = fmaxf(mint_box, 0.0f);
+    float t_end = fminf(maxt_box, maxt);
+    if (!(isfinite(t_start) && isfinite(t_end) && t_start < t_end)) return false;
+    q.t_start = t_start;
+    q.tau_end = t_end - t_start;
+#pragma unroll
+    for (int a = 0; a < 2; ++a) {
+        float gs = fmaf(d[a], t_start, o[a]);
+        float ge = fmaf(d[a], t_end, o[a]);
+        int step = d[a] > 0.0f ? 1 : -1;
+        int sv = (int)((gs - k.bmin[a]) / k.h[a]);
+        int ev = (int)((ge - k.bmin[a]) / k.h[a]);
+        sv = sv < 0 ? 0 : (sv > k.res[a] - 1 ? k.res[a] - 1 : sv);
+        ev = ev < 0 ? 0 : (ev > k.res[a] - 1 ? k.res[a] - 1 : ev);
+        float next = k.bmin[a] + (float)(sv + step) * k.h[a];
+        if (d[a] < 0.0f) next = next + k.h[a];
+        bool valid = fabsf(d[a]) > 1e-8f;
+        float dtm = valid ? (next - gs) / d[a] : TVAM_INF;
+        if (dtm < 0.0f) dtm = TVAM_INF;
+        q.dtm0[a] = dtm;
+        q.ts[a] = valid ? (k.h[a] / d[a]) * (float)step : TVAM_INF;
+        q.sv[a] = sv;
+        q.ev[a] = ev;
+        q.step[a] = step;
+    }
+    return true;
+}
+
+// Axis interval (relative times) during which the DDA's voxel index on one
+// axis lies in [lo, hi).  The reference steps this axis at relative times
+// T(n) = dtm0 + n*ts, n >= 0 (sensor.py:430-434 in exact arithmetic).
+TVAM_HD void tvam_axis_window(int sv, int step, float dtm0, float ts, int lo, int hi,
+                              float& tin, float& tout, int& nin, int& nout) {
+    if (!(dtm0 < TVAM_INF)) {  // axis never steps
+        bool inside = sv >= lo && sv < hi;
+        tin = -TVAM_INF;
+        tout = inside ? TVAM_INF : -TVAM_INF;
+        nin = 0;
+        nout = inside ? 0x7fffffff : 0;
+        return;
+    }
+    if (step > 0) {
+        nin = lo - sv;
+        nout = hi - sv;
+    } else {
+        nin = sv - hi + 1;
+        nout = sv - lo + 1;
+    }
+    tin = nin > 0 ? fmaf((float)(nin - 1), ts, dtm0) : -TVAM_INF;
+    tout = nout > 0 ? fmaf((float)(nout - 1), ts, dtm0) : -TVAM_INF;
+}
+
+// Steps taken on an axis by relative time tau, clamped to the window.
+TVAM_HD int tvam_axis_steps(float tau, float dtm0, float ts, int nin, int nout) {
+    int n = tau < dtm0 ? 0 : (int)floorf((tau - dtm0) / ts) + 1;
+    int nlo = nin > 0 ? nin : 0;
+    n = n < nlo ? nlo : n;
+    n = n > nout - 1 ? nout - 1 : n;
+    return n;
+}

@@ -1,0 +1,34 @@
+// tvam_internal.h — plan layout and kernel launchers shared by tvam_plan.hip
+// and tvam_kernels.hip (not part of the public ABI).
+#pragma once
+#include "tvam_common.h"
+#include "../../include/tvam.h"
+
+// Device tables that drive one tile launch.
+struct TvamTiles {
+    const float2* cs;          // [n_shard] (cos, sin) of each angle of the shard
+    const int32_t* slice_off;  // [res_z + 1] CSR offsets into slice_rows
+    const int32_t* slice_rows; // crop-local DMD rows feeding each z-slice
+    const int32_t* col_lo;     // [ntiles][n_shard] first crop-local column crossing the tile
+    const int32_t* col_off;    // [ntiles][n_shard + 1] prefix sums of column counts
+    int32_t ntx, nty, tsx, tsy;
+    int32_t n_shard;
+    uint32_t spp, seed;
+};
+
+enum TvamMode { TVAM_MODE_FWD = 0, TVAM_MODE_ADJ = 1, TVAM_MODE_COUNT = 2 };
+
+hipError_t tvam_launch_tiles(int mode, const TvamConsts& k, const TvamTiles& t, size_t lds_bytes,
+                             const float* pat, const int32_t* idxmap, const float* gin, float* out,
+                             unsigned long long* counter, hipStream_t stream);
+
+hipError_t tvam_launch_scatter(const TvamConsts& k, const float* data, const uint32_t* pixels,
+                               uint64_t n, float* dense, int32_t* idxmap, hipStream_t stream);
+
+hipError_t tvam_launch_gather(const TvamConsts& k, const float* dense, const uint32_t* pixels,
+                              uint64_t n, float* out, hipStream_t stream);
+
+hipError_t tvam_launch_loss_threshold(const float* dose, const float* ddose, float alpha,
+                                      const float* target, uint64_t n, int K, float tl, float tu,
+                                      float w_object, float w_void, float w_limit, float scale,
+                                      double* out, float* grad, hipStream_t stream);

@@ -1,0 +1,297 @@
+// tvam_kernels.hip — gfx950 kernels of the TVAM projection engine.
+//
+// Hot path: the DDA ray march of DDAVolumetricSensor.accumulate
+// (sensor.py:383-438) for every ray of every projector angle.
+//
+// Design (MI355X-first):
+//  * Collimated rays under circular motion around a vertical vial are planar
+//    (d.z == 0), so every ray stays in ONE z-slice of the film.  A workgroup
+//    owns one (z-slice, xy-tile) pair and keeps that tile resident in LDS.
+//  * Forward: every ray crossing the tile marches only its in-tile part and
+//    accumulates exp(-st t)(1 - exp(-st dt)) * Le into LDS with ds_add_f32;
+//    the tile is written to HBM once with coalesced stores (no global
+//    atomics, no pre-zeroing of the film).
+//  * Adjoint: the workgroup stages dL/dD * inv_vol for its tile in LDS, each
+//    ray gathers its in-tile sum from LDS and adds it to its pattern gradient
+//    with one coalesced global float atomic per (ray, tile).
+//  * The march is resumed at the tile entry in closed form: the reference
+//    DDA steps axis a at t_start + dtm0[a] + n*ts[a], so the voxel index and
+//    dtmax at any time follow without marching the skipped part.
+#include "tvam_internal.h"
+
+#define TVAM_BLOCK 256
+
+__device__ __forceinline__ float tvam_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+template <int MODE>
+__global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
+    TvamConsts k, TvamTiles tp, const float* __restrict__ pat, const int32_t* __restrict__ idxmap,
+    const float* __restrict__ gin, float* __restrict__ out, unsigned long long* __restrict__ counter) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float* tile = reinterpret_cast<float*>(smem);
+    const int tsx = tp.tsx, tsy = tp.tsy, ns = tp.n_shard;
+    int32_t* s_off = reinterpret_cast<int32_t*>(tile + tsx * tsy);
+    int32_t* s_lo = s_off + (ns + 1);
+
+    const int tile_id = blockIdx.x, kz = blockIdx.y;
+    const int x0 = (tile_id % tp.ntx) * tsx, y0 = (tile_id / tp.ntx) * tsy;
+    const int x1 = min(x0 + tsx, k.res[0]), y1 = min(y0 + tsy, k.res[1]);
+    const int wx = x1 - x0, wy = y1 - y0;
+    const size_t slice_base = (size_t)kz * (size_t)k.res[0] * (size_t)k.res[1];
+
+    for (int i = threadIdx.x; i < tsx * tsy; i += TVAM_BLOCK) {
+        float v = 0.0f;
+        if (MODE == TVAM_MODE_ADJ) {
+            int ly = i / tsx, lx = i - ly * tsx;
+            if (lx < wx && ly < wy)
+                v = gin[slice_base + (size_t)(y0 + ly) * k.res[0] + (x0 + lx)] * k.inv_vol;  // volume.py:130
+        }
+        tile[i] = v;
+    }
+    const int32_t* g_off = tp.col_off + (size_t)tile_id * (ns + 1);
+    const int32_t* g_lo = tp.col_lo + (size_t)tile_id * ns;
+    for (int i = threadIdx.x; i <= ns; i += TVAM_BLOCK) {
+        s_off[i] = g_off[i];
+        if (i < ns) s_lo[i] = g_lo[i];
+    }
+    __syncthreads();
+
+    const int rbeg = tp.slice_off[kz], rend = tp.slice_off[kz + 1];
+    const int nrt = s_off[ns];
+    const int spp = (int)tp.spp;
+    const int per_row = nrt * spp;
+    const int total = (rend - rbeg) * per_row;
+    unsigned long long nvis = 0;
+
+    for (int f = threadIdx.x; f < total; f += TVAM_BLOCK) {
+        const int ri = f / per_row;
+        const int rrem = f - ri * per_row;
+        const int g = spp == 1 ? rrem : rrem / spp;
+        const int smp = rrem - g * spp;
+        // angle of flat column slot g: largest a with s_off[a] <= g
+        int lo = 0, hi = ns;
+        while (hi - lo > 1) {
+            int mid = (lo + hi) >> 1;
+            if (s_off[mid] <= g) lo = mid;
+            else hi = mid;
+        }
+        const int al = lo;
+        const int colc = s_lo[al] + (g - s_off[al]);
+        const int rowc = tp.slice_rows[rbeg + ri];
+        const int a = k.a0 + al;
+        // global dense crop index (sampler stream) and shard-local index (data)
+        const int64_t dense = ((int64_t)a * k.crop_y + rowc) * k.crop_x + colc;
+        const int64_t local = dense - k.shard_base;
+        int64_t act = local;
+        if (idxmap) {
+            act = idxmap[local];
+            if (act < 0) continue;  // inactive pixel
+        }
+        float em = 1.0f;
+        if (MODE == TVAM_MODE_FWD) {
+            float p = pat[local];
+            if (p == 0.0f && k.skip_zero) continue;  // contributes exactly zero dose
+            em = p * k.wscale;        // Le * weight (common.py:108-111, volume.py:49)
+        }
+        // ---- ray generation (common.py:81-108) -------------------------
+        float jx = 0.5f, jy = 0.5f;
+        if (!k.regular) {
+            TvamPcg rng;
+            rng.seed(tp.seed, (uint64_t)dense * (uint64_t)spp + (uint64_t)smp);
+            jx = rng.next_float();
+            jy = rng.next_float();
+        }
+        const float2 csv = tp.cs[al];
+        float xc, yc, ox, oy, oz, dx, dy;
+        tvam_ray_camera(k, k.crop_off_x + colc, k.crop_off_y + rowc, jx, jy, xc, yc);
+        tvam_ray_world(k, csv.x, csv.y, xc, yc, ox, oy, oz, dx, dy);
+        if (tvam_slice_of(k, oz) != kz) continue;
+        // ---- vial entry / medium segment (volume.py:179-216) ------------
+        float o2x, o2y, maxt;
+        if (!tvam_segment_im(k, ox, oy, oz, dx, dy, o2x, o2y, maxt)) continue;
+        // ---- DDA setup (sensor.py:327-365) ------------------------------
+        TvamDda q;
+        if (!tvam_dda_init(k, o2x, o2y, dx, dy, maxt, q)) continue;
+        // ---- resume the march at the tile entry -------------------------
+        float tin0, tout0, tin1, tout1;
+        int nin0, nout0, nin1, nout1;
+        tvam_axis_window(q.sv[0], q.step[0], q.dtm0[0], q.ts[0], x0, x1, tin0, tout0, nin0, nout0);
+        tvam_axis_window(q.sv[1], q.step[1], q.dtm0[1], q.ts[1], y0, y1, tin1, tout1, nin1, nout1);
+        const float tau_e = fmaxf(fmaxf(tin0, tin1), 0.0f);
+        const float tau_x = fminf(fminf(tout0, tout1), q.tau_end);
+        if (!(tau_e < tau_x)) continue;
+        const int n0 = tvam_axis_steps(tau_e, q.dtm0[0], q.ts[0], nin0, nout0);
+        const int n1 = tvam_axis_steps(tau_e, q.dtm0[1], q.ts[1], nin1, nout1);
+        int vx = q.sv[0] + q.step[0] * n0;
+        int vy = q.sv[1] + q.step[1] * n1;
+        float dtx = q.dtm0[0] < TVAM_INF ? fmaxf(fmaf((float)n0, q.ts[0], q.dtm0[0]) - tau_e, 0.0f) : TVAM_INF;
+        float dty = q.dtm0[1] < TVAM_INF ? fmaxf(fmaf((float)n1, q.ts[1], q.dtm0[1]) - tau_e, 0.0f) : TVAM_INF;
+        const float tsx_ = q.ts[0], tsy_ = q.ts[1];
+        const int stx = q.step[0], sty = q.step[1], sti = q.step[1] * tsx;
+        const int evx = q.ev[0], evy = q.ev[1];
+        float rem = q.tau_end - tau_e;
+        float t = q.t_start + tau_e;
+        float e0 = em * tvam_exp2(k.nsig2 * t);
+        int lidx = (vy - y0) * tsx + (vx - x0);
+        float acc = 0.0f;
+        // ---- in-tile march (sensor.py:383-438) -------------------------
+        for (;;) {
+            const float dt = fminf(fminf(dtx, dty), rem);
+            rem -= dt;
+            t += dt;
+            const float e1 = em * tvam_exp2(k.nsig2 * t);
+            const float contrib = e0 - e1;  // em*exp(-st t)(1-exp(-st dt)) telescoped
+            if (MODE == TVAM_MODE_FWD) atomicAdd(&tile[lidx], contrib);
+            else if (MODE == TVAM_MODE_ADJ) acc = fmaf(contrib, tile[lidx], acc);
+            else ++nvis;
+            if ((vx == evx && vy == evy) || !(rem > 1e-6f)) break;
+            const bool mx = dtx == dt, my = dty == dt;
+            dtx = mx ? tsx_ : dtx - dt;
+            dty = my ? tsy_ : dty - dt;
+            vx += mx ? stx : 0;
+            vy += my ? sty : 0;
+            lidx += (mx ? stx : 0) + (my ? sti : 0);
+            if ((unsigned)(vx - x0) >= (unsigned)wx || (unsigned)(vy - y0) >= (unsigned)wy) break;
+            e0 = e1;
+        }
+        if (MODE == TVAM_MODE_ADJ) atomicAdd(&out[act], acc * k.wscale);  // backward_from(Le*em_grad)
+    }
+
+    if (MODE == TVAM_MODE_FWD) {
+        __syncthreads();
+        for (int i = threadIdx.x; i < wx * wy; i += TVAM_BLOCK) {
+            int ly = i / wx, lx = i - ly * wx;
+            out[slice_base + (size_t)(y0 + ly) * k.res[0] + (x0 + lx)] = tile[ly * tsx + lx] * k.inv_vol;
+        }
+    } else if (MODE == TVAM_MODE_COUNT) {
+        for (int off = 32; off > 0; off >>= 1) nvis += __shfl_down(nvis, off, 64);
+        if ((threadIdx.x & 63) == 0 && nvis) atomicAdd(counter, nvis);
+    }
+}
+
+hipError_t tvam_launch_tiles(int mode, const TvamConsts& k, const TvamTiles& t, size_t lds_bytes,
+                             const float* pat, const int32_t* idxmap, const float* gin, float* out,
+                             unsigned long long* counter, hipStream_t stream) {
+    dim3 grid((unsigned)(t.ntx * t.nty), (unsigned)k.res[2]);
+    dim3 block(TVAM_BLOCK);
+    switch (mode) {
+        case TVAM_MODE_FWD:
+            hipLaunchKernelGGL(tvam_tile_kernel<TVAM_MODE_FWD>, grid, block, lds_bytes, stream, k, t, pat,
+                               idxmap, gin, out, counter);
+            break;
+        case TVAM_MODE_ADJ:
+            hipLaunchKernelGGL(tvam_tile_kernel<TVAM_MODE_ADJ>, grid, block, lds_bytes, stream, k, t, pat,
+                               idxmap, gin, out, counter);
+            break;
+        default:
+            hipLaunchKernelGGL(tvam_tile_kernel<TVAM_MODE_COUNT>, grid, block, lds_bytes, stream, k, t, pat,
+                               idxmap, gin, out, counter);
+            break;
+    }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Sparse active set <-> dense crop layout (projector.py:90-98 order)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int64_t tvam_dense_index(const TvamConsts& k, uint32_t p) {
+    uint32_t hw = (uint32_t)k.res_x * (uint32_t)k.res_y;
+    uint32_t a = p / hw, r = p - a * hw;
+    uint32_t row = r / (uint32_t)k.res_x, col = r - row * (uint32_t)k.res_x;
+    int rc = (int)row - k.crop_off_y, cc = (int)col - k.crop_off_x;
+    if (a < (uint32_t)k.a0 || a >= (uint32_t)k.a1 || rc < 0 || rc >= k.crop_y || cc < 0 || cc >= k.crop_x) return -1;
+    return ((int64_t)(a - (uint32_t)k.a0) * k.crop_y + rc) * k.crop_x + cc;  // shard-local
+}
+
+__global__ void tvam_scatter_kernel(TvamConsts k, const float* __restrict__ data,
+                                    const uint32_t* __restrict__ pixels, uint64_t n, float* __restrict__ dense,
+                                    int32_t* __restrict__ idxmap) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        int64_t di = tvam_dense_index(k, pixels[i]);
+        if (di < 0) continue;
+        dense[di] = data ? data[i] : 0.0f;
+        idxmap[di] = (int32_t)i;
+    }
+}
+
+__global__ void tvam_gather_kernel(TvamConsts k, const float* __restrict__ dense, const uint32_t* __restrict__ pixels,
+                                   uint64_t n, float* __restrict__ out) {
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (uint64_t)gridDim.x * blockDim.x) {
+        int64_t di = tvam_dense_index(k, pixels[i]);
+        out[i] = di < 0 ? 0.0f : dense[di];
+    }
+}
+
+static unsigned tvam_grid_for(uint64_t n) {
+    uint64_t g = (n + 255) / 256;
+    return (unsigned)(g < 4096 ? (g ? g : 1) : 4096);
+}
+
+hipError_t tvam_launch_scatter(const TvamConsts& k, const float* data, const uint32_t* pixels, uint64_t n,
+                               float* dense, int32_t* idxmap, hipStream_t stream) {
+    hipLaunchKernelGGL(tvam_scatter_kernel, dim3(tvam_grid_for(n)), dim3(256), 0, stream, k, data, pixels, n, dense,
+                       idxmap);
+    return hipGetLastError();
+}
+
+hipError_t tvam_launch_gather(const TvamConsts& k, const float* dense, const uint32_t* pixels, uint64_t n, float* out,
+                              hipStream_t stream) {
+    hipLaunchKernelGGL(tvam_gather_kernel, dim3(tvam_grid_for(n)), dim3(256), 0, stream, k, dense, pixels, n, out);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// ThresholdedLoss (loss.py:82-132), binary target: fused value + gradient.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float tvam_powi(float x, int K) {
+    float r = 1.0f;
+    for (int i = 0; i < K; ++i) r *= x;
+    return r;
+}
+
+__global__ __launch_bounds__(256) void tvam_loss_threshold_kernel(
+    const float* __restrict__ dose, const float* __restrict__ ddose, float alpha, const float* __restrict__ target,
+    uint64_t n, int K, float tl, float tu, float w_object, float w_void, float w_limit, float scale,
+    double* __restrict__ out, float* __restrict__ grad) {
+    __shared__ double red[256 / 64];
+    double acc = 0.0;
+    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
+        float x = dose[i];
+        if (ddose) x = fmaf(alpha, ddose[i], x);  // vol + alpha * dvol (lbfgs.py:258)
+        float l, gr;
+        if (target[i] > 0.0f) {
+            float zo = tu - x, zl = x - 1.0f;
+            float ro = zo > 0.0f ? zo : 0.0f, rl = zl > 0.0f ? zl : 0.0f;
+            l = w_object * tvam_powi(ro, K) + w_limit * tvam_powi(rl, K);
+            gr = (zo > 0.0f ? -w_object * (float)K * tvam_powi(ro, K - 1) : 0.0f) +
+                 (zl > 0.0f ? w_limit * (float)K * tvam_powi(rl, K - 1) : 0.0f);
+        } else {
+            float zv = x - tl;
+            float rv = zv > 0.0f ? zv : 0.0f;
+            l = w_void * tvam_powi(rv, K);
+            gr = zv > 0.0f ? w_void * (float)K * tvam_powi(rv, K - 1) : 0.0f;
+        }
+        acc += (double)l;
+        if (grad) grad[i] = gr * scale;
+    }
+    for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = acc;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double s = 0.0;
+        for (int w = 0; w < 256 / 64; ++w) s += red[w];
+        atomicAdd(out, s * (double)scale);
+    }
+}
+
+hipError_t tvam_launch_loss_threshold(const float* dose, const float* ddose, float alpha, const float* target,
+                                      uint64_t n, int K, float tl, float tu, float w_object, float w_void,
+                                      float w_limit, float scale, double* out, float* grad, hipStream_t stream) {
+    unsigned g = (unsigned)((n + 255) / 256);
+    if (g > 2048) g = 2048;
+    if (g == 0) g = 1;
+    hipLaunchKernelGGL(tvam_loss_threshold_kernel, dim3(g), dim3(256), 0, stream, dose, ddose, alpha, target, n, K, tl,
+                       tu, w_object, w_void, w_limit, scale, out, grad);
+    return hipGetLastError();
+}

@@ -1,0 +1,467 @@
+// tvam_plan.hip — plan construction and the extern "C" boundary (include/tvam.h).
+//
+// The plan turns a tvam_desc (the reference's scene / plugin properties) into
+// the small constant tables the tile kernels consume:
+//   * per-angle (cos, sin) of the shard, computed like CircularMotion.eval
+//     (motion.py:26-36: alpha = 2*pi*time, time = angle / n_patterns);
+//   * per-z-slice list of DMD rows whose (planar) rays lie in that slice;
+//   * per-(xy-tile, angle) range of DMD columns whose rays can cross the tile.
+// Caller buffers are never allocated or copied here on the hot path; only the
+// sparse active-set path uses a lazily allocated dense scratch.
+#include "tvam_internal.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+namespace {
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+    return fail(TVAM_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+}  // namespace
+
+struct tvam_plan {
+    tvam_desc desc;
+    int device;
+    TvamConsts k;
+    TvamTiles tiles;
+    int32_t ntiles;
+    size_t lds_bytes;
+    int32_t max_rows_per_slice;
+    bool empty;  // max_depth < 2: no ray reaches the medium
+    // device tables
+    float2* d_cs = nullptr;
+    int32_t* d_slice_off = nullptr;
+    int32_t* d_slice_rows = nullptr;
+    int32_t* d_col_lo = nullptr;
+    int32_t* d_col_off = nullptr;
+    unsigned long long* d_counter = nullptr;
+    // sparse scratch (dense crop layout), allocated on first sparse call
+    float* d_dense = nullptr;
+    int32_t* d_idxmap = nullptr;
+    uint64_t dense_n = 0;
+};
+
+extern "C" void tvam_desc_init(tvam_desc* d) {
+    std::memset(d, 0, sizeof(*d));
+    d->abi_version = TVAM_ABI_VERSION;
+    d->projector_type = TVAM_PROJECTOR_COLLIMATED;
+    d->n_patterns = 1000;            // projector.py:73
+    d->res_x = d->res_y = 256;       // projector.py:74-75
+    d->crop_x = d->crop_y = 256;
+    d->pixel_size_x = d->pixel_size_y = 1.0f;
+    d->distance = 20.0f;
+    d->sensor_type = TVAM_SENSOR_DDA;
+    for (int a = 0; a < 3; ++a) {
+        d->bbox_min[a] = -0.5f;
+        d->bbox_max[a] = 0.5f;
+        d->film_res[a] = 256;        // film.py:9-11
+    }
+    d->film_channels = 1;
+    d->vial_type = TVAM_VIAL_INDEX_MATCHED;
+    d->vial_height = 40.0f;          // geometry.py:80
+    d->medium_ior = 1.0f;
+    d->vial_ior = 1.5f;
+    d->print_time = 1.0f;            // common.py:13
+    d->regular_sampling = 0;         // common.py:22
+    d->sample_time = 0;              // common.py:10
+    d->max_depth = 6;                // optimize.py:99
+    d->rr_depth = 6;                 // optimize.py:100
+    d->transmission_only = 1;        // common.py:19
+    d->angle_begin = 0;
+    d->angle_end = -1;               // -1: all angles
+    d->tile = 0;
+}
+
+extern "C" const char* tvam_last_error(void) { return g_err.c_str(); }
+extern "C" int tvam_abi_version(void) { return TVAM_ABI_VERSION; }
+
+static void plan_free(tvam_plan* p) {
+    if (!p) return;
+    (void)hipFree(p->d_cs);
+    (void)hipFree(p->d_slice_off);
+    (void)hipFree(p->d_slice_rows);
+    (void)hipFree(p->d_col_lo);
+    (void)hipFree(p->d_col_off);
+    (void)hipFree(p->d_counter);
+    (void)hipFree(p->d_dense);
+    (void)hipFree(p->d_idxmap);
+    delete p;
+}
+
+extern "C" void tvam_plan_destroy(tvam_plan* p) {
+    if (!p) return;
+    int cur = 0;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(p->device);
+    plan_free(p);
+    (void)hipSetDevice(cur);
+}
+
+static int validate(const tvam_desc& d) {
+    if (d.abi_version != TVAM_ABI_VERSION) return fail(TVAM_ERR_INVALID, "tvam_desc.abi_version mismatch");
+    if (d.projector_type != TVAM_PROJECTOR_COLLIMATED)
+        return fail(TVAM_ERR_UNSUPPORTED, "only the 'collimated' projector is implemented on the GPU path");
+    if (d.sensor_type != TVAM_SENSOR_DDA) return fail(TVAM_ERR_UNSUPPORTED, "only the 'dda' sensor is implemented");
+    if (d.vial_type != TVAM_VIAL_INDEX_MATCHED)
+        return fail(TVAM_ERR_UNSUPPORTED, "only the 'index_matched' container is implemented on the GPU path");
+    if (d.film_channels != 1) return fail(TVAM_ERR_UNSUPPORTED, "surface-aware films (2 channels) are not implemented");
+    if (d.albedo != 0.0f) return fail(TVAM_ERR_UNSUPPORTED, "scattering media (albedo > 0) are not implemented");
+    if (d.sample_time) return fail(TVAM_ERR_UNSUPPORTED, "sample_time is not implemented on the GPU path");
+    if (d.rr_depth < 1) return fail(TVAM_ERR_UNSUPPORTED, "rr_depth < 1 (Russian roulette inside the medium) is not implemented");
+    if (d.n_patterns <= 0 || d.res_x <= 0 || d.res_y <= 0) return fail(TVAM_ERR_INVALID, "projector resolution and n_patterns must be positive");
+    if (d.crop_x <= 0 || d.crop_y <= 0 || d.crop_x > d.res_x || d.crop_y > d.res_y)
+        return fail(TVAM_ERR_INVALID, "Crop resolution must be smaller than the base resolution.");  // projector.py:81-82
+    if (d.crop_offset_x < 0 || d.crop_offset_y < 0 || d.crop_offset_x + d.crop_x > d.res_x ||
+        d.crop_offset_y + d.crop_y > d.res_y)
+        return fail(TVAM_ERR_INVALID, "With the specified crop offset, the cropped region extends beyond the base resolution.");  // projector.py:87-88
+    for (int a = 0; a < 3; ++a) {
+        if (d.film_res[a] <= 0) return fail(TVAM_ERR_INVALID, "film resolution must be positive");
+        if (!(d.bbox_max[a] > d.bbox_min[a])) return fail(TVAM_ERR_INVALID, "sensor bounding box is empty");
+    }
+    if (!(d.vial_r > 0.0f)) return fail(TVAM_ERR_INVALID, "vial radius must be positive");
+    if (!(d.pixel_size_x > 0.0f && d.pixel_size_y > 0.0f)) return fail(TVAM_ERR_INVALID, "pixel_size must be positive");
+    return 0;
+}
+
+static TvamConsts make_consts(const tvam_desc& d, int a0, int a1) {
+    TvamConsts k;
+    std::memset(&k, 0, sizeof(k));
+    for (int a = 0; a < 3; ++a) {
+        k.bmin[a] = d.bbox_min[a];
+        k.bmax[a] = d.bbox_max[a];
+        k.res[a] = d.film_res[a];
+        k.h[a] = (d.bbox_max[a] - d.bbox_min[a]) / (float)d.film_res[a];  // sensor.py:19
+    }
+    float vol = k.h[0] * k.h[1] * k.h[2];
+    k.inv_vol = vol != 0.0f ? 1.0f / vol : 0.0f;  // volume.py:41-42
+    k.res_x = d.res_x;
+    k.res_y = d.res_y;
+    k.crop_x = d.crop_x;
+    k.crop_y = d.crop_y;
+    k.crop_off_x = d.crop_offset_x;
+    k.crop_off_y = d.crop_offset_y;
+    k.n_patterns = d.n_patterns;
+    k.a0 = a0;
+    k.a1 = a1;
+    k.shard_base = (int64_t)a0 * d.crop_y * d.crop_x;
+    k.ex = (float)d.res_x * d.pixel_size_x;
+    k.ey = (float)d.res_y * d.pixel_size_y;
+    k.inv_w = 1.0f / (float)d.res_x;
+    k.inv_h = 1.0f / (float)d.res_y;
+    k.dist_m_zc = d.distance - 0.005f;
+    k.clockwise = d.clockwise;
+    k.regular = d.regular_sampling;
+    k.sample_time = d.sample_time;
+    k.skip_zero = (d.flags & TVAM_FLAG_NO_ZERO_SKIP) ? 0 : 1;
+    k.vial_r = d.vial_r;
+    k.vial_half_h = 0.5f * d.vial_height;
+    k.nsig2 = -d.sigma_t * 1.44269504088896340736f;
+    k.wscale = 0.0f;  // per call
+    return k;
+}
+
+template <typename T>
+static int upload(T** dst, const std::vector<T>& v) {
+    size_t bytes = std::max<size_t>(v.size(), 1) * sizeof(T);
+    hipError_t e = hipMalloc((void**)dst, bytes);
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc");
+    if (!v.empty()) {
+        e = hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+        if (e != hipSuccess) return hip_fail(e, "hipMemcpy");
+    }
+    return 0;
+}
+
+extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** out) {
+    if (!desc || !out) return fail(TVAM_ERR_INVALID, "null argument");
+    *out = nullptr;
+    int rc = validate(*desc);
+    if (rc) return rc;
+    const tvam_desc& d = *desc;
+    int a0 = d.angle_begin, a1 = d.angle_end < 0 ? d.n_patterns : d.angle_end;
+    if (a0 < 0 || a1 > d.n_patterns || a0 > a1) return fail(TVAM_ERR_INVALID, "invalid angle shard");
+
+    hipError_t e = hipSetDevice(device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+
+    tvam_plan* p = new tvam_plan();
+    p->desc = d;
+    p->device = device;
+    p->k = make_consts(d, a0, a1);
+    p->empty = d.max_depth < 2;  // entry bounce + medium segment (volume.py:179, :271-272)
+    const TvamConsts& k = p->k;
+    const int ns = a1 - a0;
+
+    // tile geometry: LDS-resident xy tile of one z-slice
+    auto pick = [&](int res) {
+        int ts = d.tile > 0 ? d.tile : 112;
+        int nt = (res + ts - 1) / ts;
+        return (res + nt - 1) / nt;
+    };
+    int tsx = pick(k.res[0]), tsy = pick(k.res[1]);
+    int ntx = (k.res[0] + tsx - 1) / tsx, nty = (k.res[1] + tsy - 1) / tsy;
+    p->ntiles = ntx * nty;
+    p->lds_bytes = (size_t)tsx * tsy * sizeof(float) + (size_t)(2 * ns + 1) * sizeof(int32_t);
+    if (p->lds_bytes > 160 * 1024) {
+        plan_free(p);
+        return fail(TVAM_ERR_INVALID, "tile too large for LDS; lower tvam_desc.tile");
+    }
+
+    // per-angle rotation (motion.py:26-36)
+    std::vector<float2> cs(ns);
+    for (int i = 0; i < ns; ++i) {
+        float time = (float)(a0 + i) / (float)d.n_patterns;
+        float alpha = TVAM_TWO_PI * time;
+        if (d.clockwise) alpha = -alpha;
+        cs[i] = make_float2(cosf(alpha), sinf(alpha));
+    }
+
+    // per-slice DMD rows.  A ray's height is y_c of its row (+ jitter); its
+    // slice is the DDA start voxel z (tvam_slice_of).
+    std::vector<std::vector<int32_t>> rows_of(k.res[2]);
+    for (int rc = 0; rc < d.crop_y; ++rc) {
+        int row = d.crop_offset_y + rc;
+        if (d.regular_sampling) {
+            float xc, yc;
+            tvam_ray_camera(k, 0, row, 0.5f, 0.5f, xc, yc);
+            int s = tvam_slice_of(k, yc);
+            if (s >= 0) rows_of[s].push_back(rc);
+        } else {
+            float xc, ytop, ybot;
+            tvam_ray_camera(k, 0, row, 0.5f, 0.0f, xc, ytop);
+            tvam_ray_camera(k, 0, row, 0.5f, 1.0f, xc, ybot);
+            double lo = ((double)ybot - k.bmin[2]) / k.h[2] - 1.0, hi = ((double)ytop - k.bmin[2]) / k.h[2] + 1.0;
+            int s0 = std::max(0, (int)std::floor(lo)), s1 = std::min(k.res[2] - 1, (int)std::floor(hi));
+            for (int s = s0; s <= s1; ++s) rows_of[s].push_back(rc);
+        }
+    }
+    std::vector<int32_t> slice_off(k.res[2] + 1, 0), slice_rows;
+    p->max_rows_per_slice = 0;
+    for (int s = 0; s < k.res[2]; ++s) {
+        slice_off[s] = (int32_t)slice_rows.size();
+        slice_rows.insert(slice_rows.end(), rows_of[s].begin(), rows_of[s].end());
+        p->max_rows_per_slice = std::max<int32_t>(p->max_rows_per_slice, (int32_t)rows_of[s].size());
+    }
+    slice_off[k.res[2]] = (int32_t)slice_rows.size();
+
+    // per-(tile, angle) DMD column ranges.  A collimated ray's lateral
+    // coordinate is l = dot(o, (s,-c,0)) = x_c; the spawn offset moves it by
+    // less than (1+max|p|)*RayEpsilon, covered by the margin.
+    double rmax = std::max({std::fabs((double)k.bmin[0]), std::fabs((double)k.bmax[0]), std::fabs((double)k.bmin[1]),
+                            std::fabs((double)k.bmax[1]), (double)d.vial_r, (double)k.vial_half_h});
+    double marg_l = 4.0 * (1.0 + rmax) * (double)TVAM_RAY_EPS;
+    const double W = d.res_x, ex = k.ex;
+    std::vector<int32_t> col_lo((size_t)p->ntiles * ns), col_off((size_t)p->ntiles * (ns + 1));
+    int64_t max_nrt = 0;
+    for (int ty = 0; ty < nty; ++ty)
+        for (int tx = 0; tx < ntx; ++tx) {
+            int tile = ty * ntx + tx;
+            double X0 = (double)k.bmin[0] + (double)(tx * tsx) * k.h[0];
+            double X1 = (double)k.bmin[0] + (double)std::min((tx + 1) * tsx, k.res[0]) * k.h[0];
+            double Y0 = (double)k.bmin[1] + (double)(ty * tsy) * k.h[1];
+            double Y1 = (double)k.bmin[1] + (double)std::min((ty + 1) * tsy, k.res[1]) * k.h[1];
+            int64_t acc = 0;
+            for (int i = 0; i < ns; ++i) {
+                double c = cs[i].x, s = cs[i].y;
+                double l[4] = {X0 * s - Y0 * c, X1 * s - Y0 * c, X0 * s - Y1 * c, X1 * s - Y1 * c};
+                double L0 = *std::min_element(l, l + 4) - marg_l, L1 = *std::max_element(l, l + 4) + marg_l;
+                L0 = std::max(L0, -(double)d.vial_r - marg_l);
+                L1 = std::min(L1, (double)d.vial_r + marg_l);
+                int lo = 0, cnt = 0;
+                if (L0 <= L1) {
+                    double c_lo = W * (0.5 - L1 / ex) - 1.0, c_hi = W * (0.5 - L0 / ex);
+                    int cl = (int)std::floor(c_lo) - 1 - d.crop_offset_x;
+                    int ch = (int)std::ceil(c_hi) + 1 - d.crop_offset_x;
+                    cl = std::max(cl, 0);
+                    ch = std::min(ch, d.crop_x - 1);
+                    if (ch >= cl) {
+                        lo = cl;
+                        cnt = ch - cl + 1;
+                    }
+                }
+                col_lo[(size_t)tile * ns + i] = lo;
+                col_off[(size_t)tile * (ns + 1) + i] = (int32_t)acc;
+                acc += cnt;
+            }
+            col_off[(size_t)tile * (ns + 1) + ns] = (int32_t)acc;
+            max_nrt = std::max(max_nrt, acc);
+        }
+    // flat slot count per workgroup must fit int32 (rows * columns * spp)
+    if ((int64_t)p->max_rows_per_slice * max_nrt * 64 > (int64_t)0x7fffffff) {
+        plan_free(p);
+        return fail(TVAM_ERR_TOO_LARGE, "too many rays per tile for one launch");
+    }
+
+    if ((rc = upload(&p->d_cs, cs)) || (rc = upload(&p->d_slice_off, slice_off)) ||
+        (rc = upload(&p->d_slice_rows, slice_rows)) || (rc = upload(&p->d_col_lo, col_lo)) ||
+        (rc = upload(&p->d_col_off, col_off))) {
+        plan_free(p);
+        return rc;
+    }
+    e = hipMalloc((void**)&p->d_counter, sizeof(unsigned long long));
+    if (e != hipSuccess) {
+        plan_free(p);
+        return hip_fail(e, "hipMalloc");
+    }
+    p->tiles.cs = p->d_cs;
+    p->tiles.slice_off = p->d_slice_off;
+    p->tiles.slice_rows = p->d_slice_rows;
+    p->tiles.col_lo = p->d_col_lo;
+    p->tiles.col_off = p->d_col_off;
+    p->tiles.ntx = ntx;
+    p->tiles.nty = nty;
+    p->tiles.tsx = tsx;
+    p->tiles.tsy = tsy;
+    p->tiles.n_shard = ns;
+    *out = p;
+    return 0;
+}
+
+// per-call constants: spp forced to 1 under regular sampling (common.py:49-51),
+// weight = inv_pdf / n_samples * print_time (projector.py:164-165, :187; common.py:111)
+static int call_setup(tvam_plan* p, uint64_t n_active, const uint32_t* active_pixels, uint32_t& spp, TvamConsts& k) {
+    const tvam_desc& d = p->desc;
+    uint64_t dense_n = (uint64_t)(p->k.a1 - p->k.a0) * d.crop_y * d.crop_x;  // this shard's angles
+    if (!active_pixels && n_active != dense_n)
+        return fail(TVAM_ERR_INVALID, "active_data and active_pixels must have the same length.");  // projector.py:137-138
+    if (d.regular_sampling) spp = 1;
+    if (spp == 0) spp = 4;  // optimize.py:96
+    if (n_active * (uint64_t)spp > (1ull << 32))
+        return fail(TVAM_ERR_TOO_LARGE,
+                    "The total number of Monte Carlo samples required by this rendering task exceeds 2^32 = "
+                    "4294967296. Please use fewer samples per pixel or render using multiple passes.");  // common.py:60-65
+    k = p->k;
+    float area = d.pixel_size_x * d.pixel_size_y * (float)n_active;
+    float w = area / (float)(n_active * (uint64_t)spp);
+    w = w * d.print_time;
+    float ss = d.albedo * d.sigma_t;
+    float sa_st = d.sigma_t != 0.0f ? (float)(((double)d.sigma_t - (double)ss) / (double)d.sigma_t) : 0.0f;
+    k.wscale = w * sa_st;
+    hipError_t e = hipSetDevice(p->device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    return 0;
+}
+
+static int ensure_dense(tvam_plan* p) {
+    const tvam_desc& d = p->desc;
+    uint64_t n = (uint64_t)(p->k.a1 - p->k.a0) * d.crop_y * d.crop_x;
+    if (p->d_dense && p->dense_n == n) return 0;
+    hipError_t e;
+    if ((e = hipMalloc((void**)&p->d_dense, n * sizeof(float))) != hipSuccess) return hip_fail(e, "hipMalloc");
+    if ((e = hipMalloc((void**)&p->d_idxmap, n * sizeof(int32_t))) != hipSuccess) return hip_fail(e, "hipMalloc");
+    p->dense_n = n;
+    return 0;
+}
+
+extern "C" int tvam_forward(tvam_plan* p, const float* active_data, const uint32_t* active_pixels, uint64_t n_active,
+                            uint32_t spp, uint32_t seed, float* dose, void* stream_) {
+    if (!p || !dose || (!active_data && n_active)) return fail(TVAM_ERR_INVALID, "null argument");
+    hipStream_t stream = (hipStream_t)stream_;
+    TvamConsts k;
+    int rc = call_setup(p, n_active, active_pixels, spp, k);
+    if (rc) return rc;
+    const TvamConsts& kc = k;
+    size_t V = (size_t)kc.res[0] * kc.res[1] * kc.res[2];
+    hipError_t e;
+    if (p->empty || n_active == 0) {
+        e = hipMemsetAsync(dose, 0, V * sizeof(float), stream);
+        return e == hipSuccess ? 0 : hip_fail(e, "hipMemsetAsync");
+    }
+    const float* pat = active_data;
+    const int32_t* idxmap = nullptr;
+    if (active_pixels) {
+        if ((rc = ensure_dense(p))) return rc;
+        if ((e = hipMemsetAsync(p->d_dense, 0, p->dense_n * sizeof(float), stream)) != hipSuccess ||
+            (e = hipMemsetAsync(p->d_idxmap, 0xff, p->dense_n * sizeof(int32_t), stream)) != hipSuccess)
+            return hip_fail(e, "hipMemsetAsync");
+        if ((e = tvam_launch_scatter(kc, active_data, active_pixels, n_active, p->d_dense, p->d_idxmap, stream)) !=
+            hipSuccess)
+            return hip_fail(e, "scatter launch");
+        pat = p->d_dense;
+        idxmap = p->d_idxmap;
+    }
+    TvamTiles t = p->tiles;
+    t.spp = spp;
+    t.seed = seed;
+    e = tvam_launch_tiles(TVAM_MODE_FWD, kc, t, p->lds_bytes, pat, idxmap, nullptr, dose, nullptr, stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "forward launch");
+}
+
+extern "C" int tvam_adjoint(tvam_plan* p, const float* grad_dose, const uint32_t* active_pixels, uint64_t n_active,
+                            uint32_t spp, uint32_t seed, float* grad_active, void* stream_) {
+    if (!p || !grad_dose || (!grad_active && n_active)) return fail(TVAM_ERR_INVALID, "null argument");
+    hipStream_t stream = (hipStream_t)stream_;
+    TvamConsts k;
+    int rc = call_setup(p, n_active, active_pixels, spp, k);
+    if (rc) return rc;
+    hipError_t e;
+    if (n_active == 0) return 0;
+    const int32_t* idxmap = nullptr;
+    if (active_pixels) {
+        // dense (angle,row,col) -> active index map; the kernel adds each
+        // ray's gradient straight into grad_active[active index]
+        if ((rc = ensure_dense(p))) return rc;
+        if ((e = hipMemsetAsync(p->d_idxmap, 0xff, p->dense_n * sizeof(int32_t), stream)) != hipSuccess)
+            return hip_fail(e, "hipMemsetAsync");
+        if ((e = tvam_launch_scatter(k, nullptr, active_pixels, n_active, p->d_dense, p->d_idxmap, stream)) !=
+            hipSuccess)
+            return hip_fail(e, "scatter launch");
+        idxmap = p->d_idxmap;
+    }
+    if ((e = hipMemsetAsync(grad_active, 0, n_active * sizeof(float), stream)) != hipSuccess)
+        return hip_fail(e, "hipMemsetAsync");
+    if (!p->empty) {
+        TvamTiles t = p->tiles;
+        t.spp = spp;
+        t.seed = seed;
+        e = tvam_launch_tiles(TVAM_MODE_ADJ, k, t, p->lds_bytes, nullptr, idxmap, grad_dose, grad_active, nullptr,
+                              stream);
+        if (e != hipSuccess) return hip_fail(e, "adjoint launch");
+    }
+    return 0;
+}
+
+extern "C" int tvam_count_visits(tvam_plan* p, uint32_t spp, uint32_t seed, uint64_t* visits) {
+    if (!p || !visits) return fail(TVAM_ERR_INVALID, "null argument");
+    TvamConsts k;
+    const tvam_desc& d = p->desc;
+    uint64_t n = (uint64_t)(p->k.a1 - p->k.a0) * d.crop_y * d.crop_x;
+    int rc = call_setup(p, n, nullptr, spp, k);
+    if (rc) return rc;
+    *visits = 0;
+    if (p->empty) return 0;
+    hipError_t e = hipMemset(p->d_counter, 0, sizeof(unsigned long long));
+    if (e != hipSuccess) return hip_fail(e, "hipMemset");
+    TvamTiles t = p->tiles;
+    t.spp = spp;
+    t.seed = seed;
+    e = tvam_launch_tiles(TVAM_MODE_COUNT, k, t, p->lds_bytes, nullptr, nullptr, nullptr, nullptr, p->d_counter,
+                          nullptr);
+    if (e != hipSuccess) return hip_fail(e, "count launch");
+    unsigned long long h = 0;
+    e = hipMemcpy(&h, p->d_counter, sizeof(h), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpy");
+    *visits = h;
+    return 0;
+}
+
+extern "C" int tvam_loss_threshold(const float* dose, const float* ddose, float alpha, const float* target, uint64_t n,
+                                   int32_t K, float tl, float tu, float w_object, float w_void, float w_limit,
+                                   float scale, double* out, float* grad, void* stream) {
+    if (!dose || !target || !out) return fail(TVAM_ERR_INVALID, "null argument");
+    if (K < 1 || K > 16) return fail(TVAM_ERR_UNSUPPORTED, "ThresholdedLoss: integer K in [1, 16] required on the GPU path");
+    hipError_t e = tvam_launch_loss_threshold(dose, ddose, alpha, target, n, K, tl, tu, w_object, w_void, w_limit, scale,
+                                              out, grad, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "loss launch");
+}

@@ -1,0 +1,151 @@
+"""Device-side projection engine: owns a tvam_plan and exposes the forward /
+adjoint projections as torch operations.
+
+``TvamRender`` plays the role of Mitsuba's ``mi.render`` custom op
+(optimize.py:216, :294): its forward is VolumeIntegrator.render
+(integrators/volume.py:18-56) and its backward is render_backward
+(integrators/volume.py:97-134).  Both run the HIP kernels of libtvam.so; there
+is no CPU fallback.
+"""
+from __future__ import annotations
+
+import ctypes
+from typing import Optional
+
+import torch
+
+from . import _abi
+
+
+def _stream_ptr(device: torch.device) -> int:
+    return torch.cuda.current_stream(device).cuda_stream
+
+
+def derive_seed_grad(seed: int) -> int:
+    """Seed of the adjoint pass when none is given (decorrelated from the primal)."""
+    v0, v1 = seed & 0xFFFFFFFF, 1
+    s = 0
+    for _ in range(4):
+        s = (s + 0x9E3779B9) & 0xFFFFFFFF
+        v0 = (v0 + ((((v1 << 4) & 0xFFFFFFFF) + 0xA341316C) ^ ((v1 + s) & 0xFFFFFFFF) ^ ((v1 >> 5) + 0xC8013EA4))) & 0xFFFFFFFF
+        v1 = (v1 + ((((v0 << 4) & 0xFFFFFFFF) + 0xAD90777D) ^ ((v0 + s) & 0xFFFFFFFF) ^ ((v0 >> 5) + 0x7E95761E))) & 0xFFFFFFFF
+    return v0
+
+
+class Projection:
+    """One tvam_plan (scene tables) bound to one GPU."""
+
+    def __init__(self, desc: _abi.TvamDesc, device: Optional[torch.device] = None):
+        if not torch.cuda.is_available():
+            raise _abi.TvamError("the TVAM projection engine needs a ROCm GPU (torch.cuda.is_available() is False)")
+        self.lib = _abi.load_library()
+        self.desc = desc.copy()
+        self.device = torch.device("cuda") if device is None else torch.device(device)
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        plan = ctypes.c_void_p()
+        with torch.cuda.device(self.device):
+            _abi.check(self.lib.tvam_plan_create(ctypes.byref(self.desc), self.device.index, ctypes.byref(plan)))
+        self._plan = plan
+        rx, ry, rz = self.desc.film_res
+        self.film_shape = (rz, ry, rx, self.desc.film_channels)
+        self.n_dense = self.desc.n_patterns * self.desc.crop_y * self.desc.crop_x
+
+    def close(self):
+        if getattr(self, "_plan", None) is not None and self._plan.value:
+            self.lib.tvam_plan_destroy(self._plan)
+            self._plan = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def _check_tensor(self, t: torch.Tensor, dtype, name):
+        if t.device != self.device or t.dtype != dtype or not t.is_contiguous():
+            raise ValueError(f"{name} must be a contiguous {dtype} tensor on {self.device}")
+
+    def forward(self, active_data: torch.Tensor, active_pixels: Optional[torch.Tensor] = None, spp: int = 1,
+                seed: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        self._check_tensor(active_data, torch.float32, "active_data")
+        if active_pixels is not None:
+            self._check_tensor(active_pixels, torch.int32, "active_pixels")
+        if out is None:
+            out = torch.empty(self.film_shape, dtype=torch.float32, device=self.device)
+        self._check_tensor(out, torch.float32, "dose")
+        with torch.cuda.device(self.device):
+            _abi.check(self.lib.tvam_forward(
+                self._plan, active_data.data_ptr(), None if active_pixels is None else active_pixels.data_ptr(),
+                active_data.numel(), spp, seed & 0xFFFFFFFF, out.data_ptr(), _stream_ptr(self.device)))
+        return out
+
+    def adjoint(self, grad_dose: torch.Tensor, n_active: int, active_pixels: Optional[torch.Tensor] = None,
+                spp: int = 1, seed: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
+        grad_dose = grad_dose.contiguous()
+        self._check_tensor(grad_dose, torch.float32, "grad_dose")
+        if grad_dose.numel() != self.film_shape[0] * self.film_shape[1] * self.film_shape[2] * self.film_shape[3]:
+            raise ValueError("grad_dose has the wrong number of elements")
+        if active_pixels is not None:
+            self._check_tensor(active_pixels, torch.int32, "active_pixels")
+        if out is None:
+            out = torch.empty(n_active, dtype=torch.float32, device=self.device)
+        self._check_tensor(out, torch.float32, "grad_active")
+        with torch.cuda.device(self.device):
+            _abi.check(self.lib.tvam_adjoint(
+                self._plan, grad_dose.data_ptr(), None if active_pixels is None else active_pixels.data_ptr(),
+                n_active, spp, seed & 0xFFFFFFFF, out.data_ptr(), _stream_ptr(self.device)))
+        return out
+
+    def count_visits(self, spp: int = 1, seed: int = 0) -> int:
+        v = ctypes.c_uint64(0)
+        with torch.cuda.device(self.device):
+            torch.cuda.synchronize(self.device)
+            _abi.check(self.lib.tvam_count_visits(self._plan, spp, seed & 0xFFFFFFFF, ctypes.byref(v)))
+        return int(v.value)
+
+
+class TvamRender(torch.autograd.Function):
+    """dose = render(active_data); d loss / d active_data via the adjoint kernel."""
+
+    @staticmethod
+    def forward(ctx, active_data, proj: Projection, active_pixels, spp: int, spp_grad: int, seed: int,
+                seed_grad: int):
+        ctx.proj = proj
+        ctx.active_pixels = active_pixels
+        ctx.spp_grad = spp_grad
+        ctx.seed_grad = seed_grad
+        ctx.n_active = active_data.numel()
+        return proj.forward(active_data.detach().contiguous(), active_pixels, spp, seed)
+
+    @staticmethod
+    def backward(ctx, grad_dose):
+        g = ctx.proj.adjoint(grad_dose.contiguous(), ctx.n_active, ctx.active_pixels, ctx.spp_grad, ctx.seed_grad)
+        return g, None, None, None, None, None, None
+
+
+def render(proj: Projection, active_data: torch.Tensor, active_pixels: Optional[torch.Tensor] = None,
+           spp: int = 1, spp_grad: Optional[int] = None, seed: int = 0, seed_grad: Optional[int] = None):
+    spp_grad = spp if spp_grad is None else spp_grad
+    seed_grad = derive_seed_grad(seed) if seed_grad is None else seed_grad
+    return TvamRender.apply(active_data, proj, active_pixels, spp, spp_grad, seed, seed_grad)
+
+
+def loss_threshold(dose: torch.Tensor, target: torch.Tensor, K: int, tl: float, tu: float, w_object: float,
+                   w_void: float, w_limit: float, scale: float, ddose: Optional[torch.Tensor] = None,
+                   alpha: float = 0.0, grad: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Fused ThresholdedLoss value (f64 device scalar) and optional dL/dx (HIP kernel)."""
+    lib = _abi.load_library()
+    out = torch.zeros(1, dtype=torch.float64, device=dose.device)
+    for name, t in (("dose", dose), ("target", target), ("ddose", ddose), ("grad", grad)):
+        if t is not None and (t.dtype != torch.float32 or not t.is_contiguous() or t.device != dose.device):
+            raise ValueError(f"{name} must be a contiguous float32 tensor on {dose.device}")
+    n = dose.numel()
+    if target.numel() != n or (ddose is not None and ddose.numel() != n) or (grad is not None and grad.numel() != n):
+        raise ValueError("loss_threshold: size mismatch")
+    with torch.cuda.device(dose.device):
+        _abi.check(lib.tvam_loss_threshold(
+            dose.data_ptr(), None if ddose is None else ddose.data_ptr(), float(alpha), target.data_ptr(), n, int(K),
+            float(tl), float(tu), float(w_object), float(w_void), float(w_limit), float(scale), out.data_ptr(),
+            None if grad is None else grad.data_ptr(), _stream_ptr(dose.device)))
+    return out[0]

@@ -1,0 +1,365 @@
+"""Pattern optimisation driver (mirror of drtvam/optimize.py).
+
+``load_scene(config)`` assembles the scene dictionary exactly as
+optimize.py:15-79 (vial, projector, sensor with scalex/y/z, target transform).
+``TvamProblem`` holds everything one optimizer iteration touches and
+``TvamProblem.iteration(i)`` is the loop body of optimize.py:287-323:
+
+    forward render (seed=i) -> loss (+ dL/dD) -> host sync of the loss value
+    -> adjoint render -> LinearLBFGS.step (1 more forward render + Armijo)
+    -> clamp patterns at 0
+
+With ThresholdedLoss on a binary target the loss, its gradient and every
+Armijo probe run in the fused HIP loss kernel; other losses go through torch
+autograd with the same render op.  Under torch.distributed the projector
+angles are sharded across ranks: each rank renders its angles, the partial
+dose is all-reduced (RCCL), the adjoint is rank-local and L-BFGS dots are
+all-reduced scalars.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import time
+from typing import Optional
+
+import numpy as np
+import torch
+
+from .engine import derive_seed_grad
+from .geometry import geometries
+from .integrators import VolumeIntegrator
+from .lbfgs import LinearLBFGS
+from .loss import losses, ThresholdedLoss
+from .scene import load_dict
+from .utils import discretize, analytic_target, mesh_bbox, target_transform, save_vol
+
+
+def load_scene(config):
+    for key in ['target', 'vial', 'projector', 'sensor']:
+        if key not in config:
+            raise ValueError(f"Missing field '{key}' in the configuration file.")
+    if 'type' not in config['vial']:
+        raise ValueError("The vial geometry must have a 'type' field.")
+    if config['vial']['type'] not in geometries.keys():
+        raise ValueError(f"Unknown vial geometry: '{config['vial']['type']}'")
+    vial = geometries[config['vial']['type']](config['vial'])
+
+    tgt = dict(config['target'])
+    if 'filename' not in tgt and 'analytic' not in tgt:
+        raise ValueError("Missing field 'filename' for the target shape.")
+    target = {'type': 'analytic', 'kind': tgt.get('analytic')}
+    if 'filename' in tgt:
+        bmin, bmax = mesh_bbox(tgt['filename'])
+        center = (tgt.get('box_center_x', 0.), tgt.get('box_center_y', 0.), tgt.get('box_center_z', 0.))
+        target = {'type': os.path.splitext(tgt['filename'])[1][1:], 'filename': tgt['filename'],
+                  'to_world': target_transform(bmin, bmax, tgt.get('size', 1.), center), 'bsdf': {'type': 'null'}}
+
+    def sensor_dict(sd):
+        sd = dict(sd)
+        sx, sy, sz = sd.pop('scalex', 1.), sd.pop('scaley', 1.), sd.pop('scalez', 1.)
+        sd['to_world'] = np.diag([sx, sy, sz, 1.0])
+        return sd
+
+    scene_dict = {
+        'type': 'scene',
+        'projector': dict(config['projector']),
+        'sensor': sensor_dict(config['sensor']),
+        'target': target,
+        '_container': vial,
+    } | vial.to_dict()
+    if 'final_sensor' in config:
+        scene_dict['final_sensor'] = sensor_dict(config['final_sensor'])
+    return scene_dict
+
+
+def _dist():
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+        return dist
+    return None
+
+
+class TvamProblem:
+    """Scene + target + loss + optimizer state of one optimisation run (one rank's angle shard)."""
+
+    def __init__(self, config, device=None, target=None, rank=None, world_size=None):
+        self.config = config
+        self.dist = _dist()
+        self.rank = rank if rank is not None else (self.dist.get_rank() if self.dist else 0)
+        self.world = world_size if world_size is not None else (self.dist.get_world_size() if self.dist else 1)
+        dev = torch.device(device) if device is not None else torch.device('cuda', torch.cuda.current_device())
+        proj_cfg = dict(config['projector'])
+        proj_cfg['device'] = dev
+        cfg = dict(config)
+        cfg['projector'] = proj_cfg
+        self.scene_dict = load_scene(cfg)
+        self.scene = load_dict(self.scene_dict)
+        self.sensor = self.scene.sensor_by_id('sensor')
+        ids = self.scene.sensor_ids()
+        self.final_sensor = self.scene.sensor_by_id('final_sensor') if 'final_sensor' in ids else self.sensor
+        if self.final_sensor.film().surface_aware:
+            raise ValueError("The final sensor is used to generate visualizations and metrics of the final simulated print. Therefore, it must not be surface-aware. If you are using the surface-aware discretization for optimization, please specify another sensor called 'final_sensor' in the configuration file.")
+        self.device = dev
+
+        self.spp = config.get('spp', 4)
+        self.spp_ref = config.get('spp_ref', 16)
+        self.spp_grad = config.get('spp_grad', self.spp)
+        self.max_depth = config.get('max_depth', 6)
+        self.rr_depth = config.get('rr_depth', 6)
+        self.time = config.get('time', 1.)
+        self.progressive = config.get('progressive', False)
+        self.transmission_only = config.get('transmission_only', True)
+        self.regular_sampling = config.get('regular_sampling', False)
+        self.n_steps = config.get('n_steps', 40)
+
+        # angle shard of this rank (contiguous blocks)
+        A = self.scene.projector.n_patterns
+        self.a0 = (A * self.rank) // self.world
+        self.a1 = (A * (self.rank + 1)) // self.world
+        iprops = {'max_depth': 3 if self.progressive else self.max_depth, 'rr_depth': self.rr_depth,
+                  'print_time': self.time, 'transmission_only': self.transmission_only,
+                  'regular_sampling': self.regular_sampling, 'angle_range': (self.a0, self.a1),
+                  'tile': config.get('tile', 0), 'flags': config.get('flags', 0)}
+        self.integrator = VolumeIntegrator(iprops)
+        self.final_integrator = VolumeIntegrator(iprops | {'max_depth': config.get('max_depth_ref', 16),
+                                                           'rr_depth': config.get('rr_depth_ref', 8)})
+
+        if target is None:
+            if self.sensor.film().surface_aware:
+                raise NotImplementedError("surface-aware optimisation is not supported yet")
+            if 'filename' in config['target']:
+                target = discretize(self.scene, sensor=self.sensor)
+            else:
+                target = analytic_target(self.sensor.resolution(), self.sensor.bbox_min, self.sensor.bbox_max,
+                                         config['target'].get('analytic', 'box_hole'))
+        self.target = target.to(device=dev, dtype=torch.float32).contiguous()
+
+        lcfg = dict(config.get('loss', {'type': 'threshold'}))
+        ltype = lcfg.pop('type', 'threshold')
+        if ltype not in losses:
+            raise ValueError(f"Unknown loss type: '{ltype}'. Available losses are: {list(losses.keys())}")
+        self.loss_fn = losses[ltype](lcfg)
+
+        # this rank's slice of projector.active_data (dense crop order is angle-major)
+        p = self.scene.projector
+        if not p.dense:
+            raise NotImplementedError("sharded optimisation needs the dense active set")
+        per_angle = p.crop[0] * p.crop[1]
+        self.n_local = (self.a1 - self.a0) * per_angle
+        self.n_global = A * per_angle
+        self.x0 = p.active_data[self.a0 * per_angle:self.a1 * per_angle].contiguous()
+        self.proj = self.integrator.projection(self.scene, self.sensor)
+        lf = self.loss_fn
+        self.fused = (isinstance(lf, ThresholdedLoss) and dev.type == 'cuda' and float(lf.K).is_integer()
+                      and 1 <= int(lf.K) <= 16 and self.target.shape[-1] == 1)
+        self.grad_vol = torch.empty(self.proj.film_shape, dtype=torch.float32, device=dev)
+        self.opt = None
+        self.loss_hist = []
+        self.timing = []
+
+    # ---- distributed helpers ------------------------------------------------
+    def allreduce_(self, t):
+        if self.dist is not None:
+            self.dist.all_reduce(t)
+        return t
+
+    def dot(self, a, b):
+        return self.allreduce_(torch.dot(a, b))
+
+    def sparsity(self, x):
+        lf = self.loss_fn
+        w = getattr(lf, 'weight_sparsity', 0)
+        if not w:
+            return None
+        v = self.allreduce_((torch.abs(x.detach()) ** lf.M).sum(dtype=torch.float64) * w)
+        return v / self.n_global if lf.reduction_name == 'mean' else v
+
+    def sparsity_grad(self, x):
+        lf = self.loss_fn
+        w = getattr(lf, 'weight_sparsity', 0)
+        if not w:
+            return None
+        g = w * lf.M * torch.abs(x.detach()) ** (lf.M - 1) * torch.sign(x.detach())
+        return g / self.n_global if lf.reduction_name == 'mean' else g
+
+    # ---- projections ----------------------------------------------------------
+    def forward(self, x, seed, out=None):
+        vol = self.proj.forward(x.detach().contiguous(), None, self.spp, seed, out=out)
+        return self.allreduce_(vol)
+
+    def adjoint(self, grad_vol, seed):
+        return self.proj.adjoint(grad_vol, self.n_local, None, self.spp_grad, derive_seed_grad(seed))
+
+    # ---- loss -------------------------------------------------------------------
+    def loss_value_grad(self, vol, x):
+        """(loss f64 device scalar, dL/dvol) — fused kernel or torch autograd."""
+        if self.fused:
+            v = self.loss_fn.fused_value_grad(vol, self.target, x, self.grad_vol)
+            s = self.sparsity(x)
+            return (v if s is None else v + s), self.grad_vol
+        vv = vol.detach().requires_grad_(True)
+        with torch.enable_grad():
+            l = self.loss_fn(vv, self.target, torch.zeros_like(x) if getattr(self.loss_fn, 'weight_sparsity', 0) == 0 else x.detach())
+            l.backward()
+        return l.detach().to(torch.float64), vv.grad
+
+    def loss_step(self, vol, dvol, alpha, patterns):
+        if self.fused:
+            v = self.loss_fn.fused_value(vol, self.target, patterns, dvol, alpha)
+            s = self.sparsity(patterns)
+            return v if s is None else v + s
+        return self.loss_fn(vol + alpha * dvol, self.target, patterns)
+
+    # ---- optimisation -------------------------------------------------------------
+    def make_optimizer(self):
+        key = 'projector.active_data'
+
+        def render_fn(vars_):
+            return self.forward(vars_[key], self._seed)
+
+        opt = LinearLBFGS(render_fn=render_fn, loss_fn=None, dot=self.dot, loss_step=self.loss_step)
+        opt[key] = self.x0
+        self.opt = opt
+        return opt
+
+    def iteration(self, i):
+        """One optimizer iteration (optimize.py:292-320).  Returns the loss value."""
+        if self.opt is None:
+            self.make_optimizer()
+        if self.progressive and i == 5:
+            self.integrator.max_depth = self.max_depth
+            self.proj = self.integrator.projection(self.scene, self.sensor)
+        key = 'projector.active_data'
+        self._seed = i
+        x = self.opt[key]
+        vol = self.forward(x, i)
+        loss, gvol = self.loss_value_grad(vol, x)
+        loss_v = float(loss)  # host sync, optimize.py:303
+        self.loss_hist.append(loss_v)
+        g = self.adjoint(gvol, i)
+        sg = self.sparsity_grad(x)
+        if sg is not None:
+            g = g + sg
+        x.grad = g
+        if loss_v == 0.0:
+            return loss_v
+        self.opt.step(vol, loss_v)
+        with torch.no_grad():
+            self.opt[key] = torch.clamp_min(self.opt[key].detach(), 0.0)
+        return loss_v
+
+    def patterns_local(self):
+        return self.opt['projector.active_data'].detach() if self.opt is not None else self.x0
+
+    def final_render(self, spp=None):
+        proj = self.final_integrator.projection(self.scene, self.final_sensor)
+        vol = proj.forward(self.patterns_local().contiguous(), None, spp or self.spp_ref, 0)
+        return self.allreduce_(vol)
+
+
+def optimize(config, patterns_fwd=None, device=None):
+    """Optimise the patterns (optimize.py:81-368).  Returns the final dose volume."""
+    prob = TvamProblem(config, device=device)
+    output = config.get('output', '.')
+    os.makedirs(output, exist_ok=True)
+    np.save(os.path.join(output, "target.npy"), prob.target.cpu().numpy())
+    if patterns_fwd is not None:
+        print("Using provided patterns for forward mode.")
+        full = torch.as_tensor(np.asarray(patterns_fwd, dtype=np.float32).reshape(-1), device=prob.device)
+        per = full.numel() // prob.scene.projector.n_patterns
+        prob.x0 = full[prob.a0 * per:prob.a1 * per].contiguous()
+    else:
+        print("Optimizing patterns...")
+        for i in range(prob.n_steps):
+            t0 = time.perf_counter()
+            loss = prob.iteration(i)
+            torch.cuda.synchronize()
+            prob.timing.append(time.perf_counter() - t0)
+            if loss == 0.0:
+                print("Converged")
+                break
+    print("Rendering final state...")
+    vol_final = prob.final_render()
+    if prob.rank == 0:
+        np.save(os.path.join(output, "final.npy"), vol_final.cpu().numpy())
+        np.save(os.path.join(output, "loss.npy"), np.asarray(prob.loss_hist))
+        np.save(os.path.join(output, "timing.npy"), np.asarray(prob.timing))
+    pats = prob.patterns_local()
+    if prob.dist is not None:
+        parts = [torch.empty_like(pats) for _ in range(prob.world)] if prob.n_local * prob.world == prob.n_global else None
+        if parts is not None:
+            prob.dist.all_gather(parts, pats)
+            pats = torch.cat(parts)
+    if prob.rank == 0:
+        p = prob.scene.projector
+        full = pats.cpu().numpy().reshape(-1, p.crop[1], p.crop[0])
+        np.savez_compressed(os.path.join(output, "patterns.npz"), patterns=full)
+        mx = float(full.max()) if full.size else 0.0
+        if mx > 0:
+            np.savez_compressed(os.path.join(output, "patterns_normalized_uint8.npz"),
+                                patterns=(full / mx * 255).astype(np.uint8))
+    return vol_final
+
+
+class OverrideAction(argparse.Action):
+    def __init__(self, option_strings, dest, nargs=None, **kwargs):
+        super().__init__(option_strings, dest, **kwargs)
+        self.overrides = {}
+
+    def __call__(self, parser, namespace, values, option_string=None):
+        try:
+            key, value = values.split('=')
+        except ValueError:
+            raise ValueError("Invalid parameter override. Use the format '-D key=value'")
+        try:
+            value = int(value)
+        except ValueError:
+            try:
+                value = float(value)
+            except ValueError:
+                pass
+        self.overrides[key] = value
+        setattr(namespace, self.dest, self.overrides)
+
+
+def apply_overrides(config, overrides):
+    for key, value in (overrides or {}).items():
+        key = key.split('.')
+        tmp = config
+        for k in key[:-1]:
+            tmp = tmp[k]
+        tmp[key[-1]] = value
+    return config
+
+
+def main(argv=None):
+    parser = argparse.ArgumentParser("Optimize patterns for TVAM.")
+    parser.add_argument("config", type=str, help="Path to the configuration file")
+    parser.add_argument("-D", dest="overrides", metavar="key=value", action=OverrideAction,
+                        help="Override/Add a parameter in the configuration dictionary. Nested keys are separated by dots.")
+    parser.add_argument("--backend", type=str, default="hip", choices=["hip", "cuda", "llvm"],
+                        help="Kept for CLI compatibility; the engine always runs the HIP kernels.")
+    parser.add_argument("--forward_mode", action="store_true", help="Just project the patterns without optimization.")
+    parser.add_argument("--patterns", type=str, help="Path to the patterns file (a .npz file). Only used in forward mode.")
+    args = parser.parse_args(argv)
+    with open(args.config, 'r') as f:
+        config = json.load(f)
+    apply_overrides(config, args.overrides)
+    if 'output' not in config:
+        config['output'] = os.path.dirname(os.path.abspath(args.config))
+    os.makedirs(config['output'], exist_ok=True)
+    with open(os.path.join(config['output'], "opt_config.json"), 'w') as f:
+        json.dump(config, f, indent=4)
+    if args.forward_mode:
+        if not args.patterns:
+            raise ValueError("In forward mode, you must specify the patterns file.")
+        patterns = np.load(args.patterns)['patterns']
+        optimize(config, patterns_fwd=patterns)
+    else:
+        optimize(config)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,99 @@
+"""Volumetric sensors (mirror of drtvam/sensor.py).
+
+The sensor defines the voxel grid: ``bbox = to_world @ [-0.5, 0.5]^3``
+(sensor.py:14-16) and ``voxel_size = extents / film resolution`` (:19).  The
+DDA accumulation itself (:306-440) runs inside the HIP kernels; the sensor
+contributes the grid to the plan descriptor.
+"""
+from __future__ import annotations
+
+import numpy as np
+
+from .film import VolumetricFilm, films
+from . import _abi
+
+
+def _as_transform(t):
+    if t is None:
+        return np.eye(4)
+    t = np.asarray(t, dtype=np.float64)
+    if t.shape == (4, 4):
+        return t
+    if t.shape == (3,):
+        return np.diag([t[0], t[1], t[2], 1.0])
+    raise ValueError("to_world must be a 4x4 matrix or a scale triple")
+
+
+class VolumetricSensor:
+    def __init__(self, props):
+        film = props.get('film', {'type': 'vfilm'})
+        if isinstance(film, dict):
+            ftype = film.get('type', 'vfilm')
+            if ftype not in films:
+                raise ValueError("Tried to load a VolumetricSensor with a non-volumetric film. The film must be of type VolumetricFilm.")
+            film = films[ftype](film)
+        if not isinstance(film, VolumetricFilm):
+            raise ValueError("Tried to load a VolumetricSensor with a non-volumetric film. The film must be of type VolumetricFilm.")
+        self.m_film = film
+        self.to_world = _as_transform(props.get('to_world', None))
+        lin, off = self.to_world[:3, :3], self.to_world[:3, 3]
+        if np.count_nonzero(lin - np.diag(np.diag(lin))):
+            raise ValueError("only axis-aligned (scale + translate) sensor transforms are supported")
+        c0 = (lin @ np.full(3, -0.5) + off).astype(np.float32)
+        c1 = (lin @ np.full(3, 0.5) + off).astype(np.float32)
+        self.bbox_min = np.minimum(c0, c1)
+        self.bbox_max = np.maximum(c0, c1)
+        res = np.array(self.m_film.resolution(), dtype=np.float32)
+        self.voxel_size = (self.bbox_max - self.bbox_min) / res  # fp32, sensor.py:19
+        self.volumes = None
+
+    def film(self):
+        return self.m_film
+
+    def resolution(self):
+        return self.m_film.resolution()
+
+    def compute_volume(self, scene=None):
+        if not self.m_film.surface_aware:
+            return float(np.prod(self.voxel_size, dtype=np.float32))
+        raise NotImplementedError("surface-aware discretization is not supported yet")
+
+    def fill_desc(self, desc: _abi.TvamDesc) -> None:
+        for a in range(3):
+            desc.bbox_min[a] = float(self.bbox_min[a])
+            desc.bbox_max[a] = float(self.bbox_max[a])
+            desc.film_res[a] = int(self.m_film.res[a])
+        desc.film_channels = self.m_film.channels
+
+
+class DDAVolumetricSensor(VolumetricSensor):
+    """Analytic per-voxel absorption by grid traversal (sensor.py:297-440)."""
+
+    def fill_desc(self, desc):
+        super().fill_desc(desc)
+        desc.sensor_type = _abi.SENSOR_DDA
+
+
+class RatioVolumetricSensor(VolumetricSensor):
+    """Ratio-tracking estimator (sensor.py:193-295); not on the GPU path yet."""
+
+    def __init__(self, props):
+        super().__init__(props)
+        self.majorant = props['majorant']
+
+    def fill_desc(self, desc):
+        raise NotImplementedError("the 'ratio' sensor is not supported by the GPU engine yet")
+
+
+class DeltaVolumetricSensor(VolumetricSensor):
+    """Collision estimator (sensor.py:112-191); not on the GPU path yet."""
+
+    def fill_desc(self, desc):
+        raise NotImplementedError("the 'delta' sensor is not supported by the GPU engine yet")
+
+
+sensors = {
+    'delta': DeltaVolumetricSensor,
+    'ratio': RatioVolumetricSensor,
+    'dda': DDAVolumetricSensor,
+}

@@ -1,0 +1,178 @@
+/*
+ * tvam.h — C ABI of the MI355X-native TVAM projection engine (libtvam.so).
+ *
+ * This is the drop-in boundary for Dr.TVAM's hot path: the per-angle voxel-grid
+ * ray march behind the `volume` integrator + `dda` sensor + `vfilm` film +
+ * `collimated` projector plugins.  Every entry point names the reference
+ * interface it replaces (paths relative to the drtvam source tree):
+ *
+ *   tvam_plan_create   <- scene assembly: optimize.py:15-79 (load_scene),
+ *                         TVAMProjector.__init__ projector.py:41-139,
+ *                         CollimatedProjector.__init__ projector.py:167-182,
+ *                         CircularMotion motion.py:19-36,
+ *                         VolumetricSensor.__init__ sensor.py:5-22,
+ *                         VolumetricFilm.__init__ film.py:4-21,
+ *                         IndexMatchedVial.to_dict geometry.py:75-96,
+ *                         TVAMIntegrator.__init__ integrators/common.py:6-22
+ *   tvam_forward       <- VolumeIntegrator.render integrators/volume.py:18-56
+ *                         (+ sample() :136-282, DDAVolumetricSensor.accumulate
+ *                         sensor.py:306-440 primal branch, VolumetricFilm.write
+ *                         film.py:40-41)
+ *   tvam_adjoint       <- VolumeIntegrator.render_backward integrators/volume.py:97-134
+ *                         (+ accumulate backward branch sensor.py:417-423 and
+ *                         dr.backward_from(Le * em_grad) volume.py:274-276)
+ *   tvam_count_visits  <- (new) exact DDA visit count H used for the roofline
+ *   tvam_loss_threshold<- ThresholdedLoss.__call__ loss.py:28-59, :119-132 (fused
+ *                         value + dL/dx, also used for the Armijo probes of
+ *                         LinearLBFGS.step lbfgs.py:256-266)
+ *   tvam_plan_destroy, tvam_last_error  <- Python exception plumbing
+ *
+ * All buffers are caller-owned device pointers (e.g. torch tensors' data_ptr()).
+ * Calls are asynchronous on the given HIP stream; a plan is bound to one device
+ * and is not thread-safe.  Functions return 0 on success and a negative
+ * TVAM_ERR_* code on failure; tvam_last_error() then returns a thread-local
+ * message (the Python shim re-raises it with the reference's wording).
+ */
+#ifndef TVAM_H_
+#define TVAM_H_
+
+#include <stdint.h>
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define TVAM_ABI_VERSION 1
+
+/* error codes */
+#define TVAM_OK               0
+#define TVAM_ERR_INVALID     -1   /* bad descriptor / argument (ValueError)  */
+#define TVAM_ERR_UNSUPPORTED -2   /* configuration not implemented yet        */
+#define TVAM_ERR_HIP         -3   /* HIP runtime failure (RuntimeError)      */
+#define TVAM_ERR_TOO_LARGE   -4   /* > 2^32 samples, common.py:60-65          */
+
+/* projector kinds (projector.py:300-302) */
+#define TVAM_PROJECTOR_COLLIMATED 0
+/* vial / container kinds (geometry.py:312-318) */
+#define TVAM_VIAL_INDEX_MATCHED   0
+#define TVAM_VIAL_CYLINDRICAL     1
+/* sensor kinds (sensor.py:442-444) */
+#define TVAM_SENSOR_DDA           0
+
+/*
+ * Scene + integrator description.  Plain old data; every field mirrors a
+ * reference property of the same meaning.
+ */
+typedef struct tvam_desc {
+    int32_t abi_version;          /* must be TVAM_ABI_VERSION */
+
+    /* projector: TVAMProjector props (projector.py:73-99) */
+    int32_t projector_type;       /* TVAM_PROJECTOR_* */
+    int32_t n_patterns;           /* 'n_patterns' (A) */
+    int32_t res_x, res_y;         /* 'resx', 'resy' (full DMD W, H) */
+    int32_t crop_x, crop_y;       /* 'cropx', 'cropy' */
+    int32_t crop_offset_x, crop_offset_y; /* 'crop_offset_x/_y' */
+    float   pixel_size_x, pixel_size_y;   /* 'pixel_size' (projector.py:171-175) */
+
+    /* motion: CircularMotion (motion.py:19-24) */
+    float   distance;             /* 'distance' */
+    int32_t clockwise;            /* 'clockwise' */
+
+    /* sensor + film: bbox = to_world @ [-0.5,0.5]^3 (sensor.py:14-16);
+       film resolution in film order: res.x = props['resy'],
+       res.y = props['resx'], res.z = props['resz'] (film.py:9-14) */
+    int32_t sensor_type;          /* TVAM_SENSOR_* */
+    float   bbox_min[3], bbox_max[3];
+    int32_t film_res[3];
+    int32_t film_channels;        /* 1 (2 = surface_aware, not yet supported) */
+
+    /* container (geometry.py:20-35, :75-96, :142-183) */
+    int32_t vial_type;            /* TVAM_VIAL_* */
+    float   vial_r;               /* index_matched 'r' (or cylindrical 'r_int') */
+    float   vial_r_ext;           /* cylindrical 'r_ext' */
+    float   vial_height;          /* 'height' (default 40) */
+    float   vial_ior;             /* cylindrical 'ior' */
+    float   medium_ior;           /* medium 'ior' */
+    float   sigma_t;              /* medium 'extinction' */
+    float   albedo;               /* medium 'albedo' */
+
+    /* integrator props (integrators/common.py:6-22, optimize.py:96-128) */
+    float   print_time;           /* 'print_time' (config 'time') */
+    int32_t regular_sampling;     /* 'regular_sampling' */
+    int32_t sample_time;          /* 'sample_time' */
+    int32_t max_depth;            /* 'max_depth' */
+    int32_t rr_depth;             /* 'rr_depth' */
+    int32_t transmission_only;    /* 'transmission_only' */
+
+    /* execution (new): angle shard [angle_begin, angle_end) of this rank and
+       the LDS tile edge in voxels (0 = auto) */
+    int32_t angle_begin, angle_end;
+    int32_t tile;
+    int32_t flags;                /* TVAM_FLAG_* */
+} tvam_desc;
+
+/* tvam_desc.flags */
+#define TVAM_FLAG_NO_ZERO_SKIP 1  /* forward: march rays whose pattern value is 0 too */
+
+typedef struct tvam_plan tvam_plan;
+
+/* Fill *desc with the reference defaults (scene-independent fields). */
+void tvam_desc_init(tvam_desc* desc);
+
+/* Validate desc, build per-angle / per-slice / per-tile tables on `device`. */
+int  tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** plan);
+void tvam_plan_destroy(tvam_plan* plan);
+
+/*
+ * Forward projection (primal render).  Writes the whole film
+ * dose[z][y][x] (film order, C = 1) = inv_vol * sum over rays of this plan's
+ * angle shard; every voxel is overwritten (no pre-zeroing needed).
+ *   active_data   : f32, n_active entries (projector.active_data)
+ *   active_pixels : u32 flat indices angle*H*W + row*W + col into the full DMD
+ *                   (projector.active_pixels); NULL means the dense crop order
+ *                   produced by TVAMProjector.__init__ (projector.py:90-98),
+ *                   in which case n_active must equal A*crop_y*crop_x.
+ * spp / seed follow TVAMIntegrator.prepare (common.py:41-68).
+ */
+int tvam_forward(tvam_plan* plan, const float* active_data,
+                 const uint32_t* active_pixels, uint64_t n_active,
+                 uint32_t spp, uint32_t seed, float* dose, void* hip_stream);
+
+/*
+ * Adjoint projection (render_backward).  grad_active[i] (overwritten, f32,
+ * n_active entries) = d<grad_dose, forward(active_data)>/d active_data[i],
+ * i.e. the gradient Dr.TVAM accumulates into projector.active_data.grad.
+ */
+int tvam_adjoint(tvam_plan* plan, const float* grad_dose,
+                 const uint32_t* active_pixels, uint64_t n_active,
+                 uint32_t spp, uint32_t seed, float* grad_active,
+                 void* hip_stream);
+
+/* Exact number of DDA voxel visits of one pass (host-synchronous). */
+int tvam_count_visits(tvam_plan* plan, uint32_t spp, uint32_t seed,
+                      uint64_t* visits);
+
+/*
+ * ThresholdedLoss (loss.py:82-132) over a binary target, fused.
+ *   x = dose + alpha * ddose (ddose may be NULL), target: f32 (>0 = object).
+ *   out[0] += sum of the per-voxel loss (f64 accumulation, caller zeroes out);
+ *   grad (may be NULL) = dL/dx per voxel (sum reduction; scale = 1/n for mean
+ *   is applied by the caller through `scale`).
+ */
+int tvam_loss_threshold(const float* dose, const float* ddose, float alpha,
+                        const float* target, uint64_t n, int32_t K,
+                        float tl, float tu, float w_object, float w_void,
+                        float w_limit, float scale, double* out, float* grad,
+                        void* hip_stream);
+
+/* Thread-local message describing the last error ("" if none). */
+const char* tvam_last_error(void);
+
+/* ABI version of the loaded library. */
+int tvam_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* TVAM_H_ */

@@ -1,0 +1,100 @@
+"""ctypes wrapper of the CPU oracle (oracle/tvam_oracle.c).
+
+TEST INFRASTRUCTURE ONLY.  Imported by tests/, __graft_entry__.smoke() (as the
+checker) and bench.py's cpu_baseline leg (as the timed CPU port).  The product
+package drtvam_amd never imports this module.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(_HERE, "build", "liboracle.so")
+
+_lib = None
+
+
+def build(force: bool = False) -> str:
+    if force or not os.path.exists(LIB) or os.path.getmtime(LIB) < os.path.getmtime(os.path.join(_HERE, "tvam_oracle.c")):
+        subprocess.run(["make", "-s", "-C", _HERE], check=True)
+    return LIB
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        from drtvam_amd._abi import TvamDesc  # the descriptor struct is the shared ABI
+
+        if not os.path.exists(LIB):
+            build()
+        L = ctypes.CDLL(LIB)
+        P = ctypes.c_void_p
+        D = ctypes.POINTER(TvamDesc)
+        L.oracle_forward.restype = ctypes.c_int
+        L.oracle_forward.argtypes = [D, P, P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, P, P, ctypes.c_int]
+        L.oracle_adjoint.restype = ctypes.c_int
+        L.oracle_adjoint.argtypes = [D, P, P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, P, P, ctypes.c_int]
+        L.oracle_ray.restype = ctypes.c_int
+        L.oracle_ray.argtypes = [D, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32, P]
+        L.oracle_dda_ray.restype = ctypes.c_int
+        L.oracle_dda_ray.argtypes = [D, P, P, ctypes.c_float, ctypes.c_double, P, P]
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def film_shape(desc):
+    rx, ry, rz = desc.film_res
+    return (rz, ry, rx)
+
+
+def forward(desc, active_data, active_pixels=None, spp=1, seed=0, nthreads=1):
+    """Dose [z, y, x] (float64) and the DDA visit count of one forward pass."""
+    data = np.ascontiguousarray(active_data, dtype=np.float32)
+    pix = None if active_pixels is None else np.ascontiguousarray(active_pixels, dtype=np.uint32)
+    dose = np.zeros(film_shape(desc), dtype=np.float64)
+    visits = ctypes.c_uint64(0)
+    rc = lib().oracle_forward(ctypes.byref(desc), _ptr(data), _ptr(pix), data.size, spp, seed, _ptr(dose),
+                              ctypes.cast(ctypes.byref(visits), ctypes.c_void_p), nthreads)
+    if rc:
+        raise ValueError(f"oracle_forward failed ({rc})")
+    return dose, visits.value
+
+
+def adjoint(desc, grad_dose, active_pixels=None, n_active=None, spp=1, seed=0, nthreads=1):
+    """Gradient w.r.t. active_data (float64) of <grad_dose, forward(.)>."""
+    g = np.ascontiguousarray(grad_dose, dtype=np.float32).reshape(film_shape(desc))
+    pix = None if active_pixels is None else np.ascontiguousarray(active_pixels, dtype=np.uint32)
+    if n_active is None:
+        n_active = pix.size if pix is not None else desc.n_patterns * desc.crop_y * desc.crop_x
+    out = np.zeros(n_active, dtype=np.float64)
+    visits = ctypes.c_uint64(0)
+    rc = lib().oracle_adjoint(ctypes.byref(desc), _ptr(g), _ptr(pix), n_active, spp, seed, _ptr(out),
+                              ctypes.cast(ctypes.byref(visits), ctypes.c_void_p), nthreads)
+    if rc:
+        raise ValueError(f"oracle_adjoint failed ({rc})")
+    return out, visits.value
+
+
+def ray(desc, pixel, wave_index=0, seed=0):
+    out = np.zeros(11, dtype=np.float32)
+    lib().oracle_ray(ctypes.byref(desc), pixel, wave_index, seed, _ptr(out))
+    return {"o": out[0:3].copy(), "d": out[3:6].copy(), "hit": bool(out[6]), "o2": out[7:10].copy(),
+            "maxt": float(out[10])}
+
+
+def dda_ray(desc, o, d, maxt, em=1.0):
+    o = np.ascontiguousarray(o, dtype=np.float32)
+    d = np.ascontiguousarray(d, dtype=np.float32)
+    film = np.zeros(film_shape(desc), dtype=np.float64)
+    visits = ctypes.c_uint64(0)
+    lib().oracle_dda_ray(ctypes.byref(desc), _ptr(o), _ptr(d), maxt, em, _ptr(film),
+                         ctypes.cast(ctypes.byref(visits), ctypes.c_void_p))
+    return film, visits.value

@@ -1,0 +1,482 @@
+/*
+ * tvam_oracle.c — CPU restatement of Dr.TVAM's forward/adjoint ray march.
+ *
+ * TEST INFRASTRUCTURE ONLY.  Nothing in drtvam_amd/ links, loads or calls this
+ * file; it is used by tests/ (as the parity checker), by
+ * __graft_entry__.smoke() (as the checker) and by bench.py's cpu_baseline leg
+ * (as the timed CPU port).  It is an independent re-statement of the
+ * reference algorithm, written from the reference sources:
+ *
+ *   ray generation    integrators/common.py:70-116 (sample_rays)
+ *   collimated rays   projector.py:148-188 (+ Mitsuba orthographic_projection,
+ *                     restated: x_c = W*a_x*(0.5-u), y_c = H*a_y*(0.5-v),
+ *                     z_c = 0.005, dir (0,0,1))
+ *   circular motion   motion.py:26-36 (+ Mitsuba look_at, restated:
+ *                     left = (s,-c,0), up = (0,0,1), dir = (-c,-s,0))
+ *   index-matched     geometry.py:75-96: open cylinder r, height h, null BSDF;
+ *     vial            Mitsuba cylinder intersection + SurfaceInteraction
+ *                     spawn_ray/offset_p restated (RayEpsilon = 1500*2^-24)
+ *   path loop         integrators/volume.py:136-282 for the non-scattering,
+ *                     transmission-only case: one medium segment per ray
+ *   DDA accumulate    sensor.py:306-440 (op for op, fp32 geometry)
+ *   film              film.py:9-21, :40-41 (layout, scatter-add)
+ *   render scale      integrators/volume.py:41-54 (inv_vol), :130 (adjoint)
+ *   sampler           Mitsuba 'independent' sampler (TEA-scrambled PCG32),
+ *                     restated from its published algorithm; draw order of
+ *                     common.py:92-108.  Parity with Mitsuba's own stream is
+ *                     UNPINNED (mitsuba/drjit are not installed here).
+ *
+ * Geometry (ray origins, box clip, DDA stepping, voxel choice) is computed in
+ * fp32 with the same operation order the reference uses; the per-visit
+ * weight exp(-st t)(1-exp(-st dt)) and all sums are evaluated in fp64.
+ * Compile with -ffp-contract=off so no FMA is formed implicitly.
+ */
+#include "../include/tvam.h"
+
+#include <math.h>
+#include <stdint.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#define OR_RAY_EPS (1500.0f * 5.9604644775390625e-08f) /* math::RayEpsilon<float> */
+#define OR_TWO_PI 6.2831855f                           /* float(2*pi) */
+
+/* ------------------------------------------------------------------------ */
+/* Sampler: TEA-scrambled PCG32 (Mitsuba IndependentSampler restated)        */
+/* ------------------------------------------------------------------------ */
+typedef struct { uint64_t state, inc; } or_pcg32;
+
+static uint32_t or_pcg_next(or_pcg32* r) {
+    uint64_t old = r->state;
+    r->state = old * 0x5851f42d4c957f2dULL + r->inc;
+    uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+    uint32_t rot = (uint32_t)(old >> 59u);
+    return (xs >> rot) | (xs << ((~rot + 1u) & 31u));
+}
+
+static void or_pcg_seed(or_pcg32* r, uint64_t initstate, uint64_t initseq) {
+    r->state = 0u;
+    r->inc = (initseq << 1u) | 1u;
+    (void)or_pcg_next(r);
+    r->state += initstate;
+    (void)or_pcg_next(r);
+}
+
+static float or_pcg_float(or_pcg32* r) {
+    uint32_t bits = (or_pcg_next(r) >> 9) | 0x3f800000u;
+    float f;
+    memcpy(&f, &bits, 4);
+    return f - 1.0f;
+}
+
+static void or_tea(uint32_t* v0p, uint32_t* v1p) {
+    uint32_t v0 = *v0p, v1 = *v1p, sum = 0;
+    for (int i = 0; i < 4; ++i) {
+        sum += 0x9e3779b9u;
+        v0 += ((v1 << 4) + 0xa341316cu) ^ (v1 + sum) ^ ((v1 >> 5) + 0xc8013ea4u);
+        v1 += ((v0 << 4) + 0xad90777du) ^ (v0 + sum) ^ ((v0 >> 5) + 0x7e95761eu);
+    }
+    *v0p = v0;
+    *v1p = v1;
+}
+
+static void or_sampler_seed(or_pcg32* r, uint32_t seed, uint64_t wave_index) {
+    uint32_t v0 = seed, v1 = (uint32_t)wave_index;
+    or_tea(&v0, &v1);
+    or_pcg_seed(r, v0, v1);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Scene constants                                                          */
+/* ------------------------------------------------------------------------ */
+typedef struct {
+    const tvam_desc* d;
+    float h[3];         /* voxel size (sensor.py:19)            */
+    int res[3];
+    float ex, ey;       /* emitter size W*a_x, H*a_y            */
+    float inv_w, inv_h; /* rcp(ScalarVector2f(w, h)) (common.py:98) */
+    double inv_vol;     /* volume.py:41-42                      */
+    double sa_over_st;  /* sensor.py:400, :404                  */
+    float st;
+} or_scene;
+
+static void or_scene_init(or_scene* s, const tvam_desc* d) {
+    s->d = d;
+    for (int k = 0; k < 3; ++k) {
+        s->res[k] = d->film_res[k];
+        s->h[k] = (d->bbox_max[k] - d->bbox_min[k]) / (float)d->film_res[k];
+    }
+    s->ex = (float)d->res_x * d->pixel_size_x;
+    s->ey = (float)d->res_y * d->pixel_size_y;
+    s->inv_w = 1.0f / (float)d->res_x;
+    s->inv_h = 1.0f / (float)d->res_y;
+    float vol = s->h[0] * s->h[1] * s->h[2];
+    s->inv_vol = vol != 0.0f ? 1.0 / (double)vol : 0.0;
+    s->st = d->sigma_t;
+    float ss = d->albedo * d->sigma_t;
+    s->sa_over_st = d->sigma_t != 0.0f ? ((double)d->sigma_t - (double)ss) / (double)d->sigma_t : 0.0;
+}
+
+/* per-ray constant weight: inv_pdf / n_samples * print_time (projector.py:164-165,187; common.py:111) */
+static double or_ray_weight(const tvam_desc* d, uint64_t n_active, uint32_t spp) {
+    float area = d->pixel_size_x * d->pixel_size_y * (float)n_active;
+    float w = area / (float)(n_active * (uint64_t)spp);
+    w = w * d->print_time;
+    return (double)w;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Ray generation: common.py:70-116 + projector.py:148-188 + motion.py:26-36 */
+/* ------------------------------------------------------------------------ */
+typedef struct { float o[3], d[3]; } or_ray;
+
+static void or_gen_ray(const or_scene* s, uint32_t pixel, uint64_t wave_index, uint32_t seed,
+                       or_ray* ray) {
+    const tvam_desc* d = s->d;
+    uint32_t hw = (uint32_t)d->res_y * (uint32_t)d->res_x;
+    uint32_t angle = pixel / hw;
+    uint32_t pix = pixel % hw;
+    uint32_t row = pix / (uint32_t)d->res_x;
+    uint32_t col = pix - row * (uint32_t)d->res_x;
+
+    float ox = 0.5f, oy = 0.5f, ot = 0.0f;
+    if (!d->regular_sampling || d->sample_time) {
+        or_pcg32 rng;
+        or_sampler_seed(&rng, seed, wave_index);
+        if (!d->regular_sampling) {
+            ox = or_pcg_float(&rng);
+            oy = or_pcg_float(&rng);
+        }
+        if (d->sample_time) ot = or_pcg_float(&rng);
+    }
+    float u = ((float)col + ox) * s->inv_w;
+    float v = ((float)row + oy) * s->inv_h;
+    float time = (float)angle;
+    if (d->sample_time) time = time + ot;
+    time = time / (float)d->n_patterns;
+
+    float alpha = OR_TWO_PI * time;
+    if (d->clockwise) alpha = -alpha;
+    float c = cosf(alpha), sn = sinf(alpha);
+
+    float xc = (0.5f - u) * s->ex;
+    float yc = (0.5f - v) * s->ey;
+    const float zc = 0.005f;
+    float dz = d->distance - zc;
+    ray->o[0] = c * dz + sn * xc;
+    ray->o[1] = sn * dz - c * xc;
+    ray->o[2] = yc;
+    ray->d[0] = -c;
+    ray->d[1] = -sn;
+    ray->d[2] = 0.0f;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Index-matched vial: open cylinder of radius r, |z| <= height/2            */
+/* ------------------------------------------------------------------------ */
+/* Numerically stable quadratic (Mitsuba math::solve_quadratic restated). */
+static int or_solve_quadratic(float a, float b, float c, float* x0, float* x1) {
+    float disc = b * b - 4.0f * a * c;
+    if (!(disc >= 0.0f)) return 0;
+    float sq = sqrtf(disc);
+    float temp = -0.5f * (b + copysignf(sq, b));
+    float r0 = temp / a, r1 = c / temp;
+    *x0 = fminf(r0, r1);
+    *x1 = fmaxf(r0, r1);
+    return 1;
+}
+
+static int or_cyl_roots(const float o[3], const float dd[3], float r, float* t0, float* t1) {
+    float A = dd[0] * dd[0] + dd[1] * dd[1];
+    float B = 2.0f * (dd[0] * o[0] + dd[1] * o[1]);
+    float C = o[0] * o[0] + o[1] * o[1] - r * r;
+    return or_solve_quadratic(A, B, C, t0, t1);
+}
+
+/* In-medium segment of a projector ray: origin o', maxt.  Returns 0 on miss. */
+static int or_segment_index_matched(const or_scene* s, const or_ray* ray, float o2[3], float* maxt) {
+    const tvam_desc* d = s->d;
+    float half = 0.5f * d->vial_height;
+    if (!(ray->o[2] >= -half && ray->o[2] <= half)) return 0; /* passes above/below the open tube */
+    float t0, t1;
+    if (!or_cyl_roots(ray->o, ray->d, d->vial_r, &t0, &t1)) return 0;
+    if (!(t0 >= 0.0f)) return 0; /* projector outside the vial: the entry is the near root */
+    float p[3];
+    for (int k = 0; k < 3; ++k) p[k] = fmaf(ray->d[k], t0, ray->o[k]);
+    float rp = sqrtf(p[0] * p[0] + p[1] * p[1]);
+    float n[3] = {p[0] / rp, p[1] / rp, 0.0f};
+    float m = fmaxf(fmaxf(fabsf(p[0]), fabsf(p[1])), fabsf(p[2]));
+    float mag = (1.0f + m) * OR_RAY_EPS;
+    float ndd = n[0] * ray->d[0] + n[1] * ray->d[1] + n[2] * ray->d[2];
+    if (signbit(ndd)) mag = -mag;
+    for (int k = 0; k < 3; ++k) o2[k] = fmaf(mag, n[k], p[k]);
+    float u0, u1;
+    if (!or_cyl_roots(o2, ray->d, d->vial_r, &u0, &u1)) return 0;
+    if (!(u1 > 0.0f)) return 0;
+    *maxt = u1;
+    return 1;
+}
+
+/* ------------------------------------------------------------------------ */
+/* DDA (sensor.py:327-438).  mode 0: forward (accumulate into film),          */
+/* mode 1: adjoint (gather grad), mode 2: count only.                        */
+/* ------------------------------------------------------------------------ */
+static double or_dda(const or_scene* s, const float o[3], const float dd[3], float maxt, double em,
+                     int mode, double* film, const float* grad, int only_slice, uint64_t* visits) {
+    const tvam_desc* d = s->d;
+    float tbmin[3], tbmax[3];
+    for (int k = 0; k < 3; ++k) {
+        tbmin[k] = (d->bbox_min[k] - o[k]) / dd[k];
+        tbmax[k] = (d->bbox_max[k] - o[k]) / dd[k];
+    }
+    float lo[3], hi[3];
+    for (int k = 0; k < 3; ++k) {
+        lo[k] = fminf(tbmin[k], tbmax[k]);
+        hi[k] = fmaxf(tbmin[k], tbmax[k]);
+    }
+    float mint_box = fmaxf(fmaxf(fmaxf(lo[0], lo[1]), lo[2]), 0.0f);
+    float maxt_box = fminf(fminf(hi[0], hi[1]), hi[2]);
+    float t_start = fmaxf(mint_box, 0.0f);
+    float t_end = fminf(maxt_box, maxt);
+    if (!(isfinite(t_start) && isfinite(t_end) && t_start < t_end)) return 0.0;
+
+    float gs[3], ge[3];
+    int step[3], cur[3], endv[3];
+    float dtmax[3], tstep[3];
+    for (int k = 0; k < 3; ++k) {
+        gs[k] = fmaf(dd[k], t_start, o[k]);
+        ge[k] = fmaf(dd[k], t_end, o[k]);
+        step[k] = dd[k] > 0.0f ? 1 : -1;
+        int sv = (int)((gs[k] - d->bbox_min[k]) / s->h[k]);
+        int ev = (int)((ge[k] - d->bbox_min[k]) / s->h[k]);
+        sv = sv < 0 ? 0 : (sv > s->res[k] - 1 ? s->res[k] - 1 : sv);
+        ev = ev < 0 ? 0 : (ev > s->res[k] - 1 ? s->res[k] - 1 : ev);
+        cur[k] = sv;
+        endv[k] = ev;
+        float next = d->bbox_min[k] + (float)(sv + step[k]) * s->h[k];
+        if (dd[k] < 0.0f) next = next + s->h[k];
+        int valid = fabsf(dd[k]) > 1e-8f;
+        dtmax[k] = valid ? (next - gs[k]) / dd[k] : INFINITY;
+        if (dtmax[k] < 0.0f) dtmax[k] = INFINITY;
+        tstep[k] = valid ? (s->h[k] / dd[k]) * (float)step[k] : INFINITY;
+    }
+    if (only_slice >= 0 && cur[2] != only_slice) return 0.0;
+
+    float t = t_start;
+    float remaining = t_end - t_start;
+    double st = (double)s->st;
+    double acc = 0.0;
+    uint64_t nv = 0;
+    for (;;) {
+        float dt = fminf(fminf(fminf(dtmax[0], dtmax[1]), dtmax[2]), remaining);
+        remaining = remaining - dt;
+        double w = s->sa_over_st * exp(-st * (double)t) * (1.0 - exp(-st * (double)fmaxf(dt, 0.0f)));
+        size_t idx = (size_t)cur[0] + (size_t)cur[1] * (size_t)s->res[0] +
+                     (size_t)cur[2] * (size_t)s->res[0] * (size_t)s->res[1];
+        if (mode == 0) film[idx] += em * w;
+        else if (mode == 1) acc += w * (double)grad[idx];
+        ++nv;
+        int alive = (cur[0] != endv[0] || cur[1] != endv[1] || cur[2] != endv[2]) && (remaining > 1e-6f);
+        if (!alive) break;
+        for (int k = 0; k < 3; ++k) {
+            int m = dtmax[k] == dt;
+            dtmax[k] = m ? tstep[k] : dtmax[k] - dt;
+            if (m) cur[k] += step[k];
+        }
+        if (cur[0] < 0 || cur[1] < 0 || cur[2] < 0 || cur[0] >= s->res[0] || cur[1] >= s->res[1] ||
+            cur[2] >= s->res[2])
+            break;
+        t = t + dt;
+    }
+    if (visits) *visits += nv;
+    return acc;
+}
+
+/* pixel index of active entry i (dense crop order if active_pixels is NULL, projector.py:90-98) */
+static uint32_t or_pixel(const tvam_desc* d, const uint32_t* active_pixels, uint64_t i) {
+    if (active_pixels) return active_pixels[i];
+    uint64_t cs = (uint64_t)d->crop_x * (uint64_t)d->crop_y;
+    uint64_t a = i / cs, r = i % cs;
+    uint64_t row = r / (uint64_t)d->crop_x, col = r % (uint64_t)d->crop_x;
+    return (uint32_t)(a * (uint64_t)d->res_x * (uint64_t)d->res_y +
+                      ((uint64_t)d->crop_offset_y + row) * (uint64_t)d->res_x + col +
+                      (uint64_t)d->crop_offset_x);
+}
+
+/* Sampler stream of a pixel: its dense crop index (angle, crop row, crop col).
+   The reference seeds stream i*spp+k for active entry i (common.py:57-67);
+   for the dense active set i IS this index.  Sparse sets use the same
+   definition so that angle-sharded runs draw identical samples. */
+static uint64_t or_stream(const tvam_desc* d, uint32_t pixel) {
+    uint64_t hw = (uint64_t)d->res_x * (uint64_t)d->res_y;
+    uint64_t a = pixel / hw, r = pixel % hw;
+    uint64_t row = r / (uint64_t)d->res_x, col = r % (uint64_t)d->res_x;
+    return (a * (uint64_t)d->crop_y + (row - (uint64_t)d->crop_offset_y)) * (uint64_t)d->crop_x +
+           (col - (uint64_t)d->crop_offset_x);
+}
+
+static int or_check(const tvam_desc* d) {
+    if (d->vial_type != TVAM_VIAL_INDEX_MATCHED) return TVAM_ERR_UNSUPPORTED;
+    if (d->projector_type != TVAM_PROJECTOR_COLLIMATED) return TVAM_ERR_UNSUPPORTED;
+    if (d->film_channels != 1) return TVAM_ERR_UNSUPPORTED;
+    if (d->albedo != 0.0f) return TVAM_ERR_UNSUPPORTED;
+    return 0;
+}
+
+/* one ray: generate + segment + DDA.  Returns the adjoint sum (mode 1). */
+static double or_trace(const or_scene* s, uint32_t pixel, uint64_t wave_index, uint32_t seed, double em,
+                       int mode, double* film, const float* grad, int only_slice, uint64_t* visits) {
+    or_ray ray;
+    or_gen_ray(s, pixel, wave_index, seed, &ray);
+    float o2[3], maxt;
+    if (!or_segment_index_matched(s, &ray, o2, &maxt)) return 0.0;
+    return or_dda(s, o2, ray.d, maxt, em, mode, film, grad, only_slice, visits);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Public oracle entry points (called from tests/ and bench.py via ctypes)   */
+/* ------------------------------------------------------------------------ */
+int oracle_forward(const tvam_desc* d, const float* active_data, const uint32_t* active_pixels,
+                   uint64_t n_active, uint32_t spp, uint32_t seed, double* dose, uint64_t* visits,
+                   int nthreads) {
+    int rc = or_check(d);
+    if (rc) return rc;
+    if (d->regular_sampling) spp = 1;
+    or_scene s;
+    or_scene_init(&s, d);
+    size_t V = (size_t)s.res[0] * s.res[1] * s.res[2];
+    memset(dose, 0, V * sizeof(double));
+    double wr = or_ray_weight(d, n_active, spp);
+    uint64_t nv_total = 0;
+    if (nthreads <= 1) {
+        for (uint64_t i = 0; i < n_active; ++i) {
+            uint32_t pixel = or_pixel(d, active_pixels, i);
+            double em = (double)active_data[i] * wr;
+            uint64_t st = or_stream(d, pixel);
+            for (uint32_t k = 0; k < spp; ++k)
+                or_trace(&s, pixel, st * spp + k, seed, em, 0, dose, NULL, -1, &nv_total);
+        }
+    } else {
+        /* Rays are planar (collimated + circular motion + vertical vial axis):
+           every ray stays in its start z-slice, so threads own whole slices and
+           accumulate without atomics (the "z-slab private" CPU baseline).
+           Active entries are bucketed by DMD row first (CSR), so each slice
+           only visits the rows whose rays can reach it. */
+        uint32_t H = (uint32_t)d->res_y, hw = (uint32_t)d->res_y * (uint32_t)d->res_x;
+        uint64_t* row_off = (uint64_t*)calloc((size_t)H + 1, sizeof(uint64_t));
+        uint64_t* row_idx = (uint64_t*)malloc((size_t)(n_active ? n_active : 1) * sizeof(uint64_t));
+        if (!row_off || !row_idx) {
+            free(row_off);
+            free(row_idx);
+            return TVAM_ERR_INVALID;
+        }
+        for (uint64_t i = 0; i < n_active; ++i) row_off[(or_pixel(d, active_pixels, i) % hw) / (uint32_t)d->res_x + 1]++;
+        for (uint32_t r = 0; r < H; ++r) row_off[r + 1] += row_off[r];
+        {
+            uint64_t* fill = (uint64_t*)malloc((size_t)H * sizeof(uint64_t));
+            memcpy(fill, row_off, (size_t)H * sizeof(uint64_t));
+            for (uint64_t i = 0; i < n_active; ++i) {
+                uint32_t r = (or_pixel(d, active_pixels, i) % hw) / (uint32_t)d->res_x;
+                row_idx[fill[r]++] = i;
+            }
+            free(fill);
+        }
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 1) num_threads(nthreads) reduction(+ : nv_total)
+#endif
+        for (int k = 0; k < s.res[2]; ++k) {
+            float z0 = d->bbox_min[2] + (float)k * s.h[2];
+            float z1 = z0 + s.h[2];
+            float marg = 2.0f * s.h[2];
+            for (uint32_t row = 0; row < H; ++row) {
+                /* z of this row's rays lies in [(0.5-(row+1)/H)*ey, (0.5-row/H)*ey] */
+                float zt = (0.5f - (float)row * s.inv_h) * s.ey;
+                float zb = (0.5f - (float)(row + 1) * s.inv_h) * s.ey;
+                if (zb > z1 + marg || zt < z0 - marg) continue;
+                for (uint64_t j = row_off[row]; j < row_off[row + 1]; ++j) {
+                    uint64_t i = row_idx[j];
+                    uint32_t pixel = or_pixel(d, active_pixels, i);
+                    double em = (double)active_data[i] * wr;
+                    uint64_t st = or_stream(d, pixel);
+                    for (uint32_t q = 0; q < spp; ++q)
+                        or_trace(&s, pixel, st * spp + q, seed, em, 0, dose, NULL, k, &nv_total);
+                }
+            }
+        }
+        free(row_off);
+        free(row_idx);
+    }
+    for (size_t v = 0; v < V; ++v) dose[v] *= s.inv_vol;
+    if (visits) *visits = nv_total;
+    return 0;
+}
+
+int oracle_adjoint(const tvam_desc* d, const float* grad_dose, const uint32_t* active_pixels,
+                   uint64_t n_active, uint32_t spp, uint32_t seed, double* grad, uint64_t* visits,
+                   int nthreads) {
+    int rc = or_check(d);
+    if (rc) return rc;
+    if (d->regular_sampling) spp = 1;
+    or_scene s;
+    or_scene_init(&s, d);
+    double wr = or_ray_weight(d, n_active, spp);
+    /* delta_L = grad_in * inv_vol (volume.py:130), in fp32 like the reference */
+    size_t V = (size_t)s.res[0] * s.res[1] * s.res[2];
+    float* dl = (float*)malloc(V * sizeof(float));
+    if (!dl) return TVAM_ERR_INVALID;
+    float inv_vol_f = (float)s.inv_vol;
+    for (size_t v = 0; v < V; ++v) dl[v] = grad_dose[v] * inv_vol_f;
+    uint64_t nv_total = 0;
+    if (nthreads < 1) nthreads = 1;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 256) num_threads(nthreads) reduction(+ : nv_total)
+#endif
+    for (int64_t i = 0; i < (int64_t)n_active; ++i) {
+        uint32_t pixel = or_pixel(d, active_pixels, (uint64_t)i);
+        double g = 0.0;
+        uint64_t st = or_stream(d, pixel);
+        for (uint32_t k = 0; k < spp; ++k)
+            g += or_trace(&s, pixel, st * spp + k, seed, 1.0, 1, NULL, dl, -1, &nv_total);
+        grad[i] = wr * g;
+    }
+    free(dl);
+    if (visits) *visits = nv_total;
+    return 0;
+}
+
+/* Ray of one sample, for property tests (test_projector.py:7-38 analogue):
+   out = {o.x,o.y,o.z, d.x,d.y,d.z, hit, o'.x,o'.y,o'.z, maxt} */
+int oracle_ray(const tvam_desc* d, uint32_t pixel, uint64_t wave_index, uint32_t seed, float* out) {
+    or_scene s;
+    or_scene_init(&s, d);
+    or_ray ray;
+    or_gen_ray(&s, pixel, wave_index, seed, &ray);
+    for (int k = 0; k < 3; ++k) {
+        out[k] = ray.o[k];
+        out[3 + k] = ray.d[k];
+    }
+    float o2[3] = {0, 0, 0}, maxt = 0.0f;
+    int hit = d->vial_type == TVAM_VIAL_INDEX_MATCHED ? or_segment_index_matched(&s, &ray, o2, &maxt) : 0;
+    out[6] = (float)hit;
+    out[7] = o2[0];
+    out[8] = o2[1];
+    out[9] = o2[2];
+    out[10] = maxt;
+    return 0;
+}
+
+/* DDA of an explicit ray (for analytic known-answer tests). */
+int oracle_dda_ray(const tvam_desc* d, const float* o, const float* dir, float maxt, double em, double* film,
+                   uint64_t* visits) {
+    or_scene s;
+    or_scene_init(&s, d);
+    size_t V = (size_t)s.res[0] * s.res[1] * s.res[2];
+    memset(film, 0, V * sizeof(double));
+    or_dda(&s, o, dir, maxt, em, 0, film, NULL, -1, visits);
+    return 0;
+}
+
+int oracle_version(void) { return 1; }
