@@ -43,6 +43,9 @@ struct TvamConsts {
     // medium / weights
     float nsig2;         // -sigma_t * log2(e): exp(-st t) == exp2(nsig2 t)
     float wscale;        // inv_pdf/n_samples * print_time * sa/st (projector.py:164-165,187; common.py:111; sensor.py:404)
+    // fixed-point forward bound: |voxel sum| <= max|em| * vox_chord * rays_per_voxel * rows * spp
+    float vox_chord;      // min(1, sigma_t * sqrt(2) * max(hx, hy)): bound of 1 - exp(-st dt) in a voxel
+    float rays_per_voxel; // n_shard * (ceil(sqrt(2) * max(hx, hy) / pixel_size_x) + 1)
 };
 
 // --------------------------------------------------------------------------

@@ -168,6 +168,11 @@ static TvamConsts make_consts(const tvam_desc& d, int a0, int a1) {
     k.vial_half_h = 0.5f * d.vial_height;
     k.nsig2 = -d.sigma_t * 1.44269504088896340736f;
     k.wscale = 0.0f;  // per call
+    {
+        double hxy = std::max((double)k.h[0], (double)k.h[1]);
+        k.vox_chord = (float)std::min(1.0, (double)d.sigma_t * std::sqrt(2.0) * hxy);
+        k.rays_per_voxel = (float)((double)(a1 - a0) * (std::ceil(std::sqrt(2.0) * hxy / d.pixel_size_x) + 1.0));
+    }
     return k;
 }
 
@@ -205,14 +210,14 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
 
     // tile geometry: LDS-resident xy tile of one z-slice
     auto pick = [&](int res) {
-        int ts = d.tile > 0 ? d.tile : 112;
+        int ts = d.tile > 0 ? d.tile : 80;
         int nt = (res + ts - 1) / ts;
         return (res + nt - 1) / nt;
     };
     int tsx = pick(k.res[0]), tsy = pick(k.res[1]);
     int ntx = (k.res[0] + tsx - 1) / tsx, nty = (k.res[1] + tsy - 1) / tsy;
     p->ntiles = ntx * nty;
-    p->lds_bytes = (size_t)tsx * tsy * sizeof(float) + (size_t)(2 * ns + 1) * sizeof(int32_t);
+    p->lds_bytes = (size_t)tsx * tsy * sizeof(float) + (size_t)(2 * ns + 1) * sizeof(int32_t) + 16 * sizeof(float);
     if (p->lds_bytes > 160 * 1024) {
         plan_free(p);
         return fail(TVAM_ERR_INVALID, "tile too large for LDS; lower tvam_desc.tile");
