@@ -70,6 +70,7 @@ def main():
     ap.add_argument("--angles", type=int, default=None)
     ap.add_argument("--tile", type=int, default=0)
     ap.add_argument("--zero-skip", action="store_true", help="skip rays whose pattern value is 0 (exact)")
+    ap.add_argument("--stats", action="store_true", help="report float-fallback tiles per forward (syncs)")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     args = ap.parse_args()
@@ -93,7 +94,7 @@ def main():
     A = args.angles or N
     cfg = benchy_index_matched(N=N, angles=A)
     cfg["tile"] = args.tile
-    cfg["flags"] = 0 if args.zero_skip else _abi.FLAG_NO_ZERO_SKIP
+    cfg["flags"] = (0 if args.zero_skip else _abi.FLAG_NO_ZERO_SKIP) | (_abi.FLAG_FWD_STATS if args.stats else 0)
     t_setup = time.perf_counter()
     prob = TvamProblem(cfg, device=dev)
     g = torch.Generator().manual_seed(0)
@@ -120,6 +121,9 @@ def main():
             out = fn(*a, **k)
             e.record()
             acc.append((s, e))
+            if args.stats and acc is fwd_ms:
+                log(f"  forward: {prob.proj.fallback_tiles()} float-fallback tiles, "
+                    f"{s.elapsed_time(e):.2f} ms")
             return out
         return wrap
 

@@ -21,11 +21,23 @@
 
 #define TVAM_BLOCK 256
 #define TVAM_WAVES (TVAM_BLOCK / 64)
+#ifndef TVAM_FWD_ACC64
+#define TVAM_FWD_ACC64 0  // 1: forward accumulates 64-bit fixed point (8 B per voxel of LDS)
+#endif
 
 __device__ __forceinline__ float tvam_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
 // How the in-tile march consumes one visit.
-enum TvamAcc { ACC_FLOAT = 0, ACC_FIXED = 1, ACC_GATHER = 2, ACC_COUNT = 3 };
+enum TvamAcc { ACC_FLOAT = 0, ACC_FIXED = 1, ACC_GATHER = 2, ACC_COUNT = 3, ACC_FIXED64 = 4 };
+
+// Exact split of a rounded fixed-point value q = rint(c) (|q| < 2^62) into a 64-bit integer.
+__device__ __forceinline__ unsigned long long tvam_f2i64(float c) {
+    const float q = rintf(c);
+    const float hi = floorf(q * 2.3283064365386963e-10f);          // q / 2^32, exact power-of-two scale
+    const float lo = fmaf(-hi, 4294967296.0f, q);                   // exact: low bits of q, in [0, 2^32)
+    return ((unsigned long long)(unsigned)(int)hi << 32) + (unsigned long long)(unsigned)lo;
+}
+
 
 // In-tile DDA march (sensor.py:383-438) from a resumed state.  Exits (all
 // evaluated before stepping, as the reference does): end voxel reached,
@@ -46,6 +58,7 @@ __device__ __forceinline__ void tvam_march(float* __restrict__ tile, int lidx, c
         const float c = e0 - e1;
         if (ACC == ACC_FLOAT) atomicAdd(&tile[lidx], c);
         else if (ACC == ACC_FIXED) atomicAdd(reinterpret_cast<int*>(tile) + lidx, __float2int_rn(c));
+        else if (ACC == ACC_FIXED64) atomicAdd(reinterpret_cast<unsigned long long*>(tile) + lidx, tvam_f2i64(c));
         else if (ACC == ACC_GATHER) acc = fmaf(c, tile[lidx], acc);
         else ++nvis;
         const bool mx = dtx == dt, my = dty == dt;
@@ -194,7 +207,8 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float* tile = reinterpret_cast<float*>(smem);
     const int tsx = tp.tsx, tsy = tp.tsy, ns = tp.n_shard;
-    int32_t* s_off = reinterpret_cast<int32_t*>(tile + tsx * tsy);
+    const int tile_words = (MODE == TVAM_MODE_FWD && TVAM_FWD_ACC64) ? 2 * tsx * tsy : tsx * tsy;
+    int32_t* s_off = reinterpret_cast<int32_t*>(tile + tile_words);
     int32_t* s_lo = s_off + (ns + 1);
     float* s_red = reinterpret_cast<float*>(s_lo + ns);
 
@@ -204,7 +218,7 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
     const int wx = x1 - x0, wy = y1 - y0;
     const size_t slice_base = (size_t)kz * (size_t)k.res[0] * (size_t)k.res[1];
 
-    for (int i = threadIdx.x; i < tsx * tsy; i += TVAM_BLOCK) {
+    for (int i = threadIdx.x; i < tile_words; i += TVAM_BLOCK) {
         float v = 0.0f;
         if (MODE == TVAM_MODE_ADJ) {
             int ly = i / tsx, lx = i - ly * tsx;
@@ -217,7 +231,10 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
     const int32_t* g_lo = tp.col_lo + (size_t)tile_id * ns;
     for (int i = threadIdx.x; i <= ns; i += TVAM_BLOCK) {
         s_off[i] = g_off[i];
-        if (i < ns) s_lo[i] = g_lo[i];
+        if (i < ns) {
+            s_lo[i] = g_lo[i];
+            if (MODE == TVAM_MODE_FWD) reinterpret_cast<unsigned*>(s_red + 16)[i] = 0u;
+        }
     }
     __syncthreads();
 
@@ -230,14 +247,19 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
 
     // Forward: pick the accumulator.  Fixed point (int32 ds_add: ~4x the
     // throughput of ds_add_f32 on gfx950) with a per-workgroup scale 2^e
-    // chosen so that |sum| < 2^30 is guaranteed by
-    //   |sum per voxel| <= max|em| * min(1, st*sqrt2*h) * rays_through_voxel;
-    // two's complement sums are exact and order-independent.  Workgroups
-    // whose pattern values span > 2^12 in magnitude fall back to float.
+    // chosen so that |sum| < 2^30 is guaranteed: at most rays_per_voxel/n_shard
+    // rays of one angle (and sample, and row) cross a voxel, each adding at
+    // most |em| * min(1, st*sqrt2*h), so
+    //   |voxel sum| <= vox_chord * (rays_per_voxel/n_shard) * spp * rows * sum_a max|em|_a.
+    // Two's complement sums are exact and order-independent (deterministic);
+    // the step is ~1e-9 of the tile's largest possible voxel sum.  When fewer
+    // than 1/64 of the rays are within 2^10 of the largest |value| (a few
+    // outliers would set the step), the workgroup uses ds_add_f32 instead.
     int acc_mode = ACC_GATHER;
     float fscale = 1.0f;
     if (MODE == TVAM_MODE_FWD) {
-        float mx = 0.0f, sm = 0.0f, nz = 0.0f;
+        unsigned* s_amax = reinterpret_cast<unsigned*>(s_red + 16);  // per-angle max |p| (zeroed above)
+        float nz = 0.0f;
         TvamSlot sl;
         tvam_slot_init(sl, threadIdx.x, max(per_row, 1));
         for (int f = threadIdx.x; f < total; f += TVAM_BLOCK, tvam_slot_next(sl, per_row)) {
@@ -248,24 +270,52 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
                                   k.shard_base;
             if (idxmap && idxmap[local] < 0) continue;
             const float p = fabsf(pat[local]);
-            mx = fmaxf(mx, p);
-            sm += p;
+            atomicMax(&s_amax[al], __float_as_uint(p));  // non-negative floats order like their bits
             nz += p > 0.0f ? 1.0f : 0.0f;
         }
-        const float pmax = tvam_block_max(mx, s_red);
-        const float psum = tvam_block_sum(sm, s_red);
+        __syncthreads();
+        float am = 0.0f, amx = 0.0f;
+        for (int a = threadIdx.x; a < ns; a += TVAM_BLOCK) {
+            const float v = __uint_as_float(s_amax[a]);
+            am += v;
+            amx = fmaxf(amx, v);
+        }
+        const float amax_sum = tvam_block_sum(am, s_red);
+        const float pmax = tvam_block_max(amx, s_red);
         const float pcnt = tvam_block_sum(nz, s_red);
-        const float bound = pmax * fabsf(k.wscale) * k.vox_chord * k.rays_per_voxel * (float)(nrows * spp);
-        if (pmax > 0.0f && pmax * pcnt <= 4096.0f * psum && bound > 0.0f && isfinite(bound)) {
+        // outlier test: how many rays are within 2^10 of the largest |value|
+        float nbig = 0.0f;
+        if (!TVAM_FWD_ACC64 && pmax > 0.0f && isfinite(pmax)) {
+            const float thr = pmax * (1.0f / 1024.0f);
+            tvam_slot_init(sl, threadIdx.x, max(per_row, 1));
+            for (int f = threadIdx.x; f < total; f += TVAM_BLOCK, tvam_slot_next(sl, per_row)) {
+                const int g = spp == 1 ? sl.rrem : sl.rrem / spp;
+                const int al = tvam_slot_angle(sl, g, s_off, ns);
+                const int rowc = tp.slice_rows[rbeg + sl.ri];
+                const int64_t local = ((int64_t)(k.a0 + al) * k.crop_y + rowc) * k.crop_x + s_lo[al] +
+                                      (g - s_off[al]) - k.shard_base;
+                if (idxmap && idxmap[local] < 0) continue;
+                nbig += fabsf(pat[local]) >= thr ? 1.0f : 0.0f;
+            }
+            nbig = tvam_block_sum(nbig, s_red);
+        }
+        const float per_angle = k.rays_per_voxel / (float)ns;
+        const float bound = amax_sum * fabsf(k.wscale) * k.vox_chord * per_angle * (float)(nrows * spp);
+        const int headroom = TVAM_FWD_ACC64 ? 62 : 30;
+        if (!(amax_sum > 0.0f)) {
+            acc_mode = TVAM_FWD_ACC64 ? ACC_FIXED64 : ACC_FIXED;  // all-zero tile: every contribution is 0
+        } else if ((TVAM_FWD_ACC64 || 64.0f * nbig >= pcnt) && isfinite(bound)) {
             int e;
             frexpf(bound, &e);  // bound < 2^e
-            e = 30 - e;
+            e = headroom - e;
             e = e > 126 ? 126 : (e < -126 ? -126 : e);
             fscale = ldexpf(1.0f, e);
-            acc_mode = ACC_FIXED;
+            acc_mode = TVAM_FWD_ACC64 ? ACC_FIXED64 : ACC_FIXED;
         } else {
             acc_mode = ACC_FLOAT;
+            if (counter && threadIdx.x == 0) atomicAdd(counter, 1ull);  // fallback statistics
         }
+        __syncthreads();
     }
 
     unsigned long long nvis = 0;
@@ -288,7 +338,10 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
         if (!tvam_tile_ray(k, tp, kz, x0, x1, y0, y1, rowc, al, colc, smp, idxmap, r)) continue;
         float acc = 0.0f;
         if (MODE == TVAM_MODE_FWD) {
-            if (acc_mode == ACC_FIXED)
+            if (TVAM_FWD_ACC64 && acc_mode == ACC_FIXED64)
+                tvam_march<ACC_FIXED64>(tile, r.lidx, r.lend, r.t, r.rem, r.dtx, r.dty, r.tsx, r.tsy, r.sx, r.sy,
+                                        r.cx, r.cy, em * fscale, k.nsig2, acc, nvis);
+            else if (!TVAM_FWD_ACC64 && acc_mode == ACC_FIXED)
                 tvam_march<ACC_FIXED>(tile, r.lidx, r.lend, r.t, r.rem, r.dtx, r.dty, r.tsx, r.tsy, r.sx, r.sy, r.cx,
                                       r.cy, em * fscale, k.nsig2, acc, nvis);
             else
@@ -308,9 +361,13 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
         __syncthreads();
         const float outscale = k.inv_vol / fscale;
         const int* itile = reinterpret_cast<const int*>(tile);
+        const long long* ltile = reinterpret_cast<const long long*>(tile);
         for (int i = threadIdx.x; i < wx * wy; i += TVAM_BLOCK) {
             int ly = i / wx, lx = i - ly * wx;
-            float v = acc_mode == ACC_FIXED ? (float)itile[ly * tsx + lx] * outscale : tile[ly * tsx + lx] * k.inv_vol;
+            const int li = ly * tsx + lx;
+            float v = acc_mode == ACC_FIXED64 ? (float)ltile[li] * outscale
+                      : acc_mode == ACC_FIXED ? (float)itile[li] * outscale
+                                              : tile[li] * k.inv_vol;
             out[slice_base + (size_t)(y0 + ly) * k.res[0] + (x0 + lx)] = v;
         }
     } else if (MODE == TVAM_MODE_COUNT) {

@@ -217,7 +217,12 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
     int tsx = pick(k.res[0]), tsy = pick(k.res[1]);
     int ntx = (k.res[0] + tsx - 1) / tsx, nty = (k.res[1] + tsy - 1) / tsy;
     p->ntiles = ntx * nty;
-    p->lds_bytes = (size_t)tsx * tsy * sizeof(float) + (size_t)(2 * ns + 1) * sizeof(int32_t) + 16 * sizeof(float);
+    // tile + angle offsets/first columns + reduction scratch + per-angle max |p|
+#ifndef TVAM_FWD_ACC64
+#define TVAM_FWD_ACC64 0
+#endif
+    p->lds_bytes = (size_t)tsx * tsy * sizeof(float) * (TVAM_FWD_ACC64 ? 2 : 1) + (size_t)(2 * ns + 1) * sizeof(int32_t) +
+                   16 * sizeof(float) + (size_t)ns * sizeof(float);
     if (p->lds_bytes > 160 * 1024) {
         plan_free(p);
         return fail(TVAM_ERR_INVALID, "tile too large for LDS; lower tvam_desc.tile");
@@ -399,7 +404,13 @@ extern "C" int tvam_forward(tvam_plan* p, const float* active_data, const uint32
     TvamTiles t = p->tiles;
     t.spp = spp;
     t.seed = seed;
-    e = tvam_launch_tiles(TVAM_MODE_FWD, kc, t, p->lds_bytes, pat, idxmap, nullptr, dose, nullptr, stream);
+    unsigned long long* stats = nullptr;
+    if (p->desc.flags & TVAM_FLAG_FWD_STATS) {
+        if ((e = hipMemsetAsync(p->d_counter, 0, sizeof(unsigned long long), stream)) != hipSuccess)
+            return hip_fail(e, "hipMemsetAsync");
+        stats = p->d_counter;
+    }
+    e = tvam_launch_tiles(TVAM_MODE_FWD, kc, t, p->lds_bytes, pat, idxmap, nullptr, dose, stats, stream);
     return e == hipSuccess ? 0 : hip_fail(e, "forward launch");
 }
 
@@ -458,6 +469,15 @@ extern "C" int tvam_count_visits(tvam_plan* p, uint32_t spp, uint32_t seed, uint
     e = hipMemcpy(&h, p->d_counter, sizeof(h), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return hip_fail(e, "hipMemcpy");
     *visits = h;
+    return 0;
+}
+
+extern "C" int tvam_plan_stats(tvam_plan* p, uint64_t* fallback_tiles) {
+    if (!p || !fallback_tiles) return fail(TVAM_ERR_INVALID, "null argument");
+    unsigned long long h = 0;
+    hipError_t e = hipMemcpy(&h, p->d_counter, sizeof(h), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpy");
+    *fallback_tiles = h;
     return 0;
 }
 

@@ -97,6 +97,14 @@ class Projection:
                 n_active, spp, seed & 0xFFFFFFFF, out.data_ptr(), _stream_ptr(self.device)))
         return out
 
+    def fallback_tiles(self) -> int:
+        """Workgroups of the last forward that used float LDS atomics (needs FLAG_FWD_STATS)."""
+        v = ctypes.c_uint64(0)
+        with torch.cuda.device(self.device):
+            torch.cuda.synchronize(self.device)
+            _abi.check(self.lib.tvam_plan_stats(self._plan, ctypes.byref(v)))
+        return int(v.value)
+
     def count_visits(self, spp: int = 1, seed: int = 0) -> int:
         v = ctypes.c_uint64(0)
         with torch.cuda.device(self.device):

@@ -114,6 +114,7 @@ typedef struct tvam_desc {
 
 /* tvam_desc.flags */
 #define TVAM_FLAG_NO_ZERO_SKIP 1  /* forward: march rays whose pattern value is 0 too */
+#define TVAM_FLAG_FWD_STATS    2  /* forward: count tiles that fell back to float LDS atomics */
 
 typedef struct tvam_plan tvam_plan;
 
@@ -148,6 +149,11 @@ int tvam_adjoint(tvam_plan* plan, const float* grad_dose,
                  const uint32_t* active_pixels, uint64_t n_active,
                  uint32_t spp, uint32_t seed, float* grad_active,
                  void* hip_stream);
+
+/* Diagnostics (host-synchronous): number of (slice, tile) workgroups of the
+   last forward that accumulated with float atomics instead of fixed point
+   (needs TVAM_FLAG_FWD_STATS). */
+int tvam_plan_stats(tvam_plan* plan, uint64_t* fallback_tiles);
 
 /* Exact number of DDA voxel visits of one pass (host-synchronous). */
 int tvam_count_visits(tvam_plan* plan, uint32_t spp, uint32_t seed,

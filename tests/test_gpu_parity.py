@@ -156,3 +156,27 @@ def test_fused_loss_matches_torch(K, reduction):
     torch.testing.assert_close(grad, xr.grad, rtol=1e-5, atol=1e-7)
     v2 = lf.fused_value(x, tgt, pats, dx, 0.37)
     assert float(v2) == pytest.approx(float(lf(x + 0.37 * dx, tgt, pats)), rel=1e-5)
+
+
+@pytest.mark.parametrize("dist", ["signed", "heavy", "sparse_spikes"])
+def test_forward_fixed_point_and_fallback(oracle, dist):
+    """Signed (L-BFGS search direction) and heavy-tailed inputs: fixed-point and float-fallback tiles."""
+    d = make(N=40, A=36)
+    d.flags = _abi.FLAG_FWD_STATS
+    n = 36 * 40 * 40
+    rng = np.random.default_rng(7)
+    if dist == "signed":
+        pat = rng.uniform(-1, 1, n).astype(np.float32)
+    elif dist == "heavy":
+        pat = rng.standard_cauchy(n).astype(np.float32)
+    else:
+        pat = rng.uniform(0, 1e-3, n).astype(np.float32)
+        pat[rng.choice(n, 5, replace=False)] = 1e4
+    ref, _ = oracle.forward(d, pat)
+    got, proj = gpu_forward(d, pat)
+    fb = proj.fallback_tiles()
+    assert rel_l2(got, ref) < RTOL_L2, fb
+    if dist == "sparse_spikes":
+        assert fb > 0  # a few outliers set the fixed-point step: those tiles take the float path
+    elif dist == "signed":
+        assert fb == 0
