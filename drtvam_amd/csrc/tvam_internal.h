@@ -10,7 +10,8 @@ struct TvamTiles {
     const int32_t* slice_off;  // [res_z + 1] CSR offsets into slice_rows
     const int32_t* slice_rows; // crop-local DMD rows feeding each z-slice
     const int32_t* col_lo;     // [ntiles][n_shard] first crop-local column crossing the tile
-    const int32_t* col_off;    // [ntiles][n_shard + 1] prefix sums of column counts
+    const int32_t* col_hi;     // [ntiles][n_shard] last crop-local column crossing the tile
+    const int32_t* col_off;    // [ntiles][n_shard + 1] prefix sums of column-PAIR counts ceil(n/2)
     int32_t ntx, nty, tsx, tsy;
     int32_t n_shard;
     uint32_t spp, seed;

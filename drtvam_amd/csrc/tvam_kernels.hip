@@ -27,6 +27,13 @@
 
 __device__ __forceinline__ float tvam_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
+// floor(x + 0.5) in one instruction (round to nearest, ties up).
+__device__ __forceinline__ int tvam_rint(float x) {
+    int r;
+    asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
 // How the in-tile march consumes one visit.
 enum TvamAcc { ACC_FLOAT = 0, ACC_FIXED = 1, ACC_GATHER = 2, ACC_COUNT = 3, ACC_FIXED64 = 4 };
 
@@ -39,16 +46,24 @@ __device__ __forceinline__ unsigned long long tvam_f2i64(float c) {
 }
 
 
-// In-tile DDA march (sensor.py:383-438) from a resumed state.  Exits (all
-// evaluated before stepping, as the reference does): end voxel reached,
-// remaining distance <= 1e-6, or the next step leaves the tile (cx / cy =
-// steps left inside the tile on each axis).  Branch-free body: one
-// exp2 per visit (telescoped exp(-st t)(1 - exp(-st dt))).
+// In-tile DDA march (sensor.py:383-438) from a resumed state.  `rem` is the
+// distance left INSIDE the tile (tile exit or segment end, whichever is
+// first), so one test ends the march: the reference's "remaining <= 1e-6"
+// test (sensor.py:427).  Rounding can let the last step cross the tile edge
+// one visit early; the tile carries a 1-voxel guard band that absorbs that
+// visit (its dt is at rounding level, and guard cells are never stored /
+// read as 0).  The reference's separate end-voxel test only differs at that
+// same rounding level.  One exp2 per visit (telescoped
+// exp(-st t)(1 - exp(-st dt))).
 template <int ACC>
-__device__ __forceinline__ void tvam_march(float* __restrict__ tile, int lidx, const int lend, float t, float rem,
-                                           float dtx, float dty, const float tsx, const float tsy, const int sx,
-                                           const int sy, int cx, int cy, const float ems, const float nsig2,
-                                           float& acc, unsigned long long& nvis) {
+__device__ __forceinline__ void tvam_march(float* __restrict__ tile, int lidx, float t, float rem, float dtx,
+                                           float dty, const float tsx, const float tsy, const int sx, const int sy,
+                                           const float ems, const float nsig2, float& acc, unsigned long long& nvis,
+                                           const int tw = 0, const int wx = 0, const int wy = 0) {
+#if defined(TVAM_EXPERIMENT) && TVAM_EXPERIMENT == 3  // timing only: setup without the march
+    acc += t + rem + dtx + dty + (float)lidx;
+    return;
+#endif
     float e0 = ems * tvam_exp2(nsig2 * t);
     for (;;) {
         const float dt = fminf(fminf(dtx, dty), rem);
@@ -57,19 +72,19 @@ __device__ __forceinline__ void tvam_march(float* __restrict__ tile, int lidx, c
         const float e1 = ems * tvam_exp2(nsig2 * t);
         const float c = e0 - e1;
         if (ACC == ACC_FLOAT) atomicAdd(&tile[lidx], c);
-        else if (ACC == ACC_FIXED) atomicAdd(reinterpret_cast<int*>(tile) + lidx, __float2int_rn(c));
+        else if (ACC == ACC_FIXED) atomicAdd(reinterpret_cast<int*>(tile) + lidx, tvam_rint(c));
         else if (ACC == ACC_FIXED64) atomicAdd(reinterpret_cast<unsigned long long*>(tile) + lidx, tvam_f2i64(c));
         else if (ACC == ACC_GATHER) acc = fmaf(c, tile[lidx], acc);
-        else ++nvis;
+        else {  // count interior visits only (guard-band visits carry rounding-level dt)
+            const int ly = lidx / tw, lx = lidx - ly * tw;
+            nvis += (lx >= 1 && lx <= wx && ly >= 1 && ly <= wy) ? 1 : 0;
+        }
         const bool mx = dtx == dt, my = dty == dt;
-        const bool done = (lidx == lend) | !(rem > 1e-6f) | (mx & (cx == 0)) | (my & (cy == 0));
         dtx = mx ? tsx : dtx - dt;
         dty = my ? tsy : dty - dt;
         lidx += (mx ? sx : 0) + (my ? sy : 0);
-        cx -= mx ? 1 : 0;
-        cy -= my ? 1 : 0;
         e0 = e1;
-        if (done) break;
+        if (!(rem > 1e-6f)) break;
     }
 }
 
@@ -114,7 +129,7 @@ __device__ __forceinline__ int tvam_slot_angle(TvamSlot& sl, int g, const int32_
 // Everything of one ray inside one tile.
 struct TvamTileRay {
     int64_t dense, local, act;
-    int lidx, lend, sx, sy, cx, cy;
+    int lidx, sx, sy;
     float t, rem, dtx, dty, tsx, tsy;
 };
 
@@ -167,15 +182,11 @@ __device__ __forceinline__ bool tvam_tile_ray(const TvamConsts& k, const TvamTil
     r.dty = fy ? fmaxf(fmaf((float)n1, q.ts[1], q.dtm0[1]) - tau_e, 0.0f) : TVAM_INF;
     r.tsx = q.ts[0];
     r.tsy = q.ts[1];
-    const int tw = tp.tsx;
+    const int tw = tp.tsx + 2;  // guard band of one voxel on every side
     r.sx = q.step[0];
     r.sy = q.step[1] * tw;
-    r.cx = !fx ? 0x3fffffff : (q.step[0] > 0 ? (x1 - 1) - vx : vx - x0);
-    r.cy = !fy ? 0x3fffffff : (q.step[1] > 0 ? (y1 - 1) - vy : vy - y0);
-    r.lidx = (vy - y0) * tw + (vx - x0);
-    const bool end_in = q.ev[0] >= x0 && q.ev[0] < x1 && q.ev[1] >= y0 && q.ev[1] < y1;
-    r.lend = end_in ? (q.ev[1] - y0) * tw + (q.ev[0] - x0) : -1;
-    r.rem = q.tau_end - tau_e;
+    r.lidx = (vy - y0 + 1) * tw + (vx - x0 + 1);
+    r.rem = tau_x - tau_e;  // distance left inside this tile
     r.t = q.t_start + tau_e;
     return true;
 }
@@ -207,10 +218,12 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float* tile = reinterpret_cast<float*>(smem);
     const int tsx = tp.tsx, tsy = tp.tsy, ns = tp.n_shard;
-    const int tile_words = (MODE == TVAM_MODE_FWD && TVAM_FWD_ACC64) ? 2 * tsx * tsy : tsx * tsy;
+    const int tw = tsx + 2, th = tsy + 2;  // tile + 1-voxel guard band
+    const int tile_words = (MODE == TVAM_MODE_FWD && TVAM_FWD_ACC64) ? 2 * tw * th : tw * th;
     int32_t* s_off = reinterpret_cast<int32_t*>(tile + tile_words);
     int32_t* s_lo = s_off + (ns + 1);
-    float* s_red = reinterpret_cast<float*>(s_lo + ns);
+    int32_t* s_hi = s_lo + ns;
+    float* s_red = reinterpret_cast<float*>(s_hi + ns);
 
     const int tile_id = blockIdx.x, kz = blockIdx.y;
     const int x0 = (tile_id % tp.ntx) * tsx, y0 = (tile_id / tp.ntx) * tsy;
@@ -221,18 +234,20 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
     for (int i = threadIdx.x; i < tile_words; i += TVAM_BLOCK) {
         float v = 0.0f;
         if (MODE == TVAM_MODE_ADJ) {
-            int ly = i / tsx, lx = i - ly * tsx;
-            if (lx < wx && ly < wy)
+            int ly = i / tw - 1, lx = i - (ly + 1) * tw - 1;
+            if (lx >= 0 && ly >= 0 && lx < wx && ly < wy)
                 v = gin[slice_base + (size_t)(y0 + ly) * k.res[0] + (x0 + lx)] * k.inv_vol;  // volume.py:130
         }
         tile[i] = v;
     }
     const int32_t* g_off = tp.col_off + (size_t)tile_id * (ns + 1);
     const int32_t* g_lo = tp.col_lo + (size_t)tile_id * ns;
+    const int32_t* g_hi = tp.col_hi + (size_t)tile_id * ns;
     for (int i = threadIdx.x; i <= ns; i += TVAM_BLOCK) {
         s_off[i] = g_off[i];
         if (i < ns) {
             s_lo[i] = g_lo[i];
+            s_hi[i] = g_hi[i];
             if (MODE == TVAM_MODE_FWD) reinterpret_cast<unsigned*>(s_red + 16)[i] = 0u;
         }
     }
@@ -266,12 +281,18 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
             const int g = spp == 1 ? sl.rrem : sl.rrem / spp;
             const int al = tvam_slot_angle(sl, g, s_off, ns);
             const int rowc = tp.slice_rows[rbeg + sl.ri];
-            const int64_t local = ((int64_t)(k.a0 + al) * k.crop_y + rowc) * k.crop_x + s_lo[al] + (g - s_off[al]) -
-                                  k.shard_base;
-            if (idxmap && idxmap[local] < 0) continue;
-            const float p = fabsf(pat[local]);
+            const int q = g - s_off[al], c1 = s_lo[al] + q, c2 = s_hi[al] - q;
+            const int64_t base = ((int64_t)(k.a0 + al) * k.crop_y + rowc) * k.crop_x - k.shard_base;
+            float p = 0.0f;
+            for (int rep = 0; rep < 2; ++rep) {
+                if (rep && c2 <= c1) break;
+                const int64_t local = base + (rep ? c2 : c1);
+                if (idxmap && idxmap[local] < 0) continue;
+                const float v = fabsf(pat[local]);
+                p = fmaxf(p, v);
+                nz += v > 0.0f ? 1.0f : 0.0f;
+            }
             atomicMax(&s_amax[al], __float_as_uint(p));  // non-negative floats order like their bits
-            nz += p > 0.0f ? 1.0f : 0.0f;
         }
         __syncthreads();
         float am = 0.0f, amx = 0.0f;
@@ -292,10 +313,14 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
                 const int g = spp == 1 ? sl.rrem : sl.rrem / spp;
                 const int al = tvam_slot_angle(sl, g, s_off, ns);
                 const int rowc = tp.slice_rows[rbeg + sl.ri];
-                const int64_t local = ((int64_t)(k.a0 + al) * k.crop_y + rowc) * k.crop_x + s_lo[al] +
-                                      (g - s_off[al]) - k.shard_base;
-                if (idxmap && idxmap[local] < 0) continue;
-                nbig += fabsf(pat[local]) >= thr ? 1.0f : 0.0f;
+                const int q = g - s_off[al], c1 = s_lo[al] + q, c2 = s_hi[al] - q;
+                const int64_t base = ((int64_t)(k.a0 + al) * k.crop_y + rowc) * k.crop_x - k.shard_base;
+                for (int rep = 0; rep < 2; ++rep) {
+                    if (rep && c2 <= c1) break;
+                    const int64_t local = base + (rep ? c2 : c1);
+                    if (idxmap && idxmap[local] < 0) continue;
+                    nbig += fabsf(pat[local]) >= thr ? 1.0f : 0.0f;
+                }
             }
             nbig = tvam_block_sum(nbig, s_red);
         }
@@ -325,35 +350,39 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
         const int g = spp == 1 ? sl.rrem : sl.rrem / spp;
         const int smp = sl.rrem - g * spp;
         const int al = tvam_slot_angle(sl, g, s_off, ns);
-        const int colc = s_lo[al] + (g - s_off[al]);
+        const int q = g - s_off[al], c1 = s_lo[al] + q, c2 = s_hi[al] - q;
         const int rowc = tp.slice_rows[rbeg + sl.ri];
-        float em = 1.0f;
-        if (MODE == TVAM_MODE_FWD) {
-            const int64_t local = ((int64_t)(k.a0 + al) * k.crop_y + rowc) * k.crop_x + colc - k.shard_base;
-            const float p = pat[local];
-            if (p == 0.0f && k.skip_zero) continue;  // contributes exactly zero dose
-            em = p * k.wscale;                        // Le * weight (common.py:108-111, volume.py:49)
-        }
-        TvamTileRay r;
-        if (!tvam_tile_ray(k, tp, kz, x0, x1, y0, y1, rowc, al, colc, smp, idxmap, r)) continue;
-        float acc = 0.0f;
-        if (MODE == TVAM_MODE_FWD) {
-            if (TVAM_FWD_ACC64 && acc_mode == ACC_FIXED64)
-                tvam_march<ACC_FIXED64>(tile, r.lidx, r.lend, r.t, r.rem, r.dtx, r.dty, r.tsx, r.tsy, r.sx, r.sy,
-                                        r.cx, r.cy, em * fscale, k.nsig2, acc, nvis);
-            else if (!TVAM_FWD_ACC64 && acc_mode == ACC_FIXED)
-                tvam_march<ACC_FIXED>(tile, r.lidx, r.lend, r.t, r.rem, r.dtx, r.dty, r.tsx, r.tsy, r.sx, r.sy, r.cx,
-                                      r.cy, em * fscale, k.nsig2, acc, nvis);
-            else
-                tvam_march<ACC_FLOAT>(tile, r.lidx, r.lend, r.t, r.rem, r.dtx, r.dty, r.tsx, r.tsy, r.sx, r.sy, r.cx,
-                                      r.cy, em, k.nsig2, acc, nvis);
-        } else if (MODE == TVAM_MODE_ADJ) {
-            tvam_march<ACC_GATHER>(tile, r.lidx, r.lend, r.t, r.rem, r.dtx, r.dty, r.tsx, r.tsy, r.sx, r.sy, r.cx,
-                                   r.cy, 1.0f, k.nsig2, acc, nvis);
-            atomicAdd(&out[r.act], acc * k.wscale);  // backward_from(Le * em_grad), volume.py:274-276
-        } else {
-            tvam_march<ACC_COUNT>(tile, r.lidx, r.lend, r.t, r.rem, r.dtx, r.dty, r.tsx, r.tsy, r.sx, r.sy, r.cx,
-                                  r.cy, 1.0f, k.nsig2, acc, nvis);
+        for (int rep = 0; rep < 2; ++rep) {  // the column pair (q, n-1-q)
+            if (rep && c2 <= c1) break;
+            const int colc = rep ? c2 : c1;
+            float em = 1.0f;
+            if (MODE == TVAM_MODE_FWD) {
+                const int64_t local = ((int64_t)(k.a0 + al) * k.crop_y + rowc) * k.crop_x + colc - k.shard_base;
+                const float p = pat[local];
+                if (p == 0.0f && k.skip_zero) continue;  // contributes exactly zero dose
+                em = p * k.wscale;                        // Le * weight (common.py:108-111, volume.py:49)
+            }
+            TvamTileRay r;
+            if (!tvam_tile_ray(k, tp, kz, x0, x1, y0, y1, rowc, al, colc, smp, idxmap, r)) continue;
+            float acc = 0.0f;
+            if (MODE == TVAM_MODE_FWD) {
+                if (TVAM_FWD_ACC64 && acc_mode == ACC_FIXED64)
+                    tvam_march<ACC_FIXED64>(tile, r.lidx, r.t, r.rem, r.dtx, r.dty, r.tsx, r.tsy, r.sx, r.sy,
+                                            em * fscale, k.nsig2, acc, nvis);
+                else if (!TVAM_FWD_ACC64 && acc_mode == ACC_FIXED)
+                    tvam_march<ACC_FIXED>(tile, r.lidx, r.t, r.rem, r.dtx, r.dty, r.tsx, r.tsy, r.sx, r.sy,
+                                          em * fscale, k.nsig2, acc, nvis);
+                else
+                    tvam_march<ACC_FLOAT>(tile, r.lidx, r.t, r.rem, r.dtx, r.dty, r.tsx, r.tsy, r.sx, r.sy,
+                                          em, k.nsig2, acc, nvis);
+            } else if (MODE == TVAM_MODE_ADJ) {
+                tvam_march<ACC_GATHER>(tile, r.lidx, r.t, r.rem, r.dtx, r.dty, r.tsx, r.tsy, r.sx, r.sy,
+                                       1.0f, k.nsig2, acc, nvis);
+                atomicAdd(&out[r.act], acc * k.wscale);  // backward_from(Le * em_grad), volume.py:274-276
+            } else {
+                tvam_march<ACC_COUNT>(tile, r.lidx, r.t, r.rem, r.dtx, r.dty, r.tsx, r.tsy, r.sx, r.sy,
+                                      1.0f, k.nsig2, acc, nvis, tw, wx, wy);
+            }
         }
     }
 
@@ -364,7 +393,7 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
         const long long* ltile = reinterpret_cast<const long long*>(tile);
         for (int i = threadIdx.x; i < wx * wy; i += TVAM_BLOCK) {
             int ly = i / wx, lx = i - ly * wx;
-            const int li = ly * tsx + lx;
+            const int li = (ly + 1) * tw + (lx + 1);
             float v = acc_mode == ACC_FIXED64 ? (float)ltile[li] * outscale
                       : acc_mode == ACC_FIXED ? (float)itile[li] * outscale
                                               : tile[li] * k.inv_vol;

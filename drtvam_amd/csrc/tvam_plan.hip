@@ -44,6 +44,7 @@ struct tvam_plan {
     int32_t* d_slice_off = nullptr;
     int32_t* d_slice_rows = nullptr;
     int32_t* d_col_lo = nullptr;
+    int32_t* d_col_hi = nullptr;
     int32_t* d_col_off = nullptr;
     unsigned long long* d_counter = nullptr;
     // sparse scratch (dense crop layout), allocated on first sparse call
@@ -92,6 +93,7 @@ static void plan_free(tvam_plan* p) {
     (void)hipFree(p->d_slice_off);
     (void)hipFree(p->d_slice_rows);
     (void)hipFree(p->d_col_lo);
+    (void)hipFree(p->d_col_hi);
     (void)hipFree(p->d_col_off);
     (void)hipFree(p->d_counter);
     (void)hipFree(p->d_dense);
@@ -221,7 +223,7 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
 #ifndef TVAM_FWD_ACC64
 #define TVAM_FWD_ACC64 0
 #endif
-    p->lds_bytes = (size_t)tsx * tsy * sizeof(float) * (TVAM_FWD_ACC64 ? 2 : 1) + (size_t)(2 * ns + 1) * sizeof(int32_t) +
+    p->lds_bytes = (size_t)(tsx + 2) * (tsy + 2) * sizeof(float) * (TVAM_FWD_ACC64 ? 2 : 1) + (size_t)(3 * ns + 1) * sizeof(int32_t) +
                    16 * sizeof(float) + (size_t)ns * sizeof(float);
     if (p->lds_bytes > 160 * 1024) {
         plan_free(p);
@@ -272,7 +274,11 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
                             std::fabs((double)k.bmax[1]), (double)d.vial_r, (double)k.vial_half_h});
     double marg_l = 4.0 * (1.0 + rmax) * (double)TVAM_RAY_EPS;
     const double W = d.res_x, ex = k.ex;
-    std::vector<int32_t> col_lo((size_t)p->ntiles * ns), col_off((size_t)p->ntiles * (ns + 1));
+    // Columns are enumerated in PAIRS (q, n-1-q): the chord through a tile is
+    // a symmetric trapezoid in the lateral position, so a lane marching both
+    // rays of a pair does nearly the same work as every other lane.
+    std::vector<int32_t> col_lo((size_t)p->ntiles * ns), col_hi((size_t)p->ntiles * ns),
+        col_off((size_t)p->ntiles * (ns + 1));
     int64_t max_nrt = 0;
     for (int ty = 0; ty < nty; ++ty)
         for (int tx = 0; tx < ntx; ++tx) {
@@ -301,8 +307,9 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
                     }
                 }
                 col_lo[(size_t)tile * ns + i] = lo;
+                col_hi[(size_t)tile * ns + i] = lo + cnt - 1;
                 col_off[(size_t)tile * (ns + 1) + i] = (int32_t)acc;
-                acc += cnt;
+                acc += (cnt + 1) / 2;
             }
             col_off[(size_t)tile * (ns + 1) + ns] = (int32_t)acc;
             max_nrt = std::max(max_nrt, acc);
@@ -315,6 +322,7 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
 
     if ((rc = upload(&p->d_cs, cs)) || (rc = upload(&p->d_slice_off, slice_off)) ||
         (rc = upload(&p->d_slice_rows, slice_rows)) || (rc = upload(&p->d_col_lo, col_lo)) ||
+        (rc = upload(&p->d_col_hi, col_hi)) ||
         (rc = upload(&p->d_col_off, col_off))) {
         plan_free(p);
         return rc;
@@ -328,6 +336,7 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
     p->tiles.slice_off = p->d_slice_off;
     p->tiles.slice_rows = p->d_slice_rows;
     p->tiles.col_lo = p->d_col_lo;
+    p->tiles.col_hi = p->d_col_hi;
     p->tiles.col_off = p->d_col_off;
     p->tiles.ntx = ntx;
     p->tiles.nty = nty;
