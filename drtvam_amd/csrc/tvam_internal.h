@@ -12,6 +12,9 @@ struct TvamTiles {
     const int32_t* col_lo;     // [ntiles][n_shard] first crop-local column crossing the tile
     const int32_t* col_hi;     // [ntiles][n_shard] last crop-local column crossing the tile
     const int32_t* col_off;    // [ntiles][n_shard + 1] prefix sums of column-PAIR counts ceil(n/2)
+    const float4* ang;         // [n_shard] {tstep_x, tstep_y, step_x, step_y} (sensor.py:343, :360)
+    const float4* ray_f;       // [n_shard*crop_y*crop_x*spp] {t_start, tau_end, dtmax0_x, dtmax0_y}
+    const int2* ray_i;         // same index: {start voxel x | y << 16, z-slice or -1}
     int32_t ntx, nty, tsx, tsy;
     int32_t n_shard;
     uint32_t spp, seed;
@@ -22,6 +25,11 @@ enum TvamMode { TVAM_MODE_FWD = 0, TVAM_MODE_ADJ = 1, TVAM_MODE_COUNT = 2 };
 hipError_t tvam_launch_tiles(int mode, const TvamConsts& k, const TvamTiles& t, size_t lds_bytes,
                              const float* pat, const int32_t* idxmap, const float* gin, float* out,
                              unsigned long long* counter, hipStream_t stream);
+
+// Per-ray pre-pass: ray generation, vial segment and DDA initialisation of
+// every ray of the shard, stored as the records the tile kernels resume from.
+hipError_t tvam_launch_ray_setup(const TvamConsts& k, const TvamTiles& t, float4* ray_f, int2* ray_i,
+                                 hipStream_t stream);
 
 hipError_t tvam_launch_scatter(const TvamConsts& k, const float* data, const uint32_t* pixels,
                                uint64_t n, float* dense, int32_t* idxmap, hipStream_t stream);

@@ -128,66 +128,100 @@ __device__ __forceinline__ int tvam_slot_angle(TvamSlot& sl, int g, const int32_
 
 // Everything of one ray inside one tile.
 struct TvamTileRay {
-    int64_t dense, local, act;
+    int64_t local, act;
     int lidx, sx, sy;
     float t, rem, dtx, dty, tsx, tsy;
 };
 
-// Ray generation + vial segment + DDA init + resume at the tile entry.
-// Returns false when the ray does not reach the tile.
+// Ray record pre-pass (one thread per ray of the shard): ray generation
+// (common.py:81-108), index-matched vial segment (volume.py:179-216) and DDA
+// initialisation (sensor.py:327-365).  Record index = local * spp + sample.
+__global__ __launch_bounds__(256) void tvam_ray_setup_kernel(TvamConsts k, TvamTiles tp, float4* __restrict__ ray_f,
+                                                             int2* __restrict__ ray_i) {
+    const int spp = (int)tp.spp;
+    const int64_t per_angle = (int64_t)k.crop_y * k.crop_x;
+    const int64_t n = (int64_t)tp.n_shard * per_angle * spp;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t local = i / spp;
+        const int smp = (int)(i - local * spp);
+        const int al = (int)(local / per_angle);
+        const int64_t pix = local - (int64_t)al * per_angle;
+        const int rowc = (int)(pix / k.crop_x), colc = (int)(pix - (int64_t)rowc * k.crop_x);
+        const int64_t dense = local + k.shard_base;  // sampler stream (global dense crop index)
+        float jx = 0.5f, jy = 0.5f;
+        if (!k.regular) {
+            TvamPcg rng;
+            rng.seed(tp.seed, (uint64_t)dense * (uint64_t)spp + (uint64_t)smp);
+            jx = rng.next_float();
+            jy = rng.next_float();
+        }
+        const float2 csv = tp.cs[al];
+        float xc, yc, ox, oy, oz, dx, dy;
+        tvam_ray_camera(k, k.crop_off_x + colc, k.crop_off_y + rowc, jx, jy, xc, yc);
+        tvam_ray_world(k, csv.x, csv.y, xc, yc, ox, oy, oz, dx, dy);
+        int slice = tvam_slice_of(k, oz);
+        float o2x, o2y, maxt;
+        TvamDda q;
+        if (slice < 0 || !tvam_segment_im(k, ox, oy, oz, dx, dy, o2x, o2y, maxt) ||
+            !tvam_dda_init(k, o2x, o2y, dx, dy, maxt, q)) {
+            ray_f[i] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
+            ray_i[i] = make_int2(0, -1);
+            continue;
+        }
+        ray_f[i] = make_float4(q.t_start, q.tau_end, q.dtm0[0], q.dtm0[1]);
+        ray_i[i] = make_int2(q.sv[0] | (q.sv[1] << 16), slice);
+    }
+}
+
+hipError_t tvam_launch_ray_setup(const TvamConsts& k, const TvamTiles& t, float4* ray_f, int2* ray_i,
+                                 hipStream_t stream) {
+    const int64_t n = (int64_t)t.n_shard * k.crop_y * k.crop_x * t.spp;
+    int64_t g = (n + 255) / 256;
+    if (g > 65536) g = 65536;
+    if (g < 1) g = 1;
+    hipLaunchKernelGGL(tvam_ray_setup_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, t, ray_f, ray_i);
+    return hipGetLastError();
+}
+
+// Resume one ray (pre-computed record) at the tile entry, in closed form of
+// the reference march.  Returns false when the ray does not reach the tile.
 __device__ __forceinline__ bool tvam_tile_ray(const TvamConsts& k, const TvamTiles& tp, int kz, int x0, int x1, int y0,
                                               int y1, int rowc, int al, int colc, int smp,
                                               const int32_t* __restrict__ idxmap, TvamTileRay& r) {
-    const int a = k.a0 + al;
-    r.dense = ((int64_t)a * k.crop_y + rowc) * k.crop_x + colc;  // global dense crop index (sampler stream)
-    r.local = r.dense - k.shard_base;                             // shard-local data index
+    r.local = ((int64_t)(k.a0 + al) * k.crop_y + rowc) * k.crop_x + colc - k.shard_base;
     r.act = r.local;
     if (idxmap) {
         r.act = idxmap[r.local];
         if (r.act < 0) return false;  // inactive pixel
     }
-    // ---- ray generation (common.py:81-108) ------------------------------
-    float jx = 0.5f, jy = 0.5f;
-    if (!k.regular) {
-        TvamPcg rng;
-        rng.seed(tp.seed, (uint64_t)r.dense * (uint64_t)tp.spp + (uint64_t)smp);
-        jx = rng.next_float();
-        jy = rng.next_float();
-    }
-    const float2 csv = tp.cs[al];
-    float xc, yc, ox, oy, oz, dx, dy;
-    tvam_ray_camera(k, k.crop_off_x + colc, k.crop_off_y + rowc, jx, jy, xc, yc);
-    tvam_ray_world(k, csv.x, csv.y, xc, yc, ox, oy, oz, dx, dy);
-    if (tvam_slice_of(k, oz) != kz) return false;
-    // ---- vial entry / medium segment (volume.py:179-216) ----------------
-    float o2x, o2y, maxt;
-    if (!tvam_segment_im(k, ox, oy, oz, dx, dy, o2x, o2y, maxt)) return false;
-    // ---- DDA setup (sensor.py:327-365) ----------------------------------
-    TvamDda q;
-    if (!tvam_dda_init(k, o2x, o2y, dx, dy, maxt, q)) return false;
-    // ---- resume at the tile entry (closed form of the reference march) --
+    const int64_t ri = r.local * (int64_t)tp.spp + smp;
+    const int2 ii = tp.ray_i[ri];
+    if (ii.y != kz) return false;  // misses the grid / vial, or lies in another z-slice
+    const float4 ff = tp.ray_f[ri];
+    const float4 an = tp.ang[al];
+    const int svx = ii.x & 0xffff, svy = ii.x >> 16;
+    const int stx = (int)an.z, sty = (int)an.w;
     float tin0, tout0, tin1, tout1;
     int nin0, nout0, nin1, nout1;
-    tvam_axis_window(q.sv[0], q.step[0], q.dtm0[0], q.ts[0], x0, x1, tin0, tout0, nin0, nout0);
-    tvam_axis_window(q.sv[1], q.step[1], q.dtm0[1], q.ts[1], y0, y1, tin1, tout1, nin1, nout1);
+    tvam_axis_window(svx, stx, ff.z, an.x, x0, x1, tin0, tout0, nin0, nout0);
+    tvam_axis_window(svy, sty, ff.w, an.y, y0, y1, tin1, tout1, nin1, nout1);
     const float tau_e = fmaxf(fmaxf(tin0, tin1), 0.0f);
-    const float tau_x = fminf(fminf(tout0, tout1), q.tau_end);
+    const float tau_x = fminf(fminf(tout0, tout1), ff.y);
     if (!(tau_e < tau_x)) return false;
-    const int n0 = tvam_axis_steps(tau_e, q.dtm0[0], q.ts[0], nin0, nout0);
-    const int n1 = tvam_axis_steps(tau_e, q.dtm0[1], q.ts[1], nin1, nout1);
-    const int vx = q.sv[0] + q.step[0] * n0;
-    const int vy = q.sv[1] + q.step[1] * n1;
-    const bool fx = q.dtm0[0] < TVAM_INF, fy = q.dtm0[1] < TVAM_INF;
-    r.dtx = fx ? fmaxf(fmaf((float)n0, q.ts[0], q.dtm0[0]) - tau_e, 0.0f) : TVAM_INF;
-    r.dty = fy ? fmaxf(fmaf((float)n1, q.ts[1], q.dtm0[1]) - tau_e, 0.0f) : TVAM_INF;
-    r.tsx = q.ts[0];
-    r.tsy = q.ts[1];
+    const int n0 = tvam_axis_steps(tau_e, ff.z, an.x, nin0, nout0);
+    const int n1 = tvam_axis_steps(tau_e, ff.w, an.y, nin1, nout1);
+    const int vx = svx + stx * n0;
+    const int vy = svy + sty * n1;
+    r.dtx = ff.z < TVAM_INF ? fmaxf(fmaf((float)n0, an.x, ff.z) - tau_e, 0.0f) : TVAM_INF;
+    r.dty = ff.w < TVAM_INF ? fmaxf(fmaf((float)n1, an.y, ff.w) - tau_e, 0.0f) : TVAM_INF;
+    r.tsx = an.x;
+    r.tsy = an.y;
     const int tw = tp.tsx + 2;  // guard band of one voxel on every side
-    r.sx = q.step[0];
-    r.sy = q.step[1] * tw;
+    r.sx = stx;
+    r.sy = sty * tw;
     r.lidx = (vy - y0 + 1) * tw + (vx - x0 + 1);
     r.rem = tau_x - tau_e;  // distance left inside this tile
-    r.t = q.t_start + tau_e;
+    r.t = ff.x + tau_e;
     return true;
 }
 

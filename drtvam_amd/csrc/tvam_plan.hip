@@ -47,6 +47,15 @@ struct tvam_plan {
     int32_t* d_col_hi = nullptr;
     int32_t* d_col_off = nullptr;
     unsigned long long* d_counter = nullptr;
+    float4* d_ang = nullptr;
+    // per-ray records (tvam_ray_setup_kernel), cached: regular sampling makes
+    // them call-independent; otherwise they are keyed on (spp, seed)
+    float4* d_ray_f = nullptr;
+    int2* d_ray_i = nullptr;
+    uint64_t ray_cap = 0;
+    bool ray_valid = false;
+    uint32_t ray_spp = 0, ray_seed = 0;
+    hipEvent_t ray_ready = nullptr;
     // sparse scratch (dense crop layout), allocated on first sparse call
     float* d_dense = nullptr;
     int32_t* d_idxmap = nullptr;
@@ -96,6 +105,10 @@ static void plan_free(tvam_plan* p) {
     (void)hipFree(p->d_col_hi);
     (void)hipFree(p->d_col_off);
     (void)hipFree(p->d_counter);
+    (void)hipFree(p->d_ang);
+    (void)hipFree(p->d_ray_f);
+    (void)hipFree(p->d_ray_i);
+    if (p->ray_ready) (void)hipEventDestroy(p->ray_ready);
     (void)hipFree(p->d_dense);
     (void)hipFree(p->d_idxmap);
     delete p;
@@ -239,6 +252,19 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
         cs[i] = make_float2(cosf(alpha), sinf(alpha));
     }
 
+    // per-angle DDA stepping (sensor.py:343, :357-360): d = (-c, -s)
+    std::vector<float4> ang(ns);
+    for (int i = 0; i < ns; ++i) {
+        float d[2] = {-cs[i].x, -cs[i].y}, ts[2], st[2];
+        for (int a = 0; a < 2; ++a) {
+            int step = d[a] > 0.0f ? 1 : -1;
+            bool valid = fabsf(d[a]) > 1e-8f;
+            ts[a] = valid ? (k.h[a] / d[a]) * (float)step : TVAM_INF;
+            st[a] = (float)step;
+        }
+        ang[i] = make_float4(ts[0], ts[1], st[0], st[1]);
+    }
+
     // per-slice DMD rows.  A ray's height is y_c of its row (+ jitter); its
     // slice is the DDA start voxel z (tvam_slice_of).
     std::vector<std::vector<int32_t>> rows_of(k.res[2]);
@@ -322,7 +348,7 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
 
     if ((rc = upload(&p->d_cs, cs)) || (rc = upload(&p->d_slice_off, slice_off)) ||
         (rc = upload(&p->d_slice_rows, slice_rows)) || (rc = upload(&p->d_col_lo, col_lo)) ||
-        (rc = upload(&p->d_col_hi, col_hi)) ||
+        (rc = upload(&p->d_col_hi, col_hi)) || (rc = upload(&p->d_ang, ang)) ||
         (rc = upload(&p->d_col_off, col_off))) {
         plan_free(p);
         return rc;
@@ -337,6 +363,11 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
     p->tiles.slice_rows = p->d_slice_rows;
     p->tiles.col_lo = p->d_col_lo;
     p->tiles.col_hi = p->d_col_hi;
+    p->tiles.ang = p->d_ang;
+    if ((e = hipEventCreateWithFlags(&p->ray_ready, hipEventDisableTiming)) != hipSuccess) {
+        plan_free(p);
+        return hip_fail(e, "hipEventCreate");
+    }
     p->tiles.col_off = p->d_col_off;
     p->tiles.ntx = ntx;
     p->tiles.nty = nty;
@@ -383,6 +414,40 @@ static int ensure_dense(tvam_plan* p) {
     return 0;
 }
 
+// Make the per-ray records of (spp, seed) available on `stream`.  The
+// buffer grows on demand (first call with a larger spp); the pre-pass runs
+// only when the cached records do not match the call.
+static int ensure_rays(tvam_plan* p, const TvamConsts& k, TvamTiles& t, hipStream_t stream) {
+    const uint64_t n = (uint64_t)(k.a1 - k.a0) * k.crop_y * k.crop_x * t.spp;
+    hipError_t e;
+    if (n > p->ray_cap) {
+        (void)hipFree(p->d_ray_f);
+        (void)hipFree(p->d_ray_i);
+        p->d_ray_f = nullptr;
+        p->d_ray_i = nullptr;
+        p->ray_cap = 0;
+        p->ray_valid = false;
+        if ((e = hipMalloc((void**)&p->d_ray_f, std::max<uint64_t>(n, 1) * sizeof(float4))) != hipSuccess ||
+            (e = hipMalloc((void**)&p->d_ray_i, std::max<uint64_t>(n, 1) * sizeof(int2))) != hipSuccess)
+            return hip_fail(e, "hipMalloc (ray records)");
+        p->ray_cap = n;
+    }
+    t.ray_f = p->d_ray_f;
+    t.ray_i = p->d_ray_i;
+    const bool hit = p->ray_valid && p->ray_spp == t.spp && (k.regular || p->ray_seed == t.seed);
+    if (hit) {
+        e = hipStreamWaitEvent(stream, p->ray_ready, 0);
+        return e == hipSuccess ? 0 : hip_fail(e, "hipStreamWaitEvent");
+    }
+    if ((e = tvam_launch_ray_setup(k, t, p->d_ray_f, p->d_ray_i, stream)) != hipSuccess)
+        return hip_fail(e, "ray setup launch");
+    if ((e = hipEventRecord(p->ray_ready, stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
+    p->ray_valid = true;
+    p->ray_spp = t.spp;
+    p->ray_seed = t.seed;
+    return 0;
+}
+
 extern "C" int tvam_forward(tvam_plan* p, const float* active_data, const uint32_t* active_pixels, uint64_t n_active,
                             uint32_t spp, uint32_t seed, float* dose, void* stream_) {
     if (!p || !dose || (!active_data && n_active)) return fail(TVAM_ERR_INVALID, "null argument");
@@ -413,6 +478,7 @@ extern "C" int tvam_forward(tvam_plan* p, const float* active_data, const uint32
     TvamTiles t = p->tiles;
     t.spp = spp;
     t.seed = seed;
+    if ((rc = ensure_rays(p, kc, t, stream))) return rc;
     unsigned long long* stats = nullptr;
     if (p->desc.flags & TVAM_FLAG_FWD_STATS) {
         if ((e = hipMemsetAsync(p->d_counter, 0, sizeof(unsigned long long), stream)) != hipSuccess)
@@ -450,6 +516,7 @@ extern "C" int tvam_adjoint(tvam_plan* p, const float* grad_dose, const uint32_t
         TvamTiles t = p->tiles;
         t.spp = spp;
         t.seed = seed;
+        if ((rc = ensure_rays(p, k, t, stream))) return rc;
         e = tvam_launch_tiles(TVAM_MODE_ADJ, k, t, p->lds_bytes, nullptr, idxmap, grad_dose, grad_active, nullptr,
                               stream);
         if (e != hipSuccess) return hip_fail(e, "adjoint launch");
@@ -471,6 +538,7 @@ extern "C" int tvam_count_visits(tvam_plan* p, uint32_t spp, uint32_t seed, uint
     TvamTiles t = p->tiles;
     t.spp = spp;
     t.seed = seed;
+    if ((rc = ensure_rays(p, k, t, nullptr))) return rc;
     e = tvam_launch_tiles(TVAM_MODE_COUNT, k, t, p->lds_bytes, nullptr, nullptr, nullptr, nullptr, p->d_counter,
                           nullptr);
     if (e != hipSuccess) return hip_fail(e, "count launch");
