@@ -165,6 +165,12 @@ def main():
 
     alg_bytes = 8.0 * visits + 4.0 * rays  # forward = 8 B per visit + 4 B per ray
     achieved = alg_bytes / fwd_avg / 1e9
+    # HBM bytes per forward launch from the committed rocprofv3 PMC passes
+    # (profiles/pmc_traffic.json, made by tools/profile_round.sh + tools/summarize_profile.py)
+    traffic = None
+    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
+    if N == 400 and A == 400 and world == 1 and os.path.exists(tpath):
+        traffic = json.load(open(tpath))["per_launch"]["forward"]["hbm_bytes"]
     cpu = None
     if args.cpu_baseline == "auto" and world == 1:
         threads = min(16, os.cpu_count() or 1)
@@ -192,7 +198,7 @@ def main():
             "final_loss": prob.loss_hist[-1],
         },
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
+                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                      "kernel": "tvam_tile_kernel<FWD>", "alg_bytes_per_launch": alg_bytes},
         "cpu_baseline": cpu,
     }

@@ -225,7 +225,7 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
 
     // tile geometry: LDS-resident xy tile of one z-slice
     auto pick = [&](int res) {
-        int ts = d.tile > 0 ? d.tile : 80;
+        int ts = d.tile > 0 ? d.tile : 64;
         int nt = (res + ts - 1) / ts;
         return (res + nt - 1) / nt;
     };

@@ -74,6 +74,11 @@ def load_scene(config):
     return scene_dict
 
 
+def angle_shard(n_angles: int, rank: int, world: int):
+    """Contiguous angle block [a0, a1) of `rank`."""
+    return (n_angles * rank) // world, (n_angles * (rank + 1)) // world
+
+
 def _dist():
     import torch.distributed as dist
     if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
@@ -81,7 +86,124 @@ def _dist():
     return None
 
 
-class TvamProblem:
+class ShardedLoop:
+    """The optimisation loop of one angle shard (optimize.py:287-323), independent of
+    how the shard's forward / adjoint projections are computed.
+
+    Subclasses provide ``forward_local(x, seed) -> partial dose`` (this rank's
+    angles only) and ``adjoint_local(grad_vol, seed) -> dL/dx_local``; the loop
+    all-reduces the dose (torch.distributed, RCCL on GPUs / gloo on CPU), keeps
+    the adjoint rank-local and all-reduces every L-BFGS dot product.
+    Required attributes: loss_fn, target, n_global, fused, grad_vol, x0.
+    """
+
+    dist = None
+    progressive = False
+    max_depth = 6
+
+    def forward_local(self, x, seed):
+        raise NotImplementedError
+
+    def adjoint_local(self, grad_vol, seed):
+        raise NotImplementedError
+
+    def on_progressive(self):
+        pass
+
+    # ---- distributed helpers ------------------------------------------------
+    def allreduce_(self, t):
+        if self.dist is not None:
+            self.dist.all_reduce(t)
+        return t
+
+    def dot(self, a, b):
+        return self.allreduce_(torch.dot(a, b))
+
+    def sparsity(self, x):
+        lf = self.loss_fn
+        w = getattr(lf, 'weight_sparsity', 0)
+        if not w:
+            return None
+        v = self.allreduce_((torch.abs(x.detach()) ** lf.M).sum(dtype=torch.float64) * w)
+        return v / self.n_global if lf.reduction_name == 'mean' else v
+
+    def sparsity_grad(self, x):
+        lf = self.loss_fn
+        w = getattr(lf, 'weight_sparsity', 0)
+        if not w:
+            return None
+        g = w * lf.M * torch.abs(x.detach()) ** (lf.M - 1) * torch.sign(x.detach())
+        return g / self.n_global if lf.reduction_name == 'mean' else g
+
+    # ---- projections ----------------------------------------------------------
+    def forward(self, x, seed):
+        return self.allreduce_(self.forward_local(x, seed))
+
+    def adjoint(self, grad_vol, seed):
+        return self.adjoint_local(grad_vol, seed)
+
+    # ---- loss -------------------------------------------------------------------
+    def loss_value_grad(self, vol, x):
+        """(loss f64 device scalar, dL/dvol) — fused kernel or torch autograd."""
+        if self.fused:
+            v = self.loss_fn.fused_value_grad(vol, self.target, x, self.grad_vol)
+            s = self.sparsity(x)
+            return (v if s is None else v + s), self.grad_vol
+        vv = vol.detach().requires_grad_(True)
+        with torch.enable_grad():
+            l = self.loss_fn(vv, self.target, torch.zeros_like(x) if getattr(self.loss_fn, 'weight_sparsity', 0) == 0 else x.detach())
+            l.backward()
+        return l.detach().to(torch.float64), vv.grad
+
+    def loss_step(self, vol, dvol, alpha, patterns):
+        if self.fused:
+            v = self.loss_fn.fused_value(vol, self.target, patterns, dvol, alpha)
+            s = self.sparsity(patterns)
+            return v if s is None else v + s
+        return self.loss_fn(vol + alpha * dvol, self.target, patterns)
+
+    # ---- optimisation -------------------------------------------------------------
+    def make_optimizer(self):
+        key = 'projector.active_data'
+
+        def render_fn(vars_):
+            return self.forward(vars_[key], self._seed)
+
+        opt = LinearLBFGS(render_fn=render_fn, loss_fn=None, dot=self.dot, loss_step=self.loss_step)
+        opt[key] = self.x0
+        self.opt = opt
+        return opt
+
+    def iteration(self, i):
+        """One optimizer iteration (optimize.py:292-320).  Returns the loss value."""
+        if self.opt is None:
+            self.make_optimizer()
+        if self.progressive and i == 5:
+            self.on_progressive()
+        key = 'projector.active_data'
+        self._seed = i
+        x = self.opt[key]
+        vol = self.forward(x, i)
+        loss, gvol = self.loss_value_grad(vol, x)
+        loss_v = float(loss)  # host sync, optimize.py:303
+        self.loss_hist.append(loss_v)
+        g = self.adjoint(gvol, i)
+        sg = self.sparsity_grad(x)
+        if sg is not None:
+            g = g + sg
+        x.grad = g
+        if loss_v == 0.0:
+            return loss_v
+        self.opt.step(vol, loss_v)
+        with torch.no_grad():
+            self.opt[key] = torch.clamp_min(self.opt[key].detach(), 0.0)
+        return loss_v
+
+    def patterns_local(self):
+        return self.opt['projector.active_data'].detach() if self.opt is not None else self.x0
+
+
+class TvamProblem(ShardedLoop):
     """Scene + target + loss + optimizer state of one optimisation run (one rank's angle shard)."""
 
     def __init__(self, config, device=None, target=None, rank=None, world_size=None):
@@ -116,8 +238,7 @@ class TvamProblem:
 
         # angle shard of this rank (contiguous blocks)
         A = self.scene.projector.n_patterns
-        self.a0 = (A * self.rank) // self.world
-        self.a1 = (A * (self.rank + 1)) // self.world
+        self.a0, self.a1 = angle_shard(A, self.rank, self.world)
         iprops = {'max_depth': 3 if self.progressive else self.max_depth, 'rr_depth': self.rr_depth,
                   'print_time': self.time, 'transmission_only': self.transmission_only,
                   'regular_sampling': self.regular_sampling, 'angle_range': (self.a0, self.a1),
@@ -159,99 +280,15 @@ class TvamProblem:
         self.loss_hist = []
         self.timing = []
 
-    # ---- distributed helpers ------------------------------------------------
-    def allreduce_(self, t):
-        if self.dist is not None:
-            self.dist.all_reduce(t)
-        return t
+    def forward_local(self, x, seed):
+        return self.proj.forward(x.detach().contiguous(), None, self.spp, seed)
 
-    def dot(self, a, b):
-        return self.allreduce_(torch.dot(a, b))
-
-    def sparsity(self, x):
-        lf = self.loss_fn
-        w = getattr(lf, 'weight_sparsity', 0)
-        if not w:
-            return None
-        v = self.allreduce_((torch.abs(x.detach()) ** lf.M).sum(dtype=torch.float64) * w)
-        return v / self.n_global if lf.reduction_name == 'mean' else v
-
-    def sparsity_grad(self, x):
-        lf = self.loss_fn
-        w = getattr(lf, 'weight_sparsity', 0)
-        if not w:
-            return None
-        g = w * lf.M * torch.abs(x.detach()) ** (lf.M - 1) * torch.sign(x.detach())
-        return g / self.n_global if lf.reduction_name == 'mean' else g
-
-    # ---- projections ----------------------------------------------------------
-    def forward(self, x, seed, out=None):
-        vol = self.proj.forward(x.detach().contiguous(), None, self.spp, seed, out=out)
-        return self.allreduce_(vol)
-
-    def adjoint(self, grad_vol, seed):
+    def adjoint_local(self, grad_vol, seed):
         return self.proj.adjoint(grad_vol, self.n_local, None, self.spp_grad, derive_seed_grad(seed))
 
-    # ---- loss -------------------------------------------------------------------
-    def loss_value_grad(self, vol, x):
-        """(loss f64 device scalar, dL/dvol) — fused kernel or torch autograd."""
-        if self.fused:
-            v = self.loss_fn.fused_value_grad(vol, self.target, x, self.grad_vol)
-            s = self.sparsity(x)
-            return (v if s is None else v + s), self.grad_vol
-        vv = vol.detach().requires_grad_(True)
-        with torch.enable_grad():
-            l = self.loss_fn(vv, self.target, torch.zeros_like(x) if getattr(self.loss_fn, 'weight_sparsity', 0) == 0 else x.detach())
-            l.backward()
-        return l.detach().to(torch.float64), vv.grad
-
-    def loss_step(self, vol, dvol, alpha, patterns):
-        if self.fused:
-            v = self.loss_fn.fused_value(vol, self.target, patterns, dvol, alpha)
-            s = self.sparsity(patterns)
-            return v if s is None else v + s
-        return self.loss_fn(vol + alpha * dvol, self.target, patterns)
-
-    # ---- optimisation -------------------------------------------------------------
-    def make_optimizer(self):
-        key = 'projector.active_data'
-
-        def render_fn(vars_):
-            return self.forward(vars_[key], self._seed)
-
-        opt = LinearLBFGS(render_fn=render_fn, loss_fn=None, dot=self.dot, loss_step=self.loss_step)
-        opt[key] = self.x0
-        self.opt = opt
-        return opt
-
-    def iteration(self, i):
-        """One optimizer iteration (optimize.py:292-320).  Returns the loss value."""
-        if self.opt is None:
-            self.make_optimizer()
-        if self.progressive and i == 5:
-            self.integrator.max_depth = self.max_depth
-            self.proj = self.integrator.projection(self.scene, self.sensor)
-        key = 'projector.active_data'
-        self._seed = i
-        x = self.opt[key]
-        vol = self.forward(x, i)
-        loss, gvol = self.loss_value_grad(vol, x)
-        loss_v = float(loss)  # host sync, optimize.py:303
-        self.loss_hist.append(loss_v)
-        g = self.adjoint(gvol, i)
-        sg = self.sparsity_grad(x)
-        if sg is not None:
-            g = g + sg
-        x.grad = g
-        if loss_v == 0.0:
-            return loss_v
-        self.opt.step(vol, loss_v)
-        with torch.no_grad():
-            self.opt[key] = torch.clamp_min(self.opt[key].detach(), 0.0)
-        return loss_v
-
-    def patterns_local(self):
-        return self.opt['projector.active_data'].detach() if self.opt is not None else self.x0
+    def on_progressive(self):
+        self.integrator.max_depth = self.max_depth
+        self.proj = self.integrator.projection(self.scene, self.sensor)
 
     def final_render(self, spp=None):
         proj = self.final_integrator.projection(self.scene, self.final_sensor)
