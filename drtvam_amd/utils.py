@@ -123,17 +123,20 @@ def voxelize_mesh(verts, tris, bbox_min, voxel_size, res):
     occ = np.zeros((rz, ry, rx), dtype=np.uint8)
     a, b, c = verts[tris[:, 0]], verts[tris[:, 1]], verts[tris[:, 2]]
     X, Y = np.meshgrid(xs, ys, indexing='xy')  # [ry, rx]
-    px, py = X.reshape(-1), Y.reshape(-1)
+    # tiny irrational shift of the scan lines: voxel centres of grid-aligned meshes would otherwise
+    # pass exactly through shared triangle edges and break the crossing parity
+    px = X.reshape(-1) + voxel_size[0] * 1.2345679e-4 * np.sqrt(2.0)
+    py = Y.reshape(-1) + voxel_size[1] * 2.3456789e-4 * np.sqrt(3.0)
     crossings = [[] for _ in range(px.size)]
     for t in range(tris.shape[0]):
         A, B, C = a[t], b[t], c[t]
         det = (B[0] - A[0]) * (C[1] - A[1]) - (C[0] - A[0]) * (B[1] - A[1])
         if det == 0:
             continue
-        lo = np.searchsorted(xs, min(A[0], B[0], C[0]))
-        hi = np.searchsorted(xs, max(A[0], B[0], C[0]), side='right')
-        jlo = np.searchsorted(ys, min(A[1], B[1], C[1]))
-        jhi = np.searchsorted(ys, max(A[1], B[1], C[1]), side='right')
+        lo = max(np.searchsorted(xs, min(A[0], B[0], C[0])) - 1, 0)
+        hi = np.searchsorted(xs, max(A[0], B[0], C[0]), side='right') + 1
+        jlo = max(np.searchsorted(ys, min(A[1], B[1], C[1])) - 1, 0)
+        jhi = np.searchsorted(ys, max(A[1], B[1], C[1]), side='right') + 1
         if lo >= hi or jlo >= jhi:
             continue
         jj, ii = np.meshgrid(np.arange(jlo, jhi), np.arange(lo, hi), indexing='ij')
@@ -142,7 +145,7 @@ def voxelize_mesh(verts, tris, bbox_min, voxel_size, res):
         w1 = ((qx - A[0]) * (C[1] - A[1]) - (C[0] - A[0]) * (qy - A[1])) / det
         w2 = ((B[0] - A[0]) * (qy - A[1]) - (qx - A[0]) * (B[1] - A[1])) / det
         w0 = 1.0 - w1 - w2
-        inside = (w0 >= 0) & (w1 >= 0) & (w2 > 0) | (w0 > 0) & (w1 > 0) & (w2 >= 0)
+        inside = (w0 >= 0) & (w1 >= 0) & (w2 >= 0)
         zc = w0 * A[2] + w1 * B[2] + w2 * C[2]
         for k in np.nonzero(inside)[0]:
             crossings[idx[k]].append(zc[k])
