@@ -9,9 +9,9 @@ struct TvamTiles {
     const float2* cs;          // [n_shard] (cos, sin) of each angle of the shard
     const int32_t* slice_off;  // [res_z + 1] CSR offsets into slice_rows
     const int32_t* slice_rows; // crop-local DMD rows feeding each z-slice
-    const int32_t* col_lo;     // [ntiles][n_shard] first crop-local column crossing the tile
-    const int32_t* col_hi;     // [ntiles][n_shard] last crop-local column crossing the tile
-    const int32_t* col_off;    // [ntiles][n_shard + 1] prefix sums of column-PAIR counts ceil(n/2)
+    const uint32_t* slots;     // per tile: (shard angle << 16 | crop column) of every ray crossing it,
+                               // sorted by predicted in-tile visits (longest first)
+    const int64_t* slot_off;   // [ntiles + 1] offsets into slots
     const float4* ang;         // [n_shard] {tstep_x, tstep_y, step_x, step_y} (sensor.py:343, :360)
     const float4* ray_f;       // [n_shard*crop_y*crop_x*spp] {t_start, tau_end, dtmax0_x, dtmax0_y}
     const int2* ray_i;         // same index: {start voxel x | y << 16, z-slice or -1}
@@ -19,6 +19,29 @@ struct TvamTiles {
     int32_t n_shard;
     uint32_t spp, seed;
 };
+
+// Planar fast path of regular sampling (tvam_planar.hip): one ray record per
+// (angle, DMD column), shared by every DMD row.
+struct TvamPlanar {
+    const float2* cs;          // [ns] (cos, sin) of each angle of the shard
+    float4* vox;               // [ns][crop_x] {qx, qy, t_end, 0} (voxel-driven forward)
+    float4* rec_f;             // [ns][crop_x] {t_start, tau_end, dtmax0_x, dtmax0_y} (tile DDA resume)
+    int32_t* rec_i;            // [ns][crop_x] start voxel x | y << 16, -1 if the ray misses
+    const int32_t* slice_off;  // [res_z + 1] CSR: DMD rows whose rays lie in each slice
+    const int32_t* slice_rows;
+    int32_t ns;
+    int32_t ncmax;             // forward: DMD columns staged per (16x16 tile, angle)
+    float marg_u;              // forward: candidate-column margin (spawn offset of o2 + rounding), in columns
+    int32_t max_rows_chunk;    // adjoint: most DMD rows in one chunk of Z slices
+};
+
+hipError_t tvam_launch_planar_rays(const TvamConsts& k, const TvamPlanar& pl, hipStream_t stream);
+size_t tvam_planar_fwd_lds(const TvamPlanar& pl, int Z);
+hipError_t tvam_launch_fwd_planar(const TvamConsts& k, const TvamPlanar& pl, int Z, const float* pat, float* dose,
+                                  hipStream_t stream);
+size_t tvam_planar_adj_lds(const TvamPlanar& pl, const TvamTiles& t, int Z);
+hipError_t tvam_launch_adj_planar(const TvamConsts& k, const TvamPlanar& pl, const TvamTiles& t, int Z,
+                                  const int32_t* idxmap, const float* gin, float* out, hipStream_t stream);
 
 enum TvamMode { TVAM_MODE_FWD = 0, TVAM_MODE_ADJ = 1, TVAM_MODE_COUNT = 2 };
 

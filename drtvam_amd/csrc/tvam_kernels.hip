@@ -34,6 +34,11 @@ __device__ __forceinline__ int tvam_rint(float x) {
     return r;
 }
 
+#if defined(TVAM_EXPERIMENT) && TVAM_EXPERIMENT == 4
+__device__ unsigned long long g_exp_counters[2];
+extern "C" __global__ void tvam_exp_read(unsigned long long* out) { out[0] = g_exp_counters[0]; out[1] = g_exp_counters[1]; }
+#endif
+
 // How the in-tile march consumes one visit.
 enum TvamAcc { ACC_FLOAT = 0, ACC_FIXED = 1, ACC_GATHER = 2, ACC_COUNT = 3, ACC_FIXED64 = 4 };
 
@@ -46,59 +51,84 @@ __device__ __forceinline__ unsigned long long tvam_f2i64(float c) {
 }
 
 
-// In-tile DDA march (sensor.py:383-438) from a resumed state.  `rem` is the
-// distance left INSIDE the tile (tile exit or segment end, whichever is
-// first), so one test ends the march: the reference's "remaining <= 1e-6"
-// test (sensor.py:427).  Rounding can let the last step cross the tile edge
-// one visit early; the tile carries a 1-voxel guard band that absorbs that
-// visit (its dt is at rounding level, and guard cells are never stored /
-// read as 0).  The reference's separate end-voxel test only differs at that
-// same rounding level.  One exp2 per visit (telescoped
-// exp(-st t)(1 - exp(-st dt))).
+// March state of one ray inside one tile (times measured from the tile entry).
+struct TvamMarchRay {
+    char* pv;        // LDS address of the current voxel
+    float Tx, Ty;    // next x / y boundary crossing
+    float rem;       // in-tile exit: tile exit or segment end, whichever is first
+    float stop;      // rem - 1e-6: the reference's "remaining <= 1e-6" end test (sensor.py:427)
+    float nt0;       // -st * log2(e) * (distance travelled at the tile entry)
+    float e0;        // em * exp(-st * t) at the tile entry
+    float ems;       // em, pre-scaled for the accumulator
+};
+
+// In-tile DDA march (sensor.py:383-438) from a resumed state.  The march
+// tracks the NEXT x / y boundary crossing and the in-tile exit, so a visit is
+// [tp, tn = min(Tx, Ty, rem)] and one test ends the ray.  The reference
+// decrements per-axis countdowns by dt instead; both are the same DDA up to
+// fp32 rounding of the step times.  One axis steps per visit: on an exact tie
+// the other axis steps on the next visit, whose dt is exactly 0 (c == 0), i.e.
+// the reference's diagonal step.  Rounding can let the last step cross the
+// tile edge one visit early; the tile carries a 1-voxel guard band that
+// absorbs that visit (its dt is at rounding level, and guard cells are never
+// stored / read as 0).  One exp2 per visit (telescoped exp(-st t)(1 - exp(-st dt))).
 template <int ACC>
-__device__ __forceinline__ void tvam_march(float* __restrict__ tile, int lidx, float t, float rem, float dtx,
-                                           float dty, const float tsx, const float tsy, const int sx, const int sy,
-                                           const float ems, const float nsig2, float& acc, unsigned long long& nvis,
-                                           const int tw = 0, const int wx = 0, const int wy = 0) {
+__device__ __forceinline__ void tvam_march(TvamMarchRay a, const float tsx, const float tsy, const int sxb,
+                                           const int syb, const float nsig2, float& acc,
+                                           unsigned long long& nvis, const char* tile = nullptr, const int tw = 0,
+                                           const int wx = 0, const int wy = 0) {
 #if defined(TVAM_EXPERIMENT) && TVAM_EXPERIMENT == 3  // timing only: setup without the march
-    acc += t + rem + dtx + dty + (float)lidx;
+    acc += a.Tx + a.Ty + a.rem + a.e0;
     return;
 #endif
-    float e0 = ems * tvam_exp2(nsig2 * t);
+    constexpr int ESZ = ACC == ACC_FIXED64 ? 8 : 4;
+#if defined(TVAM_EXPERIMENT) && TVAM_EXPERIMENT == 4  // lane utilisation of the march loop
+    unsigned long long lane_it = 0, wave_it = 0;
+#endif
+    float tp = 0.0f;
     for (;;) {
-        const float dt = fminf(fminf(dtx, dty), rem);
-        rem -= dt;
-        t += dt;
-        const float e1 = ems * tvam_exp2(nsig2 * t);
-        const float c = e0 - e1;
-        if (ACC == ACC_FLOAT) atomicAdd(&tile[lidx], c);
-        else if (ACC == ACC_FIXED) atomicAdd(reinterpret_cast<int*>(tile) + lidx, tvam_rint(c));
-        else if (ACC == ACC_FIXED64) atomicAdd(reinterpret_cast<unsigned long long*>(tile) + lidx, tvam_f2i64(c));
-        else if (ACC == ACC_GATHER) acc = fmaf(c, tile[lidx], acc);
-        else {  // count interior visits only (guard-band visits carry rounding-level dt)
-            const int ly = lidx / tw, lx = lidx - ly * tw;
-            nvis += (lx >= 1 && lx <= wx && ly >= 1 && ly <= wy) ? 1 : 0;
+#if defined(TVAM_EXPERIMENT) && TVAM_EXPERIMENT == 4
+        ++lane_it;
+        if (__lane_id() == __builtin_ctzll(__ballot(1))) ++wave_it;
+#endif
+        const float tn = fminf(fminf(a.Tx, a.Ty), a.rem);
+        const float x1 = tvam_exp2(fmaf(nsig2, tn, a.nt0));
+        const float e1 = (ACC == ACC_GATHER || ACC == ACC_COUNT) ? x1 : a.ems * x1;
+        const float c = a.e0 - e1;
+        if (ACC == ACC_FLOAT) atomicAdd(reinterpret_cast<float*>(a.pv), c);
+        else if (ACC == ACC_FIXED) atomicAdd(reinterpret_cast<int*>(a.pv), tvam_rint(c));
+        else if (ACC == ACC_FIXED64) atomicAdd(reinterpret_cast<unsigned long long*>(a.pv), tvam_f2i64(c));
+        else if (ACC == ACC_GATHER) acc = fmaf(c, *reinterpret_cast<const float*>(a.pv), acc);
+        else {  // interior visits of nonzero length (guard-band visits carry rounding-level dt)
+            const int li = (int)(a.pv - tile) / ESZ, ly = li / tw, lx = li - ly * tw;
+            nvis += (tn > tp && lx >= 1 && lx <= wx && ly >= 1 && ly <= wy) ? 1 : 0;
+            tp = tn;
         }
-        const bool mx = dtx == dt, my = dty == dt;
-        dtx = mx ? tsx : dtx - dt;
-        dty = my ? tsy : dty - dt;
-        lidx += (mx ? sx : 0) + (my ? sy : 0);
-        e0 = e1;
-        if (!(rem > 1e-6f)) break;
+        const bool mx = a.Tx <= a.Ty;
+        a.Tx = mx ? a.Tx + tsx : a.Tx;
+        a.Ty = mx ? a.Ty : a.Ty + tsy;
+        a.pv += mx ? sxb : syb;
+        a.e0 = e1;
+        if (!(tn < a.stop)) break;
     }
+#if defined(TVAM_EXPERIMENT) && TVAM_EXPERIMENT == 4
+    if (ACC == ACC_GATHER) {
+        atomicAdd(&g_exp_counters[0], lane_it);
+        atomicAdd(&g_exp_counters[1], wave_it);
+    }
+#endif
 }
 
-// Ray slot enumeration of one workgroup: slot f -> (slice row ri, flat
-// column slot g, sample smp); g -> (shard angle al, crop column).  Slots
-// advance by the block size, so (ri, g, al) are updated incrementally.
+// Ray slot enumeration of one workgroup: slot f -> (slice row ri, entry g of
+// the tile's slot list, sample smp).  Slots advance by the block size, so
+// (ri, rrem) are updated incrementally.
 struct TvamSlot {
-    int ri, rrem, al;
+    int ri, rrem;
 };
 
 __device__ __forceinline__ void tvam_slot_init(TvamSlot& sl, int f, int per_row) {
     sl.ri = f / per_row;
     sl.rrem = f - sl.ri * per_row;
-    sl.al = 0;
 }
 
 __device__ __forceinline__ void tvam_slot_next(TvamSlot& sl, int per_row) {
@@ -106,24 +136,7 @@ __device__ __forceinline__ void tvam_slot_next(TvamSlot& sl, int per_row) {
     while (sl.rrem >= per_row) {
         sl.rrem -= per_row;
         ++sl.ri;
-        sl.al = 0;
     }
-}
-
-__device__ __forceinline__ int tvam_slot_angle(TvamSlot& sl, int g, const int32_t* s_off, int ns) {
-    if (s_off[sl.al + 1] > g) return sl.al;  // still in the same angle
-    int lo = sl.al, hi = ns;               // s_off[lo] <= g < s_off[hi]
-    if (hi - lo > 4) {
-        while (hi - lo > 1) {
-            int mid = (lo + hi) >> 1;
-            if (s_off[mid] <= g) lo = mid;
-            else hi = mid;
-        }
-    } else {
-        while (s_off[lo + 1] <= g) ++lo;
-    }
-    sl.al = lo;
-    return lo;
 }
 
 // Everything of one ray inside one tile.
@@ -254,10 +267,8 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
     const int tsx = tp.tsx, tsy = tp.tsy, ns = tp.n_shard;
     const int tw = tsx + 2, th = tsy + 2;  // tile + 1-voxel guard band
     const int tile_words = (MODE == TVAM_MODE_FWD && TVAM_FWD_ACC64) ? 2 * tw * th : tw * th;
-    int32_t* s_off = reinterpret_cast<int32_t*>(tile + tile_words);
-    int32_t* s_lo = s_off + (ns + 1);
-    int32_t* s_hi = s_lo + ns;
-    float* s_red = reinterpret_cast<float*>(s_hi + ns);
+    float* s_red = tile + tile_words;
+    unsigned* s_amax = reinterpret_cast<unsigned*>(s_red + 16);  // forward: per-angle max |p|
 
     const int tile_id = blockIdx.x, kz = blockIdx.y;
     const int x0 = (tile_id % tp.ntx) * tsx, y0 = (tile_id / tp.ntx) * tsy;
@@ -274,22 +285,15 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
         }
         tile[i] = v;
     }
-    const int32_t* g_off = tp.col_off + (size_t)tile_id * (ns + 1);
-    const int32_t* g_lo = tp.col_lo + (size_t)tile_id * ns;
-    const int32_t* g_hi = tp.col_hi + (size_t)tile_id * ns;
-    for (int i = threadIdx.x; i <= ns; i += TVAM_BLOCK) {
-        s_off[i] = g_off[i];
-        if (i < ns) {
-            s_lo[i] = g_lo[i];
-            s_hi[i] = g_hi[i];
-            if (MODE == TVAM_MODE_FWD) reinterpret_cast<unsigned*>(s_red + 16)[i] = 0u;
-        }
-    }
+    if (MODE == TVAM_MODE_FWD)
+        for (int i = threadIdx.x; i < ns; i += TVAM_BLOCK) s_amax[i] = 0u;
     __syncthreads();
 
+    // this tile's (angle, column) slots, longest predicted in-tile march first
+    const uint32_t* slots = tp.slots + tp.slot_off[tile_id];
+    const int nrt = (int)(tp.slot_off[tile_id + 1] - tp.slot_off[tile_id]);
     const int rbeg = tp.slice_off[kz], rend = tp.slice_off[kz + 1];
     const int nrows = rend - rbeg;
-    const int nrt = s_off[ns];
     const int spp = (int)tp.spp;
     const int per_row = nrt * spp;
     const int total = nrows * per_row;
@@ -307,26 +311,21 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
     int acc_mode = ACC_GATHER;
     float fscale = 1.0f;
     if (MODE == TVAM_MODE_FWD) {
-        unsigned* s_amax = reinterpret_cast<unsigned*>(s_red + 16);  // per-angle max |p| (zeroed above)
         float nz = 0.0f;
         TvamSlot sl;
         tvam_slot_init(sl, threadIdx.x, max(per_row, 1));
         for (int f = threadIdx.x; f < total; f += TVAM_BLOCK, tvam_slot_next(sl, per_row)) {
-            const int g = spp == 1 ? sl.rrem : sl.rrem / spp;
-            const int al = tvam_slot_angle(sl, g, s_off, ns);
+            if (spp > 1 && sl.rrem % spp) continue;  // one look per (angle, column)
+            const uint32_t e = slots[spp == 1 ? sl.rrem : sl.rrem / spp];
+            const int al = (int)(e >> 16), colc = (int)(e & 0xffffu);
             const int rowc = tp.slice_rows[rbeg + sl.ri];
-            const int q = g - s_off[al], c1 = s_lo[al] + q, c2 = s_hi[al] - q;
-            const int64_t base = ((int64_t)(k.a0 + al) * k.crop_y + rowc) * k.crop_x - k.shard_base;
-            float p = 0.0f;
-            for (int rep = 0; rep < 2; ++rep) {
-                if (rep && c2 <= c1) break;
-                const int64_t local = base + (rep ? c2 : c1);
-                if (idxmap && idxmap[local] < 0) continue;
-                const float v = fabsf(pat[local]);
-                p = fmaxf(p, v);
-                nz += v > 0.0f ? 1.0f : 0.0f;
+            const int64_t local = ((int64_t)(k.a0 + al) * k.crop_y + rowc) * k.crop_x + colc - k.shard_base;
+            if (idxmap && idxmap[local] < 0) continue;
+            const float v = fabsf(pat[local]);
+            if (v > 0.0f) {
+                atomicMax(&s_amax[al], __float_as_uint(v));  // non-negative floats order like their bits
+                nz += 1.0f;
             }
-            atomicMax(&s_amax[al], __float_as_uint(p));  // non-negative floats order like their bits
         }
         __syncthreads();
         float am = 0.0f, amx = 0.0f;
@@ -344,17 +343,13 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
             const float thr = pmax * (1.0f / 1024.0f);
             tvam_slot_init(sl, threadIdx.x, max(per_row, 1));
             for (int f = threadIdx.x; f < total; f += TVAM_BLOCK, tvam_slot_next(sl, per_row)) {
-                const int g = spp == 1 ? sl.rrem : sl.rrem / spp;
-                const int al = tvam_slot_angle(sl, g, s_off, ns);
+                if (spp > 1 && sl.rrem % spp) continue;
+                const uint32_t e = slots[spp == 1 ? sl.rrem : sl.rrem / spp];
+                const int al = (int)(e >> 16), colc = (int)(e & 0xffffu);
                 const int rowc = tp.slice_rows[rbeg + sl.ri];
-                const int q = g - s_off[al], c1 = s_lo[al] + q, c2 = s_hi[al] - q;
-                const int64_t base = ((int64_t)(k.a0 + al) * k.crop_y + rowc) * k.crop_x - k.shard_base;
-                for (int rep = 0; rep < 2; ++rep) {
-                    if (rep && c2 <= c1) break;
-                    const int64_t local = base + (rep ? c2 : c1);
-                    if (idxmap && idxmap[local] < 0) continue;
-                    nbig += fabsf(pat[local]) >= thr ? 1.0f : 0.0f;
-                }
+                const int64_t local = ((int64_t)(k.a0 + al) * k.crop_y + rowc) * k.crop_x + colc - k.shard_base;
+                if (idxmap && idxmap[local] < 0) continue;
+                nbig += fabsf(pat[local]) >= thr ? 1.0f : 0.0f;
             }
             nbig = tvam_block_sum(nbig, s_red);
         }
@@ -377,46 +372,50 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
         __syncthreads();
     }
 
+    constexpr int ESZ = (MODE == TVAM_MODE_FWD && TVAM_FWD_ACC64) ? 8 : 4;
     unsigned long long nvis = 0;
     TvamSlot sl;
     tvam_slot_init(sl, threadIdx.x, max(per_row, 1));
     for (int f = threadIdx.x; f < total; f += TVAM_BLOCK, tvam_slot_next(sl, per_row)) {
         const int g = spp == 1 ? sl.rrem : sl.rrem / spp;
         const int smp = sl.rrem - g * spp;
-        const int al = tvam_slot_angle(sl, g, s_off, ns);
-        const int q = g - s_off[al], c1 = s_lo[al] + q, c2 = s_hi[al] - q;
+        const uint32_t e = slots[g];
+        const int al = (int)(e >> 16), colc = (int)(e & 0xffffu);
         const int rowc = tp.slice_rows[rbeg + sl.ri];
-        for (int rep = 0; rep < 2; ++rep) {  // the column pair (q, n-1-q)
-            if (rep && c2 <= c1) break;
-            const int colc = rep ? c2 : c1;
-            float em = 1.0f;
-            if (MODE == TVAM_MODE_FWD) {
-                const int64_t local = ((int64_t)(k.a0 + al) * k.crop_y + rowc) * k.crop_x + colc - k.shard_base;
-                const float p = pat[local];
-                if (p == 0.0f && k.skip_zero) continue;  // contributes exactly zero dose
-                em = p * k.wscale;                        // Le * weight (common.py:108-111, volume.py:49)
-            }
-            TvamTileRay r;
-            if (!tvam_tile_ray(k, tp, kz, x0, x1, y0, y1, rowc, al, colc, smp, idxmap, r)) continue;
-            float acc = 0.0f;
-            if (MODE == TVAM_MODE_FWD) {
-                if (TVAM_FWD_ACC64 && acc_mode == ACC_FIXED64)
-                    tvam_march<ACC_FIXED64>(tile, r.lidx, r.t, r.rem, r.dtx, r.dty, r.tsx, r.tsy, r.sx, r.sy,
-                                            em * fscale, k.nsig2, acc, nvis);
-                else if (!TVAM_FWD_ACC64 && acc_mode == ACC_FIXED)
-                    tvam_march<ACC_FIXED>(tile, r.lidx, r.t, r.rem, r.dtx, r.dty, r.tsx, r.tsy, r.sx, r.sy,
-                                          em * fscale, k.nsig2, acc, nvis);
-                else
-                    tvam_march<ACC_FLOAT>(tile, r.lidx, r.t, r.rem, r.dtx, r.dty, r.tsx, r.tsy, r.sx, r.sy,
-                                          em, k.nsig2, acc, nvis);
-            } else if (MODE == TVAM_MODE_ADJ) {
-                tvam_march<ACC_GATHER>(tile, r.lidx, r.t, r.rem, r.dtx, r.dty, r.tsx, r.tsy, r.sx, r.sy,
-                                       1.0f, k.nsig2, acc, nvis);
-                atomicAdd(&out[r.act], acc * k.wscale);  // backward_from(Le * em_grad), volume.py:274-276
-            } else {
-                tvam_march<ACC_COUNT>(tile, r.lidx, r.t, r.rem, r.dtx, r.dty, r.tsx, r.tsy, r.sx, r.sy,
-                                      1.0f, k.nsig2, acc, nvis, tw, wx, wy);
-            }
+        float em = 1.0f;
+        if (MODE == TVAM_MODE_FWD) {
+            const int64_t local = ((int64_t)(k.a0 + al) * k.crop_y + rowc) * k.crop_x + colc - k.shard_base;
+            const float p = pat[local];
+            if (p == 0.0f && k.skip_zero) continue;  // contributes exactly zero dose
+            em = p * k.wscale;                        // Le * weight (common.py:108-111, volume.py:49)
+            if (acc_mode != ACC_FLOAT) em *= fscale;
+        }
+        TvamTileRay r;
+        if (!tvam_tile_ray(k, tp, kz, x0, x1, y0, y1, rowc, al, colc, smp, idxmap, r)) continue;
+        TvamMarchRay m;
+        m.pv = reinterpret_cast<char*>(tile) + r.lidx * ESZ;
+        m.Tx = r.dtx;
+        m.Ty = r.dty;
+        m.rem = r.rem;
+        m.stop = r.rem - 1e-6f;
+        m.nt0 = k.nsig2 * r.t;
+        m.ems = em;
+        m.e0 = em * tvam_exp2(m.nt0);
+        const int sxb = r.sx * ESZ, syb = r.sy * ESZ;
+        float acc = 0.0f;
+        if (MODE == TVAM_MODE_FWD) {
+            if (TVAM_FWD_ACC64 && acc_mode == ACC_FIXED64)
+                tvam_march<ACC_FIXED64>(m, r.tsx, r.tsy, sxb, syb, k.nsig2, acc, nvis);
+            else if (!TVAM_FWD_ACC64 && acc_mode == ACC_FIXED)
+                tvam_march<ACC_FIXED>(m, r.tsx, r.tsy, sxb, syb, k.nsig2, acc, nvis);
+            else
+                tvam_march<ACC_FLOAT>(m, r.tsx, r.tsy, sxb, syb, k.nsig2, acc, nvis);
+        } else if (MODE == TVAM_MODE_ADJ) {
+            tvam_march<ACC_GATHER>(m, r.tsx, r.tsy, sxb, syb, k.nsig2, acc, nvis);
+            atomicAdd(&out[r.act], acc * k.wscale);  // backward_from(Le * em_grad), volume.py:274-276
+        } else {
+            tvam_march<ACC_COUNT>(m, r.tsx, r.tsy, sxb, syb, k.nsig2, acc, nvis, reinterpret_cast<const char*>(tile),
+                                  tw, wx, wy);
         }
     }
 

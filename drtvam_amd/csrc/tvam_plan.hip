@@ -13,6 +13,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -43,9 +44,8 @@ struct tvam_plan {
     float2* d_cs = nullptr;
     int32_t* d_slice_off = nullptr;
     int32_t* d_slice_rows = nullptr;
-    int32_t* d_col_lo = nullptr;
-    int32_t* d_col_hi = nullptr;
-    int32_t* d_col_off = nullptr;
+    uint32_t* d_slots = nullptr;
+    int64_t* d_slot_off = nullptr;
     unsigned long long* d_counter = nullptr;
     float4* d_ang = nullptr;
     // per-ray records (tvam_ray_setup_kernel), cached: regular sampling makes
@@ -56,6 +56,15 @@ struct tvam_plan {
     bool ray_valid = false;
     uint32_t ray_spp = 0, ray_seed = 0;
     hipEvent_t ray_ready = nullptr;
+    // planar fast path (regular sampling; tvam_planar.hip)
+    bool planar = false;
+    int32_t planar_fz = 16, planar_az = 4;
+    TvamPlanar pl{};
+    int32_t* d_pl_slice_off = nullptr;
+    int32_t* d_pl_slice_rows = nullptr;
+    float4* d_pl_vox = nullptr;
+    float4* d_pl_rec_f = nullptr;
+    int32_t* d_pl_rec_i = nullptr;
     // sparse scratch (dense crop layout), allocated on first sparse call
     float* d_dense = nullptr;
     int32_t* d_idxmap = nullptr;
@@ -101,9 +110,8 @@ static void plan_free(tvam_plan* p) {
     (void)hipFree(p->d_cs);
     (void)hipFree(p->d_slice_off);
     (void)hipFree(p->d_slice_rows);
-    (void)hipFree(p->d_col_lo);
-    (void)hipFree(p->d_col_hi);
-    (void)hipFree(p->d_col_off);
+    (void)hipFree(p->d_slots);
+    (void)hipFree(p->d_slot_off);
     (void)hipFree(p->d_counter);
     (void)hipFree(p->d_ang);
     (void)hipFree(p->d_ray_f);
@@ -111,6 +119,11 @@ static void plan_free(tvam_plan* p) {
     if (p->ray_ready) (void)hipEventDestroy(p->ray_ready);
     (void)hipFree(p->d_dense);
     (void)hipFree(p->d_idxmap);
+    (void)hipFree(p->d_pl_slice_off);
+    (void)hipFree(p->d_pl_slice_rows);
+    (void)hipFree(p->d_pl_vox);
+    (void)hipFree(p->d_pl_rec_f);
+    (void)hipFree(p->d_pl_rec_i);
     delete p;
 }
 
@@ -203,6 +216,78 @@ static int upload(T** dst, const std::vector<T>& v) {
     return 0;
 }
 
+static int env_int(const char* name, int def) {
+    const char* v = std::getenv(name);
+    return v && *v ? std::atoi(v) : def;
+}
+
+// Planar fast path: regular sampling and rows whose vial entry offset is
+// row-independent (|z| <= 0.7 r < r / sqrt(2) <= max(|p_x|, |p_y|) on the
+// vial wall).  Builds the row -> slice CSR of valid rows and the per-(angle,
+// column) ray table (computed once, here).
+static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
+    const tvam_desc& d = p->desc;
+    const TvamConsts& k = p->k;
+    if (!d.regular_sampling || (d.flags & TVAM_FLAG_NO_PLANAR) || p->empty) return 0;
+    std::vector<std::vector<int32_t>> rows_of(k.res[2]);
+    for (int rc = 0; rc < d.crop_y; ++rc) {
+        float xc, yc;
+        tvam_ray_camera(k, 0, d.crop_offset_y + rc, 0.5f, 0.5f, xc, yc);
+        const int s = tvam_slice_of(k, yc);
+        if (s < 0 || !(yc >= -k.vial_half_h && yc <= k.vial_half_h)) continue;  // misses grid / vial (volume.py:179)
+        if (!(std::fabs(yc) <= 0.7f * d.vial_r)) return 0;                      // spawn offset would depend on z
+        rows_of[s].push_back(rc);
+    }
+    std::vector<int32_t> off(k.res[2] + 1, 0), rows;
+    for (int s = 0; s < k.res[2]; ++s) {
+        off[s] = (int32_t)rows.size();
+        rows.insert(rows.end(), rows_of[s].begin(), rows_of[s].end());
+    }
+    off[k.res[2]] = (int32_t)rows.size();
+    p->planar_fz = env_int("TVAM_PLANAR_FWD_Z", 16);
+    p->planar_az = env_int("TVAM_PLANAR_ADJ_Z", 4);
+    if (p->planar_fz != 8 && p->planar_fz != 16 && p->planar_fz != 32) p->planar_fz = 16;
+    if (p->planar_az != 4 && p->planar_az != 8) p->planar_az = 4;
+    const int ns = (int)cs.size();
+    int32_t mrc = 0;
+    for (int z0 = 0; z0 < k.res[2]; z0 += p->planar_az)
+        mrc = std::max<int32_t>(mrc, off[std::min(z0 + p->planar_az, k.res[2])] - off[z0]);
+    // columns whose ray can cross a 16x16-voxel tile at some angle (+ window rounding)
+    double wmax = 0.0;
+    for (int i = 0; i < ns; ++i)
+        wmax = std::max(wmax, 16.0 * ((double)k.h[0] * std::fabs((double)cs[i].y) +
+                                      (double)k.h[1] * std::fabs((double)cs[i].x)) * (double)d.res_x / (double)k.ex);
+    double rmax = std::max({std::fabs((double)k.bmin[0]), std::fabs((double)k.bmax[0]), std::fabs((double)k.bmin[1]),
+                            std::fabs((double)k.bmax[1]), (double)d.vial_r, (double)k.vial_half_h});
+    const double marg_u = 4.0 * (1.0 + rmax) * (double)TVAM_RAY_EPS * (double)d.res_x / (double)k.ex + 1e-3;
+    p->pl.ns = ns;
+    p->pl.marg_u = (float)marg_u;
+    p->pl.ncmax = (int32_t)std::ceil(wmax + 2.0 * marg_u + 0.01) + 4;
+    p->pl.max_rows_chunk = mrc;
+    if (tvam_planar_adj_lds(p->pl, p->tiles, p->planar_az) > 160 * 1024) p->planar_az = 4;
+    if (tvam_planar_adj_lds(p->pl, p->tiles, p->planar_az) > 160 * 1024) return 0;  // tile too large: general path
+    int rc;
+    const size_t nrec = (size_t)std::max(ns, 1) * d.crop_x;
+    hipError_t e;
+    if ((rc = upload(&p->d_pl_slice_off, off)) || (rc = upload(&p->d_pl_slice_rows, rows))) return rc;
+    if ((e = hipMalloc((void**)&p->d_pl_vox, nrec * sizeof(float4))) != hipSuccess ||
+        (e = hipMalloc((void**)&p->d_pl_rec_f, nrec * sizeof(float4))) != hipSuccess ||
+        (e = hipMalloc((void**)&p->d_pl_rec_i, nrec * sizeof(int32_t))) != hipSuccess)
+        return hip_fail(e, "hipMalloc (planar tables)");
+    p->pl.cs = p->d_cs;
+    p->pl.vox = p->d_pl_vox;
+    p->pl.rec_f = p->d_pl_rec_f;
+    p->pl.rec_i = p->d_pl_rec_i;
+    p->pl.slice_off = p->d_pl_slice_off;
+    p->pl.slice_rows = p->d_pl_slice_rows;
+    if (ns > 0) {
+        if ((e = tvam_launch_planar_rays(k, p->pl, nullptr)) != hipSuccess) return hip_fail(e, "planar ray table");
+        if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "planar ray table");
+    }
+    p->planar = true;
+    return 0;
+}
+
 extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** out) {
     if (!desc || !out) return fail(TVAM_ERR_INVALID, "null argument");
     *out = nullptr;
@@ -211,6 +296,9 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
     const tvam_desc& d = *desc;
     int a0 = d.angle_begin, a1 = d.angle_end < 0 ? d.n_patterns : d.angle_end;
     if (a0 < 0 || a1 > d.n_patterns || a0 > a1) return fail(TVAM_ERR_INVALID, "invalid angle shard");
+
+    if (a1 - a0 > 65536 || d.crop_x > 65536)  // slot entries pack (angle << 16 | column)
+        return fail(TVAM_ERR_UNSUPPORTED, "more than 65536 angles per shard or DMD columns");
 
     hipError_t e = hipSetDevice(device);
     if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
@@ -232,11 +320,11 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
     int tsx = pick(k.res[0]), tsy = pick(k.res[1]);
     int ntx = (k.res[0] + tsx - 1) / tsx, nty = (k.res[1] + tsy - 1) / tsy;
     p->ntiles = ntx * nty;
-    // tile + angle offsets/first columns + reduction scratch + per-angle max |p|
+    // tile (+ guard band) + reduction scratch + per-angle max |p|
 #ifndef TVAM_FWD_ACC64
 #define TVAM_FWD_ACC64 0
 #endif
-    p->lds_bytes = (size_t)(tsx + 2) * (tsy + 2) * sizeof(float) * (TVAM_FWD_ACC64 ? 2 : 1) + (size_t)(3 * ns + 1) * sizeof(int32_t) +
+    p->lds_bytes = (size_t)(tsx + 2) * (tsy + 2) * sizeof(float) * (TVAM_FWD_ACC64 ? 2 : 1) +
                    16 * sizeof(float) + (size_t)ns * sizeof(float);
     if (p->lds_bytes > 160 * 1024) {
         plan_free(p);
@@ -293,18 +381,21 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
     }
     slice_off[k.res[2]] = (int32_t)slice_rows.size();
 
-    // per-(tile, angle) DMD column ranges.  A collimated ray's lateral
-    // coordinate is l = dot(o, (s,-c,0)) = x_c; the spawn offset moves it by
-    // less than (1+max|p|)*RayEpsilon, covered by the margin.
+    // Per-tile slot lists: every (angle, DMD column) whose ray crosses the
+    // tile, in (angle, column) order so that consecutive lanes read
+    // consecutive ray records.  A collimated ray's lateral coordinate is
+    // l = dot(o, (s,-c,0)) = x_c; the spawn offset moves it by less than
+    // (1+max|p|)*RayEpsilon, covered by the margin.  (Sorting the slots by
+    // predicted in-tile length balances the lanes of a wave — 0.98 instead of
+    // 0.64 of the lanes busy in the march loop — but scatters the record reads
+    // and the adjoint's atomics over angles, which costs more than it gains.)
     double rmax = std::max({std::fabs((double)k.bmin[0]), std::fabs((double)k.bmax[0]), std::fabs((double)k.bmin[1]),
                             std::fabs((double)k.bmax[1]), (double)d.vial_r, (double)k.vial_half_h});
     double marg_l = 4.0 * (1.0 + rmax) * (double)TVAM_RAY_EPS;
     const double W = d.res_x, ex = k.ex;
-    // Columns are enumerated in PAIRS (q, n-1-q): the chord through a tile is
-    // a symmetric trapezoid in the lateral position, so a lane marching both
-    // rays of a pair does nearly the same work as every other lane.
-    std::vector<int32_t> col_lo((size_t)p->ntiles * ns), col_hi((size_t)p->ntiles * ns),
-        col_off((size_t)p->ntiles * (ns + 1));
+    const double vr = d.vial_r;
+    std::vector<int64_t> slot_off((size_t)p->ntiles + 1, 0);
+    std::vector<uint32_t> slots;
     int64_t max_nrt = 0;
     for (int ty = 0; ty < nty; ++ty)
         for (int tx = 0; tx < ntx; ++tx) {
@@ -313,43 +404,31 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
             double X1 = (double)k.bmin[0] + (double)std::min((tx + 1) * tsx, k.res[0]) * k.h[0];
             double Y0 = (double)k.bmin[1] + (double)(ty * tsy) * k.h[1];
             double Y1 = (double)k.bmin[1] + (double)std::min((ty + 1) * tsy, k.res[1]) * k.h[1];
-            int64_t acc = 0;
+            const size_t first = slots.size();
             for (int i = 0; i < ns; ++i) {
                 double c = cs[i].x, s = cs[i].y;
                 double l[4] = {X0 * s - Y0 * c, X1 * s - Y0 * c, X0 * s - Y1 * c, X1 * s - Y1 * c};
                 double L0 = *std::min_element(l, l + 4) - marg_l, L1 = *std::max_element(l, l + 4) + marg_l;
-                L0 = std::max(L0, -(double)d.vial_r - marg_l);
-                L1 = std::min(L1, (double)d.vial_r + marg_l);
-                int lo = 0, cnt = 0;
-                if (L0 <= L1) {
-                    double c_lo = W * (0.5 - L1 / ex) - 1.0, c_hi = W * (0.5 - L0 / ex);
-                    int cl = (int)std::floor(c_lo) - 1 - d.crop_offset_x;
-                    int ch = (int)std::ceil(c_hi) + 1 - d.crop_offset_x;
-                    cl = std::max(cl, 0);
-                    ch = std::min(ch, d.crop_x - 1);
-                    if (ch >= cl) {
-                        lo = cl;
-                        cnt = ch - cl + 1;
-                    }
-                }
-                col_lo[(size_t)tile * ns + i] = lo;
-                col_hi[(size_t)tile * ns + i] = lo + cnt - 1;
-                col_off[(size_t)tile * (ns + 1) + i] = (int32_t)acc;
-                acc += (cnt + 1) / 2;
+                L0 = std::max(L0, -vr - marg_l);
+                L1 = std::min(L1, vr + marg_l);
+                if (!(L0 <= L1)) continue;
+                double c_lo = W * (0.5 - L1 / ex) - 1.0, c_hi = W * (0.5 - L0 / ex);
+                int cl = std::max((int)std::floor(c_lo) - 1 - d.crop_offset_x, 0);
+                int ch = std::min((int)std::ceil(c_hi) + 1 - d.crop_offset_x, d.crop_x - 1);
+                for (int col = cl; col <= ch; ++col) slots.push_back(((uint32_t)i << 16) | (uint32_t)col);
             }
-            col_off[(size_t)tile * (ns + 1) + ns] = (int32_t)acc;
-            max_nrt = std::max(max_nrt, acc);
+            slot_off[(size_t)tile + 1] = (int64_t)slots.size();
+            max_nrt = std::max<int64_t>(max_nrt, (int64_t)(slots.size() - first));
         }
-    // flat slot count per workgroup must fit int32 (rows * columns * spp)
+    // flat slot count per workgroup must fit int32 (rows * slots * spp)
     if ((int64_t)p->max_rows_per_slice * max_nrt * 64 > (int64_t)0x7fffffff) {
         plan_free(p);
         return fail(TVAM_ERR_TOO_LARGE, "too many rays per tile for one launch");
     }
 
     if ((rc = upload(&p->d_cs, cs)) || (rc = upload(&p->d_slice_off, slice_off)) ||
-        (rc = upload(&p->d_slice_rows, slice_rows)) || (rc = upload(&p->d_col_lo, col_lo)) ||
-        (rc = upload(&p->d_col_hi, col_hi)) || (rc = upload(&p->d_ang, ang)) ||
-        (rc = upload(&p->d_col_off, col_off))) {
+        (rc = upload(&p->d_slice_rows, slice_rows)) || (rc = upload(&p->d_slots, slots)) ||
+        (rc = upload(&p->d_slot_off, slot_off)) || (rc = upload(&p->d_ang, ang))) {
         plan_free(p);
         return rc;
     }
@@ -361,19 +440,22 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
     p->tiles.cs = p->d_cs;
     p->tiles.slice_off = p->d_slice_off;
     p->tiles.slice_rows = p->d_slice_rows;
-    p->tiles.col_lo = p->d_col_lo;
-    p->tiles.col_hi = p->d_col_hi;
+    p->tiles.slots = p->d_slots;
+    p->tiles.slot_off = p->d_slot_off;
     p->tiles.ang = p->d_ang;
     if ((e = hipEventCreateWithFlags(&p->ray_ready, hipEventDisableTiming)) != hipSuccess) {
         plan_free(p);
         return hip_fail(e, "hipEventCreate");
     }
-    p->tiles.col_off = p->d_col_off;
     p->tiles.ntx = ntx;
     p->tiles.nty = nty;
     p->tiles.tsx = tsx;
     p->tiles.tsy = tsy;
     p->tiles.n_shard = ns;
+    if ((rc = planar_setup(p, cs))) {
+        plan_free(p);
+        return rc;
+    }
     *out = p;
     return 0;
 }
@@ -475,6 +557,14 @@ extern "C" int tvam_forward(tvam_plan* p, const float* active_data, const uint32
         pat = p->d_dense;
         idxmap = p->d_idxmap;
     }
+    if (p->planar) {
+        if (p->desc.flags & TVAM_FLAG_FWD_STATS) {
+            if ((e = hipMemsetAsync(p->d_counter, 0, sizeof(unsigned long long), stream)) != hipSuccess)
+                return hip_fail(e, "hipMemsetAsync");
+        }
+        e = tvam_launch_fwd_planar(kc, p->pl, p->planar_fz, pat, dose, stream);
+        return e == hipSuccess ? 0 : hip_fail(e, "planar forward launch");
+    }
     TvamTiles t = p->tiles;
     t.spp = spp;
     t.seed = seed;
@@ -512,6 +602,10 @@ extern "C" int tvam_adjoint(tvam_plan* p, const float* grad_dose, const uint32_t
     }
     if ((e = hipMemsetAsync(grad_active, 0, n_active * sizeof(float), stream)) != hipSuccess)
         return hip_fail(e, "hipMemsetAsync");
+    if (p->planar) {
+        e = tvam_launch_adj_planar(k, p->pl, p->tiles, p->planar_az, idxmap, grad_dose, grad_active, stream);
+        return e == hipSuccess ? 0 : hip_fail(e, "planar adjoint launch");
+    }
     if (!p->empty) {
         TvamTiles t = p->tiles;
         t.spp = spp;
@@ -548,6 +642,8 @@ extern "C" int tvam_count_visits(tvam_plan* p, uint32_t spp, uint32_t seed, uint
     *visits = h;
     return 0;
 }
+
+extern "C" int tvam_plan_path(const tvam_plan* p) { return p && p->planar ? 1 : 0; }
 
 extern "C" int tvam_plan_stats(tvam_plan* p, uint64_t* fallback_tiles) {
     if (!p || !fallback_tiles) return fail(TVAM_ERR_INVALID, "null argument");

@@ -1,0 +1,378 @@
+// tvam_planar.hip — the planar fast path of regular sampling.
+//
+// With a collimated projector and regular sampling every ray of DMD column
+// `col` at angle `a` has the same xy path whatever its DMD row: origin
+// o = look_at(...) @ (x_c, y_c, 0.005) differs between rows only in z
+// (common.py:81-108 with jitter 0.5), the index-matched vial is a vertical
+// cylinder (geometry.py:75-96) so the medium segment [o2, o2 + maxt d] is
+// row-independent, and the DDA (sensor.py:327-438) of a planar ray never
+// steps in z.  The spawn offset (1 + max|p|) * RayEpsilon of the vial entry
+// point p is row-independent as long as |p_z| < max(|p_x|, |p_y|), which the
+// plan guarantees (|z| <= 0.7 r <= r / sqrt(2)).  So one (angle, column)
+// record serves every row, and the per-visit weight
+//     c = exp(-st t_in) - exp(-st t_out)
+// of voxel (x, y) is the same for every z-slice.  Two kernels use that:
+//
+//   * forward, voxel-driven: a thread owns a voxel column (x, y) and Z
+//     z-slices; for every angle it finds the 1-3 DMD columns whose ray
+//     crosses the voxel, computes that ray's exact segment [t_in, t_out] in
+//     the voxel (what one DDA visit accumulates), and adds c * P(slice) for
+//     its Z slices from a per-angle pattern slab staged in LDS.  No atomics,
+//     no per-ray resume, deterministic.
+//   * adjoint, ray-driven with Z-slice sharing: the tile DDA of
+//     tvam_kernels.hip, but the LDS tile holds Z interleaved slices, so one
+//     march computes c once per visit and gathers Z gradient values with one
+//     or two ds_read_b128.
+//
+// Both work in slice space: a slice's pattern is the sum of the DMD rows
+// whose rays lie in it (usually exactly one), and a row's gradient is its
+// slice's.
+#include "tvam_internal.h"
+
+#define TVAM_PB 256
+
+__device__ __forceinline__ float pl_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+
+// ---------------------------------------------------------------------------
+// (angle, column) table: ray generation (common.py:81-108, jitter 0.5), vial
+// segment (volume.py:179-216) and DDA initialisation (sensor.py:327-365),
+// evaluated once per column instead of once per (row, column).
+//   vox[i]   = {qx, qy, maxt, 0}: t(X) = fma(X, 1/d.x, qx) is the distance
+//              from o2 at which the ray crosses x = X (likewise y); an axis
+//              with |d| <= 1e-8 (never stepped by the DDA) stores the DDA's
+//              fixed voxel index instead; maxt < 0 marks a ray that misses.
+//   rec_f[i] = {t_start, tau_end, dtmax0_x, dtmax0_y}, rec_i[i] = start voxel
+//              x | y << 16 (or -1): the tile DDA's resume record.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void tvam_planar_rays_kernel(TvamConsts k, const float2* __restrict__ cs, int ns,
+                                                               float4* __restrict__ vox, float4* __restrict__ rec_f,
+                                                               int32_t* __restrict__ rec_i) {
+    const int64_t n = (int64_t)ns * k.crop_x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int al = (int)(i / k.crop_x), col = (int)(i - (int64_t)al * k.crop_x);
+        const float2 csv = cs[al];
+        float xc, yc, ox, oy, oz, dx, dy;
+        tvam_ray_camera(k, k.crop_off_x + col, k.crop_off_y, 0.5f, 0.5f, xc, yc);
+        tvam_ray_world(k, csv.x, csv.y, xc, 0.0f, ox, oy, oz, dx, dy);
+        float o2x, o2y, maxt;
+        TvamDda q;
+        if (!tvam_segment_im(k, ox, oy, 0.0f, dx, dy, o2x, o2y, maxt) || !tvam_dda_init(k, o2x, o2y, dx, dy, maxt, q)) {
+            vox[i] = make_float4(0.0f, 0.0f, -1.0f, 0.0f);
+            rec_f[i] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
+            rec_i[i] = -1;
+            continue;
+        }
+        const bool vx = fabsf(dx) > 1e-8f, vy = fabsf(dy) > 1e-8f;
+        const float qx = vx ? -o2x * (1.0f / dx) : (float)q.sv[0];
+        const float qy = vy ? -o2y * (1.0f / dy) : (float)q.sv[1];
+        vox[i] = make_float4(qx, qy, q.t_start + q.tau_end, 0.0f);
+        rec_f[i] = make_float4(q.t_start, q.tau_end, q.dtm0[0], q.dtm0[1]);
+        rec_i[i] = q.sv[0] | (q.sv[1] << 16);
+    }
+}
+
+hipError_t tvam_launch_planar_rays(const TvamConsts& k, const TvamPlanar& pl, hipStream_t stream) {
+    const int64_t n = (int64_t)pl.ns * k.crop_x;
+    int64_t g = (n + 255) / 256;
+    g = g > 65536 ? 65536 : (g < 1 ? 1 : g);
+    hipLaunchKernelGGL(tvam_planar_rays_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, pl.cs, pl.ns, pl.vox,
+                       pl.rec_f, pl.rec_i);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Forward, voxel-driven.  Workgroup = 16 x 16 voxel columns x Z slices.
+// Per angle the workgroup stages, for the DMD columns whose rays can cross
+// its tile (a window of pl.ncmax columns), the slice-binned pattern
+// P[col][z] and the ray table entry; each thread then visits its 1-3
+// candidate columns.  The DDA's visit of ray (a, col) in voxel (x, y) covers
+// [max(t_x,near, t_y,near, 0), min(t_x,far, t_y,far, t_end)] (sensor.py:383-438
+// in exact arithmetic), so the dose is the same sum of telescoped weights
+// the DDA forms, up to fp32 rounding of the crossing times.
+// ---------------------------------------------------------------------------
+template <int Z>
+__global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, TvamPlanar pl,
+                                                                  const float* __restrict__ pat,
+                                                                  float* __restrict__ dose) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int ncm = pl.ncmax;
+    float* s_p = reinterpret_cast<float*>(smem);                  // [ncm][Z]
+    float4* s_r = reinterpret_cast<float4*>(s_p + ncm * Z);       // [ncm]
+    int* s_row = reinterpret_cast<int*>(s_r + ncm);               // [Z]: the slice's row, -1 none, -2 several
+
+    const int ntx = (k.res[0] + 15) >> 4;
+    const int bx = blockIdx.x % ntx, by = blockIdx.x / ntx;
+    const int ix = bx * 16 + (threadIdx.x & 15), iy = by * 16 + (threadIdx.x >> 4);
+    const int z0 = blockIdx.y * Z;
+    const float hx = k.h[0], hy = k.h[1];
+    // voxel edges exactly as the DDA places them (bmin + i * h, sensor.py:357)
+    const float X0 = k.bmin[0] + (float)ix * hx, X1 = k.bmin[0] + (float)(ix + 1) * hx;
+    const float Y0 = k.bmin[1] + (float)iy * hy, Y1 = k.bmin[1] + (float)(iy + 1) * hy;
+    const float Xc = k.bmin[0] + ((float)ix + 0.5f) * hx, Yc = k.bmin[1] + ((float)iy + 0.5f) * hy;
+    // tile corners for the column window
+    const float TX0 = k.bmin[0] + (float)(bx * 16) * hx, TX1 = k.bmin[0] + (float)(bx * 16 + 16) * hx;
+    const float TY0 = k.bmin[1] + (float)(by * 16) * hy, TY1 = k.bmin[1] + (float)(by * 16 + 16) * hy;
+    // lateral coordinate l -> fractional crop column u = W (0.5 - l / ex) - 0.5 - crop_off (common.py:96-99)
+    const float Wd = (float)k.res_x;
+    const float du = -Wd / k.ex, u0 = 0.5f * Wd - 0.5f - (float)k.crop_off_x;
+
+    if (threadIdx.x < Z) {
+        const int s = z0 + threadIdx.x;
+        int r = -1;
+        if (s < k.res[2]) {
+            const int b = pl.slice_off[s], e = pl.slice_off[s + 1];
+            r = e - b == 1 ? pl.slice_rows[b] : (e - b == 0 ? -1 : -2);
+        }
+        s_row[threadIdx.x] = r;
+    }
+
+    float acc[Z];
+#pragma unroll
+    for (int z = 0; z < Z; ++z) acc[z] = 0.0f;
+
+    for (int al = 0; al < pl.ns; ++al) {
+        const float2 csv = pl.cs[al];
+        const float c = csv.x, s = csv.y;
+        // window of columns whose rays can cross the tile (same for every thread)
+        const float l00 = TX0 * s - TY0 * c, l10 = TX1 * s - TY0 * c, l01 = TX0 * s - TY1 * c, l11 = TX1 * s - TY1 * c;
+        const float lmax = fmaxf(fmaxf(l00, l10), fmaxf(l01, l11));
+        const int cb = (int)floorf(fmaf(lmax, du, u0) - pl.marg_u) - 1;  // u decreases with l
+        __syncthreads();  // previous angle's readers are done
+        const float* pa = pat + (size_t)al * k.crop_y * k.crop_x;
+        for (int i = threadIdx.x; i < ncm * Z; i += TVAM_PB) {
+            const int z = i / ncm, jj = i - z * ncm;
+            const int col = cb + jj;
+            float v = 0.0f;
+            if (col >= 0 && col < k.crop_x) {
+                const int r = s_row[z];
+                if (r >= 0) v = pa[(size_t)r * k.crop_x + col];
+                else if (r == -2) {
+                    const int b = pl.slice_off[z0 + z], e = pl.slice_off[z0 + z + 1];
+                    for (int q = b; q < e; ++q) v += pa[(size_t)pl.slice_rows[q] * k.crop_x + col];
+                }
+            }
+            s_p[jj * Z + z] = v;
+        }
+        for (int jj = threadIdx.x; jj < ncm; jj += TVAM_PB) {
+            const int col = cb + jj;
+            s_r[jj] = (col >= 0 && col < k.crop_x) ? pl.vox[(size_t)al * k.crop_x + col]
+                                                   : make_float4(0.0f, 0.0f, -1.0f, 0.0f);
+        }
+        __syncthreads();
+
+        // this voxel's candidate columns: rays whose lateral line meets [l - w, l + w]
+        const float dxr = -c, dyr = -s;
+        const bool vx = fabsf(dxr) > 1e-8f, vy = fabsf(dyr) > 1e-8f;
+        const float idx = 1.0f / dxr, idy = 1.0f / dyr;
+        const float l = Xc * s - Yc * c;
+        // the vial-entry spawn offset moves a ray's line by up to (1 + max|p|) * RayEpsilon
+        // sideways (geometry.py:75-96, volume.py:191): margin pl.marg_u
+        const float w = 0.5f * (hx * fabsf(s) + hy * fabsf(c)) * fabsf(du) + pl.marg_u;
+        const float u = fmaf(l, du, u0);
+        const int j0 = max((int)ceilf(u - w), cb), j1 = min((int)floorf(u + w), cb + ncm - 1);
+        for (int j = j0; j <= j1; ++j) {
+            const int jj = j - cb;
+            const float4 q = s_r[jj];
+            float tnx, tfx, tny, tfy;
+            if (vx) {
+                const float a = fmaf(X0, idx, q.x), b = fmaf(X1, idx, q.x);
+                tnx = fminf(a, b);
+                tfx = fmaxf(a, b);
+            } else {
+                tnx = (float)ix == q.x ? -TVAM_INF : TVAM_INF;
+                tfx = TVAM_INF;
+            }
+            if (vy) {
+                const float a = fmaf(Y0, idy, q.y), b = fmaf(Y1, idy, q.y);
+                tny = fminf(a, b);
+                tfy = fmaxf(a, b);
+            } else {
+                tny = (float)iy == q.y ? -TVAM_INF : TVAM_INF;
+                tfy = TVAM_INF;
+            }
+            const float tin = fmaxf(fmaxf(tnx, tny), 0.0f);
+            const float tout = fminf(fminf(tfx, tfy), q.z);
+            if (tout > tin) {
+                const float wgt = pl_exp2(k.nsig2 * tin) - pl_exp2(k.nsig2 * tout);
+                const float4* pz = reinterpret_cast<const float4*>(s_p + jj * Z);
+#pragma unroll
+                for (int z4 = 0; z4 < Z / 4; ++z4) {
+                    const float4 pv = pz[z4];
+                    acc[4 * z4 + 0] = fmaf(wgt, pv.x, acc[4 * z4 + 0]);
+                    acc[4 * z4 + 1] = fmaf(wgt, pv.y, acc[4 * z4 + 1]);
+                    acc[4 * z4 + 2] = fmaf(wgt, pv.z, acc[4 * z4 + 2]);
+                    acc[4 * z4 + 3] = fmaf(wgt, pv.w, acc[4 * z4 + 3]);
+                }
+            }
+        }
+    }
+
+    if (ix < k.res[0] && iy < k.res[1]) {
+        const float scale = k.wscale * k.inv_vol;  // Le * weight (common.py:108-111) / voxel volume (volume.py:41-42)
+        const size_t plane = (size_t)k.res[0] * k.res[1];
+#pragma unroll
+        for (int z = 0; z < Z; ++z)
+            if (z0 + z < k.res[2]) dose[(size_t)(z0 + z) * plane + (size_t)iy * k.res[0] + ix] = acc[z] * scale;
+    }
+}
+
+size_t tvam_planar_fwd_lds(const TvamPlanar& pl, int Z) {
+    return (size_t)pl.ncmax * Z * sizeof(float) + (size_t)pl.ncmax * sizeof(float4) + (size_t)Z * sizeof(int);
+}
+
+hipError_t tvam_launch_fwd_planar(const TvamConsts& k, const TvamPlanar& pl, int Z, const float* pat, float* dose,
+                                  hipStream_t stream) {
+    const int ntx = (k.res[0] + 15) / 16, nty = (k.res[1] + 15) / 16;
+    dim3 grid((unsigned)(ntx * nty), (unsigned)((k.res[2] + Z - 1) / Z));
+    const size_t lds = tvam_planar_fwd_lds(pl, Z);
+    switch (Z) {
+        case 8:
+            hipLaunchKernelGGL(tvam_fwd_planar_kernel<8>, grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
+            break;
+        case 16:
+            hipLaunchKernelGGL(tvam_fwd_planar_kernel<16>, grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
+            break;
+        case 32:
+            hipLaunchKernelGGL(tvam_fwd_planar_kernel<32>, grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
+            break;
+        default:
+            return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Adjoint, ray-driven with Z-slice sharing.  Workgroup = (xy tile, Z
+// slices); LDS holds the gradient tile interleaved [voxel][Z] (+ 1-voxel
+// guard band).  A lane resumes ray (a, col) at the tile entry from its
+// row-independent record (closed form of the reference's stepping, as in
+// tvam_kernels.hip), marches it once, and accumulates Z dot products; each
+// row of each slice then receives its slice's value (volume.py:274-276).
+// ---------------------------------------------------------------------------
+template <int Z>
+__global__ __launch_bounds__(TVAM_PB) void tvam_adj_planar_kernel(TvamConsts k, TvamPlanar pl, TvamTiles tp,
+                                                                  const int32_t* __restrict__ idxmap,
+                                                                  const float* __restrict__ gin,
+                                                                  float* __restrict__ out) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    float* tile = reinterpret_cast<float*>(smem);
+    const int tsx = tp.tsx, tsy = tp.tsy;
+    const int tw = tsx + 2, th = tsy + 2;
+    int* s_roff = reinterpret_cast<int*>(tile + (size_t)tw * th * Z);  // [Z + 1] CSR of the chunk's rows
+    int* s_rows = s_roff + Z + 1;                                       // [pl.max_rows_chunk]
+
+    const int tile_id = blockIdx.x, z0 = blockIdx.y * Z;
+    const int x0 = (tile_id % tp.ntx) * tsx, y0 = (tile_id / tp.ntx) * tsy;
+    const int x1 = min(x0 + tsx, k.res[0]), y1 = min(y0 + tsy, k.res[1]);
+    const int wx = x1 - x0, wy = y1 - y0;
+    const size_t plane = (size_t)k.res[0] * k.res[1];
+
+    // gradient tile, [voxel][z], scaled by 1/voxel volume (volume.py:130)
+    for (int i = threadIdx.x; i < tw * th * Z; i += TVAM_PB) {
+        const int z = i / (tw * th), li = i - z * (tw * th);
+        const int ly = li / tw - 1, lx = li - (ly + 1) * tw - 1;
+        float v = 0.0f;
+        if (lx >= 0 && ly >= 0 && lx < wx && ly < wy && z0 + z < k.res[2])
+            v = gin[(size_t)(z0 + z) * plane + (size_t)(y0 + ly) * k.res[0] + (x0 + lx)] * k.inv_vol;
+        tile[(size_t)li * Z + z] = v;
+    }
+    if (threadIdx.x == 0) {
+        int n = 0;
+        for (int z = 0; z < Z; ++z) {
+            s_roff[z] = n;
+            if (z0 + z < k.res[2])
+                for (int q = pl.slice_off[z0 + z]; q < pl.slice_off[z0 + z + 1]; ++q) s_rows[n++] = pl.slice_rows[q];
+        }
+        s_roff[Z] = n;
+    }
+    __syncthreads();
+    if (s_roff[Z] == 0) return;  // no DMD row lies in these slices
+
+    const uint32_t* slots = tp.slots + tp.slot_off[tile_id];
+    const int nrt = (int)(tp.slot_off[tile_id + 1] - tp.slot_off[tile_id]);
+    for (int g = threadIdx.x; g < nrt; g += TVAM_PB) {
+        const uint32_t e = slots[g];
+        const int al = (int)(e >> 16), colc = (int)(e & 0xffffu);
+        const int ri = pl.rec_i[(size_t)al * k.crop_x + colc];
+        if (ri < 0) continue;  // misses the vial / grid
+        const float4 ff = pl.rec_f[(size_t)al * k.crop_x + colc];
+        const float4 an = tp.ang[al];
+        const int svx = ri & 0xffff, svy = ri >> 16;
+        const int stx = (int)an.z, sty = (int)an.w;
+        float tin0, tout0, tin1, tout1;
+        int nin0, nout0, nin1, nout1;
+        tvam_axis_window(svx, stx, ff.z, an.x, x0, x1, tin0, tout0, nin0, nout0);
+        tvam_axis_window(svy, sty, ff.w, an.y, y0, y1, tin1, tout1, nin1, nout1);
+        const float tau_e = fmaxf(fmaxf(tin0, tin1), 0.0f);
+        const float tau_x = fminf(fminf(tout0, tout1), ff.y);
+        if (!(tau_e < tau_x)) continue;
+        const int n0 = tvam_axis_steps(tau_e, ff.z, an.x, nin0, nout0);
+        const int n1 = tvam_axis_steps(tau_e, ff.w, an.y, nin1, nout1);
+        const int vx = svx + stx * n0, vy = svy + sty * n1;
+        float Tx = ff.z < TVAM_INF ? fmaxf(fmaf((float)n0, an.x, ff.z) - tau_e, 0.0f) : TVAM_INF;
+        float Ty = ff.w < TVAM_INF ? fmaxf(fmaf((float)n1, an.y, ff.w) - tau_e, 0.0f) : TVAM_INF;
+        const float rem = tau_x - tau_e, stop = rem - 1e-6f;
+        const float nt0 = k.nsig2 * (ff.x + tau_e);
+        const int sxb = stx * Z * 4, syb = sty * tw * Z * 4;
+        const char* pv = reinterpret_cast<const char*>(tile) + (size_t)((vy - y0 + 1) * tw + (vx - x0 + 1)) * Z * 4;
+        float acc[Z];
+#pragma unroll
+        for (int z = 0; z < Z; ++z) acc[z] = 0.0f;
+        float e0 = pl_exp2(nt0);
+        // one march, Z gathers per visit (see tvam_march in tvam_kernels.hip)
+        for (;;) {
+            const float tn = fminf(fminf(Tx, Ty), rem);
+            const float e1 = pl_exp2(fmaf(k.nsig2, tn, nt0));
+            const float cw = e0 - e1;
+            const float4* g4 = reinterpret_cast<const float4*>(pv);
+#pragma unroll
+            for (int z4 = 0; z4 < Z / 4; ++z4) {
+                const float4 gv = g4[z4];
+                acc[4 * z4 + 0] = fmaf(cw, gv.x, acc[4 * z4 + 0]);
+                acc[4 * z4 + 1] = fmaf(cw, gv.y, acc[4 * z4 + 1]);
+                acc[4 * z4 + 2] = fmaf(cw, gv.z, acc[4 * z4 + 2]);
+                acc[4 * z4 + 3] = fmaf(cw, gv.w, acc[4 * z4 + 3]);
+            }
+            const bool mx = Tx <= Ty;
+            Tx = mx ? Tx + an.x : Tx;
+            Ty = mx ? Ty : Ty + an.y;
+            pv += mx ? sxb : syb;
+            e0 = e1;
+            if (!(tn < stop)) break;
+        }
+        const int64_t base = (int64_t)(k.a0 + al) * k.crop_y * k.crop_x + colc - k.shard_base;
+#pragma unroll
+        for (int z = 0; z < Z; ++z) {
+            const float v = acc[z] * k.wscale;
+            for (int q = s_roff[z]; q < s_roff[z + 1]; ++q) {
+                int64_t act = base + (int64_t)s_rows[q] * k.crop_x;
+                if (idxmap) {
+                    act = idxmap[act];
+                    if (act < 0) continue;
+                }
+                atomicAdd(&out[act], v);  // backward_from(Le * em_grad), volume.py:274-276
+            }
+        }
+    }
+}
+
+size_t tvam_planar_adj_lds(const TvamPlanar& pl, const TvamTiles& t, int Z) {
+    return (size_t)(t.tsx + 2) * (t.tsy + 2) * Z * sizeof(float) + (size_t)(Z + 1 + pl.max_rows_chunk) * sizeof(int);
+}
+
+hipError_t tvam_launch_adj_planar(const TvamConsts& k, const TvamPlanar& pl, const TvamTiles& t, int Z,
+                                  const int32_t* idxmap, const float* gin, float* out, hipStream_t stream) {
+    dim3 grid((unsigned)(t.ntx * t.nty), (unsigned)((k.res[2] + Z - 1) / Z));
+    const size_t lds = tvam_planar_adj_lds(pl, t, Z);
+    switch (Z) {
+        case 4:
+            hipLaunchKernelGGL(tvam_adj_planar_kernel<4>, grid, dim3(TVAM_PB), lds, stream, k, pl, t, idxmap, gin, out);
+            break;
+        case 8:
+            hipLaunchKernelGGL(tvam_adj_planar_kernel<8>, grid, dim3(TVAM_PB), lds, stream, k, pl, t, idxmap, gin, out);
+            break;
+        default:
+            return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}

@@ -97,6 +97,11 @@ class Projection:
                 n_active, spp, seed & 0xFFFFFFFF, out.data_ptr(), _stream_ptr(self.device)))
         return out
 
+    @property
+    def planar(self) -> bool:
+        """True when the planar fast path (regular sampling) serves this plan."""
+        return bool(self.lib.tvam_plan_path(self._plan))
+
     def fallback_tiles(self) -> int:
         """Workgroups of the last forward that used float LDS atomics (needs FLAG_FWD_STATS)."""
         v = ctypes.c_uint64(0)

@@ -115,6 +115,7 @@ typedef struct tvam_desc {
 /* tvam_desc.flags */
 #define TVAM_FLAG_NO_ZERO_SKIP 1  /* forward: march rays whose pattern value is 0 too */
 #define TVAM_FLAG_FWD_STATS    2  /* forward: count tiles that fell back to float LDS atomics */
+#define TVAM_FLAG_NO_PLANAR    4  /* use the per-ray tile kernels even where the planar path applies */
 
 typedef struct tvam_plan tvam_plan;
 
@@ -154,6 +155,11 @@ int tvam_adjoint(tvam_plan* plan, const float* grad_dose,
    last forward that accumulated with float atomics instead of fixed point
    (needs TVAM_FLAG_FWD_STATS). */
 int tvam_plan_stats(tvam_plan* plan, uint64_t* fallback_tiles);
+
+/* Which kernels serve this plan: 1 = planar fast path (regular sampling:
+   one ray record per (angle, column), voxel-driven forward, Z-slice-sharing
+   adjoint), 0 = per-ray tile kernels. */
+int tvam_plan_path(const tvam_plan* plan);
 
 /* Exact number of DDA voxel visits of one pass (host-synchronous). */
 int tvam_count_visits(tvam_plan* plan, uint32_t spp, uint32_t seed,

@@ -24,9 +24,16 @@ def rel_l2(a, b):
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
 
 
-def make(N, A, regular=True, spp=1, tile=0, angle_range=None, **kw):
+def make(N, A, regular=True, spp=1, tile=0, angle_range=None, planar=True, zres=None, **kw):
+    """planar=False forces the per-ray tile kernels; zres != N gives 2 rows per slice
+    (zres = N/2) or empty slices (zres = 2N)."""
     cfg = benchy_index_matched(N=N, angles=A, regular_sampling=regular, spp=spp, **kw)
-    return desc_from_config(cfg, angle_range=angle_range, tile=tile)
+    d = desc_from_config(cfg, angle_range=angle_range, tile=tile)
+    if not planar:
+        d.flags |= _abi.FLAG_NO_PLANAR
+    if zres is not None:
+        d.film_res[2] = zres
+    return d
 
 
 def gpu_forward(desc, pat, spp=1, seed=0, pixels=None):
@@ -46,6 +53,12 @@ CASES = [
     dict(N=64, A=64),                   # config 1 (plumbing config, 64^3 / 64 angles)
     dict(N=32, A=16, regular=False, spp=3),
     dict(N=33, A=17, r=5.5),            # vial smaller than the grid's half-diagonal
+    dict(N=32, A=24, planar=False),     # regular sampling on the per-ray tile kernels
+    dict(N=40, A=30, tile=7, planar=False),
+    dict(N=33, A=17, r=5.5, planar=False),
+    dict(N=24, A=12, zres=12),          # two DMD rows per slice
+    dict(N=24, A=12, zres=48),          # slices without rows
+    dict(N=24, A=12, zres=12, planar=False),
 ]
 
 
@@ -58,13 +71,15 @@ def test_forward_matches_oracle(oracle, case):
     pat = np.random.default_rng(0).uniform(0.0, 0.1, n).astype(np.float32)
     ref, visits = oracle.forward(d, pat, spp=spp, seed=5, nthreads=8)
     got, proj = gpu_forward(d, pat, spp=spp, seed=5)
+    # planar path: regular sampling and every row's vial-entry offset row-independent (|z| <= 0.7 r)
+    assert proj.planar == (case.get("regular", True) and case.get("planar", True) and 5.0 <= 0.7 * case.get("r", 8.0))
     assert rel_l2(got, ref) < RTOL_L2
     assert np.max(np.abs(got - ref)) <= 1e-4 * np.max(np.abs(ref)) + 1e-7
     hv = proj.count_visits(spp, 5)
     assert abs(hv - visits) <= max(2, 1e-4 * visits)
 
 
-@pytest.mark.parametrize("case", CASES[:5] + [dict(N=32, A=16, regular=False, spp=2)],
+@pytest.mark.parametrize("case", CASES[:5] + CASES[7:] + [dict(N=32, A=16, regular=False, spp=2)],
                          ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
 def test_adjoint_matches_oracle(oracle, case):
     case = dict(case)
@@ -79,8 +94,9 @@ def test_adjoint_matches_oracle(oracle, case):
     assert rel_l2(g, ref) < RTOL_L2
 
 
-def test_dot_product_gpu():
-    d = make(N=48, A=40, regular=False, spp=2)
+@pytest.mark.parametrize("regular", [False, True])
+def test_dot_product_gpu(regular):
+    d = make(N=48, A=40, regular=regular, spp=2)
     n = d.n_patterns * d.crop_y * d.crop_x
     rng = np.random.default_rng(2)
     p = torch.as_tensor(rng.uniform(0, 1, n).astype(np.float32), device="cuda:0")
@@ -93,8 +109,9 @@ def test_dot_product_gpu():
     assert abs(lhs - rhs) <= 1e-5 * abs(lhs)
 
 
-def test_sparse_active_pixels(oracle):
-    d = make(N=24, A=12)
+@pytest.mark.parametrize("planar", [True, False])
+def test_sparse_active_pixels(oracle, planar):
+    d = make(N=24, A=12, planar=planar)
     n = 12 * 24 * 24
     rng = np.random.default_rng(3)
     pat = rng.uniform(0.01, 0.1, n).astype(np.float32)
@@ -161,8 +178,8 @@ def test_fused_loss_matches_torch(K, reduction):
 @pytest.mark.parametrize("dist", ["signed", "heavy", "sparse_spikes"])
 def test_forward_fixed_point_and_fallback(oracle, dist):
     """Signed (L-BFGS search direction) and heavy-tailed inputs: fixed-point and float-fallback tiles."""
-    d = make(N=40, A=36)
-    d.flags = _abi.FLAG_FWD_STATS
+    d = make(N=40, A=36, planar=False)
+    d.flags |= _abi.FLAG_FWD_STATS
     n = 36 * 40 * 40
     rng = np.random.default_rng(7)
     if dist == "signed":
