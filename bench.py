@@ -107,7 +107,7 @@ def main():
     log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s, angles [{prob.a0},{prob.a1}), "
         f"visits/pass {visits:.3e}, rays {rays:.3e}")
 
-    # HIP-event timing of the dominant kernel (forward tile march) on its launch stream
+    # HIP-event timing of the dominant kernels (forward / adjoint projection) on their launch stream
     fwd_ms, adj_ms = [], []
     state = {"on": False}
     orig_fwd, orig_adj = prob.proj.forward, prob.proj.adjoint
@@ -199,7 +199,11 @@ def main():
         },
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "tvam_tile_kernel<FWD>", "alg_bytes_per_launch": alg_bytes},
+                     "kernel": "tvam_fwd_planar_kernel" if prob.proj.planar else "tvam_tile_kernel<FWD>",
+                     "alg_bytes_per_launch": alg_bytes,
+                     "note": "SURVEY 8(d) algorithmic bytes (per-visit dose RMW); the LDS / register-resident "
+                             "kernels move far fewer real bytes, so frac > 1 means past the naive HBM roofline "
+                             "(the real limit is VALU / LDS issue, DESIGN.md)"},
         "cpu_baseline": cpu,
     }
     print(json.dumps(result), flush=True)

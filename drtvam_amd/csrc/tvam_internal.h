@@ -33,10 +33,12 @@ struct TvamPlanar {
     int32_t ncmax;             // forward: DMD columns staged per (16x16 tile, angle)
     float marg_u;              // forward: candidate-column margin (spawn offset of o2 + rounding), in columns
     int32_t max_rows_chunk;    // adjoint: most DMD rows in one chunk of Z slices
+    int32_t adj_pitch;         // adjoint: LDS row pitch of the gradient tile in voxels (>= tile + 2)
 };
 
 hipError_t tvam_launch_planar_rays(const TvamConsts& k, const TvamPlanar& pl, hipStream_t stream);
 size_t tvam_planar_fwd_lds(const TvamPlanar& pl, int Z);
+bool tvam_planar_fwd_fits(const TvamPlanar& pl, int Z);
 hipError_t tvam_launch_fwd_planar(const TvamConsts& k, const TvamPlanar& pl, int Z, const float* pat, float* dose,
                                   hipStream_t stream);
 size_t tvam_planar_adj_lds(const TvamPlanar& pl, const TvamTiles& t, int Z);

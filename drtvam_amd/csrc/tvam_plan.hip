@@ -264,6 +264,9 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     p->pl.marg_u = (float)marg_u;
     p->pl.ncmax = (int32_t)std::ceil(wmax + 2.0 * marg_u + 0.01) + 4;
     p->pl.max_rows_chunk = mrc;
+    p->pl.adj_pitch = p->tiles.tsx + 2 + std::max(0, env_int("TVAM_ADJ_PITCH_PAD", 0));
+    while (p->planar_fz > 8 && !tvam_planar_fwd_fits(p->pl, p->planar_fz)) p->planar_fz /= 2;
+    if (!tvam_planar_fwd_fits(p->pl, p->planar_fz)) return 0;  // DMD much finer than the voxels: general path
     if (tvam_planar_adj_lds(p->pl, p->tiles, p->planar_az) > 160 * 1024) p->planar_az = 4;
     if (tvam_planar_adj_lds(p->pl, p->tiles, p->planar_az) > 160 * 1024) return 0;  // tile too large: general path
     int rc;
@@ -313,7 +316,9 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
 
     // tile geometry: LDS-resident xy tile of one z-slice
     auto pick = [&](int res) {
-        int ts = d.tile > 0 ? d.tile : 64;
+        // measured optimum (400^3 / 400 angles): the planar adjoint (regular sampling, 4
+        // interleaved slices in LDS) at 40, the per-ray tile kernels at 64
+        int ts = d.tile > 0 ? d.tile : (d.regular_sampling && !(d.flags & TVAM_FLAG_NO_PLANAR) ? 40 : 64);
         int nt = (res + ts - 1) / ts;
         return (res + nt - 1) / nt;
     };

@@ -90,15 +90,20 @@ hipError_t tvam_launch_planar_rays(const TvamConsts& k, const TvamPlanar& pl, hi
 // in exact arithmetic), so the dose is the same sum of telescoped weights
 // the DDA forms, up to fp32 rounding of the crossing times.
 // ---------------------------------------------------------------------------
+#define TVAM_PF 4  // staged pattern values per thread and angle (host: ncmax * Z <= TVAM_PF * TVAM_PB)
+
 template <int Z>
 __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, TvamPlanar pl,
                                                                   const float* __restrict__ pat,
                                                                   float* __restrict__ dose) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int ncm = pl.ncmax;
-    float* s_p = reinterpret_cast<float*>(smem);                  // [ncm][Z]
-    float4* s_r = reinterpret_cast<float4*>(s_p + ncm * Z);       // [ncm]
-    int* s_row = reinterpret_cast<int*>(s_r + ncm);               // [Z]: the slice's row, -1 none, -2 several
+    // [2][ncm][Z + 4] (double buffer); the +4 pad puts 16 consecutive columns'
+    // 16-byte reads in 16 different bank groups
+    constexpr int ZS = Z + 4;
+    float* s_p = reinterpret_cast<float*>(smem);
+    float4* s_r = reinterpret_cast<float4*>(s_p + 2 * ncm * ZS);  // [2][ncm]
+    int* s_row = reinterpret_cast<int*>(s_r + 2 * ncm);           // [Z]: the slice's row, -1 none, -2 several
 
     const int ntx = (k.res[0] + 15) >> 4;
     const int bx = blockIdx.x % ntx, by = blockIdx.x / ntx;
@@ -125,40 +130,84 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
         }
         s_row[threadIdx.x] = r;
     }
+    __syncthreads();
+
+    // first DMD column of the window whose rays can cross the tile at angle al
+    auto window = [&](int al) -> int {
+        const float2 csv = pl.cs[al];
+        const float l00 = TX0 * csv.y - TY0 * csv.x, l10 = TX1 * csv.y - TY0 * csv.x;
+        const float l01 = TX0 * csv.y - TY1 * csv.x, l11 = TX1 * csv.y - TY1 * csv.x;
+        const float lmax = fmaxf(fmaxf(l00, l10), fmaxf(l01, l11));
+        return (int)floorf(fmaf(lmax, du, u0) - pl.marg_u) - 1;  // u decreases with l
+    };
+    // This thread's staging slots i = tid + q * 256 of the [Z][ncm] slab are
+    // angle-independent: slice z, window column jj, the slice's row offset
+    // (or -2 - z when several rows share the slice) and the LDS offset.
+    int st_jj[TVAM_PF], st_row[TVAM_PF], st_off[TVAM_PF];
+#pragma unroll
+    for (int q = 0; q < TVAM_PF; ++q) {
+        const int i = threadIdx.x + q * TVAM_PB;
+        st_jj[q] = -1;
+        st_row[q] = -1;
+        st_off[q] = 0;
+        if (i < ncm * Z) {
+            const int z = i / ncm, jj = i - z * ncm;
+            const int r = s_row[z];
+            st_jj[q] = jj;
+            st_row[q] = r >= 0 ? r * k.crop_x : (r == -1 ? -1 : -2 - z);
+            st_off[q] = jj * ZS + z;
+        }
+    }
+    // global loads of angle al's slab (slice-binned pattern + ray table) into registers
+    float pv[TVAM_PF];
+    float4 rv;
+    auto fetch = [&](int al, int cb) {
+        const float* pa = pat + (size_t)al * k.crop_y * k.crop_x;
+#pragma unroll
+        for (int q = 0; q < TVAM_PF; ++q) {
+            const int col = cb + st_jj[q], r = st_row[q];
+            float v = 0.0f;
+            if (st_jj[q] >= 0 && col >= 0 && col < k.crop_x && r != -1) {
+                if (r >= 0) v = pa[r + col];
+                else {
+                    const int z = -2 - r;
+                    for (int t = pl.slice_off[z0 + z]; t < pl.slice_off[z0 + z + 1]; ++t)
+                        v += pa[(size_t)pl.slice_rows[t] * k.crop_x + col];
+                }
+            }
+            pv[q] = v;
+        }
+        const int col = cb + (int)threadIdx.x;
+        rv = make_float4(0.0f, 0.0f, -1.0f, 0.0f);
+        if ((int)threadIdx.x < ncm && col >= 0 && col < k.crop_x) rv = pl.vox[(size_t)al * k.crop_x + col];
+    };
+    auto store = [&](int buf) {
+        float* sp = s_p + buf * ncm * ZS;
+#pragma unroll
+        for (int q = 0; q < TVAM_PF; ++q)
+            if (st_jj[q] >= 0) sp[st_off[q]] = pv[q];
+        if ((int)threadIdx.x < ncm) s_r[buf * ncm + threadIdx.x] = rv;
+    };
 
     float acc[Z];
 #pragma unroll
     for (int z = 0; z < Z; ++z) acc[z] = 0.0f;
 
+    int cb = window(0);
+    fetch(0, cb);
+    store(0);
+    __syncthreads();
     for (int al = 0; al < pl.ns; ++al) {
+        const int buf = al & 1;
+        int cb_next = 0;
+        if (al + 1 < pl.ns) {  // prefetch the next angle while this one is computed
+            cb_next = window(al + 1);
+            fetch(al + 1, cb_next);
+        }
         const float2 csv = pl.cs[al];
         const float c = csv.x, s = csv.y;
-        // window of columns whose rays can cross the tile (same for every thread)
-        const float l00 = TX0 * s - TY0 * c, l10 = TX1 * s - TY0 * c, l01 = TX0 * s - TY1 * c, l11 = TX1 * s - TY1 * c;
-        const float lmax = fmaxf(fmaxf(l00, l10), fmaxf(l01, l11));
-        const int cb = (int)floorf(fmaf(lmax, du, u0) - pl.marg_u) - 1;  // u decreases with l
-        __syncthreads();  // previous angle's readers are done
-        const float* pa = pat + (size_t)al * k.crop_y * k.crop_x;
-        for (int i = threadIdx.x; i < ncm * Z; i += TVAM_PB) {
-            const int z = i / ncm, jj = i - z * ncm;
-            const int col = cb + jj;
-            float v = 0.0f;
-            if (col >= 0 && col < k.crop_x) {
-                const int r = s_row[z];
-                if (r >= 0) v = pa[(size_t)r * k.crop_x + col];
-                else if (r == -2) {
-                    const int b = pl.slice_off[z0 + z], e = pl.slice_off[z0 + z + 1];
-                    for (int q = b; q < e; ++q) v += pa[(size_t)pl.slice_rows[q] * k.crop_x + col];
-                }
-            }
-            s_p[jj * Z + z] = v;
-        }
-        for (int jj = threadIdx.x; jj < ncm; jj += TVAM_PB) {
-            const int col = cb + jj;
-            s_r[jj] = (col >= 0 && col < k.crop_x) ? pl.vox[(size_t)al * k.crop_x + col]
-                                                   : make_float4(0.0f, 0.0f, -1.0f, 0.0f);
-        }
-        __syncthreads();
+        const float* sp = s_p + buf * ncm * ZS;
+        const float4* sr = s_r + buf * ncm;
 
         // this voxel's candidate columns: rays whose lateral line meets [l - w, l + w]
         const float dxr = -c, dyr = -s;
@@ -172,7 +221,7 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
         const int j0 = max((int)ceilf(u - w), cb), j1 = min((int)floorf(u + w), cb + ncm - 1);
         for (int j = j0; j <= j1; ++j) {
             const int jj = j - cb;
-            const float4 q = s_r[jj];
+            const float4 q = sr[jj];
             float tnx, tfx, tny, tfy;
             if (vx) {
                 const float a = fmaf(X0, idx, q.x), b = fmaf(X1, idx, q.x);
@@ -194,17 +243,20 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
             const float tout = fminf(fminf(tfx, tfy), q.z);
             if (tout > tin) {
                 const float wgt = pl_exp2(k.nsig2 * tin) - pl_exp2(k.nsig2 * tout);
-                const float4* pz = reinterpret_cast<const float4*>(s_p + jj * Z);
+                const float4* pz = reinterpret_cast<const float4*>(sp + jj * ZS);
 #pragma unroll
                 for (int z4 = 0; z4 < Z / 4; ++z4) {
-                    const float4 pv = pz[z4];
-                    acc[4 * z4 + 0] = fmaf(wgt, pv.x, acc[4 * z4 + 0]);
-                    acc[4 * z4 + 1] = fmaf(wgt, pv.y, acc[4 * z4 + 1]);
-                    acc[4 * z4 + 2] = fmaf(wgt, pv.z, acc[4 * z4 + 2]);
-                    acc[4 * z4 + 3] = fmaf(wgt, pv.w, acc[4 * z4 + 3]);
+                    const float4 p4 = pz[z4];
+                    acc[4 * z4 + 0] = fmaf(wgt, p4.x, acc[4 * z4 + 0]);
+                    acc[4 * z4 + 1] = fmaf(wgt, p4.y, acc[4 * z4 + 1]);
+                    acc[4 * z4 + 2] = fmaf(wgt, p4.z, acc[4 * z4 + 2]);
+                    acc[4 * z4 + 3] = fmaf(wgt, p4.w, acc[4 * z4 + 3]);
                 }
             }
         }
+        if (al + 1 < pl.ns) store(buf ^ 1);
+        cb = cb_next;
+        __syncthreads();
     }
 
     if (ix < k.res[0] && iy < k.res[1]) {
@@ -217,8 +269,10 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
 }
 
 size_t tvam_planar_fwd_lds(const TvamPlanar& pl, int Z) {
-    return (size_t)pl.ncmax * Z * sizeof(float) + (size_t)pl.ncmax * sizeof(float4) + (size_t)Z * sizeof(int);
+    return 2 * ((size_t)pl.ncmax * (Z + 4) * sizeof(float) + (size_t)pl.ncmax * sizeof(float4)) + (size_t)Z * sizeof(int);
 }
+
+bool tvam_planar_fwd_fits(const TvamPlanar& pl, int Z) { return pl.ncmax <= TVAM_PB && pl.ncmax * Z <= TVAM_PF * TVAM_PB; }
 
 hipError_t tvam_launch_fwd_planar(const TvamConsts& k, const TvamPlanar& pl, int Z, const float* pat, float* dose,
                                   hipStream_t stream) {
@@ -257,7 +311,7 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_adj_planar_kernel(TvamConsts k, 
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float* tile = reinterpret_cast<float*>(smem);
     const int tsx = tp.tsx, tsy = tp.tsy;
-    const int tw = tsx + 2, th = tsy + 2;
+    const int tw = pl.adj_pitch, th = tsy + 2;  // row pitch >= tsx + 2 (padded against bank conflicts)
     int* s_roff = reinterpret_cast<int*>(tile + (size_t)tw * th * Z);  // [Z + 1] CSR of the chunk's rows
     int* s_rows = s_roff + Z + 1;                                       // [pl.max_rows_chunk]
 
@@ -350,14 +404,18 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_adj_planar_kernel(TvamConsts k, 
                     act = idxmap[act];
                     if (act < 0) continue;
                 }
+#if defined(TVAM_EXPERIMENT) && TVAM_EXPERIMENT == 5  // timing only: no output atomics
+                if (v == 1234.5f) out[act] = v;
+#else
                 atomicAdd(&out[act], v);  // backward_from(Le * em_grad), volume.py:274-276
+#endif
             }
         }
     }
 }
 
 size_t tvam_planar_adj_lds(const TvamPlanar& pl, const TvamTiles& t, int Z) {
-    return (size_t)(t.tsx + 2) * (t.tsy + 2) * Z * sizeof(float) + (size_t)(Z + 1 + pl.max_rows_chunk) * sizeof(int);
+    return (size_t)pl.adj_pitch * (t.tsy + 2) * Z * sizeof(float) + (size_t)(Z + 1 + pl.max_rows_chunk) * sizeof(int);
 }
 
 hipError_t tvam_launch_adj_planar(const TvamConsts& k, const TvamPlanar& pl, const TvamTiles& t, int Z,

@@ -9,9 +9,9 @@ for d in sys.argv[1:]:
     for f in glob.glob(f"{d}/**/*counter_collection.csv", recursive=True):
         for r in csv.DictReader(open(f)):
             name = r["Kernel_Name"]
-            if "tvam_tile_kernel" not in name:
+            if "tvam_" not in name:
                 continue
-            mode = name.split("<")[1].split(">")[0]
+            mode = name.split("(")[0]
             agg[mode][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for mode, cs in sorted(agg.items()):
     m = {c: sum(v) / len(v) for c, v in cs.items()}

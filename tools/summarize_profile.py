@@ -17,10 +17,16 @@ def per_kernel(path):
     out = {}
     for r in csv.DictReader(open(path)):
         n = r["Kernel_Name"]
-        if "tvam_tile_kernel" in n:
-            key = {"0": "forward", "1": "adjoint", "2": "count"}[n.split("<")[1][0]]
+        if "tvam_fwd_planar_kernel" in n:
+            key = "forward"
+        elif "tvam_adj_planar_kernel" in n:
+            key = "adjoint"
+        elif "tvam_tile_kernel" in n:
+            key = {"0": "forward_tile", "1": "adjoint_tile", "2": "count"}[n.split("<")[1][0]]
         elif "tvam_ray_setup" in n:
             key = "ray_setup"
+        elif "tvam_planar_rays" in n:
+            key = "planar_rays"
         else:
             continue
         out.setdefault(key, []).append(float(r["Counter_Value"]))
