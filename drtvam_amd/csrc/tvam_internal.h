@@ -32,6 +32,13 @@ struct TvamPlanar {
     int32_t ns;
     int32_t ncmax;             // forward: DMD columns staged per (16x16 tile, angle)
     float marg_u;              // forward: candidate-column margin (spawn offset of o2 + rounding), in columns
+    float u0;                  // forward: crop column of lateral coordinate 0 (0.5 W - 0.5 - crop_off_x)
+    int32_t fwd_nc;            // forward: candidate columns per (voxel, angle)
+    int32_t fwd_multi;         // forward: some slice collects several DMD rows
+    const float4* fwd_ang;     // forward: [ns][2] {s du, -c du, 1/d.x, 1/d.y}, {half width + margin, axis flags}
+    const int32_t* fwd_cb;     // forward: [16x16 tiles][ns] first column of the staged window
+    int32_t xcd_remap;         // forward: XCD-aware workgroup order
+    int32_t fwd_pf;            // forward: staged values per thread and angle (2 or 4)
     int32_t max_rows_chunk;    // adjoint: most DMD rows in one chunk of Z slices
     int32_t adj_pitch;         // adjoint: LDS row pitch of the gradient tile in voxels (>= tile + 2)
 };

@@ -63,6 +63,8 @@ struct tvam_plan {
     int32_t* d_pl_slice_off = nullptr;
     int32_t* d_pl_slice_rows = nullptr;
     float4* d_pl_vox = nullptr;
+    float4* d_pl_fwd_ang = nullptr;
+    int32_t* d_pl_fwd_cb = nullptr;
     float4* d_pl_rec_f = nullptr;
     int32_t* d_pl_rec_i = nullptr;
     // sparse scratch (dense crop layout), allocated on first sparse call
@@ -122,6 +124,8 @@ static void plan_free(tvam_plan* p) {
     (void)hipFree(p->d_pl_slice_off);
     (void)hipFree(p->d_pl_slice_rows);
     (void)hipFree(p->d_pl_vox);
+    (void)hipFree(p->d_pl_fwd_ang);
+    (void)hipFree(p->d_pl_fwd_cb);
     (void)hipFree(p->d_pl_rec_f);
     (void)hipFree(p->d_pl_rec_i);
     delete p;
@@ -244,35 +248,81 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
         rows.insert(rows.end(), rows_of[s].begin(), rows_of[s].end());
     }
     off[k.res[2]] = (int32_t)rows.size();
-    p->planar_fz = env_int("TVAM_PLANAR_FWD_Z", 16);
+    p->planar_fz = env_int("TVAM_PLANAR_FWD_Z", 32);
     p->planar_az = env_int("TVAM_PLANAR_ADJ_Z", 4);
-    if (p->planar_fz != 8 && p->planar_fz != 16 && p->planar_fz != 32) p->planar_fz = 16;
+    if (p->planar_fz != 8 && p->planar_fz != 16 && p->planar_fz != 32) p->planar_fz = 32;
     if (p->planar_az != 4 && p->planar_az != 8) p->planar_az = 4;
     const int ns = (int)cs.size();
     int32_t mrc = 0;
     for (int z0 = 0; z0 < k.res[2]; z0 += p->planar_az)
         mrc = std::max<int32_t>(mrc, off[std::min(z0 + p->planar_az, k.res[2])] - off[z0]);
-    // columns whose ray can cross a 16x16-voxel tile at some angle (+ window rounding)
+    // Forward (voxel-driven) tables.  Per angle, in the kernel's fp32 ops:
+    // u(X, Y) = X * (s du) + Y * (-c du) + u0 is the crop column whose ray has
+    // lateral coordinate X s - Y c (common.py:96-99: x_c = W a (0.5 - u));
+    // w = half the voxel's lateral width in columns + the spawn-offset margin.
+    // A voxel's candidates are the NC columns from ceil(u - w) on; every
+    // (16x16 tile, angle) stages a window of ncmax columns from fwd_cb.
+    // The spawn offset moves a planar ray's line sideways by at most its length
+    // (1 + max|p|) * RayEpsilon, max|p| = r on the vial wall (|p_z| <= 0.7 r here).
+    const double marg_u = 1.5 * (1.0 + (double)d.vial_r) * (double)TVAM_RAY_EPS * (double)d.res_x / (double)k.ex + 1e-3;
+    const float du = -(float)d.res_x / k.ex;
+    const float u0 = 0.5f * (float)d.res_x - 0.5f - (float)d.crop_offset_x;
+    std::vector<float4> fang(2 * (size_t)std::max(ns, 1));
     double wmax = 0.0;
-    for (int i = 0; i < ns; ++i)
-        wmax = std::max(wmax, 16.0 * ((double)k.h[0] * std::fabs((double)cs[i].y) +
-                                      (double)k.h[1] * std::fabs((double)cs[i].x)) * (double)d.res_x / (double)k.ex);
-    double rmax = std::max({std::fabs((double)k.bmin[0]), std::fabs((double)k.bmax[0]), std::fabs((double)k.bmin[1]),
-                            std::fabs((double)k.bmax[1]), (double)d.vial_r, (double)k.vial_half_h});
-    const double marg_u = 4.0 * (1.0 + rmax) * (double)TVAM_RAY_EPS * (double)d.res_x / (double)k.ex + 1e-3;
+    for (int i = 0; i < ns; ++i) {
+        const float c = cs[i].x, sn = cs[i].y, dxr = -c, dyr = -sn;
+        const int fl = (std::fabs(dxr) > 1e-8f ? 1 : 0) | (std::fabs(dyr) > 1e-8f ? 2 : 0);
+        const float w = 0.5f * (k.h[0] * std::fabs(sn) + k.h[1] * std::fabs(c)) * std::fabs(du) + (float)marg_u;
+        int32_t flb = fl;
+        float flf;
+        std::memcpy(&flf, &flb, sizeof(flf));
+        fang[2 * (size_t)i] = make_float4(sn * du, -c * du, 1.0f / dxr, 1.0f / dyr);
+        fang[2 * (size_t)i + 1] = make_float4(w, flf, 0.0f, 0.0f);
+        wmax = std::max(wmax, (double)w);
+    }
+    const int nc = (int)std::floor(2.0 * wmax + 1e-3) + 1;
+    const int ntx16 = (k.res[0] + 15) / 16, nty16 = (k.res[1] + 15) / 16;
+    std::vector<int32_t> fcb((size_t)ntx16 * nty16 * std::max(ns, 1));
+    int need = 0;
+    for (int t = 0; t < ntx16 * nty16; ++t) {
+        const int bx = t % ntx16, by = t / ntx16;
+        const double xc0 = (double)k.bmin[0] + (bx * 16 + 0.5) * k.h[0], xc1 = xc0 + 15.0 * k.h[0];
+        const double yc0 = (double)k.bmin[1] + (by * 16 + 0.5) * k.h[1], yc1 = yc0 + 15.0 * k.h[1];
+        for (int i = 0; i < ns; ++i) {
+            const double A = fang[2 * (size_t)i].x, B = fang[2 * (size_t)i].y, w = fang[2 * (size_t)i + 1].x;
+            const double uc[4] = {xc0 * A + yc0 * B, xc1 * A + yc0 * B, xc0 * A + yc1 * B, xc1 * A + yc1 * B};
+            const double umin = *std::min_element(uc, uc + 4) + u0, umax = *std::max_element(uc, uc + 4) + u0;
+            const int cb = (int)std::floor(umin - w) - 1;  // 1 column of slack for fp32 rounding in the kernel
+            fcb[(size_t)t * ns + i] = cb;
+            need = std::max(need, (int)std::ceil(umax - w) + 1 + nc - cb);
+        }
+    }
     p->pl.ns = ns;
     p->pl.marg_u = (float)marg_u;
-    p->pl.ncmax = (int32_t)std::ceil(wmax + 2.0 * marg_u + 0.01) + 4;
+    p->pl.u0 = u0;
+    p->pl.fwd_nc = nc;
+    p->pl.xcd_remap = env_int("TVAM_XCD_REMAP", 1);
+    p->pl.ncmax = need;
+    {
+        bool multi = false;
+        for (int z = 0; z < k.res[2]; ++z) multi |= off[z + 1] - off[z] > 1;
+        p->pl.fwd_multi = multi ? 1 : 0;
+    }
     p->pl.max_rows_chunk = mrc;
     p->pl.adj_pitch = p->tiles.tsx + 2 + std::max(0, env_int("TVAM_ADJ_PITCH_PAD", 0));
     while (p->planar_fz > 8 && !tvam_planar_fwd_fits(p->pl, p->planar_fz)) p->planar_fz /= 2;
+    p->pl.fwd_pf = (p->pl.ncmax * p->planar_fz + 255) / 256 <= 2 ? 2 : 4;
     if (!tvam_planar_fwd_fits(p->pl, p->planar_fz)) return 0;  // DMD much finer than the voxels: general path
     if (tvam_planar_adj_lds(p->pl, p->tiles, p->planar_az) > 160 * 1024) p->planar_az = 4;
     if (tvam_planar_adj_lds(p->pl, p->tiles, p->planar_az) > 160 * 1024) return 0;  // tile too large: general path
     int rc;
     const size_t nrec = (size_t)std::max(ns, 1) * d.crop_x;
     hipError_t e;
-    if ((rc = upload(&p->d_pl_slice_off, off)) || (rc = upload(&p->d_pl_slice_rows, rows))) return rc;
+    if ((rc = upload(&p->d_pl_slice_off, off)) || (rc = upload(&p->d_pl_slice_rows, rows)) ||
+        (rc = upload(&p->d_pl_fwd_ang, fang)) || (rc = upload(&p->d_pl_fwd_cb, fcb)))
+        return rc;
+    p->pl.fwd_ang = p->d_pl_fwd_ang;
+    p->pl.fwd_cb = p->d_pl_fwd_cb;
     if ((e = hipMalloc((void**)&p->d_pl_vox, nrec * sizeof(float4))) != hipSuccess ||
         (e = hipMalloc((void**)&p->d_pl_rec_f, nrec * sizeof(float4))) != hipSuccess ||
         (e = hipMalloc((void**)&p->d_pl_rec_i, nrec * sizeof(int32_t))) != hipSuccess)

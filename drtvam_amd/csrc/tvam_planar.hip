@@ -90,9 +90,16 @@ hipError_t tvam_launch_planar_rays(const TvamConsts& k, const TvamPlanar& pl, hi
 // in exact arithmetic), so the dose is the same sum of telescoped weights
 // the DDA forms, up to fp32 rounding of the crossing times.
 // ---------------------------------------------------------------------------
-#define TVAM_PF 4  // staged pattern values per thread and angle (host: ncmax * Z <= TVAM_PF * TVAM_PB)
+#define TVAM_PF 4     // most staged pattern values per thread and angle (host: ncmax * Z <= TVAM_PF * TVAM_PB)
+#define TVAM_ACH 256  // angles per LDS chunk of per-angle constants
+#ifndef TVAM_FWD_DEPTH
+#define TVAM_FWD_DEPTH 1  // angles of global-load look-ahead in the forward
+#endif
 
-template <int Z>
+// Z: slices per thread; NC: candidate DMD columns per (voxel, angle), a
+// bound the plan derives from the voxel's lateral width in columns; MULTI:
+// some slice collects several DMD rows; PF: staged values per thread.
+template <int Z, int NC, bool MULTI, int PF>
 __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, TvamPlanar pl,
                                                                   const float* __restrict__ pat,
                                                                   float* __restrict__ dose) {
@@ -103,23 +110,35 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
     constexpr int ZS = Z + 4;
     float* s_p = reinterpret_cast<float*>(smem);
     float4* s_r = reinterpret_cast<float4*>(s_p + 2 * ncm * ZS);  // [2][ncm]
-    int* s_row = reinterpret_cast<int*>(s_r + 2 * ncm);           // [Z]: the slice's row, -1 none, -2 several
+    // per-angle constants of TVAM_ACH (+2 look-ahead) angles, copied to LDS so the
+    // angle loop issues no scalar loads (an s_load's lgkmcnt wait would also
+    // drain every outstanding LDS read)
+    float4* s_ang = reinterpret_cast<float4*>(s_r + 2 * ncm);     // [TVAM_ACH + 2][2]
+    int* s_cb = reinterpret_cast<int*>(s_ang + 2 * (TVAM_ACH + 2)); // [TVAM_ACH + 2]
+    int* s_row = s_cb + (TVAM_ACH + 2);                            // [Z]: the slice's row, -1 none, -2 several
 
-    const int ntx = (k.res[0] + 15) >> 4;
-    const int bx = blockIdx.x % ntx, by = blockIdx.x / ntx;
+    const int ntx = (k.res[0] + 15) >> 4, nty = (k.res[1] + 15) >> 4;
+    const int ntiles = ntx * nty, nwg = ntiles * ((k.res[2] + Z - 1) / Z);
+    // XCD-aware order: workgroup b runs on XCD b % 8; give each XCD a contiguous
+    // run of (z-chunk, tile) pairs so the tiles sharing a z-chunk's pattern rows
+    // share that XCD's L2
+    int L = blockIdx.x;
+    if (pl.xcd_remap) {
+        const int per = (int)(gridDim.x >> 3);
+        L = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
+    }
+    if (L >= nwg) return;
+    const int tile = L % ntiles;
+    const int bx = tile % ntx, by = tile / ntx;
     const int ix = bx * 16 + (threadIdx.x & 15), iy = by * 16 + (threadIdx.x >> 4);
-    const int z0 = blockIdx.y * Z;
+    const int z0 = (L / ntiles) * Z;
     const float hx = k.h[0], hy = k.h[1];
     // voxel edges exactly as the DDA places them (bmin + i * h, sensor.py:357)
     const float X0 = k.bmin[0] + (float)ix * hx, X1 = k.bmin[0] + (float)(ix + 1) * hx;
     const float Y0 = k.bmin[1] + (float)iy * hy, Y1 = k.bmin[1] + (float)(iy + 1) * hy;
     const float Xc = k.bmin[0] + ((float)ix + 0.5f) * hx, Yc = k.bmin[1] + ((float)iy + 0.5f) * hy;
-    // tile corners for the column window
-    const float TX0 = k.bmin[0] + (float)(bx * 16) * hx, TX1 = k.bmin[0] + (float)(bx * 16 + 16) * hx;
-    const float TY0 = k.bmin[1] + (float)(by * 16) * hy, TY1 = k.bmin[1] + (float)(by * 16 + 16) * hy;
-    // lateral coordinate l -> fractional crop column u = W (0.5 - l / ex) - 0.5 - crop_off (common.py:96-99)
-    const float Wd = (float)k.res_x;
-    const float du = -Wd / k.ex, u0 = 0.5f * Wd - 0.5f - (float)k.crop_off_x;
+    const float u0 = pl.u0;
+    const int32_t* cbt = pl.fwd_cb + (size_t)tile * pl.ns;  // first window column per angle
 
     if (threadIdx.x < Z) {
         const int s = z0 + threadIdx.x;
@@ -130,22 +149,27 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
         }
         s_row[threadIdx.x] = r;
     }
+    const int ns = pl.ns;
+    int tbase = 0;
+    auto load_table = [&](int base) {
+        for (int i = threadIdx.x; i < TVAM_ACH + 2; i += TVAM_PB) {
+            const int a = base + i;
+            if (a < ns) {
+                s_ang[2 * i] = pl.fwd_ang[2 * a];
+                s_ang[2 * i + 1] = pl.fwd_ang[2 * a + 1];
+                s_cb[i] = cbt[a];
+            }
+        }
+    };
+    load_table(0);
     __syncthreads();
 
-    // first DMD column of the window whose rays can cross the tile at angle al
-    auto window = [&](int al) -> int {
-        const float2 csv = pl.cs[al];
-        const float l00 = TX0 * csv.y - TY0 * csv.x, l10 = TX1 * csv.y - TY0 * csv.x;
-        const float l01 = TX0 * csv.y - TY1 * csv.x, l11 = TX1 * csv.y - TY1 * csv.x;
-        const float lmax = fmaxf(fmaxf(l00, l10), fmaxf(l01, l11));
-        return (int)floorf(fmaf(lmax, du, u0) - pl.marg_u) - 1;  // u decreases with l
-    };
     // This thread's staging slots i = tid + q * 256 of the [Z][ncm] slab are
-    // angle-independent: slice z, window column jj, the slice's row offset
-    // (or -2 - z when several rows share the slice) and the LDS offset.
-    int st_jj[TVAM_PF], st_row[TVAM_PF], st_off[TVAM_PF];
+    // angle-independent: window column jj, the slice's row offset (or -2 - z
+    // when several rows share the slice) and the LDS offset.
+    int st_jj[PF], st_row[PF], st_off[PF];
 #pragma unroll
-    for (int q = 0; q < TVAM_PF; ++q) {
+    for (int q = 0; q < PF; ++q) {
         const int i = threadIdx.x + q * TVAM_PB;
         st_jj[q] = -1;
         st_row[q] = -1;
@@ -159,105 +183,137 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
         }
     }
     // global loads of angle al's slab (slice-binned pattern + ray table) into registers
-    float pv[TVAM_PF];
-    float4 rv;
-    auto fetch = [&](int al, int cb) {
+    struct Stage {
+        float pv[PF];
+        float4 rv;
+    };
+    auto fetch = [&](int al, Stage& S) {
+        const int cb = s_cb[al - tbase];
         const float* pa = pat + (size_t)al * k.crop_y * k.crop_x;
 #pragma unroll
-        for (int q = 0; q < TVAM_PF; ++q) {
+        for (int q = 0; q < PF; ++q) {
             const int col = cb + st_jj[q], r = st_row[q];
             float v = 0.0f;
-            if (st_jj[q] >= 0 && col >= 0 && col < k.crop_x && r != -1) {
-                if (r >= 0) v = pa[r + col];
+            const bool in = st_jj[q] >= 0 && (unsigned)col < (unsigned)k.crop_x;
+            if (!MULTI) {
+                if (in && r >= 0) v = pa[(unsigned)(r + col)];
+            } else if (in && r != -1) {
+                if (r >= 0) v = pa[(unsigned)(r + col)];
                 else {
                     const int z = -2 - r;
                     for (int t = pl.slice_off[z0 + z]; t < pl.slice_off[z0 + z + 1]; ++t)
                         v += pa[(size_t)pl.slice_rows[t] * k.crop_x + col];
                 }
             }
-            pv[q] = v;
+            S.pv[q] = v;
         }
         const int col = cb + (int)threadIdx.x;
-        rv = make_float4(0.0f, 0.0f, -1.0f, 0.0f);
-        if ((int)threadIdx.x < ncm && col >= 0 && col < k.crop_x) rv = pl.vox[(size_t)al * k.crop_x + col];
+        S.rv = make_float4(0.0f, 0.0f, -1.0f, 0.0f);
+        if ((int)threadIdx.x < ncm && (unsigned)col < (unsigned)k.crop_x) S.rv = pl.vox[(size_t)al * k.crop_x + col];
     };
-    auto store = [&](int buf) {
+    auto store = [&](int buf, const Stage& S) {
         float* sp = s_p + buf * ncm * ZS;
 #pragma unroll
-        for (int q = 0; q < TVAM_PF; ++q)
-            if (st_jj[q] >= 0) sp[st_off[q]] = pv[q];
-        if ((int)threadIdx.x < ncm) s_r[buf * ncm + threadIdx.x] = rv;
+        for (int q = 0; q < PF; ++q)
+            if (st_jj[q] >= 0) sp[st_off[q]] = S.pv[q];
+        if ((int)threadIdx.x < ncm) s_r[buf * ncm + threadIdx.x] = S.rv;
     };
 
     float acc[Z];
 #pragma unroll
     for (int z = 0; z < Z; ++z) acc[z] = 0.0f;
 
-    int cb = window(0);
-    fetch(0, cb);
-    store(0);
-    __syncthreads();
-    for (int al = 0; al < pl.ns; ++al) {
-        const int buf = al & 1;
-        int cb_next = 0;
-        if (al + 1 < pl.ns) {  // prefetch the next angle while this one is computed
-            cb_next = window(al + 1);
-            fetch(al + 1, cb_next);
-        }
-        const float2 csv = pl.cs[al];
-        const float c = csv.x, s = csv.y;
+    auto compute = [&](int al, int buf) {
+        const int cb = s_cb[al - tbase];
         const float* sp = s_p + buf * ncm * ZS;
         const float4* sr = s_r + buf * ncm;
+        // per-angle constants {s*du, -c*du, 1/d.x, 1/d.y}, {half width in columns, axis flags}
+        const float4 g0 = s_ang[2 * (al - tbase)], g1 = s_ang[2 * (al - tbase) + 1];
+        const int fl = __float_as_int(g1.y);
 
-        // this voxel's candidate columns: rays whose lateral line meets [l - w, l + w]
-        const float dxr = -c, dyr = -s;
-        const bool vx = fabsf(dxr) > 1e-8f, vy = fabsf(dyr) > 1e-8f;
-        const float idx = 1.0f / dxr, idy = 1.0f / dyr;
-        const float l = Xc * s - Yc * c;
-        // the vial-entry spawn offset moves a ray's line by up to (1 + max|p|) * RayEpsilon
-        // sideways (geometry.py:75-96, volume.py:191): margin pl.marg_u
-        const float w = 0.5f * (hx * fabsf(s) + hy * fabsf(c)) * fabsf(du) + pl.marg_u;
-        const float u = fmaf(l, du, u0);
-        const int j0 = max((int)ceilf(u - w), cb), j1 = min((int)floorf(u + w), cb + ncm - 1);
-        for (int j = j0; j <= j1; ++j) {
-            const int jj = j - cb;
-            const float4 q = sr[jj];
-            float tnx, tfx, tny, tfy;
-            if (vx) {
-                const float a = fmaf(X0, idx, q.x), b = fmaf(X1, idx, q.x);
-                tnx = fminf(a, b);
-                tfx = fmaxf(a, b);
-            } else {
+        // candidate columns: the rays whose lateral line meets the voxel's lateral extent
+        const float u = fmaf(Xc, g0.x, fmaf(Yc, g0.y, u0));
+        int jj0 = (int)ceilf(u - g1.x) - cb;
+        jj0 = min(max(jj0, 0), ncm - NC);
+        // crossing times of the voxel's x / y edges relative to the ray's o2 (+ q.x / q.y)
+        const float xa = X0 * g0.z, xb = X1 * g0.z, ya = Y0 * g0.w, yb = Y1 * g0.w;
+        const float xn = fminf(xa, xb), xf = fmaxf(xa, xb), yn = fminf(ya, yb), yf = fmaxf(ya, yb);
+        float wgt[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            float4 q = sr[jj0 + c];
+            asm volatile("" : "+v"(q.w));  // keep the 16-byte LDS read (ds_read_b128, not b96)
+            float tnx = xn + q.x, tfx = xf + q.x, tny = yn + q.y, tfy = yf + q.y;
+            if (!(fl & 1)) {  // |d.x| <= 1e-8: the DDA never steps x (q.x = its voxel index)
                 tnx = (float)ix == q.x ? -TVAM_INF : TVAM_INF;
                 tfx = TVAM_INF;
             }
-            if (vy) {
-                const float a = fmaf(Y0, idy, q.y), b = fmaf(Y1, idy, q.y);
-                tny = fminf(a, b);
-                tfy = fmaxf(a, b);
-            } else {
+            if (!(fl & 2)) {
                 tny = (float)iy == q.y ? -TVAM_INF : TVAM_INF;
                 tfy = TVAM_INF;
             }
             const float tin = fmaxf(fmaxf(tnx, tny), 0.0f);
             const float tout = fminf(fminf(tfx, tfy), q.z);
-            if (tout > tin) {
-                const float wgt = pl_exp2(k.nsig2 * tin) - pl_exp2(k.nsig2 * tout);
-                const float4* pz = reinterpret_cast<const float4*>(sp + jj * ZS);
+            const float e = pl_exp2(k.nsig2 * tin) - pl_exp2(k.nsig2 * tout);
+            wgt[c] = tout > tin ? e : 0.0f;
+        }
 #pragma unroll
-                for (int z4 = 0; z4 < Z / 4; ++z4) {
-                    const float4 p4 = pz[z4];
-                    acc[4 * z4 + 0] = fmaf(wgt, p4.x, acc[4 * z4 + 0]);
-                    acc[4 * z4 + 1] = fmaf(wgt, p4.y, acc[4 * z4 + 1]);
-                    acc[4 * z4 + 2] = fmaf(wgt, p4.z, acc[4 * z4 + 2]);
-                    acc[4 * z4 + 3] = fmaf(wgt, p4.w, acc[4 * z4 + 3]);
-                }
+        for (int z4 = 0; z4 < Z / 4; ++z4) {
+#pragma unroll
+            for (int c = 0; c < NC; ++c) {
+                const float4 p4 = reinterpret_cast<const float4*>(sp + (jj0 + c) * ZS)[z4];
+                acc[4 * z4 + 0] = fmaf(wgt[c], p4.x, acc[4 * z4 + 0]);
+                acc[4 * z4 + 1] = fmaf(wgt[c], p4.y, acc[4 * z4 + 1]);
+                acc[4 * z4 + 2] = fmaf(wgt[c], p4.z, acc[4 * z4 + 2]);
+                acc[4 * z4 + 3] = fmaf(wgt[c], p4.w, acc[4 * z4 + 3]);
             }
         }
-        if (al + 1 < pl.ns) store(buf ^ 1);
-        cb = cb_next;
+    };
+
+#if TVAM_FWD_DEPTH == 2
+    // Software pipeline over angles: angle a is computed from LDS buffer a & 1
+    // while the loads of angle a + 1 (issued one step earlier) and a + 2 are in
+    // flight in the register stages SB / SA.
+    Stage SA, SB;
+    fetch(0, SA);
+    store(0, SA);
+    if (ns > 1) fetch(1, SB);
+    __syncthreads();
+    for (int al = 0; al < ns; al += 2) {
+        if (al > 0 && (al & (TVAM_ACH - 1)) == 0) {  // next chunk of per-angle constants
+            tbase = al;
+            load_table(al);
+            __syncthreads();
+        }
+        if (al + 2 < ns) fetch(al + 2, SA);
+        compute(al, 0);
+        if (al + 1 < ns) store(1, SB);
+        __syncthreads();
+        if (al + 1 >= ns) break;
+        if (al + 3 < ns) fetch(al + 3, SB);
+        compute(al + 1, 1);
+        if (al + 2 < ns) store(0, SA);
         __syncthreads();
     }
+#else
+    // Software pipeline over angles: angle a is computed from LDS buffer a & 1
+    // while the loads of angle a + 1 are in flight in registers.
+    Stage S;
+    fetch(0, S);
+    store(0, S);
+    __syncthreads();
+    for (int al = 0; al < ns; ++al) {
+        if (al > 0 && (al & (TVAM_ACH - 1)) == 0) {  // next chunk of per-angle constants
+            tbase = al;
+            load_table(al);
+            __syncthreads();
+        }
+        if (al + 1 < ns) fetch(al + 1, S);
+        compute(al, al & 1);
+        if (al + 1 < ns) store((al + 1) & 1, S);
+        __syncthreads();
+    }
+#endif
 
     if (ix < k.res[0] && iy < k.res[1]) {
         const float scale = k.wscale * k.inv_vol;  // Le * weight (common.py:108-111) / voxel volume (volume.py:41-42)
@@ -269,30 +325,51 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
 }
 
 size_t tvam_planar_fwd_lds(const TvamPlanar& pl, int Z) {
-    return 2 * ((size_t)pl.ncmax * (Z + 4) * sizeof(float) + (size_t)pl.ncmax * sizeof(float4)) + (size_t)Z * sizeof(int);
+    return 2 * ((size_t)pl.ncmax * (Z + 4) * sizeof(float) + (size_t)pl.ncmax * sizeof(float4)) +
+           (size_t)(TVAM_ACH + 2) * (2 * sizeof(float4) + sizeof(int)) + (size_t)Z * sizeof(int);
 }
 
-bool tvam_planar_fwd_fits(const TvamPlanar& pl, int Z) { return pl.ncmax <= TVAM_PB && pl.ncmax * Z <= TVAM_PF * TVAM_PB; }
+bool tvam_planar_fwd_fits(const TvamPlanar& pl, int Z) {
+    return pl.ncmax <= TVAM_PB && pl.ncmax * Z <= TVAM_PF * TVAM_PB && pl.fwd_nc >= 1 && pl.fwd_nc <= 4 &&
+           pl.fwd_nc <= pl.ncmax;
+}
+
+template <int Z, int NC>
+static void launch_fwd(dim3 grid, size_t lds, hipStream_t stream, const TvamConsts& k, const TvamPlanar& pl,
+                       const float* pat, float* dose) {
+    if (pl.fwd_multi)
+        hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, true, 4>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
+    else if (pl.fwd_pf == 2)
+        hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 2>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
+    else
+        hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 4>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
+}
+
+template <int Z>
+static hipError_t launch_fwd_z(dim3 grid, size_t lds, hipStream_t stream, const TvamConsts& k, const TvamPlanar& pl,
+                               const float* pat, float* dose) {
+    switch (pl.fwd_nc) {
+        case 1:
+        case 2: launch_fwd<Z, 2>(grid, lds, stream, k, pl, pat, dose); break;
+        case 3: launch_fwd<Z, 3>(grid, lds, stream, k, pl, pat, dose); break;
+        case 4: launch_fwd<Z, 4>(grid, lds, stream, k, pl, pat, dose); break;
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
 
 hipError_t tvam_launch_fwd_planar(const TvamConsts& k, const TvamPlanar& pl, int Z, const float* pat, float* dose,
                                   hipStream_t stream) {
     const int ntx = (k.res[0] + 15) / 16, nty = (k.res[1] + 15) / 16;
-    dim3 grid((unsigned)(ntx * nty), (unsigned)((k.res[2] + Z - 1) / Z));
+    const unsigned nwg = (unsigned)(ntx * nty) * (unsigned)((k.res[2] + Z - 1) / Z);
+    dim3 grid(pl.xcd_remap ? (nwg + 7) / 8 * 8 : nwg);
     const size_t lds = tvam_planar_fwd_lds(pl, Z);
     switch (Z) {
-        case 8:
-            hipLaunchKernelGGL(tvam_fwd_planar_kernel<8>, grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
-            break;
-        case 16:
-            hipLaunchKernelGGL(tvam_fwd_planar_kernel<16>, grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
-            break;
-        case 32:
-            hipLaunchKernelGGL(tvam_fwd_planar_kernel<32>, grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
-            break;
-        default:
-            return hipErrorInvalidValue;
+        case 8: return launch_fwd_z<8>(grid, lds, stream, k, pl, pat, dose);
+        case 16: return launch_fwd_z<16>(grid, lds, stream, k, pl, pat, dose);
+        case 32: return launch_fwd_z<32>(grid, lds, stream, k, pl, pat, dose);
+        default: return hipErrorInvalidValue;
     }
-    return hipGetLastError();
 }
 
 // ---------------------------------------------------------------------------
@@ -309,9 +386,9 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_adj_planar_kernel(TvamConsts k, 
                                                                   const float* __restrict__ gin,
                                                                   float* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    float* tile = reinterpret_cast<float*>(smem);
     const int tsx = tp.tsx, tsy = tp.tsy;
     const int tw = pl.adj_pitch, th = tsy + 2;  // row pitch >= tsx + 2 (padded against bank conflicts)
+    float* tile = reinterpret_cast<float*>(smem);
     int* s_roff = reinterpret_cast<int*>(tile + (size_t)tw * th * Z);  // [Z + 1] CSR of the chunk's rows
     int* s_rows = s_roff + Z + 1;                                       // [pl.max_rows_chunk]
 
