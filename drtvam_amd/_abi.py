@@ -28,6 +28,7 @@ SENSOR_DDA = 0
 FLAG_NO_ZERO_SKIP = 1
 FLAG_FWD_STATS = 2
 FLAG_NO_PLANAR = 4
+LBFGS_WORK_DOUBLES = 512 * 64
 
 
 class TvamDesc(ctypes.Structure):
@@ -91,6 +92,11 @@ EXPORTS = {
     "tvam_plan_destroy": (None, [_P]),
     "tvam_forward": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _P, _P]),
     "tvam_adjoint": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _P, _P]),
+    "tvam_lbfgs_history": (ctypes.c_int, [ctypes.c_uint64, _P, _P, _P, _P, ctypes.c_int32, _P, _P, _P, _P, _P, _P,
+                                          _P]),
+    "tvam_lbfgs_direction": (ctypes.c_int, [ctypes.c_uint64, _P, ctypes.c_int32, _P, _P, ctypes.c_float, _P, _P, _P,
+                                            _P]),
+    "tvam_axpy_clamp": (ctypes.c_int, [ctypes.c_uint64, _P, ctypes.c_float, _P, ctypes.c_float, _P, _P]),
     "tvam_plan_path": (ctypes.c_int, [_P]),
     "tvam_count_visits": (ctypes.c_int, [_P, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]),
     "tvam_plan_stats": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),

@@ -73,3 +73,13 @@ hipError_t tvam_launch_loss_threshold(const float* dose, const float* ddose, flo
                                       const float* target, uint64_t n, int K, float tl, float tu,
                                       float w_object, float w_void, float w_limit, float scale,
                                       double* out, float* grad, hipStream_t stream);
+
+// Fused L-BFGS vector kernels (tvam_vec.hip).
+hipError_t tvam_launch_lbfgs_history(uint64_t n, const float* p, const float* p_old, const float* g,
+                                     const float* g_old, int h, const float* const* S, const float* const* Y,
+                                     float* s_new, float* y_new, double* work, double* dots, hipStream_t stream);
+hipError_t tvam_launch_lbfgs_direction(uint64_t n, const float* g, int h, const float* const* S,
+                                       const float* const* Y, float cg, const float* cs, const float* cy, float* d,
+                                       hipStream_t stream);
+hipError_t tvam_launch_axpy_clamp(uint64_t n, const float* p, float alpha, const float* d, float lo, float* out,
+                                  hipStream_t stream);

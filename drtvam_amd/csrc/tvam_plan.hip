@@ -718,3 +718,41 @@ extern "C" int tvam_loss_threshold(const float* dose, const float* ddose, float 
                                               out, grad, (hipStream_t)stream);
     return e == hipSuccess ? 0 : hip_fail(e, "loss launch");
 }
+
+static bool aligned16(const void* q) { return ((uintptr_t)q & 15u) == 0; }
+
+extern "C" int tvam_lbfgs_history(uint64_t n, const float* p, const float* p_old, const float* g, const float* g_old,
+                                  int32_t h, const float* const* S, const float* const* Y, float* s_new,
+                                  float* y_new, double* work, double* dots, void* stream) {
+    if (!g || !work || !dots || (h > 0 && (!S || !Y))) return fail(TVAM_ERR_INVALID, "null argument");
+    if (h < 0 || h > 7) return fail(TVAM_ERR_INVALID, "tvam_lbfgs_history: 0 <= h <= 7 retained pairs");
+    if (p_old && (!p || !g_old || !s_new || !y_new)) return fail(TVAM_ERR_INVALID, "null argument");
+    bool ok = aligned16(g) && (!p_old || (aligned16(p) && aligned16(p_old) && aligned16(g_old) &&
+                                          aligned16(s_new) && aligned16(y_new)));
+    for (int j = 0; j < h; ++j) ok = ok && S[j] && Y[j] && aligned16(S[j]) && aligned16(Y[j]);
+    if (!ok) return fail(TVAM_ERR_INVALID, "tvam_lbfgs_history: vectors must be 16-byte aligned");
+    hipError_t e = tvam_launch_lbfgs_history(n, p, p_old, g, g_old, h, S, Y, s_new, y_new, work, dots,
+                                             (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "lbfgs history launch");
+}
+
+extern "C" int tvam_lbfgs_direction(uint64_t n, const float* g, int32_t h, const float* const* S,
+                                    const float* const* Y, float cg, const float* cs, const float* cy, float* d,
+                                    void* stream) {
+    if (!g || !d || (h > 0 && (!S || !Y || !cs || !cy))) return fail(TVAM_ERR_INVALID, "null argument");
+    if (h < 0 || h > 8) return fail(TVAM_ERR_INVALID, "tvam_lbfgs_direction: 0 <= h <= 8 pairs");
+    bool ok = aligned16(g) && aligned16(d);
+    for (int j = 0; j < h; ++j) ok = ok && S[j] && Y[j] && aligned16(S[j]) && aligned16(Y[j]);
+    if (!ok) return fail(TVAM_ERR_INVALID, "tvam_lbfgs_direction: vectors must be 16-byte aligned");
+    hipError_t e = tvam_launch_lbfgs_direction(n, g, h, S, Y, cg, cs, cy, d, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "lbfgs direction launch");
+}
+
+extern "C" int tvam_axpy_clamp(uint64_t n, const float* p, float alpha, const float* d, float lo, float* out,
+                               void* stream) {
+    if (!p || !d || !out) return fail(TVAM_ERR_INVALID, "null argument");
+    if (!aligned16(p) || !aligned16(d) || !aligned16(out))
+        return fail(TVAM_ERR_INVALID, "tvam_axpy_clamp: vectors must be 16-byte aligned");
+    hipError_t e = tvam_launch_axpy_clamp(n, p, alpha, d, lo, out, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "axpy launch");
+}

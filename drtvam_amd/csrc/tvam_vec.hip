@@ -1,0 +1,273 @@
+// tvam_vec.hip — fused vector kernels of the linear L-BFGS step
+// (lbfgs.py:146-275 of the reference, restated in drtvam_amd/lbfgs.py).
+//
+// The two-loop recursion only ever needs dot products between the current
+// gradient g and the history pairs (s_i, y_i); written in terms of the Gram
+// entries s_i.y_j, y_i.y_j, s_i.g, y_i.g, g.g it becomes scalar work, and the
+// search direction is one linear combination of g, s_i, y_i.  So one step
+// touches the n-vectors in three passes instead of ~4m + 10:
+//   tvam_lbfgs_history   : s_new = p - p_old, y_new = g - g_old and every dot
+//                          the recursion needs, in one read of p, p_old, g,
+//                          g_old and the retained history;
+//   tvam_lbfgs_direction : d = cg g + sum cs_j s_j + sum cy_j y_j;
+//   tvam_axpy_clamp      : p_new = max(p + alpha d, lo) (update + clamp,
+//                          optimize.py:316-318).
+// Dot products accumulate in fp64 per thread, then per block, then over a
+// fixed number of blocks in a fixed order (deterministic).
+#include "tvam_internal.h"
+
+#define TVAM_VB 256       // threads per block
+#define TVAM_VGRID 512    // blocks of the reduction kernels (work[] holds TVAM_VGRID * ndots doubles)
+#define TVAM_HMAX 8
+
+struct VecPtrs {
+    const float* s[TVAM_HMAX];
+    const float* y[TVAM_HMAX];
+};
+
+__device__ __forceinline__ double warp_sum(double v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+
+// Block-reduce ND accumulators and write this block's partials.
+template <int ND>
+__device__ __forceinline__ void block_partials(double (&acc)[ND], double* __restrict__ work) {
+    __shared__ double red[TVAM_VB / 64][ND > 0 ? ND : 1];
+#pragma unroll
+    for (int d = 0; d < ND; ++d) {
+        const double v = warp_sum(acc[d]);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6][d] = v;
+    }
+    __syncthreads();
+    for (int d = threadIdx.x; d < ND; d += TVAM_VB) {
+        double s = 0.0;
+        for (int w = 0; w < TVAM_VB / 64; ++w) s += red[w][d];
+        work[(size_t)blockIdx.x * ND + d] = s;
+    }
+}
+
+// Dots written (H = retained pairs, NEW = a new pair is formed; index j runs
+// over the retained pairs, then the new one):
+//   [0, HT)        s_j . g          HT = H + NEW
+//   [HT, 2HT)      y_j . g
+//   if NEW:
+//   [2HT, 3HT)     s_new . y_j
+//   [3HT, 4HT)     s_j . y_new
+//   [4HT, 5HT)     y_new . y_j
+//   last           g . g
+template <int H, bool NEW>
+struct HistLayout {
+    static constexpr int HT = H + (NEW ? 1 : 0);
+    static constexpr int ND = (NEW ? 5 * HT : 2 * HT) + 1;
+};
+
+template <int H, bool NEW>
+__global__ __launch_bounds__(TVAM_VB) void tvam_lbfgs_hist_kernel(uint64_t n, const float* __restrict__ p,
+                                                                   const float* __restrict__ p_old,
+                                                                   const float* __restrict__ g,
+                                                                   const float* __restrict__ g_old, VecPtrs hv,
+                                                                   float* __restrict__ s_new,
+                                                                   float* __restrict__ y_new,
+                                                                   double* __restrict__ work) {
+    using L = HistLayout<H, NEW>;
+    constexpr int HT = L::HT, ND = L::ND;
+    double acc[ND];
+#pragma unroll
+    for (int d = 0; d < ND; ++d) acc[d] = 0.0;
+
+    auto visit = [&](float pv, float pov, float gv, float gov, const float (&sv)[TVAM_HMAX],
+                     const float (&yv)[TVAM_HMAX], float& sn, float& yn) {
+        sn = NEW ? pv - pov : 0.0f;
+        yn = NEW ? gv - gov : 0.0f;
+#pragma unroll
+        for (int j = 0; j < HT; ++j) {
+            const float sj = j < H ? sv[j] : sn, yj = j < H ? yv[j] : yn;
+            acc[j] = fma((double)sj, (double)gv, acc[j]);
+            acc[HT + j] = fma((double)yj, (double)gv, acc[HT + j]);
+            if (NEW) {
+                acc[2 * HT + j] = fma((double)sn, (double)yj, acc[2 * HT + j]);
+                acc[3 * HT + j] = fma((double)sj, (double)yn, acc[3 * HT + j]);
+                acc[4 * HT + j] = fma((double)yn, (double)yj, acc[4 * HT + j]);
+            }
+        }
+        acc[ND - 1] = fma((double)gv, (double)gv, acc[ND - 1]);
+    };
+
+    const uint64_t n4 = n / 4, stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint64_t i = tid; i < n4; i += stride) {
+        const float4 g4 = reinterpret_cast<const float4*>(g)[i];
+        float4 p4 = make_float4(0, 0, 0, 0), po4 = p4, go4 = p4;
+        if (NEW) {
+            p4 = reinterpret_cast<const float4*>(p)[i];
+            po4 = reinterpret_cast<const float4*>(p_old)[i];
+            go4 = reinterpret_cast<const float4*>(g_old)[i];
+        }
+        float4 s4[TVAM_HMAX], y4[TVAM_HMAX];
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+            s4[j] = reinterpret_cast<const float4*>(hv.s[j])[i];
+            y4[j] = reinterpret_cast<const float4*>(hv.y[j])[i];
+        }
+        float sv[TVAM_HMAX], yv[TVAM_HMAX];
+        float4 sn4, yn4;
+#define TVAM_LANE(c)                                                    \
+        _Pragma("unroll") for (int j = 0; j < H; ++j) {                 \
+            sv[j] = s4[j].c;                                            \
+            yv[j] = y4[j].c;                                            \
+        }                                                               \
+        visit(p4.c, po4.c, g4.c, go4.c, sv, yv, sn4.c, yn4.c);
+        TVAM_LANE(x) TVAM_LANE(y) TVAM_LANE(z) TVAM_LANE(w)
+#undef TVAM_LANE
+        if (NEW) {
+            reinterpret_cast<float4*>(s_new)[i] = sn4;
+            reinterpret_cast<float4*>(y_new)[i] = yn4;
+        }
+    }
+    for (uint64_t i = 4 * n4 + tid; i < n; i += stride) {  // tail
+        float sv[TVAM_HMAX], yv[TVAM_HMAX];
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+            sv[j] = hv.s[j][i];
+            yv[j] = hv.y[j][i];
+        }
+        float sn, yn;
+        visit(NEW ? p[i] : 0.0f, NEW ? p_old[i] : 0.0f, g[i], NEW ? g_old[i] : 0.0f, sv, yv, sn, yn);
+        if (NEW) {
+            s_new[i] = sn;
+            y_new[i] = yn;
+        }
+    }
+    block_partials<ND>(acc, work);
+}
+
+// Sum the per-block partials of dot d over the blocks, in block order.
+__global__ __launch_bounds__(TVAM_VB) void tvam_partials_kernel(int nd, const double* __restrict__ work,
+                                                                double* __restrict__ dots) {
+    __shared__ double red[TVAM_VB / 64];
+    const int d = blockIdx.x;
+    double s = 0.0;
+    for (int b = threadIdx.x; b < TVAM_VGRID; b += TVAM_VB) s += work[(size_t)b * nd + d];
+    s = warp_sum(s);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = 0.0;
+        for (int w = 0; w < TVAM_VB / 64; ++w) t += red[w];
+        dots[d] = t;
+    }
+}
+
+template <int H, bool NEW>
+static hipError_t launch_hist(uint64_t n, const float* p, const float* p_old, const float* g, const float* g_old,
+                              const VecPtrs& hv, float* s_new, float* y_new, double* work, double* dots,
+                              hipStream_t stream) {
+    hipLaunchKernelGGL((tvam_lbfgs_hist_kernel<H, NEW>), dim3(TVAM_VGRID), dim3(TVAM_VB), 0, stream, n, p, p_old, g,
+                       g_old, hv, s_new, y_new, work);
+    hipLaunchKernelGGL(tvam_partials_kernel, dim3(HistLayout<H, NEW>::ND), dim3(TVAM_VB), 0, stream,
+                       HistLayout<H, NEW>::ND, work, dots);
+    return hipGetLastError();
+}
+
+template <bool NEW>
+static hipError_t dispatch_hist(int h, uint64_t n, const float* p, const float* p_old, const float* g,
+                                const float* g_old, const VecPtrs& hv, float* s_new, float* y_new, double* work,
+                                double* dots, hipStream_t stream) {
+    switch (h) {
+#define TVAM_H(H) \
+    case H: return launch_hist<H, NEW>(n, p, p_old, g, g_old, hv, s_new, y_new, work, dots, stream);
+        TVAM_H(0) TVAM_H(1) TVAM_H(2) TVAM_H(3) TVAM_H(4) TVAM_H(5) TVAM_H(6) TVAM_H(7)
+#undef TVAM_H
+        default: return hipErrorInvalidValue;
+    }
+}
+
+hipError_t tvam_launch_lbfgs_history(uint64_t n, const float* p, const float* p_old, const float* g,
+                                     const float* g_old, int h, const float* const* S, const float* const* Y,
+                                     float* s_new, float* y_new, double* work, double* dots, hipStream_t stream) {
+    VecPtrs hv{};
+    for (int j = 0; j < h; ++j) {
+        hv.s[j] = S[j];
+        hv.y[j] = Y[j];
+    }
+    if (p_old) return dispatch_hist<true>(h, n, p, p_old, g, g_old, hv, s_new, y_new, work, dots, stream);
+    return dispatch_hist<false>(h, n, p, p_old, g, g_old, hv, s_new, y_new, work, dots, stream);
+}
+
+// ---------------------------------------------------------------------------
+struct DirCoef {
+    float cg;
+    float cs[TVAM_HMAX], cy[TVAM_HMAX];
+};
+
+template <int H>
+__global__ __launch_bounds__(TVAM_VB) void tvam_lbfgs_dir_kernel(uint64_t n, const float* __restrict__ g, VecPtrs hv,
+                                                                  DirCoef c, float* __restrict__ d) {
+    const uint64_t n4 = n / 4, stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint64_t i = tid; i < n4; i += stride) {
+        const float4 g4 = reinterpret_cast<const float4*>(g)[i];
+        float4 r = make_float4(c.cg * g4.x, c.cg * g4.y, c.cg * g4.z, c.cg * g4.w);
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+            const float4 s4 = reinterpret_cast<const float4*>(hv.s[j])[i];
+            const float4 y4 = reinterpret_cast<const float4*>(hv.y[j])[i];
+            r.x = fmaf(c.cs[j], s4.x, fmaf(c.cy[j], y4.x, r.x));
+            r.y = fmaf(c.cs[j], s4.y, fmaf(c.cy[j], y4.y, r.y));
+            r.z = fmaf(c.cs[j], s4.z, fmaf(c.cy[j], y4.z, r.z));
+            r.w = fmaf(c.cs[j], s4.w, fmaf(c.cy[j], y4.w, r.w));
+        }
+        reinterpret_cast<float4*>(d)[i] = r;
+    }
+    for (uint64_t i = 4 * n4 + tid; i < n; i += stride) {
+        float r = c.cg * g[i];
+#pragma unroll
+        for (int j = 0; j < H; ++j) r = fmaf(c.cs[j], hv.s[j][i], fmaf(c.cy[j], hv.y[j][i], r));
+        d[i] = r;
+    }
+}
+
+hipError_t tvam_launch_lbfgs_direction(uint64_t n, const float* g, int h, const float* const* S,
+                                       const float* const* Y, float cg, const float* cs, const float* cy, float* d,
+                                       hipStream_t stream) {
+    VecPtrs hv{};
+    DirCoef c{};
+    c.cg = cg;
+    for (int j = 0; j < h; ++j) {
+        hv.s[j] = S[j];
+        hv.y[j] = Y[j];
+        c.cs[j] = cs[j];
+        c.cy[j] = cy[j];
+    }
+    const dim3 grid(2048), block(TVAM_VB);
+    switch (h) {
+#define TVAM_H(H) \
+    case H: hipLaunchKernelGGL(tvam_lbfgs_dir_kernel<H>, grid, block, 0, stream, n, g, hv, c, d); break;
+        TVAM_H(0) TVAM_H(1) TVAM_H(2) TVAM_H(3) TVAM_H(4) TVAM_H(5) TVAM_H(6) TVAM_H(7) TVAM_H(8)
+#undef TVAM_H
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(TVAM_VB) void tvam_axpy_clamp_kernel(uint64_t n, const float* __restrict__ p, float alpha,
+                                                                  const float* __restrict__ d, float lo,
+                                                                  float* __restrict__ out) {
+    const uint64_t n4 = n / 4, stride = (uint64_t)gridDim.x * blockDim.x;
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    for (uint64_t i = tid; i < n4; i += stride) {
+        const float4 p4 = reinterpret_cast<const float4*>(p)[i];
+        const float4 d4 = reinterpret_cast<const float4*>(d)[i];
+        reinterpret_cast<float4*>(out)[i] = make_float4(fmaxf(fmaf(alpha, d4.x, p4.x), lo), fmaxf(fmaf(alpha, d4.y, p4.y), lo),
+                                                        fmaxf(fmaf(alpha, d4.z, p4.z), lo), fmaxf(fmaf(alpha, d4.w, p4.w), lo));
+    }
+    for (uint64_t i = 4 * n4 + tid; i < n; i += stride) out[i] = fmaxf(fmaf(alpha, d[i], p[i]), lo);
+}
+
+hipError_t tvam_launch_axpy_clamp(uint64_t n, const float* p, float alpha, const float* d, float lo, float* out,
+                                  hipStream_t stream) {
+    hipLaunchKernelGGL(tvam_axpy_clamp_kernel, dim3(2048), dim3(TVAM_VB), 0, stream, n, p, alpha, d, lo, out);
+    return hipGetLastError();
+}

@@ -11,6 +11,8 @@ only host syncs are the Armijo decisions (as in the reference, lbfgs.py:263).
 """
 from __future__ import annotations
 
+import ctypes
+
 import torch
 
 
@@ -129,3 +131,172 @@ class LinearLBFGS:
         for k, p in self.variables.items():
             newp = (p.detach() + alpha * search_dirs[k].reshape(p.shape))
             self.variables[k] = newp.requires_grad_(True)
+
+
+def _aligned(v):
+    """v itself when 16-byte aligned and contiguous (the fused kernels read float4), else an aligned copy."""
+    return v if v.is_contiguous() and v.data_ptr() % 16 == 0 else v.clone(memory_format=torch.contiguous_format)
+
+
+class FusedLinearLBFGS(LinearLBFGS):
+    """LinearLBFGS with the vector work fused into three HIP passes (libtvam).
+
+    Same algorithm as LinearLBFGS (lbfgs.py:198-275): history update, two-loop
+    recursion with m pairs and gamma = s.y / y.y, one render of the search
+    direction, backtracking Armijo on loss(vol + alpha dvol).  The recursion is
+    evaluated on fp64 scalars from the dot products of one fused pass
+    (tvam_lbfgs_history), the direction is one linear combination of g, s_i,
+    y_i (tvam_lbfgs_direction), and the update p + alpha d is fused with the
+    clamp of optimize.py:316-318 when ``clamp_min`` is set (tvam_axpy_clamp).
+    History pairs live in a preallocated ring of m slots.  ``allreduce`` sums
+    the dot vector over angle shards (one collective per step).
+    """
+
+    def __init__(self, lr=1.0, m=5, params=None, render_fn=None, loss_fn=None, search_it=20, loss_step=None,
+                 allreduce=None, clamp_min=None):
+        if m > 7:
+            raise ValueError("FusedLinearLBFGS keeps at most 7 history pairs")
+        self.allreduce = allreduce
+        self.clamp_min = clamp_min
+        self.state = {}
+        super().__init__(lr=lr, m=m, params=params, render_fn=render_fn, loss_fn=loss_fn, search_it=search_it,
+                         loss_step=loss_step)
+
+    def __setitem__(self, key, value):
+        v = torch.as_tensor(value).detach()
+        if v.dtype != torch.float32 or not v.is_contiguous():
+            v = v.to(torch.float32).contiguous()
+        v.requires_grad_(True)
+        self.variables[key] = v
+
+    def reset(self, k):
+        self.state.pop(k, None)
+
+    def _lib(self):
+        from . import _abi
+        return _abi.load_library()
+
+    @staticmethod
+    def _stream(dev):
+        return torch.cuda.current_stream(dev).cuda_stream if dev.type == 'cuda' else None
+
+    def _st(self, k, p):
+        st = self.state.get(k)
+        n = p.numel()
+        if st is None or st['n'] != n:
+            dev = p.device
+            npad = (n + 3) // 4 * 4  # 16-byte aligned rows (the kernels read float4)
+            st = {'n': n, 't': 0, 'slots': [], 'free': list(range(self.m)), 'p_old': None, 'g_old': None,
+                  'S': torch.empty((self.m, npad), dtype=torch.float32, device=dev)[:, :n],
+                  'Y': torch.empty((self.m, npad), dtype=torch.float32, device=dev)[:, :n],
+                  'work': torch.empty(512 * 64, dtype=torch.float64, device=dev),
+                  'dots': torch.empty(5 * (self.m + 1) + 1, dtype=torch.float64, device=dev),
+                  'SY': {}, 'YY': {}}
+            self.state[k] = st
+        return st
+
+    @torch.no_grad()
+    def step(self, vol, loss):
+        import numpy as np
+        from . import _abi
+        lib = self._lib()
+        search = {}
+        gdz_total = 0.0
+        for k, p in self.variables.items():
+            st = self._st(k, p)
+            pf = _aligned(p.detach().reshape(-1))
+            g = _aligned(p.grad.detach().reshape(-1).contiguous())
+            n = st['n']
+            stream = self._stream(pf.device)
+            new = st['t'] > 0
+            if new and len(st['slots']) == self.m:  # evict the oldest pair (lbfgs.py:214-217)
+                old = st['slots'].pop(0)
+                st['free'].append(old)
+                for key in [kk for kk in st['SY'] if old in kk]:
+                    del st['SY'][key]
+                for key in [kk for kk in st['YY'] if old in kk]:
+                    del st['YY'][key]
+            kept = list(st['slots'])
+            h = len(kept)
+            S_ptrs = (ctypes.c_void_p * max(h, 1))(*[st['S'][j].data_ptr() for j in kept])
+            Y_ptrs = (ctypes.c_void_p * max(h, 1))(*[st['Y'][j].data_ptr() for j in kept])
+            slot = st['free'][0] if new else None
+            _abi.check(lib.tvam_lbfgs_history(
+                n, pf.data_ptr() if new else None, st['p_old'].data_ptr() if new else None, g.data_ptr(),
+                st['g_old'].data_ptr() if new else None, h, S_ptrs, Y_ptrs,
+                st['S'][slot].data_ptr() if new else None, st['Y'][slot].data_ptr() if new else None,
+                st['work'].data_ptr(), st['dots'].data_ptr(), stream))
+            nd = 5 * (h + 1) + 1 if new else 2 * h + 1
+            dots = st['dots'][:nd]
+            if self.allreduce is not None:
+                dots = self.allreduce(dots.clone())
+            dv = dots.cpu().numpy().astype(np.float64)
+            if new:
+                st['free'].pop(0)
+                st['slots'].append(slot)
+            order = st['slots']
+            H = len(order)
+            Sg, Yg = dv[:H], dv[H:2 * H]
+            if new:
+                sny, sjyn, yny = dv[2 * H:3 * H], dv[3 * H:4 * H], dv[4 * H:5 * H]
+                for j, sj in enumerate(order):
+                    st['SY'][(slot, sj)] = sny[j]   # s_new . y_j
+                    st['SY'][(sj, slot)] = sjyn[j]  # s_j . y_new
+                    st['YY'][(slot, sj)] = st['YY'][(sj, slot)] = yny[j]
+            gg = dv[-1]
+            st['p_old'], st['g_old'] = pf, g
+            st['t'] += 1
+            # two-loop recursion on the Gram entries (lbfgs.py:221-243)
+            SY, YY = st['SY'], st['YY']
+            a = np.zeros(H)
+            for i in range(H - 1, -1, -1):
+                si = order[i]
+                sq = Sg[i] - sum(a[j] * SY[(si, order[j])] for j in range(i + 1, H))
+                a[i] = sq / SY[(si, si)]
+            gamma = 1.0 if st['t'] == 1 else SY[(order[-1], order[-1])] / YY[(order[-1], order[-1])]
+            b = np.zeros(H)
+            for i in range(H):
+                yi = order[i]
+                yz = gamma * (Yg[i] - sum(a[j] * YY[(yi, order[j])] for j in range(H)))
+                yz += sum((a[j] - b[j]) * SY[(order[j], yi)] for j in range(i))
+                b[i] = yz / SY[(yi, yi)]
+            # d = -z, z = gamma (g - sum a_j y_j) + sum (a_j - b_j) s_j
+            cg = -gamma
+            cy = gamma * a
+            cs = -(a - b)
+            d = torch.empty_like(g)
+            cs_c = (ctypes.c_float * max(H, 1))(*[float(v) for v in cs])
+            cy_c = (ctypes.c_float * max(H, 1))(*[float(v) for v in cy])
+            S2 = (ctypes.c_void_p * max(H, 1))(*[st['S'][j].data_ptr() for j in order])
+            Y2 = (ctypes.c_void_p * max(H, 1))(*[st['Y'][j].data_ptr() for j in order])
+            _abi.check(lib.tvam_lbfgs_direction(n, g.data_ptr(), H, S2, Y2, float(cg), cs_c, cy_c, d.data_ptr(),
+                                                stream))
+            search[k] = d
+            gdz_total += cg * gg + float(np.dot(cs, Sg)) + float(np.dot(cy, Yg))  # g . d
+
+        c1 = 1e-4
+        params = {k: search[k].reshape(self.variables[k].shape) for k in self.variables}
+        dvol = self.render_fn(params)
+        loss_v = float(loss)
+        key = 'projector.active_data' if 'projector.active_data' in params else next(iter(params))
+        alpha = 1.0
+        steps = 0
+        for _ in range(self.search_it):
+            steps += 1
+            if self.loss_step is not None:
+                f_new = self.loss_step(vol, dvol, alpha, params[key])
+            else:
+                f_new = self.loss_fn(vol + alpha * dvol, params[key])
+            if float(f_new) <= loss_v + c1 * alpha * gdz_total:
+                break
+            alpha *= 0.5
+        self.last_alpha = alpha
+        self.last_search_steps = steps
+
+        lo = -float('inf') if self.clamp_min is None else float(self.clamp_min)
+        for k, p in self.variables.items():
+            pf = _aligned(p.detach().reshape(-1))
+            out = torch.empty_like(pf)
+            _abi.check(lib.tvam_axpy_clamp(pf.numel(), pf.data_ptr(), float(alpha), search[k].data_ptr(), lo,
+                                           out.data_ptr(), self._stream(pf.device)))
+            self.variables[k] = out.reshape(p.shape).requires_grad_(True)

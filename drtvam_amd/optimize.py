@@ -30,7 +30,7 @@ import torch
 from .engine import derive_seed_grad
 from .geometry import geometries
 from .integrators import VolumeIntegrator
-from .lbfgs import LinearLBFGS
+from .lbfgs import FusedLinearLBFGS, LinearLBFGS
 from .loss import losses, ThresholdedLoss
 from .scene import load_dict
 from .utils import discretize, analytic_target, mesh_bbox, target_transform, save_vol
@@ -100,6 +100,7 @@ class ShardedLoop:
     dist = None
     progressive = False
     max_depth = 6
+    fused_lbfgs = True
 
     def forward_local(self, x, seed):
         raise NotImplementedError
@@ -169,7 +170,13 @@ class ShardedLoop:
         def render_fn(vars_):
             return self.forward(vars_[key], self._seed)
 
-        opt = LinearLBFGS(render_fn=render_fn, loss_fn=None, dot=self.dot, loss_step=self.loss_step)
+        dev = getattr(self, 'device', None) or self.x0.device
+        if dev.type == 'cuda' and self.fused_lbfgs:
+            # three fused HIP passes per step and one all-reduce of the dot vector
+            opt = FusedLinearLBFGS(render_fn=render_fn, loss_fn=None, loss_step=self.loss_step,
+                                   allreduce=self.allreduce_ if self.dist is not None else None, clamp_min=0.0)
+        else:
+            opt = LinearLBFGS(render_fn=render_fn, loss_fn=None, dot=self.dot, loss_step=self.loss_step)
         opt[key] = self.x0
         self.opt = opt
         return opt
@@ -195,8 +202,9 @@ class ShardedLoop:
         if loss_v == 0.0:
             return loss_v
         self.opt.step(vol, loss_v)
-        with torch.no_grad():
-            self.opt[key] = torch.clamp_min(self.opt[key].detach(), 0.0)
+        if getattr(self.opt, 'clamp_min', None) != 0.0:  # the fused optimizer clamps in its update pass
+            with torch.no_grad():
+                self.opt[key] = torch.clamp_min(self.opt[key].detach(), 0.0)
         return loss_v
 
     def patterns_local(self):

@@ -161,6 +161,28 @@ int tvam_plan_stats(tvam_plan* plan, uint64_t* fallback_tiles);
    adjoint), 0 = per-ray tile kernels. */
 int tvam_plan_path(const tvam_plan* plan);
 
+/*
+ * Fused vector kernels of the linear L-BFGS step (lbfgs.py:146-275,
+ * optimize.py:316-318).  All vectors are f32, n entries, 16-byte aligned.
+ *
+ * tvam_lbfgs_history: with p_old != NULL forms s_new = p - p_old and
+ *   y_new = g - g_old (written to s_new / y_new) and, over the h retained
+ *   pairs S[j], Y[j] (oldest first, 0 <= h <= 7) followed by the new pair,
+ *   writes to dots (f64): s_j.g | y_j.g | s_new.y_j | s_j.y_new | y_new.y_j
+ *   (h + 1 entries each) | g.g.  With p_old == NULL only s_j.g | y_j.g | g.g
+ *   (h entries each).  work: >= TVAM_LBFGS_WORK_DOUBLES f64 of scratch.
+ * tvam_lbfgs_direction: d = cg g + sum_j (cs[j] S[j] + cy[j] Y[j]), h <= 8.
+ * tvam_axpy_clamp: out = max(p + alpha d, lo) (out may alias p).
+ */
+#define TVAM_LBFGS_WORK_DOUBLES (512 * 64)
+int tvam_lbfgs_history(uint64_t n, const float* p, const float* p_old, const float* g, const float* g_old,
+                       int32_t h, const float* const* S, const float* const* Y, float* s_new, float* y_new,
+                       double* work, double* dots, void* hip_stream);
+int tvam_lbfgs_direction(uint64_t n, const float* g, int32_t h, const float* const* S, const float* const* Y,
+                         float cg, const float* cs, const float* cy, float* d, void* hip_stream);
+int tvam_axpy_clamp(uint64_t n, const float* p, float alpha, const float* d, float lo, float* out,
+                    void* hip_stream);
+
 /* Exact number of DDA voxel visits of one pass (host-synchronous). */
 int tvam_count_visits(tvam_plan* plan, uint32_t spp, uint32_t seed,
                       uint64_t* visits);
