@@ -73,6 +73,9 @@ def main():
     ap.add_argument("--stats", action="store_true", help="report float-fallback tiles per forward (syncs)")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--shard", choices=["auto", "angle", "slab"], default="auto",
+                    help="multi-GPU partition: z-slabs of the film + DMD row bands (planar scenes, no dose "
+                         "all-reduce; auto) or angle blocks + RCCL dose all-reduce")
     args = ap.parse_args()
 
     import torch
@@ -94,17 +97,18 @@ def main():
     A = args.angles or N
     cfg = benchy_index_matched(N=N, angles=A)
     cfg["tile"] = args.tile
+    cfg["shard"] = args.shard
     cfg["flags"] = (0 if args.zero_skip else _abi.FLAG_NO_ZERO_SKIP) | (_abi.FLAG_FWD_STATS if args.stats else 0)
     t_setup = time.perf_counter()
     prob = TvamProblem(cfg, device=dev)
     g = torch.Generator().manual_seed(0)
     full = torch.rand(prob.n_global, generator=g) * 0.1
-    per = prob.n_global // A
-    prob.x0 = full[prob.a0 * per:prob.a1 * per].to(dev).contiguous()
+    prob.x0 = prob.local_from_global(full)
     del full
     visits = prob.proj.count_visits(prob.spp, 0)
     rays = prob.n_local * prob.spp
-    log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s, angles [{prob.a0},{prob.a1}), "
+    log(f"[rank {rank}] setup {time.perf_counter() - t_setup:.1f}s, shard {prob.shard}: angles [{prob.a0},{prob.a1}), "
+        f"slices [{prob.z0},{prob.z1}), rows [{prob.r0},{prob.r1}), "
         f"visits/pass {visits:.3e}, rays {rays:.3e}")
 
     # HIP-event timing of the dominant kernels (forward / adjoint projection) on their launch stream
@@ -192,7 +196,9 @@ def main():
         "config": {
             "workload": f"config2: index-matched, {N}^3 voxels, {A} angles, {N}x{N} DMD, 1 ray/px, regular sampling",
             "voxels": N ** 3, "angles": A, "dmd": [N, N], "spp": prob.spp, "sigma_t": cfg["vial"]["medium"]["extinction"],
-            "parallelism": f"angle-shard x{world} + RCCL dose all-reduce" if world > 1 else "single GPU",
+            "parallelism": ("single GPU" if world == 1 else
+                            f"z-slab x{world} (film slabs + DMD row bands, scalar all-reduces only)"
+                            if prob.shard == "slab" else f"angle-shard x{world} + RCCL dose all-reduce"),
             "zero_skip": bool(args.zero_skip), "tile": prob.proj.desc.tile,
             "fwd_ms": fwd_avg * 1e3, "adj_ms": adj_avg * 1e3, "visits_per_pass": visits, "rays_per_pass": rays,
             "final_loss": prob.loss_hist[-1],

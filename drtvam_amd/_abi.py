@@ -12,7 +12,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libtvam.so")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 TVAM_OK = 0
 TVAM_ERR_INVALID = -1
@@ -69,6 +69,8 @@ class TvamDesc(ctypes.Structure):
         ("angle_end", ctypes.c_int32),
         ("tile", ctypes.c_int32),
         ("flags", ctypes.c_int32),
+        ("slab_begin", ctypes.c_int32),
+        ("slab_end", ctypes.c_int32),
     ]
 
     def copy(self) -> "TvamDesc":
@@ -97,6 +99,7 @@ EXPORTS = {
     "tvam_lbfgs_direction": (ctypes.c_int, [ctypes.c_uint64, _P, ctypes.c_int32, _P, _P, ctypes.c_float, _P, _P, _P,
                                             _P]),
     "tvam_axpy_clamp": (ctypes.c_int, [ctypes.c_uint64, _P, ctypes.c_float, _P, ctypes.c_float, _P, _P]),
+    "tvam_row_slices": (ctypes.c_int, [ctypes.POINTER(TvamDesc), _P]),
     "tvam_plan_path": (ctypes.c_int, [_P]),
     "tvam_count_visits": (ctypes.c_int, [_P, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]),
     "tvam_plan_stats": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),

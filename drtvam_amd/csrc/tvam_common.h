@@ -26,7 +26,8 @@
 struct TvamConsts {
     // film / sensor (sensor.py:14-19, film.py:9-14)
     float bmin[3], bmax[3], h[3];
-    int32_t res[3];
+    int32_t res[3];      // whole film (res[2] = all z-slices: the row -> slice map)
+    int32_t z0, nz;      // film slab rendered by this plan: slices [z0, z0 + nz)
     float inv_vol;       // volume.py:41-42 (fp32, like the reference)
     // projector (projector.py:73-99, :171-182)
     int32_t res_x, res_y, crop_x, crop_y, crop_off_x, crop_off_y;

@@ -209,7 +209,7 @@ __device__ __forceinline__ bool tvam_tile_ray(const TvamConsts& k, const TvamTil
     }
     const int64_t ri = r.local * (int64_t)tp.spp + smp;
     const int2 ii = tp.ray_i[ri];
-    if (ii.y != kz) return false;  // misses the grid / vial, or lies in another z-slice
+    if (ii.y != kz + k.z0) return false;  // misses the grid / vial, or lies in another z-slice
     const float4 ff = tp.ray_f[ri];
     const float4 an = tp.ang[al];
     const int svx = ii.x & 0xffff, svy = ii.x >> 16;
@@ -441,7 +441,7 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
 hipError_t tvam_launch_tiles(int mode, const TvamConsts& k, const TvamTiles& t, size_t lds_bytes,
                              const float* pat, const int32_t* idxmap, const float* gin, float* out,
                              unsigned long long* counter, hipStream_t stream) {
-    dim3 grid((unsigned)(t.ntx * t.nty), (unsigned)k.res[2]);
+    dim3 grid((unsigned)(t.ntx * t.nty), (unsigned)k.nz);
     dim3 block(TVAM_BLOCK);
     switch (mode) {
         case TVAM_MODE_FWD:

@@ -102,6 +102,8 @@ extern "C" void tvam_desc_init(tvam_desc* d) {
     d->angle_begin = 0;
     d->angle_end = -1;               // -1: all angles
     d->tile = 0;
+    d->slab_begin = 0;
+    d->slab_end = -1;                // -1: all slices
 }
 
 extern "C" const char* tvam_last_error(void) { return g_err.c_str(); }
@@ -162,6 +164,11 @@ static int validate(const tvam_desc& d) {
         if (!(d.bbox_max[a] > d.bbox_min[a])) return fail(TVAM_ERR_INVALID, "sensor bounding box is empty");
     }
     if (!(d.vial_r > 0.0f)) return fail(TVAM_ERR_INVALID, "vial radius must be positive");
+    {
+        const int z1 = d.slab_end < 0 ? d.film_res[2] : d.slab_end;
+        if (d.slab_begin < 0 || z1 > d.film_res[2] || d.slab_begin >= z1)
+            return fail(TVAM_ERR_INVALID, "invalid film slab [slab_begin, slab_end)");
+    }
     if (!(d.pixel_size_x > 0.0f && d.pixel_size_y > 0.0f)) return fail(TVAM_ERR_INVALID, "pixel_size must be positive");
     return 0;
 }
@@ -175,6 +182,8 @@ static TvamConsts make_consts(const tvam_desc& d, int a0, int a1) {
         k.res[a] = d.film_res[a];
         k.h[a] = (d.bbox_max[a] - d.bbox_min[a]) / (float)d.film_res[a];  // sensor.py:19
     }
+    k.z0 = d.slab_begin;
+    k.nz = (d.slab_end < 0 ? d.film_res[2] : d.slab_end) - d.slab_begin;
     float vol = k.h[0] * k.h[1] * k.h[2];
     k.inv_vol = vol != 0.0f ? 1.0f / vol : 0.0f;  // volume.py:41-42
     k.res_x = d.res_x;
@@ -233,29 +242,29 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     const tvam_desc& d = p->desc;
     const TvamConsts& k = p->k;
     if (!d.regular_sampling || (d.flags & TVAM_FLAG_NO_PLANAR) || p->empty) return 0;
-    std::vector<std::vector<int32_t>> rows_of(k.res[2]);
+    std::vector<std::vector<int32_t>> rows_of(k.nz);
     for (int rc = 0; rc < d.crop_y; ++rc) {
         float xc, yc;
         tvam_ray_camera(k, 0, d.crop_offset_y + rc, 0.5f, 0.5f, xc, yc);
-        const int s = tvam_slice_of(k, yc);
-        if (s < 0 || !(yc >= -k.vial_half_h && yc <= k.vial_half_h)) continue;  // misses grid / vial (volume.py:179)
-        if (!(std::fabs(yc) <= 0.7f * d.vial_r)) return 0;                      // spawn offset would depend on z
+        const int s = tvam_slice_of(k, yc) - k.z0;
+        if (s < 0 || s >= k.nz || !(yc >= -k.vial_half_h && yc <= k.vial_half_h)) continue;  // misses grid / vial / slab
+        if (!(std::fabs(yc) <= 0.7f * d.vial_r)) return 0;  // spawn offset would depend on z
         rows_of[s].push_back(rc);
     }
-    std::vector<int32_t> off(k.res[2] + 1, 0), rows;
-    for (int s = 0; s < k.res[2]; ++s) {
+    std::vector<int32_t> off(k.nz + 1, 0), rows;
+    for (int s = 0; s < k.nz; ++s) {
         off[s] = (int32_t)rows.size();
         rows.insert(rows.end(), rows_of[s].begin(), rows_of[s].end());
     }
-    off[k.res[2]] = (int32_t)rows.size();
+    off[k.nz] = (int32_t)rows.size();
     p->planar_fz = env_int("TVAM_PLANAR_FWD_Z", 32);
     p->planar_az = env_int("TVAM_PLANAR_ADJ_Z", 4);
     if (p->planar_fz != 8 && p->planar_fz != 16 && p->planar_fz != 32) p->planar_fz = 32;
     if (p->planar_az != 4 && p->planar_az != 8) p->planar_az = 4;
     const int ns = (int)cs.size();
     int32_t mrc = 0;
-    for (int z0 = 0; z0 < k.res[2]; z0 += p->planar_az)
-        mrc = std::max<int32_t>(mrc, off[std::min(z0 + p->planar_az, k.res[2])] - off[z0]);
+    for (int z0 = 0; z0 < k.nz; z0 += p->planar_az)
+        mrc = std::max<int32_t>(mrc, off[std::min(z0 + p->planar_az, k.nz)] - off[z0]);
     // Forward (voxel-driven) tables.  Per angle, in the kernel's fp32 ops:
     // u(X, Y) = X * (s du) + Y * (-c du) + u0 is the crop column whose ray has
     // lateral coordinate X s - Y c (common.py:96-99: x_c = W a (0.5 - u));
@@ -305,7 +314,7 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     p->pl.ncmax = need;
     {
         bool multi = false;
-        for (int z = 0; z < k.res[2]; ++z) multi |= off[z + 1] - off[z] > 1;
+        for (int z = 0; z < k.nz; ++z) multi |= off[z + 1] - off[z] > 1;
         p->pl.fwd_multi = multi ? 1 : 0;
     }
     p->pl.max_rows_chunk = mrc;
@@ -410,31 +419,32 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
 
     // per-slice DMD rows.  A ray's height is y_c of its row (+ jitter); its
     // slice is the DDA start voxel z (tvam_slice_of).
-    std::vector<std::vector<int32_t>> rows_of(k.res[2]);
+    // (local slice s of the slab = global slice k.z0 + s)
+    std::vector<std::vector<int32_t>> rows_of(k.nz);
     for (int rc = 0; rc < d.crop_y; ++rc) {
         int row = d.crop_offset_y + rc;
         if (d.regular_sampling) {
             float xc, yc;
             tvam_ray_camera(k, 0, row, 0.5f, 0.5f, xc, yc);
-            int s = tvam_slice_of(k, yc);
-            if (s >= 0) rows_of[s].push_back(rc);
+            int s = tvam_slice_of(k, yc) - k.z0;
+            if (s >= 0 && s < k.nz) rows_of[s].push_back(rc);
         } else {
             float xc, ytop, ybot;
             tvam_ray_camera(k, 0, row, 0.5f, 0.0f, xc, ytop);
             tvam_ray_camera(k, 0, row, 0.5f, 1.0f, xc, ybot);
             double lo = ((double)ybot - k.bmin[2]) / k.h[2] - 1.0, hi = ((double)ytop - k.bmin[2]) / k.h[2] + 1.0;
-            int s0 = std::max(0, (int)std::floor(lo)), s1 = std::min(k.res[2] - 1, (int)std::floor(hi));
-            for (int s = s0; s <= s1; ++s) rows_of[s].push_back(rc);
+            int s0 = std::max(k.z0, (int)std::floor(lo)), s1 = std::min(k.z0 + k.nz - 1, (int)std::floor(hi));
+            for (int s = s0; s <= s1; ++s) rows_of[s - k.z0].push_back(rc);
         }
     }
-    std::vector<int32_t> slice_off(k.res[2] + 1, 0), slice_rows;
+    std::vector<int32_t> slice_off(k.nz + 1, 0), slice_rows;
     p->max_rows_per_slice = 0;
-    for (int s = 0; s < k.res[2]; ++s) {
+    for (int s = 0; s < k.nz; ++s) {
         slice_off[s] = (int32_t)slice_rows.size();
         slice_rows.insert(slice_rows.end(), rows_of[s].begin(), rows_of[s].end());
         p->max_rows_per_slice = std::max<int32_t>(p->max_rows_per_slice, (int32_t)rows_of[s].size());
     }
-    slice_off[k.res[2]] = (int32_t)slice_rows.size();
+    slice_off[k.nz] = (int32_t)slice_rows.size();
 
     // Per-tile slot lists: every (angle, DMD column) whose ray crosses the
     // tile, in (angle, column) order so that consecutive lanes read
@@ -593,7 +603,7 @@ extern "C" int tvam_forward(tvam_plan* p, const float* active_data, const uint32
     int rc = call_setup(p, n_active, active_pixels, spp, k);
     if (rc) return rc;
     const TvamConsts& kc = k;
-    size_t V = (size_t)kc.res[0] * kc.res[1] * kc.res[2];
+    size_t V = (size_t)kc.res[0] * kc.res[1] * kc.nz;
     hipError_t e;
     if (p->empty || n_active == 0) {
         e = hipMemsetAsync(dose, 0, V * sizeof(float), stream);
@@ -755,4 +765,19 @@ extern "C" int tvam_axpy_clamp(uint64_t n, const float* p, float alpha, const fl
         return fail(TVAM_ERR_INVALID, "tvam_axpy_clamp: vectors must be 16-byte aligned");
     hipError_t e = tvam_launch_axpy_clamp(n, p, alpha, d, lo, out, (hipStream_t)stream);
     return e == hipSuccess ? 0 : hip_fail(e, "axpy launch");
+}
+
+extern "C" int tvam_row_slices(const tvam_desc* desc, int32_t* slice_of_row) {
+    if (!desc || !slice_of_row) return fail(TVAM_ERR_INVALID, "null argument");
+    int rc = validate(*desc);
+    if (rc) return rc;
+    const tvam_desc& d = *desc;
+    const TvamConsts k = make_consts(d, 0, d.n_patterns);
+    for (int r = 0; r < d.crop_y; ++r) {
+        float xc, yc;
+        tvam_ray_camera(k, 0, d.crop_offset_y + r, 0.5f, 0.5f, xc, yc);
+        const int s = tvam_slice_of(k, yc);
+        slice_of_row[r] = (s >= 0 && yc >= -k.vial_half_h && yc <= k.vial_half_h) ? s : -1;
+    }
+    return 0;
 }

@@ -118,7 +118,7 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
     int* s_row = s_cb + (TVAM_ACH + 2);                            // [Z]: the slice's row, -1 none, -2 several
 
     const int ntx = (k.res[0] + 15) >> 4, nty = (k.res[1] + 15) >> 4;
-    const int ntiles = ntx * nty, nwg = ntiles * ((k.res[2] + Z - 1) / Z);
+    const int ntiles = ntx * nty, nwg = ntiles * ((k.nz + Z - 1) / Z);
     // XCD-aware order: workgroup b runs on XCD b % 8; give each XCD a contiguous
     // run of (z-chunk, tile) pairs so the tiles sharing a z-chunk's pattern rows
     // share that XCD's L2
@@ -143,7 +143,7 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
     if (threadIdx.x < Z) {
         const int s = z0 + threadIdx.x;
         int r = -1;
-        if (s < k.res[2]) {
+        if (s < k.nz) {
             const int b = pl.slice_off[s], e = pl.slice_off[s + 1];
             r = e - b == 1 ? pl.slice_rows[b] : (e - b == 0 ? -1 : -2);
         }
@@ -320,7 +320,7 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
         const size_t plane = (size_t)k.res[0] * k.res[1];
 #pragma unroll
         for (int z = 0; z < Z; ++z)
-            if (z0 + z < k.res[2]) dose[(size_t)(z0 + z) * plane + (size_t)iy * k.res[0] + ix] = acc[z] * scale;
+            if (z0 + z < k.nz) dose[(size_t)(z0 + z) * plane + (size_t)iy * k.res[0] + ix] = acc[z] * scale;
     }
 }
 
@@ -361,7 +361,7 @@ static hipError_t launch_fwd_z(dim3 grid, size_t lds, hipStream_t stream, const 
 hipError_t tvam_launch_fwd_planar(const TvamConsts& k, const TvamPlanar& pl, int Z, const float* pat, float* dose,
                                   hipStream_t stream) {
     const int ntx = (k.res[0] + 15) / 16, nty = (k.res[1] + 15) / 16;
-    const unsigned nwg = (unsigned)(ntx * nty) * (unsigned)((k.res[2] + Z - 1) / Z);
+    const unsigned nwg = (unsigned)(ntx * nty) * (unsigned)((k.nz + Z - 1) / Z);
     dim3 grid(pl.xcd_remap ? (nwg + 7) / 8 * 8 : nwg);
     const size_t lds = tvam_planar_fwd_lds(pl, Z);
     switch (Z) {
@@ -403,7 +403,7 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_adj_planar_kernel(TvamConsts k, 
         const int z = i / (tw * th), li = i - z * (tw * th);
         const int ly = li / tw - 1, lx = li - (ly + 1) * tw - 1;
         float v = 0.0f;
-        if (lx >= 0 && ly >= 0 && lx < wx && ly < wy && z0 + z < k.res[2])
+        if (lx >= 0 && ly >= 0 && lx < wx && ly < wy && z0 + z < k.nz)
             v = gin[(size_t)(z0 + z) * plane + (size_t)(y0 + ly) * k.res[0] + (x0 + lx)] * k.inv_vol;
         tile[(size_t)li * Z + z] = v;
     }
@@ -411,7 +411,7 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_adj_planar_kernel(TvamConsts k, 
         int n = 0;
         for (int z = 0; z < Z; ++z) {
             s_roff[z] = n;
-            if (z0 + z < k.res[2])
+            if (z0 + z < k.nz)
                 for (int q = pl.slice_off[z0 + z]; q < pl.slice_off[z0 + z + 1]; ++q) s_rows[n++] = pl.slice_rows[q];
         }
         s_roff[Z] = n;
@@ -497,7 +497,7 @@ size_t tvam_planar_adj_lds(const TvamPlanar& pl, const TvamTiles& t, int Z) {
 
 hipError_t tvam_launch_adj_planar(const TvamConsts& k, const TvamPlanar& pl, const TvamTiles& t, int Z,
                                   const int32_t* idxmap, const float* gin, float* out, hipStream_t stream) {
-    dim3 grid((unsigned)(t.ntx * t.nty), (unsigned)((k.res[2] + Z - 1) / Z));
+    dim3 grid((unsigned)(t.ntx * t.nty), (unsigned)((k.nz + Z - 1) / Z));
     const size_t lds = tvam_planar_adj_lds(pl, t, Z);
     switch (Z) {
         case 4:

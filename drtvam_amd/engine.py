@@ -48,6 +48,8 @@ class Projection:
             _abi.check(self.lib.tvam_plan_create(ctypes.byref(self.desc), self.device.index, ctypes.byref(plan)))
         self._plan = plan
         rx, ry, rz = self.desc.film_res
+        if self.desc.slab_end >= 0:  # film slab of this plan (z-slab sharding)
+            rz = self.desc.slab_end - self.desc.slab_begin
         self.film_shape = (rz, ry, rx, self.desc.film_channels)
         self.n_dense = self.desc.n_patterns * self.desc.crop_y * self.desc.crop_x
 

@@ -25,6 +25,8 @@ class TVAMIntegrator:
         self.transmission_only = props.get('transmission_only', True)
         self.regular_sampling = props.get('regular_sampling', False)
         self.angle_range = props.get('angle_range', None)  # (begin, end): angle shard of this rank
+        self.row_band = props.get('row_band', None)  # (begin, end): crop rows of this rank (z-slab sharding)
+        self.slab = props.get('slab', None)          # (begin, end): film z-slices of this rank
         self.tile = props.get('tile', 0)
         self.flags = props.get('flags', 0)
         self._plans = {}
@@ -48,6 +50,12 @@ class TVAMIntegrator:
         d.transmission_only = int(bool(self.transmission_only))
         if self.angle_range is not None:
             d.angle_begin, d.angle_end = int(self.angle_range[0]), int(self.angle_range[1])
+        if self.row_band is not None:
+            r0, r1 = int(self.row_band[0]), int(self.row_band[1])
+            d.crop_offset_y += r0
+            d.crop_y = r1 - r0
+        if self.slab is not None:
+            d.slab_begin, d.slab_end = int(self.slab[0]), int(self.slab[1])
         d.tile = int(self.tile)
         d.flags = int(self.flags)
         return d

@@ -124,25 +124,28 @@ class ThresholdedLoss(Loss):
                 and target.dtype == torch.float32 and target.numel() == x.numel())
 
     def _sparsity_value(self, patterns):
-        if not self.weight_sparsity:
+        if not self.weight_sparsity or patterns is None:
             return None
         p = patterns.detach()
         return self.reduction(torch.abs(p) ** self.M * self.weight_sparsity).to(torch.float64)
 
-    def fused_value(self, x, target, patterns, dx=None, alpha=0.0):
-        """Loss of x (+ alpha*dx) as an f64 device scalar, one kernel pass."""
+    def fused_value(self, x, target, patterns, dx=None, alpha=0.0, count=None):
+        """Loss of x (+ alpha*dx) as an f64 device scalar, one kernel pass.  ``patterns=None``
+        leaves out the sparsity term; ``count`` is the element count of a 'mean' reduction
+        when x is one slab of the film."""
         from .engine import loss_threshold
-        scale = 1.0 / x.numel() if self.reduction_name == 'mean' else 1.0
+        scale = 1.0 / (count or x.numel()) if self.reduction_name == 'mean' else 1.0
         v = loss_threshold(x.reshape(-1), target.reshape(-1), int(self.K), self.tl, self.tu, self.weight_object,
                            self.weight_void, self.weight_limit, scale,
                            None if dx is None else dx.reshape(-1), alpha)
         s = self._sparsity_value(patterns)
         return v if s is None else v + s
 
-    def fused_value_grad(self, x, target, patterns, grad_out):
-        """Loss value (f64 device scalar) and dL/dx written into grad_out, one kernel pass."""
+    def fused_value_grad(self, x, target, patterns, grad_out, count=None):
+        """Loss value (f64 device scalar) and dL/dx written into grad_out, one kernel pass
+        (``patterns`` / ``count`` as in fused_value)."""
         from .engine import loss_threshold
-        scale = 1.0 / x.numel() if self.reduction_name == 'mean' else 1.0
+        scale = 1.0 / (count or x.numel()) if self.reduction_name == 'mean' else 1.0
         v = loss_threshold(x.reshape(-1), target.reshape(-1), int(self.K), self.tl, self.tu, self.weight_object,
                            self.weight_void, self.weight_limit, scale, grad=grad_out.reshape(-1))
         s = self._sparsity_value(patterns)

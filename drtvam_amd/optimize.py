@@ -19,6 +19,7 @@ all-reduced scalars.
 from __future__ import annotations
 
 import argparse
+import ctypes
 import json
 import os
 import time
@@ -101,6 +102,8 @@ class ShardedLoop:
     progressive = False
     max_depth = 6
     fused_lbfgs = True
+    dose_sharded = False  # z-slab sharding: each rank owns a slab of the dose (no dose all-reduce)
+    n_vox = None          # voxels of the whole film (normalises a 'mean' loss on a slab)
 
     def forward_local(self, x, seed):
         raise NotImplementedError
@@ -138,30 +141,41 @@ class ShardedLoop:
 
     # ---- projections ----------------------------------------------------------
     def forward(self, x, seed):
-        return self.allreduce_(self.forward_local(x, seed))
+        vol = self.forward_local(x, seed)
+        return vol if self.dose_sharded else self.allreduce_(vol)
 
     def adjoint(self, grad_vol, seed):
         return self.adjoint_local(grad_vol, seed)
 
     # ---- loss -------------------------------------------------------------------
     def loss_value_grad(self, vol, x):
-        """(loss f64 device scalar, dL/dvol) — fused kernel or torch autograd."""
+        """(loss f64 device scalar, dL/dvol) — fused kernel or torch autograd.  The film
+        term is summed over the slabs when the dose is sharded; the sparsity term
+        (loss.py:54-59) is added once, summed over the pattern shards."""
+        s = self.sparsity(x)
         if self.fused:
-            v = self.loss_fn.fused_value_grad(vol, self.target, x, self.grad_vol)
-            s = self.sparsity(x)
+            v = self.loss_fn.fused_value_grad(vol, self.target, None, self.grad_vol, count=self.n_vox)
+            if self.dose_sharded:
+                v = self.allreduce_(v)
             return (v if s is None else v + s), self.grad_vol
         vv = vol.detach().requires_grad_(True)
         with torch.enable_grad():
-            l = self.loss_fn(vv, self.target, torch.zeros_like(x) if getattr(self.loss_fn, 'weight_sparsity', 0) == 0 else x.detach())
+            l = self.loss_fn(vv, self.target, torch.zeros_like(x))
             l.backward()
-        return l.detach().to(torch.float64), vv.grad
+        l = l.detach().to(torch.float64)
+        if self.dose_sharded:
+            l = self.allreduce_(l)
+        return (l if s is None else l + s), vv.grad
 
     def loss_step(self, vol, dvol, alpha, patterns):
+        s = self.sparsity(patterns)
         if self.fused:
-            v = self.loss_fn.fused_value(vol, self.target, patterns, dvol, alpha)
-            s = self.sparsity(patterns)
-            return v if s is None else v + s
-        return self.loss_fn(vol + alpha * dvol, self.target, patterns)
+            v = self.loss_fn.fused_value(vol, self.target, None, dvol, alpha, count=self.n_vox)
+        else:
+            v = self.loss_fn(vol + alpha * dvol, self.target, torch.zeros_like(patterns)).to(torch.float64)
+        if self.dose_sharded:
+            v = self.allreduce_(v)
+        return v if s is None else v + s
 
     # ---- optimisation -------------------------------------------------------------
     def make_optimizer(self):
@@ -244,13 +258,50 @@ class TvamProblem(ShardedLoop):
         self.regular_sampling = config.get('regular_sampling', False)
         self.n_steps = config.get('n_steps', 40)
 
-        # angle shard of this rank (contiguous blocks)
+        lcfg = dict(config.get('loss', {'type': 'threshold'}))
+        ltype = lcfg.pop('type', 'threshold')
+        if ltype not in losses:
+            raise ValueError(f"Unknown loss type: '{ltype}'. Available losses are: {list(losses.keys())}")
+        self.loss_fn = losses[ltype](lcfg)
+        lf = self.loss_fn
+        fusable = (isinstance(lf, ThresholdedLoss) and dev.type == 'cuda' and float(lf.K).is_integer()
+                   and 1 <= int(lf.K) <= 16)
+
+        # Sharding.  'angle': contiguous angle blocks, the
+        # partial doses are all-reduced.  'slab': planar rays (regular sampling)
+        # never leave their z-slice, so rank k owns a slab of film slices and the
+        # band of DMD rows whose rays lie in it, for every angle: no dose
+        # communication at all (only scalar loss / dot all-reduces).
         A = self.scene.projector.n_patterns
-        self.a0, self.a1 = angle_shard(A, self.rank, self.world)
-        iprops = {'max_depth': 3 if self.progressive else self.max_depth, 'rr_depth': self.rr_depth,
-                  'print_time': self.time, 'transmission_only': self.transmission_only,
-                  'regular_sampling': self.regular_sampling, 'angle_range': (self.a0, self.a1),
-                  'tile': config.get('tile', 0), 'flags': config.get('flags', 0)}
+        shard = config.get('shard', 'auto')
+        if shard not in ('auto', 'angle', 'slab'):
+            raise ValueError(f"Unknown shard mode '{shard}' (auto, angle, slab)")
+        if shard == 'slab' and not (self.regular_sampling and fusable):
+            raise ValueError("z-slab sharding needs regular sampling and the fused thresholded loss")
+        self.shard = 'slab' if (shard == 'slab' or (shard == 'auto' and self.world > 1 and self.regular_sampling
+                                                     and fusable)) else 'angle'
+        base = {'max_depth': 3 if self.progressive else self.max_depth, 'rr_depth': self.rr_depth,
+                'print_time': self.time, 'transmission_only': self.transmission_only,
+                'regular_sampling': self.regular_sampling, 'tile': config.get('tile', 0),
+                'flags': config.get('flags', 0)}
+        p = self.scene.projector
+        if not p.dense:
+            raise NotImplementedError("sharded optimisation needs the dense active set")
+        self.crop_x, self.crop_y = p.crop[0], p.crop[1]
+        full_desc = VolumeIntegrator(base).desc(self.scene, self.sensor)
+        self.res_z = int(full_desc.film_res[2])
+        self.n_vox = int(full_desc.film_res[0]) * int(full_desc.film_res[1]) * self.res_z
+        if self.shard == 'slab':
+            self.a0, self.a1 = 0, A
+            self.z0, self.z1 = angle_shard(self.res_z, self.rank, self.world)
+            self.r0, self.r1 = self._row_band(full_desc)
+            shard_props = {'angle_range': (0, A), 'row_band': (self.r0, self.r1), 'slab': (self.z0, self.z1)}
+            self.dose_sharded = True
+        else:
+            self.a0, self.a1 = angle_shard(A, self.rank, self.world)
+            self.z0, self.z1, self.r0, self.r1 = 0, self.res_z, 0, self.crop_y
+            shard_props = {'angle_range': (self.a0, self.a1)}
+        iprops = base | shard_props
         self.integrator = VolumeIntegrator(iprops)
         self.final_integrator = VolumeIntegrator(iprops | {'max_depth': config.get('max_depth_ref', 16),
                                                            'rr_depth': config.get('rr_depth_ref', 8)})
@@ -263,30 +314,80 @@ class TvamProblem(ShardedLoop):
             else:
                 target = analytic_target(self.sensor.resolution(), self.sensor.bbox_min, self.sensor.bbox_max,
                                          config['target'].get('analytic', 'box_hole'))
-        self.target = target.to(device=dev, dtype=torch.float32).contiguous()
+        self.target_full = target.to(dtype=torch.float32)
+        self.target = self.target_full[self.z0:self.z1].to(device=dev).contiguous()
 
-        lcfg = dict(config.get('loss', {'type': 'threshold'}))
-        ltype = lcfg.pop('type', 'threshold')
-        if ltype not in losses:
-            raise ValueError(f"Unknown loss type: '{ltype}'. Available losses are: {list(losses.keys())}")
-        self.loss_fn = losses[ltype](lcfg)
-
-        # this rank's slice of projector.active_data (dense crop order is angle-major)
-        p = self.scene.projector
-        if not p.dense:
-            raise NotImplementedError("sharded optimisation needs the dense active set")
-        per_angle = p.crop[0] * p.crop[1]
-        self.n_local = (self.a1 - self.a0) * per_angle
+        # this rank's part of projector.active_data (dense crop order [angle][row][col])
+        per_angle = self.crop_x * self.crop_y
         self.n_global = A * per_angle
-        self.x0 = p.active_data[self.a0 * per_angle:self.a1 * per_angle].contiguous()
+        self.n_local = (self.a1 - self.a0) * (self.r1 - self.r0) * self.crop_x
+        self.x0 = self.local_from_global(p.active_data)
         self.proj = self.integrator.projection(self.scene, self.sensor)
-        lf = self.loss_fn
-        self.fused = (isinstance(lf, ThresholdedLoss) and dev.type == 'cuda' and float(lf.K).is_integer()
-                      and 1 <= int(lf.K) <= 16 and self.target.shape[-1] == 1)
+        self.fused = fusable and self.target.shape[-1] == 1
         self.grad_vol = torch.empty(self.proj.film_shape, dtype=torch.float32, device=dev)
         self.opt = None
         self.loss_hist = []
         self.timing = []
+
+    def _row_band(self, desc):
+        """Crop rows [r0, r1) whose rays lie in this rank's slab (rows outside the grid go to the
+        outermost bands, so the bands tile all crop rows)."""
+        from . import _abi
+        m = np.empty(desc.crop_y, dtype=np.int32)
+        _abi.check(_abi.load_library().tvam_row_slices(ctypes.byref(desc), m.ctypes.data_as(ctypes.c_void_p)))
+        bands = []
+        for k in range(self.world):
+            z0, z1 = angle_shard(self.res_z, k, self.world)
+            rows = np.nonzero((m >= z0) & (m < z1))[0]
+            bands.append((int(rows.min()), int(rows.max()) + 1) if rows.size else None)
+            if rows.size and not np.all((m[rows.min():rows.max() + 1] >= z0) & (m[rows.min():rows.max() + 1] < z1)
+                                        | (m[rows.min():rows.max() + 1] < 0)):
+                raise ValueError("z-slab sharding: the rows of a slab are not contiguous")
+        order = sorted((b[0], k) for k, b in enumerate(bands) if b is not None)
+        if not order:
+            raise ValueError("z-slab sharding: no DMD row reaches the grid")
+        edges = {}
+        for i, (_, k) in enumerate(order):  # extend bands over unmapped rows: [start of band, start of next)
+            lo = 0 if i == 0 else bands[k][0]
+            hi = desc.crop_y if i == len(order) - 1 else bands[order[i + 1][1]][0]
+            edges[k] = (lo, hi)
+        return edges.get(self.rank, (0, 0))
+
+    def local_from_global(self, full):
+        """This rank's part (angle block or row band) of a global dense pattern vector."""
+        full = torch.as_tensor(full).reshape(-1, self.crop_y, self.crop_x)
+        return full[self.a0:self.a1, self.r0:self.r1, :].reshape(-1).to(self.device).contiguous()
+
+    def gather_patterns(self, local):
+        """The global dense pattern vector (every rank), from the ranks' parts."""
+        if self.dist is None:
+            return local
+        A = self.scene.projector.n_patterns
+        shapes = [None] * self.world
+        self.dist.all_gather_object(shapes, (self.a0, self.a1, self.r0, self.r1))
+        m = max((a1 - a0) * (r1 - r0) * self.crop_x for a0, a1, r0, r1 in shapes)
+        buf = torch.zeros(m, dtype=local.dtype, device=local.device)
+        buf[:local.numel()] = local
+        parts = [torch.empty_like(buf) for _ in range(self.world)]
+        self.dist.all_gather(parts, buf)
+        full = torch.zeros((A, self.crop_y, self.crop_x), dtype=local.dtype, device=local.device)
+        for (a0, a1, r0, r1), part in zip(shapes, parts):
+            n = (a1 - a0) * (r1 - r0) * self.crop_x
+            full[a0:a1, r0:r1, :] = part[:n].reshape(a1 - a0, r1 - r0, self.crop_x)
+        return full.reshape(-1)
+
+    def gather_dose(self, vol):
+        """The whole film from the ranks' slabs (slab sharding; the angle mode all-reduces)."""
+        if self.dist is None or not self.dose_sharded:
+            return vol
+        slabs = [None] * self.world
+        self.dist.all_gather_object(slabs, (self.z0, self.z1))
+        m = max(z1 - z0 for z0, z1 in slabs)
+        buf = torch.zeros((m,) + tuple(vol.shape[1:]), dtype=vol.dtype, device=vol.device)
+        buf[:vol.shape[0]] = vol
+        parts = [torch.empty_like(buf) for _ in range(self.world)]
+        self.dist.all_gather(parts, buf)
+        return torch.cat([part[:z1 - z0] for (z0, z1), part in zip(slabs, parts)])
 
     def forward_local(self, x, seed):
         return self.proj.forward(x.detach().contiguous(), None, self.spp, seed)
@@ -301,7 +402,7 @@ class TvamProblem(ShardedLoop):
     def final_render(self, spp=None):
         proj = self.final_integrator.projection(self.scene, self.final_sensor)
         vol = proj.forward(self.patterns_local().contiguous(), None, spp or self.spp_ref, 0)
-        return self.allreduce_(vol)
+        return self.gather_dose(vol) if self.dose_sharded else self.allreduce_(vol)
 
 
 def optimize(config, patterns_fwd=None, device=None):
@@ -309,12 +410,11 @@ def optimize(config, patterns_fwd=None, device=None):
     prob = TvamProblem(config, device=device)
     output = config.get('output', '.')
     os.makedirs(output, exist_ok=True)
-    np.save(os.path.join(output, "target.npy"), prob.target.cpu().numpy())
+    if prob.rank == 0:
+        np.save(os.path.join(output, "target.npy"), prob.target_full.cpu().numpy())
     if patterns_fwd is not None:
         print("Using provided patterns for forward mode.")
-        full = torch.as_tensor(np.asarray(patterns_fwd, dtype=np.float32).reshape(-1), device=prob.device)
-        per = full.numel() // prob.scene.projector.n_patterns
-        prob.x0 = full[prob.a0 * per:prob.a1 * per].contiguous()
+        prob.x0 = prob.local_from_global(np.asarray(patterns_fwd, dtype=np.float32).reshape(-1))
     else:
         print("Optimizing patterns...")
         for i in range(prob.n_steps):
@@ -331,12 +431,7 @@ def optimize(config, patterns_fwd=None, device=None):
         np.save(os.path.join(output, "final.npy"), vol_final.cpu().numpy())
         np.save(os.path.join(output, "loss.npy"), np.asarray(prob.loss_hist))
         np.save(os.path.join(output, "timing.npy"), np.asarray(prob.timing))
-    pats = prob.patterns_local()
-    if prob.dist is not None:
-        parts = [torch.empty_like(pats) for _ in range(prob.world)] if prob.n_local * prob.world == prob.n_global else None
-        if parts is not None:
-            prob.dist.all_gather(parts, pats)
-            pats = torch.cat(parts)
+    pats = prob.gather_patterns(prob.patterns_local().float())
     if prob.rank == 0:
         p = prob.scene.projector
         full = pats.cpu().numpy().reshape(-1, p.crop[1], p.crop[0])

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define TVAM_ABI_VERSION 1
+#define TVAM_ABI_VERSION 2
 
 /* error codes */
 #define TVAM_OK               0
@@ -110,6 +110,10 @@ typedef struct tvam_desc {
     int32_t angle_begin, angle_end;
     int32_t tile;
     int32_t flags;                /* TVAM_FLAG_* */
+    /* film slab [slab_begin, slab_end) of z-slices this plan renders (-1 =
+       whole film): the dose / grad_dose buffers hold only these slices, and
+       rays of other slices are skipped (z-slab sharding of planar scenes) */
+    int32_t slab_begin, slab_end;
 } tvam_desc;
 
 /* tvam_desc.flags */
@@ -182,6 +186,12 @@ int tvam_lbfgs_direction(uint64_t n, const float* g, int32_t h, const float* con
                          float cg, const float* cs, const float* cy, float* d, void* hip_stream);
 int tvam_axpy_clamp(uint64_t n, const float* p, float alpha, const float* d, float lo, float* out,
                     void* hip_stream);
+
+/* Global film z-slice of every crop row's rays under regular sampling
+   (slice_of_row[crop_y]; -1 when the row's rays miss the grid or the vial),
+   computed with the plan's own fp32 ray generation: the row <-> slice map
+   that z-slab sharding of planar scenes partitions. */
+int tvam_row_slices(const tvam_desc* desc, int32_t* slice_of_row);
 
 /* Exact number of DDA voxel visits of one pass (host-synchronous). */
 int tvam_count_visits(tvam_plan* plan, uint32_t spp, uint32_t seed,

@@ -17,40 +17,36 @@ pytestmark = pytest.mark.gpu
 CFG = dict(N=24, angles=12)
 
 
-def _run(rank, world, steps):
+def _run(rank, world, steps, shard):
     from drtvam_amd.configs import benchy_index_matched
     from drtvam_amd.optimize import TvamProblem
 
     cfg = benchy_index_matched(**CFG)
+    cfg["shard"] = shard
     prob = TvamProblem(cfg, device=torch.device("cuda", 0), rank=rank, world_size=world)
+    assert prob.shard == shard
     g = torch.Generator().manual_seed(0)
-    full = torch.rand(prob.n_global, generator=g) * 0.1
-    per = prob.n_global // CFG["angles"]
-    prob.x0 = full[prob.a0 * per:prob.a1 * per].cuda().contiguous()
+    prob.x0 = prob.local_from_global(torch.rand(prob.n_global, generator=g) * 0.1)
     assert prob.proj.planar
     for i in range(steps):
         prob.iteration(i)
-    x = prob.patterns_local().float()
-    if world > 1:
-        sizes = [torch.zeros(1, dtype=torch.int64, device="cuda") for _ in range(world)]
-        dist.all_gather(sizes, torch.tensor([x.numel()], device="cuda"))
-        m = int(max(int(s) for s in sizes))
-        parts = [torch.zeros(m, device="cuda") for _ in range(world)]
-        pad = torch.zeros(m, device="cuda")
-        pad[:x.numel()] = x
-        dist.all_gather(parts, pad)
-        x = torch.cat([p[:int(s)] for p, s in zip(parts, sizes)])
-    return np.asarray(prob.loss_hist), x.cpu().numpy()
+    x = prob.gather_patterns(prob.patterns_local().float())
+    dose = prob.final_render(spp=1)
+    return np.asarray(prob.loss_hist), x.cpu().numpy(), dose.cpu().numpy()
 
 
-def _worker(rank, world, port, steps, q):
+def _worker(rank, world, port, steps, shard, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        loss, x = _run(rank, world, steps)
+        res = _run(rank, world, steps, shard)
         if rank == 0:
-            q.put((loss, x))
+            q.put(res)
+    except BaseException as e:  # report instead of leaving the parent waiting
+        import traceback
+        q.put(("error", rank, traceback.format_exc()))
+        raise
     finally:
         dist.destroy_process_group()
 
@@ -61,24 +57,34 @@ def _free_port():
         return s.getsockname()[1]
 
 
-def test_two_rank_gpu_loop_matches_single_rank():
+@pytest.mark.parametrize("shard", ["slab", "angle"])
+def test_two_rank_gpu_loop_matches_single_rank(shard):
     steps = 4
     ctx = mp.get_context("spawn")
-    q = ctx.SimpleQueue()
-    p1 = ctx.Process(target=_worker, args=(0, 1, _free_port(), steps, q))
+    q = ctx.Queue()
+
+    def result(procs):
+        try:
+            res = q.get(timeout=240)
+        finally:
+            for p in procs:
+                p.join(timeout=60)
+                if p.is_alive():
+                    p.kill()
+        assert not (isinstance(res[0], str) and res[0] == "error"), res[2]
+        assert all(p.exitcode == 0 for p in procs)
+        return res
+
+    p1 = ctx.Process(target=_worker, args=(0, 1, _free_port(), steps, shard, q))
     p1.start()
-    ref_loss, ref_x = q.get()
-    p1.join(timeout=300)
-    assert p1.exitcode == 0
+    ref_loss, ref_x, ref_dose = result([p1])
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, steps, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, steps, shard, q)) for r in range(2)]
     for p in procs:
         p.start()
-    loss, x = q.get()
-    for p in procs:
-        p.join(timeout=300)
-        assert p.exitcode == 0
+    loss, x, dose = result(procs)
     assert ref_loss[-1] < ref_loss[0]
-    # partial doses sum in a different order: fp32 rounding only
+    # the same sums in a different order (partial doses / slab losses): fp32 rounding only
     np.testing.assert_allclose(loss, ref_loss, rtol=1e-4)
     np.testing.assert_allclose(x, ref_x, rtol=1e-3, atol=1e-5)
+    np.testing.assert_allclose(dose, ref_dose, rtol=1e-3, atol=1e-6)

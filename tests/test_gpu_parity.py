@@ -197,3 +197,40 @@ def test_forward_fixed_point_and_fallback(oracle, dist):
         assert fb > 0  # a few outliers set the fixed-point step: those tiles take the float path
     elif dist == "signed":
         assert fb == 0
+
+
+@pytest.mark.parametrize("planar", [True, False])
+@pytest.mark.parametrize("band", [False, True])
+def test_slab_plan_matches_full_film(planar, band):
+    """A plan restricted to film slab [z0, z1) (and, like a z-slab rank, to the DMD rows
+    feeding it) renders exactly those slices of the full forward, and its adjoint is the
+    full adjoint of a gradient that vanishes outside the slab."""
+    import ctypes
+    N, A, z0, z1 = 32, 16, 9, 21
+    d = make(N=N, A=A, planar=planar)
+    n = A * N * N
+    rng = np.random.default_rng(11)
+    pat = rng.uniform(0, 0.1, n).astype(np.float32)
+    full, proj = gpu_forward(d, pat)
+    ds = d.copy()
+    ds.slab_begin, ds.slab_end = z0, z1
+    pats = pat
+    r0, r1 = 0, N
+    if band:
+        m = np.empty(N, dtype=np.int32)
+        _abi.check(_abi.load_library().tvam_row_slices(ctypes.byref(d), m.ctypes.data_as(ctypes.c_void_p)))
+        rows = np.nonzero((m >= z0) & (m < z1))[0]
+        r0, r1 = int(rows.min()), int(rows.max()) + 1
+        ds.crop_offset_y, ds.crop_y = r0, r1 - r0
+        pats = pat.reshape(A, N, N)[:, r0:r1, :].reshape(-1).copy()
+    part, ps = gpu_forward(ds, pats)
+    assert part.shape == (z1 - z0, N, N)
+    assert ps.planar == planar
+    np.testing.assert_allclose(part, full[z0:z1], rtol=1e-5, atol=1e-7 * np.abs(full).max())
+    G = rng.uniform(-1, 1, (N, N, N)).astype(np.float32)
+    Gz = np.zeros_like(G)
+    Gz[z0:z1] = G[z0:z1]
+    gfull = proj.adjoint(torch.as_tensor(Gz, device="cuda:0"), n, None, 1, 0).cpu().numpy()
+    gs = ps.adjoint(torch.as_tensor(G[z0:z1].copy(), device="cuda:0"), pats.size, None, 1, 0).cpu().numpy()
+    ref = gfull.reshape(A, N, N)[:, r0:r1, :].reshape(-1)
+    assert rel_l2(gs, ref) < 1e-5
