@@ -205,7 +205,7 @@ def main():
         },
         "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "tvam_fwd_planar_kernel" if prob.proj.planar else "tvam_tile_kernel<FWD>",
+                     "kernel": "tvam_fwd_planar_kernel" if prob.proj.planar_forward else "tvam_tile_kernel<FWD>",
                      "alg_bytes_per_launch": alg_bytes,
                      "note": "SURVEY 8(d) algorithmic bytes (per-visit dose RMW); the LDS / register-resident "
                              "kernels move far fewer real bytes, so frac > 1 means past the naive HBM roofline "

@@ -33,6 +33,18 @@ def benchy_index_matched(N: int = 400, angles: int | None = None, size_mm: float
     }
 
 
+def cylindrical_refraction(N: int = 400, angles: int | None = None, size_mm: float = 10.0, r_int: float = 8.0,
+                           r_ext: float = 9.0, vial_ior: float = 1.54, medium_ior: float = 1.40,
+                           sigma_t: float = 0.03, spp: int = 1, regular_sampling: bool = True, n_steps: int = 40):
+    """Config 3 (BASELINE.json): the config 2 scene in a glass tube (r_int / r_ext, dielectric
+    interfaces air|glass|resin; IORs of tests/files/box_hole_cylindrical.json), no scattering."""
+    cfg = benchy_index_matched(N=N, angles=angles, size_mm=size_mm, sigma_t=sigma_t, spp=spp,
+                               regular_sampling=regular_sampling, n_steps=n_steps)
+    cfg["vial"] = {"type": "cylindrical", "r_int": r_int, "r_ext": r_ext, "ior": vial_ior, "height": 40.0,
+                   "medium": {"ior": medium_ior, "extinction": sigma_t, "albedo": 0.0}}
+    return cfg
+
+
 # tests/files/box_hole_index_matched.json of the reference (data, restated)
 BOX_HOLE_INDEX_MATCHED = {
     "vial": {"type": "index_matched", "r": 2.9,

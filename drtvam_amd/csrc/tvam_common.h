@@ -39,8 +39,12 @@ struct TvamConsts {
     float dist_m_zc;     // distance - 0.005 (camera-space z of ray origins)
     int32_t clockwise, regular, sample_time;
     int32_t skip_zero;   // forward: rays with pattern value 0 add exactly 0 -> skipped
-    // container (geometry.py:75-96)
-    float vial_r, vial_half_h;
+    // container (geometry.py:75-96, :142-183)
+    int32_t vial_type;   // TVAM_VIAL_*
+    int32_t max_depth;   // path depth limit (volume.py:272)
+    float vial_r, vial_half_h;  // index-matched r / cylindrical r_int; half height
+    float vial_r_ext;    // cylindrical: outer glass radius
+    float eta_ext, eta_int;     // cylindrical: int/ext IOR of the outer (glass/air) and inner (medium/glass) surface
     // medium / weights
     float nsig2;         // -sigma_t * log2(e): exp(-st t) == exp2(nsig2 t)
     float wscale;        // inv_pdf/n_samples * print_time * sa/st (projector.py:164-165,187; common.py:111; sensor.py:404)
@@ -142,6 +146,102 @@ TVAM_HD bool tvam_segment_im(const TvamConsts& k, float ox, float oy, float oz, 
     if (!(u1 > 0.0f)) return false;
     maxt = u1;
     return true;
+}
+
+#define TVAM_IOR_AIR 1.000277f  // Mitsuba ior table: 'air'
+
+// Nearest hit t >= 0 of the open tube of radius r (Mitsuba cylinder restated;
+// planar rays: the z test is the caller's).
+TVAM_HD float tvam_tube_hit(float ox, float oy, float dx, float dy, float r) {
+    float t0, t1;
+    if (!tvam_cyl_roots(ox, oy, dx, dy, r, t0, t1)) return TVAM_INF;
+    if (!(t1 >= 0.0f)) return TVAM_INF;
+    return t0 >= 0.0f ? t0 : t1;
+}
+
+// Mitsuba dielectric sample() with only the transmission lobe, in the tube's
+// shading frame (s = dp_du / |dp_du| = (-n.y, n.x), n outward): fresnel(),
+// refract(wi, cos_t, eta_ti), weight (1 - F) eta_ti^2 (Radiance mode).
+// eta = int_ior / ext_ior.  Returns the weight, 0 on total internal reflection.
+TVAM_HD float tvam_transmit(float nx, float ny, float dx, float dy, float eta, float& wx, float& wy) {
+    const float sx = -ny, sy = nx;
+    const float wl_x = -(dx * sx + dy * sy);  // wi = to_local(-d)
+    const float cos_i = -(dx * nx + dy * ny);
+    const bool outside = cos_i >= 0.0f;
+    const float rcp_eta = 1.0f / eta;
+    const float eta_it = outside ? eta : rcp_eta, eta_ti = outside ? rcp_eta : eta;
+    const float ct2 = 1.0f - (1.0f - cos_i * cos_i) * (eta_ti * eta_ti);
+    const float ci = fabsf(cos_i), ct = sqrtf(fmaxf(ct2, 0.0f));
+    float r;
+    if (eta == 1.0f) r = 0.0f;
+    else if (ci == 0.0f) r = 1.0f;
+    else {
+        const float a_s = (ci - eta_it * ct) / (ci + eta_it * ct);
+        const float a_p = (ct - eta_it * ci) / (ct + eta_it * ci);
+        r = 0.5f * (a_s * a_s + a_p * a_p);
+    }
+    const float cos_t = outside ? -ct : ct;
+    const float t = 1.0f - r;
+    if (!(t > 0.0f)) return 0.0f;
+    const float ox = -eta_ti * wl_x;  // refract: (-eta_ti wi.x, -eta_ti wi.y, cos_t)
+    wx = sx * ox + nx * cos_t;        // to_world
+    wy = sy * ox + ny * cos_t;
+    return t * (eta_ti * eta_ti);
+}
+
+// Cylindrical vial (geometry.py:142-183, volume.py:179-272 transmission-only):
+// surface hits in order (nearest of the r_ext / r_int tubes), transmission
+// and spawn_ray at each, until the ray runs inside r_int; the medium segment
+// (o2, d2, [0, maxt]) ends at its next hit.  weight = product of the
+// interfaces' transmission weights.
+TVAM_HD bool tvam_segment_cyl(const TvamConsts& k, float ox, float oy, float oz, float dx, float dy, float& o2x,
+                              float& o2y, float& d2x, float& d2y, float& maxt, float& weight) {
+    if (!(oz >= -k.vial_half_h && oz <= k.vial_half_h)) return false;  // passes above / below the tubes
+    float px = ox, py = oy, vx = dx, vy = dy, att = 1.0f;
+    bool in_medium = false;
+    for (int depth = 0; depth < k.max_depth; ++depth) {
+        const float te = tvam_tube_hit(px, py, vx, vy, k.vial_r_ext), ti = tvam_tube_hit(px, py, vx, vy, k.vial_r);
+        const bool inner = ti <= te;
+        const float t = inner ? ti : te;
+        if (!(t < TVAM_INF)) return false;
+        if (in_medium) {
+            o2x = px;
+            o2y = py;
+            d2x = vx;
+            d2y = vy;
+            maxt = t;
+            weight = att;
+            return true;
+        }
+        const float hx = fmaf(vx, t, px), hy = fmaf(vy, t, py);
+        const float rp = sqrtf(hx * hx + hy * hy);
+        const float nx = hx / rp, ny = hy / rp;
+        float wx, wy;
+        const float w = tvam_transmit(nx, ny, vx, vy, inner ? k.eta_int : k.eta_ext, wx, wy);
+        if (!(w > 0.0f)) return false;
+        att = att * w;
+        const float m = fmaxf(fmaxf(fabsf(hx), fabsf(hy)), fabsf(oz));
+        float mag = (1.0f + m) * TVAM_RAY_EPS;
+        const float nwo = nx * wx + ny * wy + 0.0f;
+        if (__builtin_signbit(nwo)) mag = -mag;
+        px = fmaf(mag, nx, hx);
+        py = fmaf(mag, ny, hy);
+        vx = wx;
+        vy = wy;
+        in_medium = inner && nwo < 0.0f;
+    }
+    return false;
+}
+
+// The medium segment of a planar projector ray for the plan's container.
+TVAM_HD bool tvam_segment(const TvamConsts& k, float ox, float oy, float oz, float dx, float dy, float& o2x,
+                          float& o2y, float& d2x, float& d2y, float& maxt, float& weight) {
+    if (k.vial_type == 1 /* TVAM_VIAL_CYLINDRICAL */)
+        return tvam_segment_cyl(k, ox, oy, oz, dx, dy, o2x, o2y, d2x, d2y, maxt, weight);
+    d2x = dx;
+    d2y = dy;
+    weight = 1.0f;
+    return tvam_segment_im(k, ox, oy, oz, dx, dy, o2x, o2y, maxt);
 }
 
 // z slice of a planar ray with origin height oz: the DDA's start voxel z

@@ -15,6 +15,8 @@ struct TvamTiles {
     const float4* ang;         // [n_shard] {tstep_x, tstep_y, step_x, step_y} (sensor.py:343, :360)
     const float4* ray_f;       // [n_shard*crop_y*crop_x*spp] {t_start, tau_end, dtmax0_x, dtmax0_y}
     const int2* ray_i;         // same index: {start voxel x | y << 16, z-slice or -1}
+    const float4* ray_g;       // same index, refracting vials only: {+-tstep_x, +-tstep_y (sign = step),
+                               // interface weight, 0}; nullptr: straight rays (per-angle ang[])
     int32_t ntx, nty, tsx, tsy;
     int32_t n_shard;
     uint32_t spp, seed;
@@ -27,6 +29,7 @@ struct TvamPlanar {
     float4* vox;               // [ns][crop_x] {qx, qy, t_end, 0} (voxel-driven forward)
     float4* rec_f;             // [ns][crop_x] {t_start, tau_end, dtmax0_x, dtmax0_y} (tile DDA resume)
     int32_t* rec_i;            // [ns][crop_x] start voxel x | y << 16, -1 if the ray misses
+    float4* rec_g;             // [ns][crop_x] refracting vials: {+-tstep_x, +-tstep_y, weight, 0}; else nullptr
     const int32_t* slice_off;  // [res_z + 1] CSR: DMD rows whose rays lie in each slice
     const int32_t* slice_rows;
     int32_t ns;
@@ -61,7 +64,7 @@ hipError_t tvam_launch_tiles(int mode, const TvamConsts& k, const TvamTiles& t, 
 // Per-ray pre-pass: ray generation, vial segment and DDA initialisation of
 // every ray of the shard, stored as the records the tile kernels resume from.
 hipError_t tvam_launch_ray_setup(const TvamConsts& k, const TvamTiles& t, float4* ray_f, int2* ray_i,
-                                 hipStream_t stream);
+                                 float4* ray_g, hipStream_t stream);
 
 hipError_t tvam_launch_scatter(const TvamConsts& k, const float* data, const uint32_t* pixels,
                                uint64_t n, float* dense, int32_t* idxmap, hipStream_t stream);

@@ -144,13 +144,14 @@ struct TvamTileRay {
     int64_t local, act;
     int lidx, sx, sy;
     float t, rem, dtx, dty, tsx, tsy;
+    float weight;  // interfaces' transmission weight (refracting vials; 1 otherwise)
 };
 
 // Ray record pre-pass (one thread per ray of the shard): ray generation
 // (common.py:81-108), index-matched vial segment (volume.py:179-216) and DDA
 // initialisation (sensor.py:327-365).  Record index = local * spp + sample.
 __global__ __launch_bounds__(256) void tvam_ray_setup_kernel(TvamConsts k, TvamTiles tp, float4* __restrict__ ray_f,
-                                                             int2* __restrict__ ray_i) {
+                                                             int2* __restrict__ ray_i, float4* __restrict__ ray_g) {
     const int spp = (int)tp.spp;
     const int64_t per_angle = (int64_t)k.crop_y * k.crop_x;
     const int64_t n = (int64_t)tp.n_shard * per_angle * spp;
@@ -173,26 +174,29 @@ __global__ __launch_bounds__(256) void tvam_ray_setup_kernel(TvamConsts k, TvamT
         tvam_ray_camera(k, k.crop_off_x + colc, k.crop_off_y + rowc, jx, jy, xc, yc);
         tvam_ray_world(k, csv.x, csv.y, xc, yc, ox, oy, oz, dx, dy);
         int slice = tvam_slice_of(k, oz);
-        float o2x, o2y, maxt;
+        float o2x, o2y, d2x, d2y, maxt, wgt;
         TvamDda q;
-        if (slice < 0 || !tvam_segment_im(k, ox, oy, oz, dx, dy, o2x, o2y, maxt) ||
-            !tvam_dda_init(k, o2x, o2y, dx, dy, maxt, q)) {
+        if (slice < 0 || !tvam_segment(k, ox, oy, oz, dx, dy, o2x, o2y, d2x, d2y, maxt, wgt) ||
+            !tvam_dda_init(k, o2x, o2y, d2x, d2y, maxt, q)) {
             ray_f[i] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
             ray_i[i] = make_int2(0, -1);
+            if (ray_g) ray_g[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             continue;
         }
         ray_f[i] = make_float4(q.t_start, q.tau_end, q.dtm0[0], q.dtm0[1]);
         ray_i[i] = make_int2(q.sv[0] | (q.sv[1] << 16), slice);
+        if (ray_g)
+            ray_g[i] = make_float4(q.step[0] > 0 ? q.ts[0] : -q.ts[0], q.step[1] > 0 ? q.ts[1] : -q.ts[1], wgt, 0.0f);
     }
 }
 
 hipError_t tvam_launch_ray_setup(const TvamConsts& k, const TvamTiles& t, float4* ray_f, int2* ray_i,
-                                 hipStream_t stream) {
+                                 float4* ray_g, hipStream_t stream) {
     const int64_t n = (int64_t)t.n_shard * k.crop_y * k.crop_x * t.spp;
     int64_t g = (n + 255) / 256;
     if (g > 65536) g = 65536;
     if (g < 1) g = 1;
-    hipLaunchKernelGGL(tvam_ray_setup_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, t, ray_f, ray_i);
+    hipLaunchKernelGGL(tvam_ray_setup_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, t, ray_f, ray_i, ray_g);
     return hipGetLastError();
 }
 
@@ -211,7 +215,15 @@ __device__ __forceinline__ bool tvam_tile_ray(const TvamConsts& k, const TvamTil
     const int2 ii = tp.ray_i[ri];
     if (ii.y != kz + k.z0) return false;  // misses the grid / vial, or lies in another z-slice
     const float4 ff = tp.ray_f[ri];
-    const float4 an = tp.ang[al];
+    float4 an;
+    r.weight = 1.0f;
+    if (tp.ray_g) {  // refracted ray: its own direction (signed step times) and weight
+        const float4 gg = tp.ray_g[ri];
+        an = make_float4(fabsf(gg.x), fabsf(gg.y), gg.x < 0.0f ? -1.0f : 1.0f, gg.y < 0.0f ? -1.0f : 1.0f);
+        r.weight = gg.z;
+    } else {
+        an = tp.ang[al];
+    }
     const int svx = ii.x & 0xffff, svy = ii.x >> 16;
     const int stx = (int)an.z, sty = (int)an.w;
     float tin0, tout0, tin1, tout1;
@@ -392,6 +404,7 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
         }
         TvamTileRay r;
         if (!tvam_tile_ray(k, tp, kz, x0, x1, y0, y1, rowc, al, colc, smp, idxmap, r)) continue;
+        if (MODE == TVAM_MODE_FWD) em *= r.weight;  // attenuation of the vial's interfaces (sensor.py:404)
         TvamMarchRay m;
         m.pv = reinterpret_cast<char*>(tile) + r.lidx * ESZ;
         m.Tx = r.dtx;
@@ -412,7 +425,7 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
                 tvam_march<ACC_FLOAT>(m, r.tsx, r.tsy, sxb, syb, k.nsig2, acc, nvis);
         } else if (MODE == TVAM_MODE_ADJ) {
             tvam_march<ACC_GATHER>(m, r.tsx, r.tsy, sxb, syb, k.nsig2, acc, nvis);
-            atomicAdd(&out[r.act], acc * k.wscale);  // backward_from(Le * em_grad), volume.py:274-276
+            atomicAdd(&out[r.act], acc * (k.wscale * r.weight));  // backward_from(Le * em_grad), volume.py:274-276
         } else {
             tvam_march<ACC_COUNT>(m, r.tsx, r.tsy, sxb, syb, k.nsig2, acc, nvis, reinterpret_cast<const char*>(tile),
                                   tw, wx, wy);

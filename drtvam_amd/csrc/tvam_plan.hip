@@ -39,7 +39,8 @@ struct tvam_plan {
     int32_t ntiles;
     size_t lds_bytes;
     int32_t max_rows_per_slice;
-    bool empty;  // max_depth < 2: no ray reaches the medium
+    bool empty;  // max_depth too small for any ray to reach the medium
+    bool cyl;    // refracting (cylindrical) vial: per-ray directions and weights
     // device tables
     float2* d_cs = nullptr;
     int32_t* d_slice_off = nullptr;
@@ -52,12 +53,14 @@ struct tvam_plan {
     // them call-independent; otherwise they are keyed on (spp, seed)
     float4* d_ray_f = nullptr;
     int2* d_ray_i = nullptr;
+    float4* d_ray_g = nullptr;
     uint64_t ray_cap = 0;
     bool ray_valid = false;
     uint32_t ray_spp = 0, ray_seed = 0;
     hipEvent_t ray_ready = nullptr;
     // planar fast path (regular sampling; tvam_planar.hip)
-    bool planar = false;
+    bool planar = false;      // planar adjoint
+    bool planar_fwd = false;  // voxel-driven planar forward (straight rays only)
     int32_t planar_fz = 16, planar_az = 4;
     TvamPlanar pl{};
     int32_t* d_pl_slice_off = nullptr;
@@ -67,6 +70,9 @@ struct tvam_plan {
     int32_t* d_pl_fwd_cb = nullptr;
     float4* d_pl_rec_f = nullptr;
     int32_t* d_pl_rec_i = nullptr;
+    float4* d_pl_rec_g = nullptr;
+    std::vector<float4> fwd_ang_h;  // host staging of the forward tables (plan creation only)
+    std::vector<int32_t> fwd_cb_h;
     // sparse scratch (dense crop layout), allocated on first sparse call
     float* d_dense = nullptr;
     int32_t* d_idxmap = nullptr;
@@ -120,6 +126,7 @@ static void plan_free(tvam_plan* p) {
     (void)hipFree(p->d_ang);
     (void)hipFree(p->d_ray_f);
     (void)hipFree(p->d_ray_i);
+    (void)hipFree(p->d_ray_g);
     if (p->ray_ready) (void)hipEventDestroy(p->ray_ready);
     (void)hipFree(p->d_dense);
     (void)hipFree(p->d_idxmap);
@@ -130,6 +137,7 @@ static void plan_free(tvam_plan* p) {
     (void)hipFree(p->d_pl_fwd_cb);
     (void)hipFree(p->d_pl_rec_f);
     (void)hipFree(p->d_pl_rec_i);
+    (void)hipFree(p->d_pl_rec_g);
     delete p;
 }
 
@@ -147,12 +155,15 @@ static int validate(const tvam_desc& d) {
     if (d.projector_type != TVAM_PROJECTOR_COLLIMATED)
         return fail(TVAM_ERR_UNSUPPORTED, "only the 'collimated' projector is implemented on the GPU path");
     if (d.sensor_type != TVAM_SENSOR_DDA) return fail(TVAM_ERR_UNSUPPORTED, "only the 'dda' sensor is implemented");
-    if (d.vial_type != TVAM_VIAL_INDEX_MATCHED)
-        return fail(TVAM_ERR_UNSUPPORTED, "only the 'index_matched' container is implemented on the GPU path");
+    if (d.vial_type != TVAM_VIAL_INDEX_MATCHED && d.vial_type != TVAM_VIAL_CYLINDRICAL)
+        return fail(TVAM_ERR_UNSUPPORTED, "only the 'index_matched' and 'cylindrical' containers are implemented on the GPU path");
     if (d.film_channels != 1) return fail(TVAM_ERR_UNSUPPORTED, "surface-aware films (2 channels) are not implemented");
     if (d.albedo != 0.0f) return fail(TVAM_ERR_UNSUPPORTED, "scattering media (albedo > 0) are not implemented");
     if (d.sample_time) return fail(TVAM_ERR_UNSUPPORTED, "sample_time is not implemented on the GPU path");
-    if (d.rr_depth < 1) return fail(TVAM_ERR_UNSUPPORTED, "rr_depth < 1 (Russian roulette inside the medium) is not implemented");
+    // the medium segment is path vertex 1 (index matched) or 2 (behind two glass
+    // surfaces); Russian roulette starts at depth > rr_depth (volume.py:182-185)
+    if (d.rr_depth < (d.vial_type == TVAM_VIAL_CYLINDRICAL ? 2 : 1))
+        return fail(TVAM_ERR_UNSUPPORTED, "Russian roulette before the medium segment (rr_depth too small) is not implemented");
     if (d.n_patterns <= 0 || d.res_x <= 0 || d.res_y <= 0) return fail(TVAM_ERR_INVALID, "projector resolution and n_patterns must be positive");
     if (d.crop_x <= 0 || d.crop_y <= 0 || d.crop_x > d.res_x || d.crop_y > d.res_y)
         return fail(TVAM_ERR_INVALID, "Crop resolution must be smaller than the base resolution.");  // projector.py:81-82
@@ -164,6 +175,9 @@ static int validate(const tvam_desc& d) {
         if (!(d.bbox_max[a] > d.bbox_min[a])) return fail(TVAM_ERR_INVALID, "sensor bounding box is empty");
     }
     if (!(d.vial_r > 0.0f)) return fail(TVAM_ERR_INVALID, "vial radius must be positive");
+    if (d.vial_type == TVAM_VIAL_CYLINDRICAL &&
+        !(d.vial_r_ext > d.vial_r && d.vial_ior > 0.0f && d.medium_ior > 0.0f && d.vial_height > 0.0f))
+        return fail(TVAM_ERR_INVALID, "cylindrical vial: need r_ext > r_int > 0 and positive IORs");
     {
         const int z1 = d.slab_end < 0 ? d.film_res[2] : d.slab_end;
         if (d.slab_begin < 0 || z1 > d.film_res[2] || d.slab_begin >= z1)
@@ -205,8 +219,13 @@ static TvamConsts make_consts(const tvam_desc& d, int a0, int a1) {
     k.regular = d.regular_sampling;
     k.sample_time = d.sample_time;
     k.skip_zero = (d.flags & TVAM_FLAG_NO_ZERO_SKIP) ? 0 : 1;
+    k.vial_type = d.vial_type;
+    k.max_depth = d.max_depth;
     k.vial_r = d.vial_r;
     k.vial_half_h = 0.5f * d.vial_height;
+    k.vial_r_ext = d.vial_r_ext;
+    k.eta_ext = d.vial_ior / TVAM_IOR_AIR;   // int/ext IOR of the outer surface (geometry.py:160-170)
+    k.eta_int = d.medium_ior / d.vial_ior;   // and of the inner one (geometry.py:171-183)
     k.nsig2 = -d.sigma_t * 1.44269504088896340736f;
     k.wscale = 0.0f;  // per call
     {
@@ -238,6 +257,8 @@ static int env_int(const char* name, int def) {
 // row-independent (|z| <= 0.7 r < r / sqrt(2) <= max(|p_x|, |p_y|) on the
 // vial wall).  Builds the row -> slice CSR of valid rows and the per-(angle,
 // column) ray table (computed once, here).
+static bool planar_fwd_setup(tvam_plan* p, const std::vector<float2>& cs, const std::vector<int32_t>& off);
+
 static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     const tvam_desc& d = p->desc;
     const TvamConsts& k = p->k;
@@ -265,6 +286,55 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     int32_t mrc = 0;
     for (int z0 = 0; z0 < k.nz; z0 += p->planar_az)
         mrc = std::max<int32_t>(mrc, off[std::min(z0 + p->planar_az, k.nz)] - off[z0]);
+    p->pl.ns = ns;
+    p->pl.max_rows_chunk = mrc;
+    p->pl.adj_pitch = p->tiles.tsx + 2 + std::max(0, env_int("TVAM_ADJ_PITCH_PAD", 0));
+    p->pl.xcd_remap = env_int("TVAM_XCD_REMAP", 1);
+    // Refracted rays are not parallel: only the ray-driven adjoint (one record
+    // per (angle, column), shared by all slices) applies; the forward runs the
+    // per-ray tile kernel.
+    p->planar_fwd = !p->cyl;
+    if (p->planar_fwd && !planar_fwd_setup(p, cs, off)) p->planar_fwd = false;
+    if (!p->planar_fwd && !p->cyl) return 0;  // DMD much finer than the voxels: general path
+    if (tvam_planar_adj_lds(p->pl, p->tiles, p->planar_az) > 160 * 1024) p->planar_az = 4;
+    if (tvam_planar_adj_lds(p->pl, p->tiles, p->planar_az) > 160 * 1024) return 0;  // tile too large: general path
+    int rc;
+    const size_t nrec = (size_t)std::max(ns, 1) * d.crop_x;
+    hipError_t e;
+    if ((rc = upload(&p->d_pl_slice_off, off)) || (rc = upload(&p->d_pl_slice_rows, rows))) return rc;
+    if (p->planar_fwd) {
+        if ((rc = upload(&p->d_pl_fwd_ang, p->fwd_ang_h)) || (rc = upload(&p->d_pl_fwd_cb, p->fwd_cb_h))) return rc;
+        p->pl.fwd_ang = p->d_pl_fwd_ang;
+        p->pl.fwd_cb = p->d_pl_fwd_cb;
+    }
+    p->fwd_ang_h.clear();
+    p->fwd_cb_h.clear();
+    if ((e = hipMalloc((void**)&p->d_pl_vox, nrec * sizeof(float4))) != hipSuccess ||
+        (e = hipMalloc((void**)&p->d_pl_rec_f, nrec * sizeof(float4))) != hipSuccess ||
+        (e = hipMalloc((void**)&p->d_pl_rec_i, nrec * sizeof(int32_t))) != hipSuccess ||
+        (p->cyl && (e = hipMalloc((void**)&p->d_pl_rec_g, nrec * sizeof(float4))) != hipSuccess))
+        return hip_fail(e, "hipMalloc (planar tables)");
+    p->pl.cs = p->d_cs;
+    p->pl.vox = p->d_pl_vox;
+    p->pl.rec_f = p->d_pl_rec_f;
+    p->pl.rec_i = p->d_pl_rec_i;
+    p->pl.rec_g = p->d_pl_rec_g;
+    p->pl.slice_off = p->d_pl_slice_off;
+    p->pl.slice_rows = p->d_pl_slice_rows;
+    if (ns > 0) {
+        if ((e = tvam_launch_planar_rays(k, p->pl, nullptr)) != hipSuccess) return hip_fail(e, "planar ray table");
+        if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "planar ray table");
+    }
+    p->planar = true;
+    return 0;
+}
+
+// Voxel-driven forward tables (straight rays); false when the DMD is too fine
+// for the staged column window.
+static bool planar_fwd_setup(tvam_plan* p, const std::vector<float2>& cs, const std::vector<int32_t>& off) {
+    const tvam_desc& d = p->desc;
+    const TvamConsts& k = p->k;
+    const int ns = (int)cs.size();
     // Forward (voxel-driven) tables.  Per angle, in the kernel's fp32 ops:
     // u(X, Y) = X * (s du) + Y * (-c du) + u0 is the crop column whose ray has
     // lateral coordinate X s - Y c (common.py:96-99: x_c = W a (0.5 - u));
@@ -306,48 +376,136 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
             need = std::max(need, (int)std::ceil(umax - w) + 1 + nc - cb);
         }
     }
-    p->pl.ns = ns;
     p->pl.marg_u = (float)marg_u;
     p->pl.u0 = u0;
     p->pl.fwd_nc = nc;
-    p->pl.xcd_remap = env_int("TVAM_XCD_REMAP", 1);
     p->pl.ncmax = need;
     {
         bool multi = false;
         for (int z = 0; z < k.nz; ++z) multi |= off[z + 1] - off[z] > 1;
         p->pl.fwd_multi = multi ? 1 : 0;
     }
-    p->pl.max_rows_chunk = mrc;
-    p->pl.adj_pitch = p->tiles.tsx + 2 + std::max(0, env_int("TVAM_ADJ_PITCH_PAD", 0));
     while (p->planar_fz > 8 && !tvam_planar_fwd_fits(p->pl, p->planar_fz)) p->planar_fz /= 2;
     p->pl.fwd_pf = (p->pl.ncmax * p->planar_fz + 255) / 256 <= 2 ? 2 : 4;
-    if (!tvam_planar_fwd_fits(p->pl, p->planar_fz)) return 0;  // DMD much finer than the voxels: general path
-    if (tvam_planar_adj_lds(p->pl, p->tiles, p->planar_az) > 160 * 1024) p->planar_az = 4;
-    if (tvam_planar_adj_lds(p->pl, p->tiles, p->planar_az) > 160 * 1024) return 0;  // tile too large: general path
-    int rc;
-    const size_t nrec = (size_t)std::max(ns, 1) * d.crop_x;
-    hipError_t e;
-    if ((rc = upload(&p->d_pl_slice_off, off)) || (rc = upload(&p->d_pl_slice_rows, rows)) ||
-        (rc = upload(&p->d_pl_fwd_ang, fang)) || (rc = upload(&p->d_pl_fwd_cb, fcb)))
-        return rc;
-    p->pl.fwd_ang = p->d_pl_fwd_ang;
-    p->pl.fwd_cb = p->d_pl_fwd_cb;
-    if ((e = hipMalloc((void**)&p->d_pl_vox, nrec * sizeof(float4))) != hipSuccess ||
-        (e = hipMalloc((void**)&p->d_pl_rec_f, nrec * sizeof(float4))) != hipSuccess ||
-        (e = hipMalloc((void**)&p->d_pl_rec_i, nrec * sizeof(int32_t))) != hipSuccess)
-        return hip_fail(e, "hipMalloc (planar tables)");
-    p->pl.cs = p->d_cs;
-    p->pl.vox = p->d_pl_vox;
-    p->pl.rec_f = p->d_pl_rec_f;
-    p->pl.rec_i = p->d_pl_rec_i;
-    p->pl.slice_off = p->d_pl_slice_off;
-    p->pl.slice_rows = p->d_pl_slice_rows;
-    if (ns > 0) {
-        if ((e = tvam_launch_planar_rays(k, p->pl, nullptr)) != hipSuccess) return hip_fail(e, "planar ray table");
-        if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "planar ray table");
-    }
-    p->planar = true;
-    return 0;
+    if (!tvam_planar_fwd_fits(p->pl, p->planar_fz)) return false;
+    p->fwd_ang_h = std::move(fang);
+    p->fwd_cb_h = std::move(fcb);
+    return true;
+}
+
+
+// Slot lists behind a refracting (cylindrical) vial.  A column's rays are no
+// longer one straight line per angle: each sub-pixel position u is traced
+// through the glass (tvam_segment, the kernels' own fp32 code) to its medium
+// chord, and the tiles within `marg` of that chord are marked.  Jittered
+// sampling covers u in [0, 1] by bisection until neighbouring chords' end
+// points are within a quarter voxel (or their hit status flips at a grazing /
+// total-internal-reflection boundary, refined to 2^-12 of a pixel), and marks
+// each pair with their end-point distance as extra margin: the chords of the
+// rays in between lie in the quadrilateral the pair spans.
+namespace {
+struct CylChord {
+    bool hit;
+    double ax, ay, bx, by;
+};
+
+CylChord cyl_chord(const TvamConsts& k, float c, float s, int col, float u) {
+    CylChord ch{false, 0, 0, 0, 0};
+    float xc, yc, ox, oy, oz, dx, dy, o2x, o2y, d2x, d2y, maxt, w;
+    tvam_ray_camera(k, col, 0, u, 0.5f, xc, yc);
+    tvam_ray_world(k, c, s, xc, 0.0f, ox, oy, oz, dx, dy);
+    if (!tvam_segment(k, ox, oy, 0.0f, dx, dy, o2x, o2y, d2x, d2y, maxt, w)) return ch;
+    ch.hit = true;
+    ch.ax = o2x;
+    ch.ay = o2y;
+    ch.bx = (double)o2x + (double)maxt * d2x;
+    ch.by = (double)o2y + (double)maxt * d2y;
+    return ch;
+}
+
+double chord_dist(const CylChord& a, const CylChord& b) {
+    return std::max(std::hypot(a.ax - b.ax, a.ay - b.ay), std::hypot(a.bx - b.bx, a.by - b.by));
+}
+
+struct TileGrid {
+    double x0, y0, wx, wy;  // origin and tile size
+    int ntx, nty;
+};
+
+// Mark the tiles whose box, grown by m, meets the segment a -> b (slab clip).
+template <typename F>
+void mark_tiles(const TileGrid& g, const CylChord& ch, double m, F&& mark) {
+    const double lox = std::min(ch.ax, ch.bx) - m, hix = std::max(ch.ax, ch.bx) + m;
+    const double loy = std::min(ch.ay, ch.by) - m, hiy = std::max(ch.ay, ch.by) + m;
+    const int tx0 = std::max(0, (int)std::floor((lox - g.x0) / g.wx)), tx1 = std::min(g.ntx - 1, (int)std::floor((hix - g.x0) / g.wx));
+    const int ty0 = std::max(0, (int)std::floor((loy - g.y0) / g.wy)), ty1 = std::min(g.nty - 1, (int)std::floor((hiy - g.y0) / g.wy));
+    const double dx = ch.bx - ch.ax, dy = ch.by - ch.ay;
+    for (int ty = ty0; ty <= ty1; ++ty)
+        for (int tx = tx0; tx <= tx1; ++tx) {
+            const double bx0 = g.x0 + tx * g.wx - m, bx1 = g.x0 + (tx + 1) * g.wx + m;
+            const double by0 = g.y0 + ty * g.wy - m, by1 = g.y0 + (ty + 1) * g.wy + m;
+            double t0 = 0.0, t1 = 1.0;
+            auto clip = [&](double o, double d, double lo, double hi) {
+                if (std::fabs(d) < 1e-300) return o >= lo && o <= hi;
+                double a = (lo - o) / d, b = (hi - o) / d;
+                if (a > b) std::swap(a, b);
+                t0 = std::max(t0, a);
+                t1 = std::min(t1, b);
+                return t0 <= t1;
+            };
+            if (clip(ch.ax, dx, bx0, bx1) && clip(ch.ay, dy, by0, by1)) mark(ty * g.ntx + tx);
+        }
+}
+}  // namespace
+
+static void cyl_slot_lists(const tvam_desc& d, const TvamConsts& k, const std::vector<float2>& cs, int tsx, int tsy,
+                           int ntx, int nty, double marg, std::vector<std::vector<uint32_t>>& per_tile) {
+    const TileGrid g{(double)k.bmin[0], (double)k.bmin[1], tsx * (double)k.h[0], tsy * (double)k.h[1], ntx, nty};
+    const double hmin = std::min(k.h[0], k.h[1]);
+    per_tile.assign((size_t)ntx * nty, {});
+    std::vector<uint32_t> last((size_t)ntx * nty, 0xffffffffu);
+    const int ns = (int)cs.size();
+    for (int i = 0; i < ns; ++i)
+        for (int col = 0; col < d.crop_x; ++col) {
+            const uint32_t key = ((uint32_t)i << 16) | (uint32_t)col;
+            auto mark = [&](int t) {
+                if (last[t] != key) {
+                    last[t] = key;
+                    per_tile[t].push_back(key);
+                }
+            };
+            const float c = cs[i].x, s = cs[i].y;
+            const int colg = d.crop_offset_x + col;
+            if (d.regular_sampling) {
+                const CylChord ch = cyl_chord(k, c, s, colg, 0.5f);
+                if (ch.hit) mark_tiles(g, ch, marg, mark);
+                continue;
+            }
+            struct Iv {
+                float u0, u1;
+                CylChord a, b;
+                int depth;
+            };
+            std::vector<Iv> st;
+            st.push_back({0.0f, 1.0f, cyl_chord(k, c, s, colg, 0.0f), cyl_chord(k, c, s, colg, 1.0f), 0});
+            while (!st.empty()) {
+                Iv v = st.back();
+                st.pop_back();
+                if (!v.a.hit && !v.b.hit && v.depth >= 4) continue;  // both miss on a 1/16 pixel: between them too
+                const bool mixed = v.a.hit != v.b.hit;
+                const double dd = (v.a.hit && v.b.hit) ? chord_dist(v.a, v.b) : 0.0;
+                if ((mixed || dd > 0.25 * hmin || v.depth < 4) && v.depth < 12) {
+                    const float um = 0.5f * (v.u0 + v.u1);
+                    const CylChord cm = cyl_chord(k, c, s, colg, um);
+                    st.push_back({v.u0, um, v.a, cm, v.depth + 1});
+                    st.push_back({um, v.u1, cm, v.b, v.depth + 1});
+                    continue;
+                }
+                const double m = marg + (mixed ? hmin : dd);
+                if (v.a.hit) mark_tiles(g, v.a, m, mark);
+                if (v.b.hit) mark_tiles(g, v.b, m, mark);
+            }
+        }
 }
 
 extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** out) {
@@ -369,7 +527,10 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
     p->desc = d;
     p->device = device;
     p->k = make_consts(d, a0, a1);
-    p->empty = d.max_depth < 2;  // entry bounce + medium segment (volume.py:179, :271-272)
+    p->cyl = d.vial_type == TVAM_VIAL_CYLINDRICAL;
+    // index matched: entry bounce + medium segment; cylindrical: two glass
+    // surfaces + medium segment (volume.py:179, :271-272)
+    p->empty = d.max_depth < (p->cyl ? 3 : 2);
     const TvamConsts& k = p->k;
     const int ns = a1 - a0;
 
@@ -462,6 +623,15 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
     std::vector<int64_t> slot_off((size_t)p->ntiles + 1, 0);
     std::vector<uint32_t> slots;
     int64_t max_nrt = 0;
+    if (p->cyl) {
+        std::vector<std::vector<uint32_t>> per_tile;
+        cyl_slot_lists(d, k, cs, tsx, tsy, ntx, nty, marg_l + 1e-3 * std::min(k.h[0], k.h[1]), per_tile);
+        for (int t = 0; t < p->ntiles; ++t) {
+            slots.insert(slots.end(), per_tile[t].begin(), per_tile[t].end());
+            slot_off[(size_t)t + 1] = (int64_t)slots.size();
+            max_nrt = std::max<int64_t>(max_nrt, (int64_t)per_tile[t].size());
+        }
+    } else
     for (int ty = 0; ty < nty; ++ty)
         for (int tx = 0; tx < ntx; ++tx) {
             int tile = ty * ntx + tx;
@@ -570,23 +740,27 @@ static int ensure_rays(tvam_plan* p, const TvamConsts& k, TvamTiles& t, hipStrea
     if (n > p->ray_cap) {
         (void)hipFree(p->d_ray_f);
         (void)hipFree(p->d_ray_i);
+        (void)hipFree(p->d_ray_g);
         p->d_ray_f = nullptr;
         p->d_ray_i = nullptr;
+        p->d_ray_g = nullptr;
         p->ray_cap = 0;
         p->ray_valid = false;
         if ((e = hipMalloc((void**)&p->d_ray_f, std::max<uint64_t>(n, 1) * sizeof(float4))) != hipSuccess ||
-            (e = hipMalloc((void**)&p->d_ray_i, std::max<uint64_t>(n, 1) * sizeof(int2))) != hipSuccess)
+            (e = hipMalloc((void**)&p->d_ray_i, std::max<uint64_t>(n, 1) * sizeof(int2))) != hipSuccess ||
+            (p->cyl && (e = hipMalloc((void**)&p->d_ray_g, std::max<uint64_t>(n, 1) * sizeof(float4))) != hipSuccess))
             return hip_fail(e, "hipMalloc (ray records)");
         p->ray_cap = n;
     }
     t.ray_f = p->d_ray_f;
     t.ray_i = p->d_ray_i;
+    t.ray_g = p->d_ray_g;
     const bool hit = p->ray_valid && p->ray_spp == t.spp && (k.regular || p->ray_seed == t.seed);
     if (hit) {
         e = hipStreamWaitEvent(stream, p->ray_ready, 0);
         return e == hipSuccess ? 0 : hip_fail(e, "hipStreamWaitEvent");
     }
-    if ((e = tvam_launch_ray_setup(k, t, p->d_ray_f, p->d_ray_i, stream)) != hipSuccess)
+    if ((e = tvam_launch_ray_setup(k, t, p->d_ray_f, p->d_ray_i, p->d_ray_g, stream)) != hipSuccess)
         return hip_fail(e, "ray setup launch");
     if ((e = hipEventRecord(p->ray_ready, stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     p->ray_valid = true;
@@ -622,7 +796,7 @@ extern "C" int tvam_forward(tvam_plan* p, const float* active_data, const uint32
         pat = p->d_dense;
         idxmap = p->d_idxmap;
     }
-    if (p->planar) {
+    if (p->planar_fwd) {
         if (p->desc.flags & TVAM_FLAG_FWD_STATS) {
             if ((e = hipMemsetAsync(p->d_counter, 0, sizeof(unsigned long long), stream)) != hipSuccess)
                 return hip_fail(e, "hipMemsetAsync");
@@ -708,7 +882,8 @@ extern "C" int tvam_count_visits(tvam_plan* p, uint32_t spp, uint32_t seed, uint
     return 0;
 }
 
-extern "C" int tvam_plan_path(const tvam_plan* p) { return p && p->planar ? 1 : 0; }
+// bit 0: planar adjoint, bit 1: voxel-driven planar forward
+extern "C" int tvam_plan_path(const tvam_plan* p) { return p ? (p->planar ? 1 : 0) | (p->planar_fwd ? 2 : 0) : 0; }
 
 extern "C" int tvam_plan_stats(tvam_plan* p, uint64_t* fallback_tiles) {
     if (!p || !fallback_tiles) return fail(TVAM_ERR_INVALID, "null argument");

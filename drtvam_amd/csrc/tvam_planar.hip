@@ -46,7 +46,8 @@ __device__ __forceinline__ float pl_exp2(float x) { return __builtin_amdgcn_exp2
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void tvam_planar_rays_kernel(TvamConsts k, const float2* __restrict__ cs, int ns,
                                                                float4* __restrict__ vox, float4* __restrict__ rec_f,
-                                                               int32_t* __restrict__ rec_i) {
+                                                               int32_t* __restrict__ rec_i,
+                                                               float4* __restrict__ rec_g) {
     const int64_t n = (int64_t)ns * k.crop_x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int al = (int)(i / k.crop_x), col = (int)(i - (int64_t)al * k.crop_x);
@@ -54,14 +55,20 @@ __global__ __launch_bounds__(256) void tvam_planar_rays_kernel(TvamConsts k, con
         float xc, yc, ox, oy, oz, dx, dy;
         tvam_ray_camera(k, k.crop_off_x + col, k.crop_off_y, 0.5f, 0.5f, xc, yc);
         tvam_ray_world(k, csv.x, csv.y, xc, 0.0f, ox, oy, oz, dx, dy);
-        float o2x, o2y, maxt;
+        float o2x, o2y, d2x, d2y, maxt, wgt;
         TvamDda q;
-        if (!tvam_segment_im(k, ox, oy, 0.0f, dx, dy, o2x, o2y, maxt) || !tvam_dda_init(k, o2x, o2y, dx, dy, maxt, q)) {
+        if (!tvam_segment(k, ox, oy, 0.0f, dx, dy, o2x, o2y, d2x, d2y, maxt, wgt) ||
+            !tvam_dda_init(k, o2x, o2y, d2x, d2y, maxt, q)) {
             vox[i] = make_float4(0.0f, 0.0f, -1.0f, 0.0f);
             rec_f[i] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
             rec_i[i] = -1;
+            if (rec_g) rec_g[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             continue;
         }
+        if (rec_g)
+            rec_g[i] = make_float4(q.step[0] > 0 ? q.ts[0] : -q.ts[0], q.step[1] > 0 ? q.ts[1] : -q.ts[1], wgt, 0.0f);
+        dx = d2x;  // the voxel-driven forward only serves straight rays (d2 == d)
+        dy = d2y;
         const bool vx = fabsf(dx) > 1e-8f, vy = fabsf(dy) > 1e-8f;
         const float qx = vx ? -o2x * (1.0f / dx) : (float)q.sv[0];
         const float qy = vy ? -o2y * (1.0f / dy) : (float)q.sv[1];
@@ -76,7 +83,7 @@ hipError_t tvam_launch_planar_rays(const TvamConsts& k, const TvamPlanar& pl, hi
     int64_t g = (n + 255) / 256;
     g = g > 65536 ? 65536 : (g < 1 ? 1 : g);
     hipLaunchKernelGGL(tvam_planar_rays_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, pl.cs, pl.ns, pl.vox,
-                       pl.rec_f, pl.rec_i);
+                       pl.rec_f, pl.rec_i, pl.rec_g);
     return hipGetLastError();
 }
 
@@ -427,7 +434,15 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_adj_planar_kernel(TvamConsts k, 
         const int ri = pl.rec_i[(size_t)al * k.crop_x + colc];
         if (ri < 0) continue;  // misses the vial / grid
         const float4 ff = pl.rec_f[(size_t)al * k.crop_x + colc];
-        const float4 an = tp.ang[al];
+        float4 an;
+        float wray = 1.0f;
+        if (pl.rec_g) {  // refracted ray: its own direction (signed step times) and weight
+            const float4 gg = pl.rec_g[(size_t)al * k.crop_x + colc];
+            an = make_float4(fabsf(gg.x), fabsf(gg.y), gg.x < 0.0f ? -1.0f : 1.0f, gg.y < 0.0f ? -1.0f : 1.0f);
+            wray = gg.z;
+        } else {
+            an = tp.ang[al];
+        }
         const int svx = ri & 0xffff, svy = ri >> 16;
         const int stx = (int)an.z, sty = (int)an.w;
         float tin0, tout0, tin1, tout1;
@@ -474,7 +489,7 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_adj_planar_kernel(TvamConsts k, 
         const int64_t base = (int64_t)(k.a0 + al) * k.crop_y * k.crop_x + colc - k.shard_base;
 #pragma unroll
         for (int z = 0; z < Z; ++z) {
-            const float v = acc[z] * k.wscale;
+            const float v = acc[z] * (k.wscale * wray);
             for (int q = s_roff[z]; q < s_roff[z + 1]; ++q) {
                 int64_t act = base + (int64_t)s_rows[q] * k.crop_x;
                 if (idxmap) {

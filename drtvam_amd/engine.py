@@ -101,8 +101,13 @@ class Projection:
 
     @property
     def planar(self) -> bool:
-        """True when the planar fast path (regular sampling) serves this plan."""
-        return bool(self.lib.tvam_plan_path(self._plan))
+        """True when the planar fast path (regular sampling) serves this plan's adjoint."""
+        return bool(self.lib.tvam_plan_path(self._plan) & 1)
+
+    @property
+    def planar_forward(self) -> bool:
+        """True when the voxel-driven planar forward serves this plan (straight rays)."""
+        return bool(self.lib.tvam_plan_path(self._plan) & 2)
 
     def fallback_tiles(self) -> int:
         """Workgroups of the last forward that used float LDS atomics (needs FLAG_FWD_STATS)."""

@@ -48,9 +48,27 @@ class Container:
     def _fill_medium(self, desc):
         desc.sigma_t = float(self.sigma_t)
         desc.albedo = float(self.albedo)
-        desc.medium_ior = float(self.medium_ior) if not isinstance(self.medium_ior, str) else 1.0
+        desc.medium_ior = lookup_ior(self.medium_ior)
         if self.occlusions:
             raise NotImplementedError("occluder meshes are not supported by the GPU engine yet")
+
+
+# Named refractive indices (Mitsuba's ior table, restated for the names a config may use)
+IOR_TABLE = {
+    'vacuum': 1.0, 'helium': 1.000036, 'hydrogen': 1.000132, 'air': 1.000277, 'carbon dioxide': 1.00045,
+    'water': 1.3330, 'acetone': 1.36, 'ethanol': 1.361, 'carbon tetrachloride': 1.461, 'glycerol': 1.4729,
+    'benzene': 1.501, 'silicone oil': 1.52045, 'bromine': 1.661, 'water ice': 1.31, 'fused quartz': 1.458,
+    'pyrex': 1.470, 'acrylic glass': 1.49, 'polypropylene': 1.49, 'bk7': 1.5046, 'sodium chloride': 1.544,
+    'amber': 1.55, 'pet': 1.5750, 'diamond': 2.419,
+}
+
+
+def lookup_ior(v) -> float:
+    if isinstance(v, str):
+        if v not in IOR_TABLE:
+            raise ValueError(f"Unknown IOR name '{v}'")
+        return float(IOR_TABLE[v])
+    return float(v)
 
 
 class IndexMatchedVial(Container):
@@ -102,6 +120,14 @@ class CylindricalVial(Container):
                               'bsdf': {'type': 'dielectric', 'ext_ior': self.vial_ior, 'int_ior': self.medium_ior},
                               'interior': {'type': 'ref', 'id': 'printing_medium'}},
         }
+
+    def fill_desc(self, desc):
+        self._fill_medium(desc)
+        desc.vial_type = _abi.VIAL_CYLINDRICAL
+        desc.vial_r = float(self.r_int)
+        desc.vial_r_ext = float(self.r_ext)
+        desc.vial_height = float(self.height)
+        desc.vial_ior = lookup_ior(self.vial_ior)
 
 
 class SquareVial(Container):

@@ -160,9 +160,10 @@ int tvam_adjoint(tvam_plan* plan, const float* grad_dose,
    (needs TVAM_FLAG_FWD_STATS). */
 int tvam_plan_stats(tvam_plan* plan, uint64_t* fallback_tiles);
 
-/* Which kernels serve this plan: 1 = planar fast path (regular sampling:
-   one ray record per (angle, column), voxel-driven forward, Z-slice-sharing
-   adjoint), 0 = per-ray tile kernels. */
+/* Which kernels serve this plan (bit mask; 0 = per-ray tile kernels):
+   bit 0 = planar adjoint (regular sampling: one ray record per (angle,
+   column), Z-slice-sharing adjoint); bit 1 = voxel-driven planar forward
+   (straight rays only: not behind a refracting vial). */
 int tvam_plan_path(const tvam_plan* plan);
 
 /*

@@ -84,10 +84,11 @@ def adjoint(desc, grad_dose, active_pixels=None, n_active=None, spp=1, seed=0, n
 
 
 def ray(desc, pixel, wave_index=0, seed=0):
-    out = np.zeros(11, dtype=np.float32)
+    """Projector ray of one sample and its medium segment (o2, d2, maxt) + interface weight."""
+    out = np.zeros(15, dtype=np.float32)
     lib().oracle_ray(ctypes.byref(desc), pixel, wave_index, seed, _ptr(out))
     return {"o": out[0:3].copy(), "d": out[3:6].copy(), "hit": bool(out[6]), "o2": out[7:10].copy(),
-            "maxt": float(out[10])}
+            "maxt": float(out[10]), "d2": out[11:14].copy(), "weight": float(out[14])}
 
 
 def dda_ray(desc, o, d, maxt, em=1.0):

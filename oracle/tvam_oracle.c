@@ -16,6 +16,14 @@
  *   index-matched     geometry.py:75-96: open cylinder r, height h, null BSDF;
  *     vial            Mitsuba cylinder intersection + SurfaceInteraction
  *                     spawn_ray/offset_p restated (RayEpsilon = 1500*2^-24)
+ *   cylindrical vial  geometry.py:142-183: glass tubes r_ext (air|glass) and
+ *                     r_int (glass|medium), 'dielectric' BSDFs; the path loop
+ *                     of volume.py:179-272 with transmission_only (common.py:19):
+ *                     Mitsuba dielectric sample() restated (fresnel(), refract()
+ *                     in the cylinder's shading frame s = dp_du, n outward,
+ *                     weight (1 - F) * eta_ti^2 in Radiance mode), ior 'air' =
+ *                     1.000277 (Mitsuba ior table).  UNPINNED like the rest of
+ *                     the Mitsuba internals.
  *   path loop         integrators/volume.py:136-282 for the non-scattering,
  *                     transmission-only case: one medium segment per ray
  *   DDA accumulate    sensor.py:306-440 (op for op, fp32 geometry)
@@ -221,6 +229,112 @@ static int or_segment_index_matched(const or_scene* s, const or_ray* ray, float 
 }
 
 /* ------------------------------------------------------------------------ */
+/* Cylindrical vial (geometry.py:142-183): glass tube between r_int and r_ext */
+/* ------------------------------------------------------------------------ */
+#define OR_IOR_AIR 1.000277f
+
+/* Nearest hit t >= 0 of an open tube |z| <= half (Mitsuba cylinder restated). */
+static float or_tube_hit(const float o[3], const float dd[3], float r, float half) {
+    float t0, t1;
+    if (!or_cyl_roots(o, dd, r, &t0, &t1)) return INFINITY;
+    if (!(t1 >= 0.0f)) return INFINITY;
+    float zn = fmaf(dd[2], t0, o[2]), zf = fmaf(dd[2], t1, o[2]);
+    if (t0 >= 0.0f && zn >= -half && zn <= half) return t0;
+    if (zf >= -half && zf <= half) return t1;
+    return INFINITY;
+}
+
+/* Mitsuba fresnel(cos_theta_i, eta): reflectance, cos_theta_t, eta_ti. */
+static float or_fresnel(float cos_i, float eta, float* cos_t, float* eta_ti) {
+    int outside = cos_i >= 0.0f;
+    float rcp_eta = 1.0f / eta;
+    float eta_it = outside ? eta : rcp_eta;
+    *eta_ti = outside ? rcp_eta : eta;
+    float ct2 = 1.0f - (1.0f - cos_i * cos_i) * (*eta_ti * *eta_ti);
+    float ci = fabsf(cos_i), ct = sqrtf(fmaxf(ct2, 0.0f));
+    float r;
+    if (eta == 1.0f) r = 0.0f;
+    else if (ci == 0.0f) r = 1.0f;
+    else {
+        float a_s = (ci - eta_it * ct) / (ci + eta_it * ct);
+        float a_p = (ct - eta_it * ci) / (ct + eta_it * ci);
+        r = 0.5f * (a_s * a_s + a_p * a_p);
+    }
+    *cos_t = outside ? -ct : ct;
+    return r;
+}
+
+/* Transmission through the tube surface point p (outward normal n) for a ray
+   of direction d; eta = int_ior / ext_ior.  Mitsuba dielectric sample() with
+   only the transmission lobe (volume.py:230-237): wo = refract(wi) in the
+   frame (s = dp_du/|dp_du|, t = z, n), weight (1 - F) * eta_ti^2.  Returns
+   the weight (0 on total internal reflection). */
+static float or_transmit(const float n[3], const float d[3], float eta, float wo[3]) {
+    float sx = -n[1], sy = n[0];                           /* dp_du = (-y, x, 0) normalised */
+    float wl_x = -(d[0] * sx + d[1] * sy);                 /* wi = to_local(-d) */
+    float wl_y = -d[2];
+    float wl_z = -(d[0] * n[0] + d[1] * n[1]);
+    float cos_t, eta_ti;
+    float r = or_fresnel(wl_z, eta, &cos_t, &eta_ti);
+    float t = 1.0f - r;
+    if (!(t > 0.0f)) return 0.0f;
+    float ox = -eta_ti * wl_x, oy = -eta_ti * wl_y;        /* refract(wi, cos_t, eta_ti) */
+    wo[0] = sx * ox + n[0] * cos_t;                        /* to_world */
+    wo[1] = sy * ox + n[1] * cos_t;
+    wo[2] = oy;
+    return t * (eta_ti * eta_ti);
+}
+
+/* Medium segment of a projector ray through the glass tube: surface hits in
+   order (nearest of the two tubes), transmission at each, until the ray runs
+   inside the inner tube; the segment ends at its next hit.  Returns 0 when
+   the ray never enters the medium (misses, TIR, or runs out of max_depth). */
+static int or_segment_cylindrical(const or_scene* s, const or_ray* ray, float o2[3], float d2[3], float* maxt,
+                                  double* weight) {
+    const tvam_desc* d = s->d;
+    float half = 0.5f * d->vial_height;
+    float o[3] = {ray->o[0], ray->o[1], ray->o[2]}, dd[3] = {ray->d[0], ray->d[1], ray->d[2]};
+    float att = 1.0f; /* Spectrum attenuation: fp32 products (volume.py:265) */
+    int in_medium = 0;
+    for (int depth = 0; depth < d->max_depth; ++depth) {
+        float te = or_tube_hit(o, dd, d->vial_r_ext, half), ti = or_tube_hit(o, dd, d->vial_r, half);
+        int inner = ti <= te;
+        float t = inner ? ti : te;
+        if (!(t < INFINITY)) return 0;
+        if (in_medium) { /* the medium segment [0, t] (volume.py:209-216) */
+            for (int k = 0; k < 3; ++k) {
+                o2[k] = o[k];
+                d2[k] = dd[k];
+            }
+            *maxt = t;
+            *weight = (double)att;
+            return 1;
+        }
+        float p[3];
+        for (int k = 0; k < 3; ++k) p[k] = fmaf(dd[k], t, o[k]);
+        float rp = sqrtf(p[0] * p[0] + p[1] * p[1]);
+        float n[3] = {p[0] / rp, p[1] / rp, 0.0f};
+        float eta = inner ? d->medium_ior / d->vial_ior : d->vial_ior / OR_IOR_AIR;
+        float wo[3];
+        float w = or_transmit(n, dd, eta, wo);
+        if (!(w > 0.0f)) return 0;
+        att = att * w;
+        /* spawn_ray(si.to_world(bs.wo)): offset_p along n, towards wo */
+        float m = fmaxf(fmaxf(fabsf(p[0]), fabsf(p[1])), fabsf(p[2]));
+        float mag = (1.0f + m) * OR_RAY_EPS;
+        float nwo = n[0] * wo[0] + n[1] * wo[1] + n[2] * wo[2];
+        if (signbit(nwo)) mag = -mag;
+        for (int k = 0; k < 3; ++k) {
+            o[k] = fmaf(mag, n[k], p[k]);
+            dd[k] = wo[k];
+        }
+        /* the inner tube's interior is the printing medium (volume.py:268) */
+        in_medium = inner && nwo < 0.0f;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------ */
 /* DDA (sensor.py:327-438).  mode 0: forward (accumulate into film),          */
 /* mode 1: adjoint (gather grad), mode 2: count only.                        */
 /* ------------------------------------------------------------------------ */
@@ -319,10 +433,13 @@ static uint64_t or_stream(const tvam_desc* d, uint32_t pixel) {
 }
 
 static int or_check(const tvam_desc* d) {
-    if (d->vial_type != TVAM_VIAL_INDEX_MATCHED) return TVAM_ERR_UNSUPPORTED;
+    if (d->vial_type != TVAM_VIAL_INDEX_MATCHED && d->vial_type != TVAM_VIAL_CYLINDRICAL) return TVAM_ERR_UNSUPPORTED;
     if (d->projector_type != TVAM_PROJECTOR_COLLIMATED) return TVAM_ERR_UNSUPPORTED;
     if (d->film_channels != 1) return TVAM_ERR_UNSUPPORTED;
     if (d->albedo != 0.0f) return TVAM_ERR_UNSUPPORTED;
+    /* Russian roulette (volume.py:182-185, depth > rr_depth) before the medium
+       segment (path vertex 1 index matched, 2 behind the glass) is not restated */
+    if (d->rr_depth < (d->vial_type == TVAM_VIAL_CYLINDRICAL ? 2 : 1)) return TVAM_ERR_UNSUPPORTED;
     return 0;
 }
 
@@ -332,6 +449,15 @@ static double or_trace(const or_scene* s, uint32_t pixel, uint64_t wave_index, u
     or_ray ray;
     or_gen_ray(s, pixel, wave_index, seed, &ray);
     float o2[3], maxt;
+    if (s->d->vial_type == TVAM_VIAL_CYLINDRICAL) {
+        float d2[3];
+        double att;
+        if (!or_segment_cylindrical(s, &ray, o2, d2, &maxt, &att)) return 0.0;
+        /* the interfaces' attenuation scales every contribution (sensor.py:404) */
+        if (mode == 0) return or_dda(s, o2, d2, maxt, em * att, mode, film, grad, only_slice, visits);
+        return att * or_dda(s, o2, d2, maxt, em, mode, film, grad, only_slice, visits);
+    }
+    if (s->d->max_depth < 2) return 0.0;
     if (!or_segment_index_matched(s, &ray, o2, &maxt)) return 0.0;
     return or_dda(s, o2, ray.d, maxt, em, mode, film, grad, only_slice, visits);
 }
@@ -448,7 +574,8 @@ int oracle_adjoint(const tvam_desc* d, const float* grad_dose, const uint32_t* a
 }
 
 /* Ray of one sample, for property tests (test_projector.py:7-38 analogue):
-   out = {o.x,o.y,o.z, d.x,d.y,d.z, hit, o'.x,o'.y,o'.z, maxt} */
+   out = {o.x,o.y,o.z, d.x,d.y,d.z, hit, o'.x,o'.y,o'.z, maxt, d'.x,d'.y,d'.z, weight}
+   (o', d', maxt: the medium segment; weight: the interfaces' attenuation). */
 int oracle_ray(const tvam_desc* d, uint32_t pixel, uint64_t wave_index, uint32_t seed, float* out) {
     or_scene s;
     or_scene_init(&s, d);
@@ -458,13 +585,20 @@ int oracle_ray(const tvam_desc* d, uint32_t pixel, uint64_t wave_index, uint32_t
         out[k] = ray.o[k];
         out[3 + k] = ray.d[k];
     }
-    float o2[3] = {0, 0, 0}, maxt = 0.0f;
-    int hit = d->vial_type == TVAM_VIAL_INDEX_MATCHED ? or_segment_index_matched(&s, &ray, o2, &maxt) : 0;
+    float o2[3] = {0, 0, 0}, d2[3] = {ray.d[0], ray.d[1], ray.d[2]}, maxt = 0.0f;
+    double att = 1.0;
+    int hit = 0;
+    if (d->vial_type == TVAM_VIAL_INDEX_MATCHED) hit = or_segment_index_matched(&s, &ray, o2, &maxt);
+    else if (d->vial_type == TVAM_VIAL_CYLINDRICAL) hit = or_segment_cylindrical(&s, &ray, o2, d2, &maxt, &att);
     out[6] = (float)hit;
     out[7] = o2[0];
     out[8] = o2[1];
     out[9] = o2[2];
     out[10] = maxt;
+    out[11] = d2[0];
+    out[12] = d2[1];
+    out[13] = d2[2];
+    out[14] = (float)att;
     return 0;
 }
 
