@@ -8,6 +8,9 @@ index-matched scene, 400^3 voxels, 400 angles, 400x400 DMD, 1 ray/pixel,
 synthetic patterns U[0, 0.1) (seed 0) and an analytic target (benchy.ply is
 not available).  Every ray is marched (zero-pattern skipping disabled).
 
+--config 3 runs BASELINE.json configs[2] instead: the same scene behind a
+cylindrical glass vial (two refracting interfaces per ray).
+
 Multi-GPU: one process per GPU (torch.distributed.run), angles sharded in
 contiguous blocks, dose all-reduced over RCCL twice per iteration, L-BFGS
 dots all-reduced.  Rank 0 prints one JSON line.
@@ -28,16 +31,21 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def cpu_baseline(N, seconds, threads):
+def scene_config(config, N, A):
+    from drtvam_amd.configs import benchy_index_matched, cylindrical_refraction
+    return (cylindrical_refraction if config == 3 else benchy_index_matched)(N=N, angles=A)
+
+
+def cpu_baseline(config, N, seconds, threads):
     """Oracle (C/OpenMP port of the reference march) on a bounded angle subset of the same workload."""
     import numpy as np
     from oracle import oracle
-    from drtvam_amd.configs import benchy_index_matched, desc_from_config
+    from drtvam_amd.configs import desc_from_config
 
     oracle.build()
 
     def run(na):
-        d = desc_from_config(benchy_index_matched(N=N, angles=N))
+        d = desc_from_config(scene_config(config, N, N))
         # the first na angles of the N-angle scene, as a sparse active set (dense order)
         pix = np.arange(na * N * N, dtype=np.uint32)
         pat = np.random.default_rng(0).uniform(0.0, 0.1, na * N * N).astype(np.float32)
@@ -56,7 +64,7 @@ def cpu_baseline(N, seconds, threads):
     t_iter = (2 * tf + ta) * (N / na)
     return {"value": 1.0 / t_iter, "unit": "it/s", "cores": threads, "kind": "port",
             "sample": f"oracle/tvam_oracle.c (C/OpenMP, {threads} threads, slice-private accumulation) on {na} of {N} "
-                      f"angles of the {N}^3 index-matched workload: fwd {tf:.2f}s + adj {ta:.2f}s, "
+                      f"angles of the {N}^3 config-{config} workload: fwd {tf:.2f}s + adj {ta:.2f}s, "
                       f"{v / tf / 1e6:.0f} M visits/s; iteration = 2 fwd + 1 adj scaled to {N} angles "
                       f"(loss/L-BFGS vector work not included)"}
 
@@ -66,6 +74,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--config", type=int, choices=[2, 3], default=2,
+                    help="BASELINE.json configs[1] (2: index-matched, the metric's workload) or configs[2] "
+                         "(3: cylindrical vial, refraction)")
     ap.add_argument("--n", type=int, default=400, help="voxels per axis = DMD pixels per axis = angles")
     ap.add_argument("--angles", type=int, default=None)
     ap.add_argument("--tile", type=int, default=0)
@@ -80,7 +91,6 @@ def main():
 
     import torch
     from drtvam_amd import _abi
-    from drtvam_amd.configs import benchy_index_matched
     from drtvam_amd.optimize import TvamProblem
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -95,7 +105,7 @@ def main():
 
     N = args.n
     A = args.angles or N
-    cfg = benchy_index_matched(N=N, angles=A)
+    cfg = scene_config(args.config, N, A)
     cfg["tile"] = args.tile
     cfg["shard"] = args.shard
     cfg["flags"] = (0 if args.zero_skip else _abi.FLAG_NO_ZERO_SKIP) | (_abi.FLAG_FWD_STATS if args.stats else 0)
@@ -173,13 +183,13 @@ def main():
     # (profiles/pmc_traffic.json, made by tools/profile_round.sh + tools/summarize_profile.py)
     traffic = None
     tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if N == 400 and A == 400 and world == 1 and os.path.exists(tpath):
+    if N == 400 and A == 400 and world == 1 and args.config == 2 and os.path.exists(tpath):
         traffic = json.load(open(tpath))["per_launch"]["forward"]["hbm_bytes"]
     cpu = None
     if args.cpu_baseline == "auto" and world == 1:
         threads = min(16, os.cpu_count() or 1)
         log(f"cpu baseline ({threads} threads, ~{args.cpu_seconds:.0f}s) ...")
-        cpu = cpu_baseline(N, args.cpu_seconds, threads)
+        cpu = cpu_baseline(args.config, N, args.cpu_seconds, threads)
     result = {
         "metric": "optimizer iterations/sec (fwd+adjoint), 400³ voxels × 400 angles",
         "value": args.steps / elapsed,
@@ -194,7 +204,10 @@ def main():
         "dtype": "f32",
         "data": "synthetic",
         "config": {
-            "workload": f"config2: index-matched, {N}^3 voxels, {A} angles, {N}x{N} DMD, 1 ray/px, regular sampling",
+            "workload": (f"config2: index-matched, {N}^3 voxels, {A} angles, {N}x{N} DMD, 1 ray/px, regular sampling"
+                         if args.config == 2 else
+                         f"config3: cylindrical vial (glass r 8/9 mm, n 1.54 | resin n 1.40), {N}^3 voxels, {A} angles, "
+                         f"{N}x{N} DMD, 1 ray/px, regular sampling"),
             "voxels": N ** 3, "angles": A, "dmd": [N, N], "spp": prob.spp, "sigma_t": cfg["vial"]["medium"]["extinction"],
             "parallelism": ("single GPU" if world == 1 else
                             f"z-slab x{world} (film slabs + DMD row bands, scalar all-reduces only)"

@@ -59,6 +59,22 @@ BOX_HOLE_INDEX_MATCHED = {
     "n_steps": 30,
 }
 
+# tests/files/box_hole_cylindrical.json of the reference (data, restated): glass tube
+# r_int 7 / r_ext 8 (ior 1.54) around a scattering resin (ior 1.40, albedo 0.5)
+BOX_HOLE_CYLINDRICAL = {
+    "vial": {"type": "cylindrical", "r_int": 7, "r_ext": 8, "ior": 1.54,
+             "medium": {"ior": 1.40, "phase": {"type": "rayleigh"}, "extinction": 0.1, "albedo": 0.5}},
+    "projector": {"type": "collimated", "n_patterns": 200, "resx": 200, "resy": 20, "pixel_size": 50e-3,
+                  "motion": "circular", "distance": 20},
+    "sensor": {"type": "dda", "scalex": 5, "scaley": 5, "scalez": 1.25,
+               "film": {"type": "vfilm", "resx": 100, "resy": 100, "resz": 50}},
+    "target": {"filename": "tests/files/box_hole.ply", "size": 4.0,
+               "box_center_x": 0, "box_center_y": 0, "box_center_z": 0},
+    "loss": {"type": "threshold", "tl": 0.85, "tu": 0.95},
+    "progressive": True,
+    "n_steps": 30,
+}
+
 
 def desc_from_config(config, angle_range=None, tile: int = 0) -> _abi.TvamDesc:
     """tvam_desc of a config through the plugin classes (no GPU needed)."""

@@ -44,6 +44,7 @@ struct TvamPlanar {
     int32_t fwd_pf;            // forward: staged values per thread and angle (2 or 4)
     int32_t max_rows_chunk;    // adjoint: most DMD rows in one chunk of Z slices
     int32_t adj_pitch;         // adjoint: LDS row pitch of the gradient tile in voxels (>= tile + 2)
+    int32_t max_rows_slice;    // ray-driven forward: most DMD rows in one slice (fixed-point bound)
 };
 
 hipError_t tvam_launch_planar_rays(const TvamConsts& k, const TvamPlanar& pl, hipStream_t stream);
@@ -54,6 +55,12 @@ hipError_t tvam_launch_fwd_planar(const TvamConsts& k, const TvamPlanar& pl, int
 size_t tvam_planar_adj_lds(const TvamPlanar& pl, const TvamTiles& t, int Z);
 hipError_t tvam_launch_adj_planar(const TvamConsts& k, const TvamPlanar& pl, const TvamTiles& t, int Z,
                                   const int32_t* idxmap, const float* gin, float* out, hipStream_t stream);
+// Ray-driven planar forward (refracted rays, fine DMDs): per-angle max |pattern| ->
+// fixed-point scale (amax: [ns] scratch, scale: [2]) -> Z-slice-sharing march.
+size_t tvam_planar_rayfwd_lds(const TvamPlanar& pl, const TvamTiles& t, int Z);
+hipError_t tvam_launch_fwd_rays_planar(const TvamConsts& k, const TvamPlanar& pl, const TvamTiles& t, int Z,
+                                       const float* pat, unsigned* amax, float* scale, float* dose,
+                                       hipStream_t stream);
 
 enum TvamMode { TVAM_MODE_FWD = 0, TVAM_MODE_ADJ = 1, TVAM_MODE_COUNT = 2 };
 

@@ -71,6 +71,9 @@ struct tvam_plan {
     float4* d_pl_rec_f = nullptr;
     int32_t* d_pl_rec_i = nullptr;
     float4* d_pl_rec_g = nullptr;
+    unsigned* d_amax = nullptr;  // ray-driven forward: per-angle max |pattern|, fixed-point scale
+    float* d_fscale = nullptr;
+    int32_t planar_rz = 4;
     std::vector<float4> fwd_ang_h;  // host staging of the forward tables (plan creation only)
     std::vector<int32_t> fwd_cb_h;
     // sparse scratch (dense crop layout), allocated on first sparse call
@@ -138,6 +141,8 @@ static void plan_free(tvam_plan* p) {
     (void)hipFree(p->d_pl_rec_f);
     (void)hipFree(p->d_pl_rec_i);
     (void)hipFree(p->d_pl_rec_g);
+    (void)hipFree(p->d_amax);
+    (void)hipFree(p->d_fscale);
     delete p;
 }
 
@@ -288,16 +293,22 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
         mrc = std::max<int32_t>(mrc, off[std::min(z0 + p->planar_az, k.nz)] - off[z0]);
     p->pl.ns = ns;
     p->pl.max_rows_chunk = mrc;
+    p->pl.max_rows_slice = 0;
+    for (int z = 0; z < k.nz; ++z) p->pl.max_rows_slice = std::max(p->pl.max_rows_slice, off[z + 1] - off[z]);
+    p->planar_rz = env_int("TVAM_RAY_FWD_Z", 4);
+    if (p->planar_rz != 4 && p->planar_rz != 8) p->planar_rz = 4;
     p->pl.adj_pitch = p->tiles.tsx + 2 + std::max(0, env_int("TVAM_ADJ_PITCH_PAD", 0));
     p->pl.xcd_remap = env_int("TVAM_XCD_REMAP", 1);
-    // Refracted rays are not parallel: only the ray-driven adjoint (one record
-    // per (angle, column), shared by all slices) applies; the forward runs the
-    // per-ray tile kernel.
-    p->planar_fwd = !p->cyl;
+    // Refracted rays are not parallel, and a DMD much finer than the voxels
+    // overflows the voxel-driven forward's column window: there the forward
+    // is ray-driven like the adjoint (one record per (angle, column), shared
+    // by all slices).
+    p->planar_fwd = !p->cyl && !(d.flags & TVAM_FLAG_RAY_FWD);
     if (p->planar_fwd && !planar_fwd_setup(p, cs, off)) p->planar_fwd = false;
-    if (!p->planar_fwd && !p->cyl) return 0;  // DMD much finer than the voxels: general path
     if (tvam_planar_adj_lds(p->pl, p->tiles, p->planar_az) > 160 * 1024) p->planar_az = 4;
     if (tvam_planar_adj_lds(p->pl, p->tiles, p->planar_az) > 160 * 1024) return 0;  // tile too large: general path
+    if (tvam_planar_rayfwd_lds(p->pl, p->tiles, p->planar_rz) > 160 * 1024) p->planar_rz = 4;
+    if (tvam_planar_rayfwd_lds(p->pl, p->tiles, p->planar_rz) > 160 * 1024) return 0;
     int rc;
     const size_t nrec = (size_t)std::max(ns, 1) * d.crop_x;
     hipError_t e;
@@ -312,7 +323,9 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     if ((e = hipMalloc((void**)&p->d_pl_vox, nrec * sizeof(float4))) != hipSuccess ||
         (e = hipMalloc((void**)&p->d_pl_rec_f, nrec * sizeof(float4))) != hipSuccess ||
         (e = hipMalloc((void**)&p->d_pl_rec_i, nrec * sizeof(int32_t))) != hipSuccess ||
-        (p->cyl && (e = hipMalloc((void**)&p->d_pl_rec_g, nrec * sizeof(float4))) != hipSuccess))
+        (p->cyl && (e = hipMalloc((void**)&p->d_pl_rec_g, nrec * sizeof(float4))) != hipSuccess) ||
+        (e = hipMalloc((void**)&p->d_amax, (size_t)std::max(ns, 1) * sizeof(unsigned))) != hipSuccess ||
+        (e = hipMalloc((void**)&p->d_fscale, 2 * sizeof(float))) != hipSuccess)
         return hip_fail(e, "hipMalloc (planar tables)");
     p->pl.cs = p->d_cs;
     p->pl.vox = p->d_pl_vox;
@@ -407,10 +420,11 @@ namespace {
 struct CylChord {
     bool hit;
     double ax, ay, bx, by;
+    float w;  // interface weight
 };
 
 CylChord cyl_chord(const TvamConsts& k, float c, float s, int col, float u) {
-    CylChord ch{false, 0, 0, 0, 0};
+    CylChord ch{false, 0, 0, 0, 0, 0.0f};
     float xc, yc, ox, oy, oz, dx, dy, o2x, o2y, d2x, d2y, maxt, w;
     tvam_ray_camera(k, col, 0, u, 0.5f, xc, yc);
     tvam_ray_world(k, c, s, xc, 0.0f, ox, oy, oz, dx, dy);
@@ -420,6 +434,7 @@ CylChord cyl_chord(const TvamConsts& k, float c, float s, int col, float u) {
     ch.ay = o2y;
     ch.bx = (double)o2x + (double)maxt * d2x;
     ch.by = (double)o2y + (double)maxt * d2y;
+    ch.w = w;
     return ch;
 }
 
@@ -457,6 +472,40 @@ void mark_tiles(const TileGrid& g, const CylChord& ch, double m, F&& mark) {
         }
 }
 }  // namespace
+
+// Fixed-point bound behind a refracting vial (replaces TvamConsts::rays_per_voxel):
+// the beam converges, so more than one ray per pixel pitch of one angle may
+// cross a voxel.  From the chords of one angle (the optics are rotation
+// invariant) at 1 (regular) or 8 (jittered) positions per column: the least
+// perpendicular spacing of neighbouring chords per column, s_min (the distance
+// of a point moving along one chord to the other's line is linear, so its
+// minimum is at an end point), and the largest interface weight.  At most
+// ceil(sqrt2 h / s_min) + 2 columns' rays cross a voxel; a factor 2 covers the
+// approximation.  Chords that cross (or touch) inside the medium: infinite
+// (the kernels then add in float).
+static float cyl_rays_per_voxel(const tvam_desc& d, const TvamConsts& k, int ns) {
+    const int sub = d.regular_sampling ? 1 : 8;
+    std::vector<CylChord> ch;
+    for (int col = 0; col < d.crop_x; ++col)
+        for (int j = 0; j < sub; ++j)
+            ch.push_back(cyl_chord(k, 1.0f, 0.0f, d.crop_offset_x + col, ((float)j + 0.5f) / (float)sub));
+    double smin = INFINITY, wmax = 1.0;
+    for (size_t i = 0; i < ch.size(); ++i) {
+        if (!ch[i].hit) continue;
+        wmax = std::max(wmax, (double)ch[i].w);
+        if (i + 1 == ch.size() || !ch[i + 1].hit) continue;
+        const double dx = ch[i].bx - ch[i].ax, dy = ch[i].by - ch[i].ay, L = std::hypot(dx, dy);
+        if (!(L > 1e-12)) continue;
+        const double nx = -dy / L, ny = dx / L;
+        const double da = (ch[i + 1].ax - ch[i].ax) * nx + (ch[i + 1].ay - ch[i].ay) * ny;
+        const double db = (ch[i + 1].bx - ch[i].ax) * nx + (ch[i + 1].by - ch[i].ay) * ny;
+        if (!(da * db > 0.0)) return INFINITY;
+        smin = std::min(smin, std::min(std::fabs(da), std::fabs(db)) * sub);
+    }
+    if (!(smin < INFINITY)) return k.rays_per_voxel;  // fewer than two chords: the straight-ray bound
+    const double hxy = std::max((double)k.h[0], (double)k.h[1]);
+    return (float)((double)ns * (std::ceil(2.0 * std::sqrt(2.0) * hxy / smin) + 2.0) * wmax * 1.01);
+}
 
 static void cyl_slot_lists(const tvam_desc& d, const TvamConsts& k, const std::vector<float2>& cs, int tsx, int tsy,
                            int ntx, int nty, double marg, std::vector<std::vector<uint32_t>>& per_tile) {
@@ -626,6 +675,7 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
     if (p->cyl) {
         std::vector<std::vector<uint32_t>> per_tile;
         cyl_slot_lists(d, k, cs, tsx, tsy, ntx, nty, marg_l + 1e-3 * std::min(k.h[0], k.h[1]), per_tile);
+        p->k.rays_per_voxel = cyl_rays_per_voxel(d, k, ns);
         for (int t = 0; t < p->ntiles; ++t) {
             slots.insert(slots.end(), per_tile[t].begin(), per_tile[t].end());
             slot_off[(size_t)t + 1] = (int64_t)slots.size();
@@ -804,6 +854,10 @@ extern "C" int tvam_forward(tvam_plan* p, const float* active_data, const uint32
         e = tvam_launch_fwd_planar(kc, p->pl, p->planar_fz, pat, dose, stream);
         return e == hipSuccess ? 0 : hip_fail(e, "planar forward launch");
     }
+    if (p->planar) {
+        e = tvam_launch_fwd_rays_planar(kc, p->pl, p->tiles, p->planar_rz, pat, p->d_amax, p->d_fscale, dose, stream);
+        return e == hipSuccess ? 0 : hip_fail(e, "planar ray forward launch");
+    }
     TvamTiles t = p->tiles;
     t.spp = spp;
     t.seed = seed;
@@ -882,7 +936,7 @@ extern "C" int tvam_count_visits(tvam_plan* p, uint32_t spp, uint32_t seed, uint
     return 0;
 }
 
-// bit 0: planar adjoint, bit 1: voxel-driven planar forward
+// bit 0: planar adjoint (+ ray-driven planar forward unless bit 1), bit 1: voxel-driven planar forward
 extern "C" int tvam_plan_path(const tvam_plan* p) { return p ? (p->planar ? 1 : 0) | (p->planar_fwd ? 2 : 0) : 0; }
 
 extern "C" int tvam_plan_stats(tvam_plan* p, uint64_t* fallback_tiles) {

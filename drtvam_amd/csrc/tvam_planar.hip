@@ -526,3 +526,247 @@ hipError_t tvam_launch_adj_planar(const TvamConsts& k, const TvamPlanar& pl, con
     }
     return hipGetLastError();
 }
+
+// ---------------------------------------------------------------------------
+// Forward, ray-driven with Z-slice sharing: the adjoint's march with its
+// gathers turned into LDS adds.  Serves the planar scenes the voxel-driven
+// forward cannot: refracted rays (cylindrical vial: not parallel) and DMDs
+// finer than the voxels.  Per visit, Z adds of cw * E[z], E[z] = the sum of
+// the slice's rows' pattern values (every row of a slice shares the ray's xy
+// path).  The LDS dose tile is slice-major ([z][voxel], plane pitch padded):
+// a wave's Z adds then hit Z planes with the lanes' voxels spread over the
+// banks (the adjoint's [voxel][z] interleave would put every 4th voxel on one
+// bank).  Fixed point (ds_add_u32, exact and order-independent) with the
+// call's scale 2^e from tvam_fwd_scale_kernel; float adds when that bound is
+// not finite.
+// ---------------------------------------------------------------------------
+
+// Per-angle max |pattern| of the shard (bits of non-negative floats order like
+// the floats): grid (chunks, angles).
+__global__ __launch_bounds__(256) void tvam_pattern_amax_kernel(int64_t per_angle, const float* __restrict__ pat,
+                                                               unsigned* __restrict__ amax) {
+    __shared__ unsigned s_m[4];
+    const int al = blockIdx.y;
+    const float* pa = pat + (int64_t)al * per_angle;
+    float m = 0.0f;
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < per_angle; i += (int64_t)gridDim.x * 256)
+        m = fmaxf(m, fabsf(pa[i]));
+    for (int off = 32; off > 0; off >>= 1) m = fmaxf(m, __shfl_down(m, off, 64));
+    if ((threadIdx.x & 63) == 0) s_m[threadIdx.x >> 6] = __float_as_uint(m);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned v = max(max(s_m[0], s_m[1]), max(s_m[2], s_m[3]));
+        if (v) atomicMax(&amax[al], v);
+    }
+}
+
+// scale[0] = 2^e with |voxel sum| < 2^30 / 2^e guaranteed, scale[1] = 1
+// (fixed point) or 0 (float adds).  Bound as in tvam_tile_kernel: per angle at
+// most rays_per_voxel / ns lines cross a voxel (rays_per_voxel includes the
+// refracting vial's beam compression and interface weight), each adding at
+// most vox_chord * rows * max|em|.  Deterministic: fixed-order sum.
+__global__ __launch_bounds__(256) void tvam_fwd_scale_kernel(TvamConsts k, int ns, int rows,
+                                                            const unsigned* __restrict__ amax,
+                                                            float* __restrict__ scale) {
+    __shared__ float s_sum[256];
+    float a = 0.0f;
+    for (int i = threadIdx.x; i < ns; i += 256) a += __uint_as_float(amax[i]);
+    s_sum[threadIdx.x] = a;
+    __syncthreads();
+    for (int w = 128; w > 0; w >>= 1) {
+        if (threadIdx.x < w) s_sum[threadIdx.x] += s_sum[threadIdx.x + w];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const float sum = s_sum[0];
+        const float bound = sum * fabsf(k.wscale) * k.vox_chord * (k.rays_per_voxel / (float)ns) * (float)rows;
+        if (!(sum > 0.0f)) {
+            scale[0] = 1.0f;
+            scale[1] = 1.0f;
+        } else if (isfinite(bound) && bound > 0.0f) {
+            int e;
+            frexpf(bound, &e);
+            e = 30 - e;
+            e = e > 126 ? 126 : (e < -126 ? -126 : e);
+            scale[0] = ldexpf(1.0f, e);
+            scale[1] = 1.0f;
+        } else {
+            scale[0] = 1.0f;
+            scale[1] = 0.0f;
+        }
+    }
+}
+
+// LDS plane pitch (words) of the ray-driven forward's [z][voxel] tile: the
+// (tile + guard) area rounded up to 32 words + 8 (planes start 8 banks apart).
+static __host__ __device__ inline int tvam_ray_fwd_plane(int tw, int th) { return (tw * th + 31) / 32 * 32 + 8; }
+
+size_t tvam_planar_rayfwd_lds(const TvamPlanar& pl, const TvamTiles& t, int Z) {
+    return (size_t)tvam_ray_fwd_plane(pl.adj_pitch, t.tsy + 2) * Z * sizeof(float) +
+           (size_t)(Z + 1 + pl.max_rows_chunk) * sizeof(int);
+}
+
+__device__ __forceinline__ int pl_rint(float x) {
+    int r;
+    asm("v_cvt_rpi_i32_f32 %0, %1" : "=v"(r) : "v"(x));
+    return r;
+}
+
+template <int Z, bool FIXED>
+__device__ __forceinline__ void fwd_rays_body(const TvamConsts& k, const TvamPlanar& pl, const TvamTiles& tp,
+                                              const float* __restrict__ pat, float fscale, unsigned char* smem,
+                                              const int* s_roff, const int* s_rows, int tile_id, int tw,
+                                              int pstride, int x0, int x1, int y0, int y1) {
+    float* tile = reinterpret_cast<float*>(smem);
+    const uint32_t* slots = tp.slots + tp.slot_off[tile_id];
+    const int nrt = (int)(tp.slot_off[tile_id + 1] - tp.slot_off[tile_id]);
+    const int64_t per_angle = (int64_t)k.crop_y * k.crop_x;
+    for (int g = threadIdx.x; g < nrt; g += TVAM_PB) {
+        const uint32_t e = slots[g];
+        const int al = (int)(e >> 16), colc = (int)(e & 0xffffu);
+        const int ri = pl.rec_i[(size_t)al * k.crop_x + colc];
+        if (ri < 0) continue;  // misses the vial / grid
+        // the Z slices' pattern sums (volume.py:49: Le of every row's ray)
+        const float* pc = pat + (int64_t)al * per_angle + colc;
+        float em[Z];
+        bool any = false;
+#pragma unroll
+        for (int z = 0; z < Z; ++z) {
+            float v = 0.0f;
+            for (int q = s_roff[z]; q < s_roff[z + 1]; ++q) v += pc[(int64_t)s_rows[q] * k.crop_x];
+            em[z] = v;
+            any |= v != 0.0f;
+        }
+        if (!any && k.skip_zero) continue;  // contributes exactly zero dose
+        const float4 ff = pl.rec_f[(size_t)al * k.crop_x + colc];
+        float4 an;
+        float wray = 1.0f;
+        if (pl.rec_g) {
+            const float4 gg = pl.rec_g[(size_t)al * k.crop_x + colc];
+            an = make_float4(fabsf(gg.x), fabsf(gg.y), gg.x < 0.0f ? -1.0f : 1.0f, gg.y < 0.0f ? -1.0f : 1.0f);
+            wray = gg.z;
+        } else {
+            an = tp.ang[al];
+        }
+        const float sc = k.wscale * wray * fscale;  // weight (common.py:111) x interfaces (sensor.py:404)
+#pragma unroll
+        for (int z = 0; z < Z; ++z) em[z] *= sc;
+        const int svx = ri & 0xffff, svy = ri >> 16;
+        const int stx = (int)an.z, sty = (int)an.w;
+        float tin0, tout0, tin1, tout1;
+        int nin0, nout0, nin1, nout1;
+        tvam_axis_window(svx, stx, ff.z, an.x, x0, x1, tin0, tout0, nin0, nout0);
+        tvam_axis_window(svy, sty, ff.w, an.y, y0, y1, tin1, tout1, nin1, nout1);
+        const float tau_e = fmaxf(fmaxf(tin0, tin1), 0.0f);
+        const float tau_x = fminf(fminf(tout0, tout1), ff.y);
+        if (!(tau_e < tau_x)) continue;
+        const int n0 = tvam_axis_steps(tau_e, ff.z, an.x, nin0, nout0);
+        const int n1 = tvam_axis_steps(tau_e, ff.w, an.y, nin1, nout1);
+        const int vx = svx + stx * n0, vy = svy + sty * n1;
+        float Tx = ff.z < TVAM_INF ? fmaxf(fmaf((float)n0, an.x, ff.z) - tau_e, 0.0f) : TVAM_INF;
+        float Ty = ff.w < TVAM_INF ? fmaxf(fmaf((float)n1, an.y, ff.w) - tau_e, 0.0f) : TVAM_INF;
+        const float rem = tau_x - tau_e, stop = rem - 1e-6f;
+        const float nt0 = k.nsig2 * (ff.x + tau_e);
+        const int sxb = stx * 4, syb = sty * tw * 4;
+        char* pv = reinterpret_cast<char*>(tile) + (size_t)((vy - y0 + 1) * tw + (vx - x0 + 1)) * 4;
+        float e0 = pl_exp2(nt0);
+        for (;;) {
+            const float tn = fminf(fminf(Tx, Ty), rem);
+            const float e1 = pl_exp2(fmaf(k.nsig2, tn, nt0));
+            const float cw = e0 - e1;
+#pragma unroll
+            for (int z = 0; z < Z; ++z) {
+                if (FIXED)
+                    __hip_atomic_fetch_add(reinterpret_cast<int*>(pv + z * pstride), pl_rint(cw * em[z]),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                else
+                    __hip_atomic_fetch_add(reinterpret_cast<float*>(pv + z * pstride), cw * em[z], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+            const bool mx = Tx <= Ty;
+            Tx = mx ? Tx + an.x : Tx;
+            Ty = mx ? Ty : Ty + an.y;
+            pv += mx ? sxb : syb;
+            e0 = e1;
+            if (!(tn < stop)) break;
+        }
+    }
+}
+
+template <int Z>
+__global__ __launch_bounds__(TVAM_PB) void tvam_fwd_rays_planar_kernel(TvamConsts k, TvamPlanar pl, TvamTiles tp,
+                                                                       const float* __restrict__ pat,
+                                                                       const float* __restrict__ scale,
+                                                                       float* __restrict__ dose) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    const int tsx = tp.tsx, tsy = tp.tsy;
+    const int tw = pl.adj_pitch, th = tsy + 2;
+    const int pw = tvam_ray_fwd_plane(tw, th);  // plane pitch in words
+    int* itile = reinterpret_cast<int*>(smem);
+    int* s_roff = itile + (size_t)pw * Z;
+    int* s_rows = s_roff + Z + 1;
+
+    const int tile_id = blockIdx.x, z0 = blockIdx.y * Z;
+    const int x0 = (tile_id % tp.ntx) * tsx, y0 = (tile_id / tp.ntx) * tsy;
+    const int x1 = min(x0 + tsx, k.res[0]), y1 = min(y0 + tsy, k.res[1]);
+    const int wx = x1 - x0, wy = y1 - y0;
+    const size_t plane = (size_t)k.res[0] * k.res[1];
+    const float fscale = scale[0];
+    const bool fixed = scale[1] != 0.0f;
+
+    for (int i = threadIdx.x; i < pw * Z; i += TVAM_PB) itile[i] = 0;  // 0 == 0.0f
+    if (threadIdx.x == 0) {
+        int n = 0;
+        for (int z = 0; z < Z; ++z) {
+            s_roff[z] = n;
+            if (z0 + z < k.nz)
+                for (int q = pl.slice_off[z0 + z]; q < pl.slice_off[z0 + z + 1]; ++q) s_rows[n++] = pl.slice_rows[q];
+        }
+        s_roff[Z] = n;
+    }
+    __syncthreads();
+    if (s_roff[Z] > 0) {
+        if (fixed)
+            fwd_rays_body<Z, true>(k, pl, tp, pat, fscale, smem, s_roff, s_rows, tile_id, tw, pw * 4, x0, x1, y0, y1);
+        else
+            fwd_rays_body<Z, false>(k, pl, tp, pat, fscale, smem, s_roff, s_rows, tile_id, tw, pw * 4, x0, x1, y0, y1);
+    }
+    __syncthreads();
+    // dose = sum / voxel volume (volume.py:41-42, sensor.py:404)
+    const float outscale = k.inv_vol / fscale;
+    const float* ftile = reinterpret_cast<const float*>(smem);
+    for (int z = 0; z < Z && z0 + z < k.nz; ++z)
+        for (int i = threadIdx.x; i < wx * wy; i += TVAM_PB) {
+            const int ly = i / wx, lx = i - ly * wx;
+            const size_t li = (size_t)z * pw + (size_t)(ly + 1) * tw + (lx + 1);
+            const float v = fixed ? (float)itile[li] * outscale : ftile[li] * k.inv_vol;
+            dose[(size_t)(z0 + z) * plane + (size_t)(y0 + ly) * k.res[0] + (x0 + lx)] = v;
+        }
+}
+
+hipError_t tvam_launch_fwd_rays_planar(const TvamConsts& k, const TvamPlanar& pl, const TvamTiles& t, int Z,
+                                       const float* pat, unsigned* amax, float* scale, float* dose,
+                                       hipStream_t stream) {
+    const int64_t per_angle = (int64_t)k.crop_y * k.crop_x;
+    hipError_t e = hipMemsetAsync(amax, 0, (size_t)pl.ns * sizeof(unsigned), stream);
+    if (e != hipSuccess) return e;
+    const unsigned chunks = (unsigned)std::min<int64_t>((per_angle + 4095) / 4096, 64);
+    hipLaunchKernelGGL(tvam_pattern_amax_kernel, dim3(chunks, (unsigned)pl.ns), dim3(256), 0, stream, per_angle, pat,
+                       amax);
+    hipLaunchKernelGGL(tvam_fwd_scale_kernel, dim3(1), dim3(256), 0, stream, k, pl.ns, pl.max_rows_slice, amax, scale);
+    dim3 grid((unsigned)(t.ntx * t.nty), (unsigned)((k.nz + Z - 1) / Z));
+    const size_t lds = tvam_planar_rayfwd_lds(pl, t, Z);
+    switch (Z) {
+        case 4:
+            hipLaunchKernelGGL(tvam_fwd_rays_planar_kernel<4>, grid, dim3(TVAM_PB), lds, stream, k, pl, t, pat, scale,
+                               dose);
+            break;
+        case 8:
+            hipLaunchKernelGGL(tvam_fwd_rays_planar_kernel<8>, grid, dim3(TVAM_PB), lds, stream, k, pl, t, pat, scale,
+                               dose);
+            break;
+        default:
+            return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}

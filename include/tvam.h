@@ -120,6 +120,7 @@ typedef struct tvam_desc {
 #define TVAM_FLAG_NO_ZERO_SKIP 1  /* forward: march rays whose pattern value is 0 too */
 #define TVAM_FLAG_FWD_STATS    2  /* forward: count tiles that fell back to float LDS atomics */
 #define TVAM_FLAG_NO_PLANAR    4  /* use the per-ray tile kernels even where the planar path applies */
+#define TVAM_FLAG_RAY_FWD      8  /* planar path: ray-driven forward instead of the voxel-driven one */
 
 typedef struct tvam_plan tvam_plan;
 

@@ -24,15 +24,21 @@ def rel_l2(a, b):
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
 
 
-def make(N, A, regular=True, spp=1, tile=0, angle_range=None, planar=True, zres=None, **kw):
+def make(N, A, regular=True, spp=1, tile=0, angle_range=None, planar=True, zres=None, ray_fwd=False, xyres=None,
+         **kw):
     """planar=False forces the per-ray tile kernels; zres != N gives 2 rows per slice
-    (zres = N/2) or empty slices (zres = 2N)."""
+    (zres = N/2) or empty slices (zres = 2N); ray_fwd=True forces the ray-driven planar
+    forward; xyres = N/4 makes the DMD 4x finer than the voxels (ray-driven forward)."""
     cfg = benchy_index_matched(N=N, angles=A, regular_sampling=regular, spp=spp, **kw)
     d = desc_from_config(cfg, angle_range=angle_range, tile=tile)
     if not planar:
         d.flags |= _abi.FLAG_NO_PLANAR
+    if ray_fwd:
+        d.flags |= _abi.FLAG_RAY_FWD
     if zres is not None:
         d.film_res[2] = zres
+    if xyres is not None:
+        d.film_res[0] = d.film_res[1] = xyres
     return d
 
 
@@ -59,6 +65,11 @@ CASES = [
     dict(N=24, A=12, zres=12),          # two DMD rows per slice
     dict(N=24, A=12, zres=48),          # slices without rows
     dict(N=24, A=12, zres=12, planar=False),
+    dict(N=32, A=24, ray_fwd=True),     # ray-driven planar forward
+    dict(N=40, A=30, tile=7, ray_fwd=True),
+    dict(N=24, A=12, zres=12, ray_fwd=True),
+    dict(N=24, A=12, zres=48, ray_fwd=True),
+    dict(N=64, A=16, xyres=16),         # DMD 4x finer than the voxels: ray-driven forward
 ]
 
 
@@ -73,6 +84,7 @@ def test_forward_matches_oracle(oracle, case):
     got, proj = gpu_forward(d, pat, spp=spp, seed=5)
     # planar path: regular sampling and every row's vial-entry offset row-independent (|z| <= 0.7 r)
     assert proj.planar == (case.get("regular", True) and case.get("planar", True) and 5.0 <= 0.7 * case.get("r", 8.0))
+    assert proj.planar_forward == (proj.planar and not case.get("ray_fwd") and case.get("xyres") is None)
     assert rel_l2(got, ref) < RTOL_L2
     assert np.max(np.abs(got - ref)) <= 1e-4 * np.max(np.abs(ref)) + 1e-7
     hv = proj.count_visits(spp, 5)
