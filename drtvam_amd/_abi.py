@@ -12,7 +12,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libtvam.so")
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 TVAM_OK = 0
 TVAM_ERR_INVALID = -1
@@ -23,6 +23,9 @@ TVAM_ERR_TOO_LARGE = -4
 PROJECTOR_COLLIMATED = 0
 VIAL_INDEX_MATCHED = 0
 VIAL_CYLINDRICAL = 1
+PHASE_ISOTROPIC = 0
+PHASE_RAYLEIGH = 1
+PHASE_HG = 2
 SENSOR_DDA = 0
 
 FLAG_NO_ZERO_SKIP = 1
@@ -72,6 +75,8 @@ class TvamDesc(ctypes.Structure):
         ("flags", ctypes.c_int32),
         ("slab_begin", ctypes.c_int32),
         ("slab_end", ctypes.c_int32),
+        ("phase_type", ctypes.c_int32),
+        ("phase_g", ctypes.c_float),
     ]
 
     def copy(self) -> "TvamDesc":

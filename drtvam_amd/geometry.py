@@ -48,6 +48,12 @@ class Container:
     def _fill_medium(self, desc):
         desc.sigma_t = float(self.sigma_t)
         desc.albedo = float(self.albedo)
+        phase = self.medium_phase or {"type": "isotropic"}  # Mitsuba's default phase function
+        kinds = {"isotropic": _abi.PHASE_ISOTROPIC, "rayleigh": _abi.PHASE_RAYLEIGH, "hg": _abi.PHASE_HG}
+        if phase.get("type") not in kinds:
+            raise NotImplementedError(f"phase function '{phase.get('type')}' is not supported by the GPU engine")
+        desc.phase_type = kinds[phase["type"]]
+        desc.phase_g = float(phase.get("g", 0.8))  # Mitsuba hg default g
         desc.medium_ior = lookup_ior(self.medium_ior)
         if self.occlusions:
             raise NotImplementedError("occluder meshes are not supported by the GPU engine yet")

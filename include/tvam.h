@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define TVAM_ABI_VERSION 2
+#define TVAM_ABI_VERSION 3
 
 /* error codes */
 #define TVAM_OK               0
@@ -57,6 +57,11 @@ extern "C" {
 /* vial / container kinds (geometry.py:312-318) */
 #define TVAM_VIAL_INDEX_MATCHED   0
 #define TVAM_VIAL_CYLINDRICAL     1
+
+/* medium phase functions (Mitsuba 'isotropic', 'rayleigh', 'hg'; geometry.py:29-39) */
+#define TVAM_PHASE_ISOTROPIC      0
+#define TVAM_PHASE_RAYLEIGH       1
+#define TVAM_PHASE_HG             2
 /* sensor kinds (sensor.py:442-444) */
 #define TVAM_SENSOR_DDA           0
 
@@ -114,6 +119,9 @@ typedef struct tvam_desc {
        whole film): the dose / grad_dose buffers hold only these slices, and
        rays of other slices are skipped (z-slab sharding of planar scenes) */
     int32_t slab_begin, slab_end;
+    /* scattering media (albedo > 0): medium 'phase' {'type', 'g'} */
+    int32_t phase_type;           /* TVAM_PHASE_* */
+    float   phase_g;              /* 'hg' asymmetry g */
 } tvam_desc;
 
 /* tvam_desc.flags */

@@ -40,6 +40,10 @@ def lib():
         L.oracle_adjoint.argtypes = [D, P, P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, P, P, ctypes.c_int]
         L.oracle_ray.restype = ctypes.c_int
         L.oracle_ray.argtypes = [D, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_uint32, P]
+        L.oracle_forward_part.restype = ctypes.c_int
+        L.oracle_forward_part.argtypes = L.oracle_forward.argtypes + [ctypes.c_int]
+        L.oracle_phase.restype = ctypes.c_int
+        L.oracle_phase.argtypes = [D, P, ctypes.c_float, ctypes.c_float, P]
         L.oracle_dda_ray.restype = ctypes.c_int
         L.oracle_dda_ray.argtypes = [D, P, P, ctypes.c_float, ctypes.c_double, P, P]
         _lib = L
@@ -55,14 +59,15 @@ def film_shape(desc):
     return (rz, ry, rx)
 
 
-def forward(desc, active_data, active_pixels=None, spp=1, seed=0, nthreads=1):
-    """Dose [z, y, x] (float64) and the DDA visit count of one forward pass."""
+def forward(desc, active_data, active_pixels=None, spp=1, seed=0, nthreads=1, part=-1):
+    """Dose [z, y, x] (float64) and the DDA visit count of one forward pass.
+    Scattering media: part=1 keeps only each path's first medium segment, part=0 the rest."""
     data = np.ascontiguousarray(active_data, dtype=np.float32)
     pix = None if active_pixels is None else np.ascontiguousarray(active_pixels, dtype=np.uint32)
     dose = np.zeros(film_shape(desc), dtype=np.float64)
     visits = ctypes.c_uint64(0)
-    rc = lib().oracle_forward(ctypes.byref(desc), _ptr(data), _ptr(pix), data.size, spp, seed, _ptr(dose),
-                              ctypes.cast(ctypes.byref(visits), ctypes.c_void_p), nthreads)
+    rc = lib().oracle_forward_part(ctypes.byref(desc), _ptr(data), _ptr(pix), data.size, spp, seed, _ptr(dose),
+                                   ctypes.cast(ctypes.byref(visits), ctypes.c_void_p), nthreads, part)
     if rc:
         raise ValueError(f"oracle_forward failed ({rc})")
     return dose, visits.value
@@ -89,6 +94,14 @@ def ray(desc, pixel, wave_index=0, seed=0):
     lib().oracle_ray(ctypes.byref(desc), pixel, wave_index, seed, _ptr(out))
     return {"o": out[0:3].copy(), "d": out[3:6].copy(), "hit": bool(out[6]), "o2": out[7:10].copy(),
             "maxt": float(out[10]), "d2": out[11:14].copy(), "weight": float(out[14])}
+
+
+def phase(desc, d, u1, u2):
+    """Scattered direction for a ray of direction d (the desc's phase function)."""
+    d = np.ascontiguousarray(d, dtype=np.float32)
+    wo = np.zeros(3, dtype=np.float32)
+    lib().oracle_phase(ctypes.byref(desc), _ptr(d), u1, u2, _ptr(wo))
+    return wo
 
 
 def dda_ray(desc, o, d, maxt, em=1.0):

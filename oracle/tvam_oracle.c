@@ -109,6 +109,7 @@ typedef struct {
     double inv_vol;     /* volume.py:41-42                      */
     double sa_over_st;  /* sensor.py:400, :404                  */
     float st;
+    int part;           /* scattering paths: -1 all segments, 0 all but the first, 1 the first only */
 } or_scene;
 
 static void or_scene_init(or_scene* s, const tvam_desc* d) {
@@ -124,6 +125,7 @@ static void or_scene_init(or_scene* s, const tvam_desc* d) {
     float vol = s->h[0] * s->h[1] * s->h[2];
     s->inv_vol = vol != 0.0f ? 1.0 / (double)vol : 0.0;
     s->st = d->sigma_t;
+    s->part = -1;
     float ss = d->albedo * d->sigma_t;
     s->sa_over_st = d->sigma_t != 0.0f ? ((double)d->sigma_t - (double)ss) / (double)d->sigma_t : 0.0;
 }
@@ -141,8 +143,13 @@ static double or_ray_weight(const tvam_desc* d, uint64_t n_active, uint32_t spp)
 /* ------------------------------------------------------------------------ */
 typedef struct { float o[3], d[3]; } or_ray;
 
-static void or_gen_ray(const or_scene* s, uint32_t pixel, uint64_t wave_index, uint32_t seed,
-                       or_ray* ray) {
+/* Ray of `pixel` for sampler stream `wave_index`.  Draw order of
+   common.py:92-108: position (next_2d, jittered sampling only), time
+   (next_1d, sample_time only), then the aperture sample of sample_ray
+   (next_2d, always drawn, unused by the collimated projector).  If rng is
+   given, it is left after those draws (the path loop continues the stream). */
+static void or_gen_ray_rng(const or_scene* s, uint32_t pixel, uint64_t wave_index, uint32_t seed,
+                           or_ray* ray, or_pcg32* rng_out) {
     const tvam_desc* d = s->d;
     uint32_t hw = (uint32_t)d->res_y * (uint32_t)d->res_x;
     uint32_t angle = pixel / hw;
@@ -151,7 +158,7 @@ static void or_gen_ray(const or_scene* s, uint32_t pixel, uint64_t wave_index, u
     uint32_t col = pix - row * (uint32_t)d->res_x;
 
     float ox = 0.5f, oy = 0.5f, ot = 0.0f;
-    if (!d->regular_sampling || d->sample_time) {
+    if (!d->regular_sampling || d->sample_time || rng_out) {
         or_pcg32 rng;
         or_sampler_seed(&rng, seed, wave_index);
         if (!d->regular_sampling) {
@@ -159,6 +166,11 @@ static void or_gen_ray(const or_scene* s, uint32_t pixel, uint64_t wave_index, u
             oy = or_pcg_float(&rng);
         }
         if (d->sample_time) ot = or_pcg_float(&rng);
+        if (rng_out) {
+            (void)or_pcg_float(&rng); /* aperture sample (projector.py:160) */
+            (void)or_pcg_float(&rng);
+            *rng_out = rng;
+        }
     }
     float u = ((float)col + ox) * s->inv_w;
     float v = ((float)row + oy) * s->inv_h;
@@ -180,6 +192,10 @@ static void or_gen_ray(const or_scene* s, uint32_t pixel, uint64_t wave_index, u
     ray->d[0] = -c;
     ray->d[1] = -sn;
     ray->d[2] = 0.0f;
+}
+
+static void or_gen_ray(const or_scene* s, uint32_t pixel, uint64_t wave_index, uint32_t seed, or_ray* ray) {
+    or_gen_ray_rng(s, pixel, wave_index, seed, ray, NULL);
 }
 
 /* ------------------------------------------------------------------------ */
@@ -334,6 +350,175 @@ static int or_segment_cylindrical(const or_scene* s, const or_ray* ray, float o2
     return 0;
 }
 
+/* DDA declared ahead for the scattering path */
+static double or_dda(const or_scene* s, const float o[3], const float dd[3], float maxt, double em,
+                     int mode, double* film, const float* grad, int only_slice, uint64_t* visits);
+
+/* ------------------------------------------------------------------------ */
+/* Scattering media: the full path loop of volume.py:179-272  */
+/* with has_scattering (sigma_s != 0).  Mitsuba internals restated (UNPINNED):*/
+/*   homogeneous medium  sample_interaction: t = -log(1 - u) / sigma_t        */
+/*                       (mint 0, unbounded medium); transmittance_eval_pdf:  */
+/*                       tr = exp(-min(t_mi, t_si) sigma_t), pdf = tr at a    */
+/*                       surface, tr * sigma_t at a medium interaction;       */
+/*                       sigma_s = albedo * sigma_t                          */
+/*   phase functions     isotropic (square_to_uniform_sphere), rayleigh      */
+/*                       (cbrt inversion of the (1 + cos^2) CDF), hg; local   */
+/*                       directions mapped by Frame3f(wi = -d) built with     */
+/*                       coordinate_system() (Duff et al.)                    */
+/*   medium spawn_ray    origin p = o + t d, no offset (n = 0)               */
+/* Draw order per loop iteration: RR next_1d (every iteration), the medium   */
+/* next_1d (every iteration), BSDF next_1d + next_2d (surface lanes only),   */
+/* phase next_1d + next_2d (scattering lanes only).                          */
+/* Every medium segment deposits its analytic absorption up to the next      */
+/* surface (sensor.py:383-438 with maxt = si.t), weighted by the path        */
+/* attenuation (sensor.py:367-381: throughput * exp(-st t_prev) * ss^n_scat  */
+/* == attenuation in primal mode); the path continues from the sampled       */
+/* interaction.  A segment whose ray escapes through an open tube end has no */
+/* surface (si invalid) and deposits nothing (volume.py:191-196).            */
+/* ------------------------------------------------------------------------ */
+static void or_coordinate_system(const float n[3], float s[3], float t[3]) {
+    float sign = copysignf(1.0f, n[2]);
+    float a = -1.0f / (sign + n[2]);
+    float b = n[0] * n[1] * a;
+    s[0] = copysignf(1.0f, n[2]) * (n[0] * n[0] * a) + 1.0f; /* mulsign(x^2 a, n.z) + 1 */
+    s[1] = copysignf(1.0f, n[2]) * b;
+    s[2] = -copysignf(1.0f, n[2]) * n[0];                   /* mulsign_neg(n.x, n.z) */
+    t[0] = b;
+    t[1] = fmaf(n[1], n[1] * a, sign);
+    t[2] = -n[1];
+}
+
+/* Phase-function sample: direction wo for a ray of direction dd (wi = -dd). */
+static void or_phase_sample(const tvam_desc* d, const float dd[3], float u1, float u2, float wo[3]) {
+    float lx, ly, lz;
+    if (d->phase_type == TVAM_PHASE_ISOTROPIC) {
+        float z = 1.0f - 2.0f * u1; /* warp::square_to_uniform_sphere: world space */
+        float r = sqrtf(fmaxf(1.0f - z * z, 0.0f));
+        float sp = sinf(OR_TWO_PI * u2), cp = cosf(OR_TWO_PI * u2);
+        wo[0] = r * cp;
+        wo[1] = r * sp;
+        wo[2] = z;
+        return;
+    }
+    if (d->phase_type == TVAM_PHASE_RAYLEIGH) {
+        float z = 2.0f * (2.0f * u1 - 1.0f);
+        float tmp = sqrtf(z * z + 1.0f);
+        float A = cbrtf(z + tmp), B = cbrtf(z - tmp);
+        float ct = A + B;
+        float st = sqrtf(fmaxf(1.0f - ct * ct, 0.0f));
+        float sp = sinf(OR_TWO_PI * u2), cp = cosf(OR_TWO_PI * u2);
+        lx = st * cp;
+        ly = st * sp;
+        lz = ct;
+    } else { /* Henyey-Greenstein */
+        float g = d->phase_g;
+        float ct;
+        if (fabsf(g) < 5.9604644775390625e-08f) {
+            ct = 1.0f - 2.0f * u1;
+        } else {
+            float sq = (1.0f - g * g) / (1.0f - g + 2.0f * g * u1);
+            ct = (1.0f + g * g - sq * sq) / (2.0f * g);
+        }
+        float st = sqrtf(fmaxf(1.0f - ct * ct, 0.0f));
+        float sp = sinf(OR_TWO_PI * u2), cp = cosf(OR_TWO_PI * u2);
+        lx = st * cp;
+        ly = st * sp;
+        lz = -ct;
+    }
+    float n[3] = {-dd[0], -dd[1], -dd[2]}, sv[3], tv[3];
+    or_coordinate_system(n, sv, tv);
+    for (int k = 0; k < 3; ++k) wo[k] = sv[k] * lx + tv[k] * ly + n[k] * lz;
+}
+
+/* Nearest container surface along (o, dd): t, hit point, outward normal and
+   which tube (0 outer glass, 1 inner / index-matched tube).  INFINITY on a miss. */
+static float or_container_hit(const or_scene* s, const float o[3], const float dd[3], int* which) {
+    const tvam_desc* d = s->d;
+    float half = 0.5f * d->vial_height;
+    float ti = or_tube_hit(o, dd, d->vial_r, half);
+    *which = 1;
+    if (d->vial_type == TVAM_VIAL_CYLINDRICAL) {
+        float te = or_tube_hit(o, dd, d->vial_r_ext, half);
+        if (!(ti <= te)) {
+            *which = 0;
+            return te;
+        }
+    }
+    return ti;
+}
+
+/* One scattering path (volume.py:179-272).  The first medium segment is the
+   non-scattering one (or_segment_*), then free flights until the path
+   leaves the medium, escapes, hits max_depth, or Russian roulette ends it.
+   first_only < 0: every segment; 0: all but the first (the GPU's scatter
+   pass); 1: only the first. */
+static double or_trace_scatter(const or_scene* s, uint32_t pixel, uint64_t wave_index, uint32_t seed, double em,
+                               int mode, double* film, const float* grad, uint64_t* visits, int first_only) {
+    const tvam_desc* d = s->d;
+    or_ray ray;
+    or_pcg32 rng;
+    or_gen_ray_rng(s, pixel, wave_index, seed, &ray, &rng);
+    float o[3], dd[3], maxt;
+    double attd = 1.0;
+    int nsurf;
+    if (d->vial_type == TVAM_VIAL_CYLINDRICAL) {
+        if (!or_segment_cylindrical(s, &ray, o, dd, &maxt, &attd)) return 0.0;
+        nsurf = 2;
+    } else {
+        if (d->max_depth < 2 || !or_segment_index_matched(s, &ray, o, &maxt)) return 0.0;
+        for (int k = 0; k < 3; ++k) dd[k] = ray.d[k];
+        nsurf = 1;
+    }
+    /* the surface iterations before the medium: RR, medium, BSDF 1d + 2d */
+    for (int i = 0; i < 5 * nsurf; ++i) (void)or_pcg_float(&rng);
+    float att = (float)attd;
+    int depth = nsurf;
+    const float st = d->sigma_t, ss = d->albedo * d->sigma_t;
+    double acc = 0.0;
+    for (int seg = 0;; ++seg) {
+        const float q = fminf(0.99f, att);
+        const float u_rr = or_pcg_float(&rng);
+        if (depth > d->rr_depth) { /* volume.py:182-185 */
+            if (!(u_rr < q)) break;
+            att = att * (1.0f / q);
+        }
+        if (!(att != 0.0f)) break;
+        float tsi = maxt;
+        if (seg > 0) {
+            int which;
+            tsi = or_container_hit(s, o, dd, &which);
+            if (!(tsi < INFINITY)) break; /* escapes through an open end: no surface, no deposit */
+        }
+        const float u_m = or_pcg_float(&rng);
+        const float tmi = -logf(1.0f - u_m) / st;
+        const int reached = tsi < tmi;
+        /* deposit along [0, si.t] */
+        if (first_only < 0 || (first_only == 0 && seg > 0) || (first_only == 1 && seg == 0)) {
+            if (mode == 0 || mode == 3) (void)or_dda(s, o, dd, tsi, em * (double)att, mode, film, NULL, -1, visits);
+            else acc += (double)att * or_dda(s, o, dd, tsi, em, mode, NULL, grad, -1, visits);
+        }
+        if (reached || first_only == 1) break; /* leaves the medium for good (transmission only, convex) */
+        const float tr = expf(-tmi * st);
+        const float pdf = tr * st;
+        const float inv = pdf > 0.0f ? 1.0f / pdf : 0.0f;
+        float w = tr * inv;
+        w = w * ss;
+        (void)or_pcg_float(&rng); /* phase next_1d (unused) */
+        const float u1 = or_pcg_float(&rng), u2 = or_pcg_float(&rng);
+        float wo[3];
+        or_phase_sample(d, dd, u1, u2, wo);
+        for (int k = 0; k < 3; ++k) {
+            o[k] = fmaf(dd[k], tmi, o[k]);
+            dd[k] = wo[k];
+        }
+        att = att * w;
+        ++depth;
+        if (depth >= d->max_depth) break;
+    }
+    return acc;
+}
+
 /* ------------------------------------------------------------------------ */
 /* DDA (sensor.py:327-438).  mode 0: forward (accumulate into film),          */
 /* mode 1: adjoint (gather grad), mode 2: count only.                        */
@@ -391,6 +576,12 @@ static double or_dda(const or_scene* s, const float o[3], const float dd[3], flo
         size_t idx = (size_t)cur[0] + (size_t)cur[1] * (size_t)s->res[0] +
                      (size_t)cur[2] * (size_t)s->res[0] * (size_t)s->res[1];
         if (mode == 0) film[idx] += em * w;
+        else if (mode == 3) {
+#ifdef _OPENMP
+#pragma omp atomic
+#endif
+            film[idx] += em * w;
+        }
         else if (mode == 1) acc += w * (double)grad[idx];
         ++nv;
         int alive = (cur[0] != endv[0] || cur[1] != endv[1] || cur[2] != endv[2]) && (remaining > 1e-6f);
@@ -436,16 +627,21 @@ static int or_check(const tvam_desc* d) {
     if (d->vial_type != TVAM_VIAL_INDEX_MATCHED && d->vial_type != TVAM_VIAL_CYLINDRICAL) return TVAM_ERR_UNSUPPORTED;
     if (d->projector_type != TVAM_PROJECTOR_COLLIMATED) return TVAM_ERR_UNSUPPORTED;
     if (d->film_channels != 1) return TVAM_ERR_UNSUPPORTED;
-    if (d->albedo != 0.0f) return TVAM_ERR_UNSUPPORTED;
+    if (d->albedo < 0.0f || d->albedo > 1.0f) return TVAM_ERR_INVALID;
+    if (d->albedo != 0.0f && !(d->sigma_t > 0.0f)) return TVAM_ERR_INVALID;
+    if (d->phase_type < TVAM_PHASE_ISOTROPIC || d->phase_type > TVAM_PHASE_HG) return TVAM_ERR_INVALID;
     /* Russian roulette (volume.py:182-185, depth > rr_depth) before the medium
        segment (path vertex 1 index matched, 2 behind the glass) is not restated */
     if (d->rr_depth < (d->vial_type == TVAM_VIAL_CYLINDRICAL ? 2 : 1)) return TVAM_ERR_UNSUPPORTED;
     return 0;
 }
 
-/* one ray: generate + segment + DDA.  Returns the adjoint sum (mode 1). */
+/* one ray: generate + segment + DDA.  Returns the adjoint sum (mode 1).
+   mode 0: forward, 3: forward with atomic film adds (shared film). */
 static double or_trace(const or_scene* s, uint32_t pixel, uint64_t wave_index, uint32_t seed, double em,
                        int mode, double* film, const float* grad, int only_slice, uint64_t* visits) {
+    if (s->d->albedo != 0.0f)  /* has_scattering (volume.py:159) */
+        return or_trace_scatter(s, pixel, wave_index, seed, em, mode, film, grad, visits, s->part);
     or_ray ray;
     or_gen_ray(s, pixel, wave_index, seed, &ray);
     float o2[3], maxt;
@@ -465,19 +661,52 @@ static double or_trace(const or_scene* s, uint32_t pixel, uint64_t wave_index, u
 /* ------------------------------------------------------------------------ */
 /* Public oracle entry points (called from tests/ and bench.py via ctypes)   */
 /* ------------------------------------------------------------------------ */
-int oracle_forward(const tvam_desc* d, const float* active_data, const uint32_t* active_pixels,
-                   uint64_t n_active, uint32_t spp, uint32_t seed, double* dose, uint64_t* visits,
-                   int nthreads) {
+int oracle_forward_part(const tvam_desc* d, const float* active_data, const uint32_t* active_pixels,
+                        uint64_t n_active, uint32_t spp, uint32_t seed, double* dose, uint64_t* visits,
+                        int nthreads, int part) {
     int rc = or_check(d);
     if (rc) return rc;
     if (d->regular_sampling) spp = 1;
     or_scene s;
     or_scene_init(&s, d);
+    s.part = part;
     size_t V = (size_t)s.res[0] * s.res[1] * s.res[2];
     memset(dose, 0, V * sizeof(double));
     double wr = or_ray_weight(d, n_active, spp);
     uint64_t nv_total = 0;
-    if (nthreads <= 1) {
+    if (d->albedo != 0.0f && nthreads > 1) {
+        /* scattered paths leave their slice: per-thread films (static
+           schedule, fixed-order reduction), or atomics when those would not fit */
+        const int priv = (double)V * (double)nthreads * 8.0 <= 2.0e9;
+        double* films = priv ? (double*)calloc(V * (size_t)nthreads, sizeof(double)) : NULL;
+        if (priv && !films) return TVAM_ERR_INVALID;
+#ifdef _OPENMP
+#pragma omp parallel num_threads(nthreads) reduction(+ : nv_total)
+#endif
+        {
+#ifdef _OPENMP
+            const int tid = omp_get_thread_num();
+#else
+            const int tid = 0;
+#endif
+            double* mine = priv ? films + (size_t)tid * V : dose;
+#ifdef _OPENMP
+#pragma omp for schedule(static)
+#endif
+            for (int64_t i = 0; i < (int64_t)n_active; ++i) {
+                uint32_t pixel = or_pixel(d, active_pixels, (uint64_t)i);
+                double em = (double)active_data[i] * wr;
+                uint64_t st = or_stream(d, pixel);
+                for (uint32_t k = 0; k < spp; ++k)
+                    or_trace(&s, pixel, st * spp + k, seed, em, priv ? 0 : 3, mine, NULL, -1, &nv_total);
+            }
+        }
+        if (priv) {
+            for (int t = 0; t < nthreads; ++t)
+                for (size_t v = 0; v < V; ++v) dose[v] += films[(size_t)t * V + v];
+            free(films);
+        }
+    } else if (nthreads <= 1) {
         for (uint64_t i = 0; i < n_active; ++i) {
             uint32_t pixel = or_pixel(d, active_pixels, i);
             double em = (double)active_data[i] * wr;
@@ -537,6 +766,18 @@ int oracle_forward(const tvam_desc* d, const float* active_data, const uint32_t*
     }
     for (size_t v = 0; v < V; ++v) dose[v] *= s.inv_vol;
     if (visits) *visits = nv_total;
+    return 0;
+}
+
+int oracle_forward(const tvam_desc* d, const float* active_data, const uint32_t* active_pixels,
+                   uint64_t n_active, uint32_t spp, uint32_t seed, double* dose, uint64_t* visits,
+                   int nthreads) {
+    return oracle_forward_part(d, active_data, active_pixels, n_active, spp, seed, dose, visits, nthreads, -1);
+}
+
+/* Phase-function sample for a ray of direction dd (tests: distribution KATs). */
+int oracle_phase(const tvam_desc* d, const float* dd, float u1, float u2, float* wo) {
+    or_phase_sample(d, dd, u1, u2, wo);
     return 0;
 }
 
