@@ -9,7 +9,8 @@ synthetic patterns U[0, 0.1) (seed 0) and an analytic target (benchy.ply is
 not available).  Every ray is marched (zero-pattern skipping disabled).
 
 --config 3 runs BASELINE.json configs[2] instead: the same scene behind a
-cylindrical glass vial (two refracting interfaces per ray).
+cylindrical glass vial (two refracting interfaces per ray); --config 4 runs
+configs[3]: that vial around a scattering resin, 16 jittered rays per pixel.
 
 Multi-GPU: one process per GPU (torch.distributed.run), angles sharded in
 contiguous blocks, dose all-reduced over RCCL twice per iteration, L-BFGS
@@ -32,8 +33,8 @@ def log(*a):
 
 
 def scene_config(config, N, A):
-    from drtvam_amd.configs import benchy_index_matched, cylindrical_refraction
-    return (cylindrical_refraction if config == 3 else benchy_index_matched)(N=N, angles=A)
+    from drtvam_amd.configs import benchy_index_matched, cylindrical_refraction, cylindrical_scattering
+    return {2: benchy_index_matched, 3: cylindrical_refraction, 4: cylindrical_scattering}[config](N=N, angles=A)
 
 
 def cpu_baseline(config, N, seconds, threads):
@@ -45,15 +46,17 @@ def cpu_baseline(config, N, seconds, threads):
     oracle.build()
 
     def run(na):
-        d = desc_from_config(scene_config(config, N, N))
+        cfg = scene_config(config, N, N)
+        spp = cfg.get("spp", 1) if not cfg.get("regular_sampling") else 1
+        d = desc_from_config(cfg)
         # the first na angles of the N-angle scene, as a sparse active set (dense order)
         pix = np.arange(na * N * N, dtype=np.uint32)
         pat = np.random.default_rng(0).uniform(0.0, 0.1, na * N * N).astype(np.float32)
         G = np.random.default_rng(1).uniform(-1.0, 1.0, (N, N, N)).astype(np.float32)
         t0 = time.perf_counter()
-        _, v = oracle.forward(d, pat, active_pixels=pix, nthreads=threads)
+        _, v = oracle.forward(d, pat, active_pixels=pix, spp=spp, nthreads=threads)
         t1 = time.perf_counter()
-        oracle.adjoint(d, G, active_pixels=pix, nthreads=threads)
+        oracle.adjoint(d, G, active_pixels=pix, spp=spp, nthreads=threads)
         t2 = time.perf_counter()
         return t1 - t0, t2 - t1, v
 
@@ -74,9 +77,10 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", type=int, choices=[2, 3], default=2,
-                    help="BASELINE.json configs[1] (2: index-matched, the metric's workload) or configs[2] "
-                         "(3: cylindrical vial, refraction)")
+    ap.add_argument("--config", type=int, choices=[2, 3, 4], default=2,
+                    help="BASELINE.json configs[1] (2: index-matched, the metric's workload), configs[2] "
+                         "(3: cylindrical vial, refraction) or configs[3] (4: cylindrical vial, scattering "
+                         "resin, 16 jittered rays per pixel)")
     ap.add_argument("--n", type=int, default=400, help="voxels per axis = DMD pixels per axis = angles")
     ap.add_argument("--angles", type=int, default=None)
     ap.add_argument("--tile", type=int, default=0)
@@ -207,7 +211,9 @@ def main():
             "workload": (f"config2: index-matched, {N}^3 voxels, {A} angles, {N}x{N} DMD, 1 ray/px, regular sampling"
                          if args.config == 2 else
                          f"config3: cylindrical vial (glass r 8/9 mm, n 1.54 | resin n 1.40), {N}^3 voxels, {A} angles, "
-                         f"{N}x{N} DMD, 1 ray/px, regular sampling"),
+                         f"{N}x{N} DMD, 1 ray/px, regular sampling" if args.config == 3 else
+                         f"config4: cylindrical vial, scattering resin (sigma_t 0.1/mm, albedo 0.5, Rayleigh), "
+                         f"{N}^3 voxels, {A} angles, {N}x{N} DMD, {prob.spp} jittered rays/px"),
             "voxels": N ** 3, "angles": A, "dmd": [N, N], "spp": prob.spp, "sigma_t": cfg["vial"]["medium"]["extinction"],
             "parallelism": ("single GPU" if world == 1 else
                             f"z-slab x{world} (film slabs + DMD row bands, scalar all-reduces only)"

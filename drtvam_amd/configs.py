@@ -45,6 +45,18 @@ def cylindrical_refraction(N: int = 400, angles: int | None = None, size_mm: flo
     return cfg
 
 
+def cylindrical_scattering(N: int = 400, angles: int | None = None, spp: int = 16, sigma_t: float = 0.1,
+                           albedo: float = 0.5, phase: str = "rayleigh", n_steps: int = 40):
+    """Config 4 (BASELINE.json): the config 3 tube around a scattering resin (the medium of
+    tests/files/box_hole_cylindrical.json: extinction 0.1 / mm, albedo 0.5, Rayleigh phase),
+    16 jittered rays per pixel."""
+    cfg = cylindrical_refraction(N=N, angles=angles, sigma_t=sigma_t, spp=spp, regular_sampling=False,
+                                 n_steps=n_steps)
+    cfg["vial"]["medium"]["albedo"] = albedo
+    cfg["vial"]["medium"]["phase"] = {"type": phase}
+    return cfg
+
+
 # tests/files/box_hole_index_matched.json of the reference (data, restated)
 BOX_HOLE_INDEX_MATCHED = {
     "vial": {"type": "index_matched", "r": 2.9,

@@ -46,6 +46,10 @@ struct TvamConsts {
     float vial_r_ext;    // cylindrical: outer glass radius
     float eta_ext, eta_int;     // cylindrical: int/ext IOR of the outer (glass/air) and inner (medium/glass) surface
     // medium / weights
+    float sig_t, sig_s;  // scattering media: sigma_t, sigma_s = albedo * sigma_t (fp32, Mitsuba homogeneous)
+    int32_t rr_depth;    // Russian roulette from depth > rr_depth (volume.py:182)
+    int32_t phase_type;  // TVAM_PHASE_*
+    float phase_g;       // hg asymmetry
     float nsig2;         // -sigma_t * log2(e): exp(-st t) == exp2(nsig2 t)
     float wscale;        // inv_pdf/n_samples * print_time * sa/st (projector.py:164-165,187; common.py:111; sensor.py:404)
     // fixed-point forward bound: |voxel sum| <= max|em| * vox_chord * rays_per_voxel * rows * spp

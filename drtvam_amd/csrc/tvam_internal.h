@@ -68,6 +68,12 @@ hipError_t tvam_launch_tiles(int mode, const TvamConsts& k, const TvamTiles& t, 
                              const float* pat, const int32_t* idxmap, const float* gin, float* out,
                              unsigned long long* counter, hipStream_t stream);
 
+// Scattering media: every path's segments after its first medium segment
+// (free flights, phase sampling, 3-D DDA; tvam_scatter.hip).
+hipError_t tvam_launch_scatter_paths(int mode, const TvamConsts& k, const TvamTiles& t, const float* pat,
+                                     const int32_t* idxmap, const float* gin, float* out,
+                                     unsigned long long* counter, hipStream_t stream);
+
 // Per-ray pre-pass: ray generation, vial segment and DDA initialisation of
 // every ray of the shard, stored as the records the tile kernels resume from.
 hipError_t tvam_launch_ray_setup(const TvamConsts& k, const TvamTiles& t, float4* ray_f, int2* ray_i,

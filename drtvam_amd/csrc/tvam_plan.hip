@@ -163,7 +163,14 @@ static int validate(const tvam_desc& d) {
     if (d.vial_type != TVAM_VIAL_INDEX_MATCHED && d.vial_type != TVAM_VIAL_CYLINDRICAL)
         return fail(TVAM_ERR_UNSUPPORTED, "only the 'index_matched' and 'cylindrical' containers are implemented on the GPU path");
     if (d.film_channels != 1) return fail(TVAM_ERR_UNSUPPORTED, "surface-aware films (2 channels) are not implemented");
-    if (d.albedo != 0.0f) return fail(TVAM_ERR_UNSUPPORTED, "scattering media (albedo > 0) are not implemented");
+    if (!(d.albedo >= 0.0f && d.albedo <= 1.0f)) return fail(TVAM_ERR_INVALID, "medium albedo must lie in [0, 1]");
+    if (d.albedo != 0.0f) {
+        if (!(d.sigma_t > 0.0f)) return fail(TVAM_ERR_INVALID, "scattering medium: extinction must be positive");
+        if (d.phase_type < TVAM_PHASE_ISOTROPIC || d.phase_type > TVAM_PHASE_HG)
+            return fail(TVAM_ERR_UNSUPPORTED, "unknown phase function");
+        if (d.slab_begin != 0 || (d.slab_end >= 0 && d.slab_end != d.film_res[2]))
+            return fail(TVAM_ERR_UNSUPPORTED, "scattered paths leave their slice: film slabs need a non-scattering medium");
+    }
     if (d.sample_time) return fail(TVAM_ERR_UNSUPPORTED, "sample_time is not implemented on the GPU path");
     // the medium segment is path vertex 1 (index matched) or 2 (behind two glass
     // surfaces); Russian roulette starts at depth > rr_depth (volume.py:182-185)
@@ -232,6 +239,11 @@ static TvamConsts make_consts(const tvam_desc& d, int a0, int a1) {
     k.eta_ext = d.vial_ior / TVAM_IOR_AIR;   // int/ext IOR of the outer surface (geometry.py:160-170)
     k.eta_int = d.medium_ior / d.vial_ior;   // and of the inner one (geometry.py:171-183)
     k.nsig2 = -d.sigma_t * 1.44269504088896340736f;
+    k.sig_t = d.sigma_t;
+    k.sig_s = d.albedo * d.sigma_t;
+    k.rr_depth = d.rr_depth;
+    k.phase_type = d.phase_type;
+    k.phase_g = d.phase_g;
     k.wscale = 0.0f;  // per call
     {
         double hxy = std::max((double)k.h[0], (double)k.h[1]);
@@ -852,24 +864,32 @@ extern "C" int tvam_forward(tvam_plan* p, const float* active_data, const uint32
                 return hip_fail(e, "hipMemsetAsync");
         }
         e = tvam_launch_fwd_planar(kc, p->pl, p->planar_fz, pat, dose, stream);
-        return e == hipSuccess ? 0 : hip_fail(e, "planar forward launch");
-    }
-    if (p->planar) {
+        if (e != hipSuccess) return hip_fail(e, "planar forward launch");
+    } else if (p->planar) {
         e = tvam_launch_fwd_rays_planar(kc, p->pl, p->tiles, p->planar_rz, pat, p->d_amax, p->d_fscale, dose, stream);
-        return e == hipSuccess ? 0 : hip_fail(e, "planar ray forward launch");
+        if (e != hipSuccess) return hip_fail(e, "planar ray forward launch");
+    } else {
+        TvamTiles t = p->tiles;
+        t.spp = spp;
+        t.seed = seed;
+        if ((rc = ensure_rays(p, kc, t, stream))) return rc;
+        unsigned long long* stats = nullptr;
+        if (p->desc.flags & TVAM_FLAG_FWD_STATS) {
+            if ((e = hipMemsetAsync(p->d_counter, 0, sizeof(unsigned long long), stream)) != hipSuccess)
+                return hip_fail(e, "hipMemsetAsync");
+            stats = p->d_counter;
+        }
+        e = tvam_launch_tiles(TVAM_MODE_FWD, kc, t, p->lds_bytes, pat, idxmap, nullptr, dose, stats, stream);
+        if (e != hipSuccess) return hip_fail(e, "forward launch");
     }
-    TvamTiles t = p->tiles;
-    t.spp = spp;
-    t.seed = seed;
-    if ((rc = ensure_rays(p, kc, t, stream))) return rc;
-    unsigned long long* stats = nullptr;
-    if (p->desc.flags & TVAM_FLAG_FWD_STATS) {
-        if ((e = hipMemsetAsync(p->d_counter, 0, sizeof(unsigned long long), stream)) != hipSuccess)
-            return hip_fail(e, "hipMemsetAsync");
-        stats = p->d_counter;
+    if (p->desc.albedo != 0.0f) {  // scattered segments (after each path's first medium segment)
+        TvamTiles t = p->tiles;
+        t.spp = spp;
+        t.seed = seed;
+        e = tvam_launch_scatter_paths(TVAM_MODE_FWD, kc, t, pat, idxmap, nullptr, dose, nullptr, stream);
+        if (e != hipSuccess) return hip_fail(e, "scatter forward launch");
     }
-    e = tvam_launch_tiles(TVAM_MODE_FWD, kc, t, p->lds_bytes, pat, idxmap, nullptr, dose, stats, stream);
-    return e == hipSuccess ? 0 : hip_fail(e, "forward launch");
+    return 0;
 }
 
 extern "C" int tvam_adjoint(tvam_plan* p, const float* grad_dose, const uint32_t* active_pixels, uint64_t n_active,
@@ -897,9 +917,8 @@ extern "C" int tvam_adjoint(tvam_plan* p, const float* grad_dose, const uint32_t
         return hip_fail(e, "hipMemsetAsync");
     if (p->planar) {
         e = tvam_launch_adj_planar(k, p->pl, p->tiles, p->planar_az, idxmap, grad_dose, grad_active, stream);
-        return e == hipSuccess ? 0 : hip_fail(e, "planar adjoint launch");
-    }
-    if (!p->empty) {
+        if (e != hipSuccess) return hip_fail(e, "planar adjoint launch");
+    } else if (!p->empty) {
         TvamTiles t = p->tiles;
         t.spp = spp;
         t.seed = seed;
@@ -907,6 +926,13 @@ extern "C" int tvam_adjoint(tvam_plan* p, const float* grad_dose, const uint32_t
         e = tvam_launch_tiles(TVAM_MODE_ADJ, k, t, p->lds_bytes, nullptr, idxmap, grad_dose, grad_active, nullptr,
                               stream);
         if (e != hipSuccess) return hip_fail(e, "adjoint launch");
+    }
+    if (p->desc.albedo != 0.0f && !p->empty) {
+        TvamTiles t = p->tiles;
+        t.spp = spp;
+        t.seed = seed;
+        e = tvam_launch_scatter_paths(TVAM_MODE_ADJ, k, t, nullptr, idxmap, grad_dose, grad_active, nullptr, stream);
+        if (e != hipSuccess) return hip_fail(e, "scatter adjoint launch");
     }
     return 0;
 }
@@ -929,6 +955,10 @@ extern "C" int tvam_count_visits(tvam_plan* p, uint32_t spp, uint32_t seed, uint
     e = tvam_launch_tiles(TVAM_MODE_COUNT, k, t, p->lds_bytes, nullptr, nullptr, nullptr, nullptr, p->d_counter,
                           nullptr);
     if (e != hipSuccess) return hip_fail(e, "count launch");
+    if (p->desc.albedo != 0.0f) {
+        e = tvam_launch_scatter_paths(TVAM_MODE_COUNT, k, t, nullptr, nullptr, nullptr, nullptr, p->d_counter, nullptr);
+        if (e != hipSuccess) return hip_fail(e, "scatter count launch");
+    }
     unsigned long long h = 0;
     e = hipMemcpy(&h, p->d_counter, sizeof(h), hipMemcpyDeviceToHost);
     if (e != hipSuccess) return hip_fail(e, "hipMemcpy");

@@ -276,10 +276,6 @@ class TvamProblem(ShardedLoop):
         shard = config.get('shard', 'auto')
         if shard not in ('auto', 'angle', 'slab'):
             raise ValueError(f"Unknown shard mode '{shard}' (auto, angle, slab)")
-        if shard == 'slab' and not (self.regular_sampling and fusable):
-            raise ValueError("z-slab sharding needs regular sampling and the fused thresholded loss")
-        self.shard = 'slab' if (shard == 'slab' or (shard == 'auto' and self.world > 1 and self.regular_sampling
-                                                     and fusable)) else 'angle'
         base = {'max_depth': 3 if self.progressive else self.max_depth, 'rr_depth': self.rr_depth,
                 'print_time': self.time, 'transmission_only': self.transmission_only,
                 'regular_sampling': self.regular_sampling, 'tile': config.get('tile', 0),
@@ -290,6 +286,12 @@ class TvamProblem(ShardedLoop):
         self.crop_x, self.crop_y = p.crop[0], p.crop[1]
         full_desc = VolumeIntegrator(base).desc(self.scene, self.sensor)
         self.res_z = int(full_desc.film_res[2])
+        planar = self.regular_sampling and full_desc.albedo == 0.0  # scattered paths leave their slice
+        if shard == 'slab' and not (planar and fusable):
+            raise ValueError("z-slab sharding needs regular sampling, a non-scattering medium and the fused "
+                             "thresholded loss")
+        self.shard = 'slab' if (shard == 'slab' or (shard == 'auto' and self.world > 1 and planar
+                                                     and fusable)) else 'angle'
         self.n_vox = int(full_desc.film_res[0]) * int(full_desc.film_res[1]) * self.res_z
         if self.shard == 'slab':
             self.a0, self.a1 = 0, A

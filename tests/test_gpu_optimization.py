@@ -2,8 +2,8 @@
 reference for the index-matched box-with-hole config (tests/files/box_hole_index_matched.json):
 after the optimisation, > 99.4 % of the voxels thresholded at (tl + tu) / 2 must match the
 voxelised reference of test_optimization.py:130-144.  The cylindrical config
-(tests/files/box_hole_cylindrical.json) runs with its resin's albedo set to 0: the scattering
-medium is not on the GPU path yet."""
+(tests/files/box_hole_cylindrical.json) runs as given (scattering resin, albedo 0.5, Rayleigh)
+and with its albedo set to 0."""
 import copy
 import os
 
@@ -38,9 +38,10 @@ def test_box_hole_index_matched_optimization(tmp_path):
     assert (tmp_path / "patterns.npz").exists() and (tmp_path / "final.npy").exists()
 
 
-def test_box_hole_cylindrical_optimization(tmp_path):
+@pytest.mark.parametrize("albedo", [0.5, 0.0])
+def test_box_hole_cylindrical_optimization(tmp_path, albedo):
     cfg = copy.deepcopy(BOX_HOLE_CYLINDRICAL)
-    cfg["vial"]["medium"]["albedo"] = 0.0  # non-scattering variant
+    cfg["vial"]["medium"]["albedo"] = albedo  # 0.5: the reference file; 0: non-scattering variant
     cfg["target"]["filename"] = os.path.join(GOLDEN, "box_hole.ply")
     cfg["output"] = str(tmp_path)
     vol = optimize(cfg, device="cuda:0")
