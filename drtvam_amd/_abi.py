@@ -12,7 +12,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libtvam.so")
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 TVAM_OK = 0
 TVAM_ERR_INVALID = -1
@@ -23,6 +23,7 @@ TVAM_ERR_TOO_LARGE = -4
 PROJECTOR_COLLIMATED = 0
 VIAL_INDEX_MATCHED = 0
 VIAL_CYLINDRICAL = 1
+VIAL_SQUARE = 2
 PHASE_ISOTROPIC = 0
 PHASE_RAYLEIGH = 1
 PHASE_HG = 2
@@ -77,12 +78,24 @@ class TvamDesc(ctypes.Structure):
         ("slab_end", ctypes.c_int32),
         ("phase_type", ctypes.c_int32),
         ("phase_g", ctypes.c_float),
+        ("occluder_tris", ctypes.c_void_p),
+        ("n_occluder_tris", ctypes.c_int32),
     ]
 
     def copy(self) -> "TvamDesc":
         d = TvamDesc()
         ctypes.pointer(d)[0] = self
+        if hasattr(self, "_occluders"):  # keep the occluder triangle array alive with the copy
+            d._occluders = self._occluders
         return d
+
+    def set_occluders(self, tris) -> None:
+        """Occluder triangles [n][3][3] (float32, host); the desc keeps the array alive."""
+        import numpy as np
+        t = np.ascontiguousarray(tris, dtype=np.float32).reshape(-1, 3, 3)
+        self._occluders = t
+        self.occluder_tris = t.ctypes.data if t.size else None
+        self.n_occluder_tris = int(t.shape[0])
 
     def as_dict(self) -> dict:
         out = {}

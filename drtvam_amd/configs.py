@@ -57,6 +57,71 @@ def cylindrical_scattering(N: int = 400, angles: int | None = None, spp: int = 1
     return cfg
 
 
+def square_vial(N: int = 400, angles: int | None = None, size_mm: float = 5.0, w_int: float = 7.191,
+                w_ext: float = 7.6, vial_ior: float = 1.3, medium_ior: float = 1.15, sigma_t: float = 0.06,
+                spp: int = 1, regular_sampling: bool = True, occluders=(), n_steps: int = 40):
+    """A square glass vial (the vial and resin of tests/files/box_hole_occlusion.json: w_int 7.191,
+    w_ext 7.6, glass ior 1.3, resin ior 1.15, extinction 0.06 / mm), optional occluder PLY meshes."""
+    cfg = benchy_index_matched(N=N, angles=angles, size_mm=size_mm, sigma_t=sigma_t, spp=spp,
+                               regular_sampling=regular_sampling, n_steps=n_steps)
+    cfg["vial"] = {"type": "square", "w_int": w_int, "w_ext": w_ext, "ior": vial_ior,
+                   "medium": {"ior": medium_ior, "extinction": sigma_t, "albedo": 0.0},
+                   "occlusions": [{"filename": f} for f in occluders]}
+    return cfg
+
+
+def square_occluded(N: int = 800, angles: int | None = None, spp: int = 4, occluder: str | None = None,
+                    n_steps: int = 40):
+    """Config 5 (BASELINE.json): overprinting around an occluder in a square vial -- the scene of
+    tests/files/box_hole_occlusion.json (5 mm film, square vial, the 2 x 1 x 0.5 mm occluder box
+    of tests/files/occlusion.ply) at N^3 voxels, N angles, N x N DMD, 4 jittered rays per pixel."""
+    import os
+    occ = occluder or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tests", "golden",
+                                   "occlusion.ply")
+    return square_vial(N=N, angles=angles, spp=spp, regular_sampling=False, occluders=(occ,), n_steps=n_steps)
+
+
+# tests/files/box_hole_square.json, box_hole_occlusion.json and box_hole_scattering.json of
+# the reference (data, restated; the occluder / target paths are set by the caller)
+BOX_HOLE_SQUARE = {
+    "vial": {"type": "square", "w_int": 10.191, "w_ext": 12.408, "ior": 1.54,
+             "medium": {"ior": 1.347, "phase": {"type": "rayleigh"}, "extinction": 0.03, "albedo": 0.0}},
+    "projector": {"type": "collimated", "n_patterns": 200, "resx": 200, "resy": 20, "pixel_size": 50e-3,
+                  "motion": "circular", "distance": 20},
+    "sensor": {"type": "dda", "scalex": 5, "scaley": 5, "scalez": 1.25,
+               "film": {"type": "vfilm", "resx": 100, "resy": 100, "resz": 50}},
+    "target": {"filename": "tests/files/box_hole.ply", "size": 4.0},
+    "loss": {"type": "threshold", "tl": 0.85, "tu": 0.95},
+    "progressive": True,
+    "n_steps": 30,
+}
+BOX_HOLE_OCCLUSION = {
+    "vial": {"type": "square", "w_int": 7.191, "w_ext": 7.6, "ior": 1.3,
+             "medium": {"ior": 1.15, "phase": {"type": "rayleigh"}, "extinction": 0.06, "albedo": 0.0},
+             "occlusions": [{"filename": "tests/files/occlusion.ply"}]},
+    "projector": BOX_HOLE_SQUARE["projector"],
+    "sensor": BOX_HOLE_SQUARE["sensor"],
+    "target": {"filename": "tests/files/box_hole.ply", "size": 4.0},
+    "loss": {"type": "threshold", "tl": 0.9, "tu": 0.97},
+    "progressive": True,
+    "n_steps": 30,
+}
+BOX_HOLE_SCATTERING = {
+    "vial": {"type": "square", "w_int": 7.0, "w_ext": 8.0, "ior": 1.24,
+             "medium": {"ior": 1.347, "phase": {"type": "rayleigh"}, "extinction": 0.09, "albedo": 0.9}},
+    "projector": BOX_HOLE_SQUARE["projector"],
+    "sensor": BOX_HOLE_SQUARE["sensor"],
+    "target": {"filename": "tests/files/box_hole.ply", "size": 4.0},
+    "loss": {"type": "threshold", "tl": 0.35, "tu": 0.55},
+    "filter_radon": True,
+    "spp_ref": 16,
+    "spp": 4,
+    "spp_grad": 16,
+    "progressive": True,
+    "n_steps": 30,
+}
+
+
 # tests/files/box_hole_index_matched.json of the reference (data, restated)
 BOX_HOLE_INDEX_MATCHED = {
     "vial": {"type": "index_matched", "r": 2.9,

@@ -43,7 +43,10 @@ struct TvamConsts {
     int32_t vial_type;   // TVAM_VIAL_*
     int32_t max_depth;   // path depth limit (volume.py:272)
     float vial_r, vial_half_h;  // index-matched r / cylindrical r_int; half height
-    float vial_r_ext;    // cylindrical: outer glass radius
+    float vial_r_ext;    // cylindrical: outer glass radius; square: w_ext / 2 (vial_r = w_int / 2)
+    float vial_hz_int;   // square: half height of the inner cuboid (0.45 height, geometry.py:207)
+    const float* occ;    // occluder triangles [n_occ][3][3] (device; geometry.py:55-72), nullptr if none
+    int32_t n_occ;
     float eta_ext, eta_int;     // cylindrical: int/ext IOR of the outer (glass/air) and inner (medium/glass) surface
     // medium / weights
     float sig_t, sig_s;  // scattering media: sigma_t, sigma_s = albedo * sigma_t (fp32, Mitsuba homogeneous)
@@ -129,6 +132,8 @@ TVAM_HD bool tvam_cyl_roots(float ox, float oy, float dx, float dy, float r, flo
     return tvam_quadratic(A, B, C, t0, t1);
 }
 
+TVAM_HD float tvam_occ_hit(const TvamConsts& k, float ox, float oy, float oz, float dx, float dy, float dz);
+
 // Index-matched vial: the medium segment (o2, maxt) of a projector ray.
 TVAM_HD bool tvam_segment_im(const TvamConsts& k, float ox, float oy, float oz, float dx, float dy,
                              float& o2x, float& o2y, float& maxt) {
@@ -136,6 +141,7 @@ TVAM_HD bool tvam_segment_im(const TvamConsts& k, float ox, float oy, float oz, 
     float t0, t1;
     if (!tvam_cyl_roots(ox, oy, dx, dy, k.vial_r, t0, t1)) return false;
     if (!(t0 >= 0.0f)) return false;
+    if (k.n_occ && tvam_occ_hit(k, ox, oy, oz, dx, dy, 0.0f) < t0) return false;  // blocked before the vial
     float px = fmaf(dx, t0, ox), py = fmaf(dy, t0, oy), pz = oz;
     float rp = sqrtf(px * px + py * py);
     float nx = px / rp, ny = py / rp;
@@ -149,6 +155,7 @@ TVAM_HD bool tvam_segment_im(const TvamConsts& k, float ox, float oy, float oz, 
     if (!tvam_cyl_roots(o2x, o2y, dx, dy, k.vial_r, u0, u1)) return false;
     if (!(u1 > 0.0f)) return false;
     maxt = u1;
+    if (k.n_occ) maxt = fminf(u1, tvam_occ_hit(k, o2x, o2y, oz, dx, dy, 0.0f));  // ends on an occluder
     return true;
 }
 
@@ -193,6 +200,155 @@ TVAM_HD float tvam_transmit(float nx, float ny, float dx, float dy, float eta, f
     return t * (eta_ti * eta_ti);
 }
 
+// Occluders: nearest triangle hit (Mitsuba ray_intersect_triangle restated,
+// Moller-Trumbore, t >= 0); oracle or_tri_hit / or_occ_hit.
+TVAM_HD float tvam_tri_hit(const float* v, float ox, float oy, float oz, float dx, float dy, float dz) {
+    const float e1x = v[3] - v[0], e1y = v[4] - v[1], e1z = v[5] - v[2];
+    const float e2x = v[6] - v[0], e2y = v[7] - v[1], e2z = v[8] - v[2];
+    const float tx = ox - v[0], ty = oy - v[1], tz = oz - v[2];
+    const float px = dy * e2z - dz * e2y, py = dz * e2x - dx * e2z, pz = dx * e2y - dy * e2x;
+    const float inv_det = 1.0f / (e1x * px + e1y * py + e1z * pz);
+    const float u = (tx * px + ty * py + tz * pz) * inv_det;
+    if (!(u >= 0.0f && u <= 1.0f)) return TVAM_INF;
+    const float qx = ty * e1z - tz * e1y, qy = tz * e1x - tx * e1z, qz = tx * e1y - ty * e1x;
+    const float w = (dx * qx + dy * qy + dz * qz) * inv_det;
+    if (!(w >= 0.0f && u + w <= 1.0f)) return TVAM_INF;
+    const float t = (e2x * qx + e2y * qy + e2z * qz) * inv_det;
+    return t >= 0.0f ? t : TVAM_INF;
+}
+
+TVAM_HD float tvam_occ_hit(const TvamConsts& k, float ox, float oy, float oz, float dx, float dy, float dz) {
+    float best = TVAM_INF;
+    for (int i = 0; i < k.n_occ; ++i) best = fminf(best, tvam_tri_hit(k.occ + 9 * i, ox, oy, oz, dx, dy, dz));
+    return best;
+}
+
+// Closed box [-h, h] (Mitsuba 'cube' scaled): nearest t >= 0, outward face
+// normal (oracle or_box_hit; same axis order and tie rule).
+TVAM_HD float tvam_box_hit(float ox, float oy, float oz, float dx, float dy, float dz, float hx, float hy, float hz,
+                           float& nx, float& ny, float& nz) {
+    const float o[3] = {ox, oy, oz}, d[3] = {dx, dy, dz}, h[3] = {hx, hy, hz};
+    float tn = -TVAM_INF, tf = TVAM_INF;
+    int an = 0, af = 0;
+    for (int a = 0; a < 3; ++a) {
+        if (d[a] == 0.0f) {
+            if (!(o[a] >= -h[a] && o[a] <= h[a])) return TVAM_INF;
+            continue;
+        }
+        const float t0 = (-h[a] - o[a]) / d[a], t1 = (h[a] - o[a]) / d[a];
+        const float lo = fminf(t0, t1), hi = fmaxf(t0, t1);
+        if (lo > tn) {
+            tn = lo;
+            an = a;
+        }
+        if (hi < tf) {
+            tf = hi;
+            af = a;
+        }
+    }
+    if (!(tn <= tf)) return TVAM_INF;
+    float n[3] = {0.0f, 0.0f, 0.0f};
+    float t = TVAM_INF;
+    if (tn >= 0.0f) {
+        n[an] = d[an] > 0.0f ? -1.0f : 1.0f;
+        t = tn;
+    } else if (tf >= 0.0f) {
+        n[af] = d[af] > 0.0f ? 1.0f : -1.0f;
+        t = tf;
+    }
+    nx = n[0];
+    ny = n[1];
+    nz = n[2];
+    return t;
+}
+
+// Mitsuba fresnel() (oracle or_fresnel): reflectance, signed cos_theta_t, eta_ti.
+TVAM_HD float tvam_fresnel(float cos_i, float eta, float& cos_t, float& eta_ti) {
+    const bool outside = cos_i >= 0.0f;
+    const float rcp_eta = 1.0f / eta;
+    const float eta_it = outside ? eta : rcp_eta;
+    eta_ti = outside ? rcp_eta : eta;
+    const float ct2 = 1.0f - (1.0f - cos_i * cos_i) * (eta_ti * eta_ti);
+    const float ci = fabsf(cos_i), ct = sqrtf(fmaxf(ct2, 0.0f));
+    float r;
+    if (eta == 1.0f) r = 0.0f;
+    else if (ci == 0.0f) r = 1.0f;
+    else {
+        const float a_s = (ci - eta_it * ct) / (ci + eta_it * ct);
+        const float a_p = (ct - eta_it * ci) / (ct + eta_it * ci);
+        r = 0.5f * (a_s * a_s + a_p * a_p);
+    }
+    cos_t = outside ? -ct : ct;
+    return r;
+}
+
+// Transmission in world space (the cube's faces; oracle or_transmit_world):
+// wo = -eta_ti wi + (eta_ti cos_i + cos_t) n, weight (1 - F) eta_ti^2.
+TVAM_HD float tvam_transmit_world(float nx, float ny, float nz, float dx, float dy, float dz, float eta, float& wx,
+                                  float& wy, float& wz) {
+    const float cos_i = -(dx * nx + dy * ny + dz * nz);
+    float cos_t, eta_ti;
+    const float r = tvam_fresnel(cos_i, eta, cos_t, eta_ti);
+    const float t = 1.0f - r;
+    if (!(t > 0.0f)) return 0.0f;
+    const float c = eta_ti * cos_i + cos_t;
+    wx = eta_ti * dx + c * nx;
+    wy = eta_ti * dy + c * ny;
+    wz = eta_ti * dz + c * nz;
+    return t * (eta_ti * eta_ti);
+}
+
+// Square vial (geometry.py:186-219; oracle or_segment_square): the glass
+// cuboids' faces in order, transmission and spawn_ray at each, until the ray
+// runs inside the inner cuboid; the segment ends at its next hit (or an
+// occluder).  Planar rays (d.z = 0) meet only vertical faces.
+TVAM_HD bool tvam_segment_square(const TvamConsts& k, float ox, float oy, float oz, float dx, float dy, float& o2x,
+                                 float& o2y, float& d2x, float& d2y, float& maxt, float& weight) {
+    float px = ox, py = oy, vx = dx, vy = dy, att = 1.0f;
+    bool in_medium = false;
+    for (int depth = 0; depth < k.max_depth; ++depth) {
+        float nex, ney, nez, nix, niy, niz;
+        const float te = tvam_box_hit(px, py, oz, vx, vy, 0.0f, k.vial_r_ext, k.vial_r_ext, k.vial_half_h, nex, ney,
+                                      nez);
+        const float ti = tvam_box_hit(px, py, oz, vx, vy, 0.0f, k.vial_r, k.vial_r, k.vial_hz_int, nix, niy, niz);
+        const bool inner = ti <= te;
+        float t = inner ? ti : te;
+        if (k.n_occ) {
+            const float toc = tvam_occ_hit(k, px, py, oz, vx, vy, 0.0f);
+            if (toc < t) {
+                if (!in_medium) return false;
+                t = toc;
+            }
+        }
+        if (!(t < TVAM_INF)) return false;
+        if (in_medium) {
+            o2x = px;
+            o2y = py;
+            d2x = vx;
+            d2y = vy;
+            maxt = t;
+            weight = att;
+            return true;
+        }
+        const float nx = inner ? nix : nex, ny = inner ? niy : ney, nz = inner ? niz : nez;
+        const float hx = fmaf(vx, t, px), hy = fmaf(vy, t, py), hz = fmaf(0.0f, t, oz);
+        float wx, wy, wz;
+        const float w = tvam_transmit_world(nx, ny, nz, vx, vy, 0.0f, inner ? k.eta_int : k.eta_ext, wx, wy, wz);
+        if (!(w > 0.0f)) return false;
+        att = att * w;
+        const float m = fmaxf(fmaxf(fabsf(hx), fabsf(hy)), fabsf(hz));
+        float mag = (1.0f + m) * TVAM_RAY_EPS;
+        const float nwo = nx * wx + ny * wy + nz * wz;
+        if (__builtin_signbit(nwo)) mag = -mag;
+        px = fmaf(mag, nx, hx);
+        py = fmaf(mag, ny, hy);
+        vx = wx;
+        vy = wy;
+        in_medium = inner && nwo < 0.0f;
+    }
+    return false;
+}
+
 // Cylindrical vial (geometry.py:142-183, volume.py:179-272 transmission-only):
 // surface hits in order (nearest of the r_ext / r_int tubes), transmission
 // and spawn_ray at each, until the ray runs inside r_int; the medium segment
@@ -206,7 +362,14 @@ TVAM_HD bool tvam_segment_cyl(const TvamConsts& k, float ox, float oy, float oz,
     for (int depth = 0; depth < k.max_depth; ++depth) {
         const float te = tvam_tube_hit(px, py, vx, vy, k.vial_r_ext), ti = tvam_tube_hit(px, py, vx, vy, k.vial_r);
         const bool inner = ti <= te;
-        const float t = inner ? ti : te;
+        float t = inner ? ti : te;
+        if (k.n_occ) {
+            const float toc = tvam_occ_hit(k, px, py, oz, vx, vy, 0.0f);
+            if (toc < t) {  // an occluder: the segment ends there, or the ray dies outside the medium
+                if (!in_medium) return false;
+                t = toc;
+            }
+        }
         if (!(t < TVAM_INF)) return false;
         if (in_medium) {
             o2x = px;
@@ -242,6 +405,8 @@ TVAM_HD bool tvam_segment(const TvamConsts& k, float ox, float oy, float oz, flo
                           float& o2y, float& d2x, float& d2y, float& maxt, float& weight) {
     if (k.vial_type == 1 /* TVAM_VIAL_CYLINDRICAL */)
         return tvam_segment_cyl(k, ox, oy, oz, dx, dy, o2x, o2y, d2x, d2y, maxt, weight);
+    if (k.vial_type == 2 /* TVAM_VIAL_SQUARE */)
+        return tvam_segment_square(k, ox, oy, oz, dx, dy, o2x, o2y, d2x, d2y, maxt, weight);
     d2x = dx;
     d2y = dy;
     weight = 1.0f;

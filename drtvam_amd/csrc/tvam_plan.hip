@@ -40,7 +40,8 @@ struct tvam_plan {
     size_t lds_bytes;
     int32_t max_rows_per_slice;
     bool empty;  // max_depth too small for any ray to reach the medium
-    bool cyl;    // refracting (cylindrical) vial: per-ray directions and weights
+    bool cyl;    // refracting (cylindrical / square) vial: per-ray directions and weights
+    float* d_occ = nullptr;  // occluder triangles
     // device tables
     float2* d_cs = nullptr;
     int32_t* d_slice_off = nullptr;
@@ -142,6 +143,7 @@ static void plan_free(tvam_plan* p) {
     (void)hipFree(p->d_pl_rec_i);
     (void)hipFree(p->d_pl_rec_g);
     (void)hipFree(p->d_amax);
+    (void)hipFree(p->d_occ);
     (void)hipFree(p->d_fscale);
     delete p;
 }
@@ -160,8 +162,11 @@ static int validate(const tvam_desc& d) {
     if (d.projector_type != TVAM_PROJECTOR_COLLIMATED)
         return fail(TVAM_ERR_UNSUPPORTED, "only the 'collimated' projector is implemented on the GPU path");
     if (d.sensor_type != TVAM_SENSOR_DDA) return fail(TVAM_ERR_UNSUPPORTED, "only the 'dda' sensor is implemented");
-    if (d.vial_type != TVAM_VIAL_INDEX_MATCHED && d.vial_type != TVAM_VIAL_CYLINDRICAL)
-        return fail(TVAM_ERR_UNSUPPORTED, "only the 'index_matched' and 'cylindrical' containers are implemented on the GPU path");
+    if (d.vial_type != TVAM_VIAL_INDEX_MATCHED && d.vial_type != TVAM_VIAL_CYLINDRICAL &&
+        d.vial_type != TVAM_VIAL_SQUARE)
+        return fail(TVAM_ERR_UNSUPPORTED, "only the 'index_matched', 'cylindrical' and 'square' containers are implemented on the GPU path");
+    if (d.n_occluder_tris < 0 || (d.n_occluder_tris > 0 && !d.occluder_tris))
+        return fail(TVAM_ERR_INVALID, "occluder_tris is null");
     if (d.film_channels != 1) return fail(TVAM_ERR_UNSUPPORTED, "surface-aware films (2 channels) are not implemented");
     if (!(d.albedo >= 0.0f && d.albedo <= 1.0f)) return fail(TVAM_ERR_INVALID, "medium albedo must lie in [0, 1]");
     if (d.albedo != 0.0f) {
@@ -174,7 +179,7 @@ static int validate(const tvam_desc& d) {
     if (d.sample_time) return fail(TVAM_ERR_UNSUPPORTED, "sample_time is not implemented on the GPU path");
     // the medium segment is path vertex 1 (index matched) or 2 (behind two glass
     // surfaces); Russian roulette starts at depth > rr_depth (volume.py:182-185)
-    if (d.rr_depth < (d.vial_type == TVAM_VIAL_CYLINDRICAL ? 2 : 1))
+    if (d.rr_depth < (d.vial_type == TVAM_VIAL_INDEX_MATCHED ? 1 : 2))
         return fail(TVAM_ERR_UNSUPPORTED, "Russian roulette before the medium segment (rr_depth too small) is not implemented");
     if (d.n_patterns <= 0 || d.res_x <= 0 || d.res_y <= 0) return fail(TVAM_ERR_INVALID, "projector resolution and n_patterns must be positive");
     if (d.crop_x <= 0 || d.crop_y <= 0 || d.crop_x > d.res_x || d.crop_y > d.res_y)
@@ -187,9 +192,9 @@ static int validate(const tvam_desc& d) {
         if (!(d.bbox_max[a] > d.bbox_min[a])) return fail(TVAM_ERR_INVALID, "sensor bounding box is empty");
     }
     if (!(d.vial_r > 0.0f)) return fail(TVAM_ERR_INVALID, "vial radius must be positive");
-    if (d.vial_type == TVAM_VIAL_CYLINDRICAL &&
+    if (d.vial_type != TVAM_VIAL_INDEX_MATCHED &&
         !(d.vial_r_ext > d.vial_r && d.vial_ior > 0.0f && d.medium_ior > 0.0f && d.vial_height > 0.0f))
-        return fail(TVAM_ERR_INVALID, "cylindrical vial: need r_ext > r_int > 0 and positive IORs");
+        return fail(TVAM_ERR_INVALID, "glass vial: need r_ext > r_int > 0 (w_ext > w_int) and positive IORs");
     {
         const int z1 = d.slab_end < 0 ? d.film_res[2] : d.slab_end;
         if (d.slab_begin < 0 || z1 > d.film_res[2] || d.slab_begin >= z1)
@@ -236,6 +241,7 @@ static TvamConsts make_consts(const tvam_desc& d, int a0, int a1) {
     k.vial_r = d.vial_r;
     k.vial_half_h = 0.5f * d.vial_height;
     k.vial_r_ext = d.vial_r_ext;
+    k.vial_hz_int = (float)(0.5 * 0.9 * (double)d.vial_height);  // geometry.py:207 (inner cuboid)
     k.eta_ext = d.vial_ior / TVAM_IOR_AIR;   // int/ext IOR of the outer surface (geometry.py:160-170)
     k.eta_int = d.medium_ior / d.vial_ior;   // and of the inner one (geometry.py:171-183)
     k.nsig2 = -d.sigma_t * 1.44269504088896340736f;
@@ -279,7 +285,8 @@ static bool planar_fwd_setup(tvam_plan* p, const std::vector<float2>& cs, const 
 static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     const tvam_desc& d = p->desc;
     const TvamConsts& k = p->k;
-    if (!d.regular_sampling || (d.flags & TVAM_FLAG_NO_PLANAR) || p->empty) return 0;
+    // occluders end segments at z-dependent points: rows no longer share a path
+    if (!d.regular_sampling || (d.flags & TVAM_FLAG_NO_PLANAR) || p->empty || d.n_occluder_tris > 0) return 0;
     std::vector<std::vector<int32_t>> rows_of(k.nz);
     for (int rc = 0; rc < d.crop_y; ++rc) {
         float xc, yc;
@@ -495,13 +502,19 @@ void mark_tiles(const TileGrid& g, const CylChord& ch, double m, F&& mark) {
 // ceil(sqrt2 h / s_min) + 2 columns' rays cross a voxel; a factor 2 covers the
 // approximation.  Chords that cross (or touch) inside the medium: infinite
 // (the kernels then add in float).
-static float cyl_rays_per_voxel(const tvam_desc& d, const TvamConsts& k, int ns) {
+static float cyl_rays_per_voxel(const tvam_desc& d, const TvamConsts& k, const std::vector<float2>& cs) {
     const int sub = d.regular_sampling ? 1 : 8;
+    const int ns = (int)cs.size();
+    // a tube is rotation invariant (one angle); a cuboid is not (every angle)
+    const int nang = d.vial_type == TVAM_VIAL_SQUARE ? ns : std::min(ns, 1);
+    double smin = INFINITY, wmax = 1.0;
     std::vector<CylChord> ch;
+    for (int ai = 0; ai < nang; ++ai) {
+    const float c = d.vial_type == TVAM_VIAL_SQUARE ? cs[ai].x : 1.0f, sn = d.vial_type == TVAM_VIAL_SQUARE ? cs[ai].y : 0.0f;
+    ch.clear();
     for (int col = 0; col < d.crop_x; ++col)
         for (int j = 0; j < sub; ++j)
-            ch.push_back(cyl_chord(k, 1.0f, 0.0f, d.crop_offset_x + col, ((float)j + 0.5f) / (float)sub));
-    double smin = INFINITY, wmax = 1.0;
+            ch.push_back(cyl_chord(k, c, sn, d.crop_offset_x + col, ((float)j + 0.5f) / (float)sub));
     for (size_t i = 0; i < ch.size(); ++i) {
         if (!ch[i].hit) continue;
         wmax = std::max(wmax, (double)ch[i].w);
@@ -513,6 +526,7 @@ static float cyl_rays_per_voxel(const tvam_desc& d, const TvamConsts& k, int ns)
         const double db = (ch[i + 1].bx - ch[i].ax) * nx + (ch[i + 1].by - ch[i].ay) * ny;
         if (!(da * db > 0.0)) return INFINITY;
         smin = std::min(smin, std::min(std::fabs(da), std::fabs(db)) * sub);
+    }
     }
     if (!(smin < INFINITY)) return k.rays_per_voxel;  // fewer than two chords: the straight-ray bound
     const double hxy = std::max((double)k.h[0], (double)k.h[1]);
@@ -588,10 +602,19 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
     p->desc = d;
     p->device = device;
     p->k = make_consts(d, a0, a1);
-    p->cyl = d.vial_type == TVAM_VIAL_CYLINDRICAL;
-    // index matched: entry bounce + medium segment; cylindrical: two glass
+    p->cyl = d.vial_type == TVAM_VIAL_CYLINDRICAL || d.vial_type == TVAM_VIAL_SQUARE;
+    // index matched: entry bounce + medium segment; glass vials: two glass
     // surfaces + medium segment (volume.py:179, :271-272)
     p->empty = d.max_depth < (p->cyl ? 3 : 2);
+    if (d.n_occluder_tris > 0) {  // occluder triangles to the device (TvamConsts::occ)
+        std::vector<float> tri(d.occluder_tris, d.occluder_tris + 9 * (size_t)d.n_occluder_tris);
+        if ((rc = upload(&p->d_occ, tri))) {
+            plan_free(p);
+            return rc;
+        }
+        p->k.occ = p->d_occ;
+        p->k.n_occ = d.n_occluder_tris;
+    }
     const TvamConsts& k = p->k;
     const int ns = a1 - a0;
 
@@ -686,8 +709,12 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
     int64_t max_nrt = 0;
     if (p->cyl) {
         std::vector<std::vector<uint32_t>> per_tile;
-        cyl_slot_lists(d, k, cs, tsx, tsy, ntx, nty, marg_l + 1e-3 * std::min(k.h[0], k.h[1]), per_tile);
-        p->k.rays_per_voxel = cyl_rays_per_voxel(d, k, ns);
+        // host tracing without occluders (device memory; they only shorten chords: a superset)
+        TvamConsts kh = k;
+        kh.occ = nullptr;
+        kh.n_occ = 0;
+        cyl_slot_lists(d, kh, cs, tsx, tsy, ntx, nty, marg_l + 1e-3 * std::min(k.h[0], k.h[1]), per_tile);
+        p->k.rays_per_voxel = cyl_rays_per_voxel(d, kh, cs);
         for (int t = 0; t < p->ntiles; ++t) {
             slots.insert(slots.end(), per_tile[t].begin(), per_tile[t].end());
             slot_off[(size_t)t + 1] = (int64_t)slots.size();

@@ -41,14 +41,23 @@ __device__ __forceinline__ float sc_tube_hit(float ox, float oy, float oz, float
 
 // Next container surface from inside the medium (the inner / index-matched tube
 // comes first; the outer tube is only reached through it).
+// Square vial: the inner cuboid (closed: its top and bottom faces end a
+// segment too).  Occluders end a segment where they are nearer.
 __device__ __forceinline__ float sc_container_hit(const TvamConsts& k, float ox, float oy, float oz, float dx,
                                                   float dy, float dz) {
-    const float ti = sc_tube_hit(ox, oy, oz, dx, dy, dz, k.vial_r, k.vial_half_h);
-    if (k.vial_type == 1) {
-        const float te = sc_tube_hit(ox, oy, oz, dx, dy, dz, k.vial_r_ext, k.vial_half_h);
-        if (!(ti <= te)) return te;  // (never from inside; kept like the oracle)
+    float t;
+    if (k.vial_type == 2) {
+        float nx, ny, nz;
+        t = tvam_box_hit(ox, oy, oz, dx, dy, dz, k.vial_r, k.vial_r, k.vial_hz_int, nx, ny, nz);
+    } else {
+        t = sc_tube_hit(ox, oy, oz, dx, dy, dz, k.vial_r, k.vial_half_h);
+        if (k.vial_type == 1) {
+            const float te = sc_tube_hit(ox, oy, oz, dx, dy, dz, k.vial_r_ext, k.vial_half_h);
+            if (!(t <= te)) t = te;  // (never from inside; kept like the oracle)
+        }
     }
-    return ti;
+    if (k.n_occ) t = fminf(t, tvam_occ_hit(k, ox, oy, oz, dx, dy, dz));
+    return t;
 }
 
 // Mitsuba coordinate_system() (Duff et al. 2017) and the phase functions'
@@ -176,7 +185,7 @@ __global__ __launch_bounds__(256) void tvam_scatter_kernel(TvamConsts k, TvamTil
     const int64_t per_angle = (int64_t)k.crop_y * k.crop_x;
     const int64_t n = (int64_t)tp.n_shard * per_angle * spp;
     const float st = k.sig_t, ss = k.sig_s;
-    const int nsurf = k.vial_type == 1 ? 2 : 1;
+    const int nsurf = k.vial_type == 0 ? 1 : 2;  // glass vials: two surfaces before the medium
     uint64_t nvis = 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t local = i / spp;

@@ -56,7 +56,17 @@ class Container:
         desc.phase_g = float(phase.get("g", 0.8))  # Mitsuba hg default g
         desc.medium_ior = lookup_ior(self.medium_ior)
         if self.occlusions:
-            raise NotImplementedError("occluder meshes are not supported by the GPU engine yet")
+            import numpy as np
+            from .utils import read_ply
+            tris = []
+            for occ in self.occlusions:
+                bsdf = occ.get("bsdf")
+                if bsdf is not None and not (bsdf.get("type") == "diffuse" and
+                                             float(bsdf.get("reflectance", {}).get("value", 0.0)) == 0.0):
+                    raise NotImplementedError("occluders must be black diffuse (the reference default)")
+                v, f = read_ply(occ["filename"])
+                tris.append(np.asarray(v, np.float32)[np.asarray(f)])
+            desc.set_occluders(np.concatenate(tris))
 
 
 # Named refractive indices (Mitsuba's ior table, restated for the names a config may use)
@@ -145,6 +155,14 @@ class SquareVial(Container):
         self.w_ext = params['w_ext']
         self.height = params.get('height', 100.)
         self.vial_ior = params['ior']
+
+    def fill_desc(self, desc):
+        self._fill_medium(desc)
+        desc.vial_type = _abi.VIAL_SQUARE
+        desc.vial_r = 0.5 * float(self.w_int)
+        desc.vial_r_ext = 0.5 * float(self.w_ext)
+        desc.vial_height = float(self.height)
+        desc.vial_ior = lookup_ior(self.vial_ior)
 
     def to_dict(self):
         return {'printing_medium': self.medium_dict(),

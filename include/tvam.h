@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define TVAM_ABI_VERSION 3
+#define TVAM_ABI_VERSION 4
 
 /* error codes */
 #define TVAM_OK               0
@@ -57,6 +57,7 @@ extern "C" {
 /* vial / container kinds (geometry.py:312-318) */
 #define TVAM_VIAL_INDEX_MATCHED   0
 #define TVAM_VIAL_CYLINDRICAL     1
+#define TVAM_VIAL_SQUARE          2  /* glass cuboids w_ext / w_int (vial_r = w_int/2, vial_r_ext = w_ext/2) */
 
 /* medium phase functions (Mitsuba 'isotropic', 'rayleigh', 'hg'; geometry.py:29-39) */
 #define TVAM_PHASE_ISOTROPIC      0
@@ -122,6 +123,11 @@ typedef struct tvam_desc {
     /* scattering media (albedo > 0): medium 'phase' {'type', 'g'} */
     int32_t phase_type;           /* TVAM_PHASE_* */
     float   phase_g;              /* 'hg' asymmetry g */
+    /* occluder meshes ('occlusions', geometry.py:55-72): black diffuse
+       triangles; host array [n_occluder_tris][3 vertices][x, y, z], read by
+       tvam_plan_create (not kept) */
+    const float* occluder_tris;
+    int32_t n_occluder_tris;
 } tvam_desc;
 
 /* tvam_desc.flags */

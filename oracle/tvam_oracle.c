@@ -220,6 +220,70 @@ static int or_cyl_roots(const float o[3], const float dd[3], float r, float* t0,
     return or_solve_quadratic(A, B, C, t0, t1);
 }
 
+/* ------------------------------------------------------------------------ */
+/* Occluders ('occlusions', geometry.py:55-72): black diffuse triangle       */
+/* meshes.  Mitsuba's ray_intersect_triangle restated (Moller-Trumbore,     */
+/* t in [0, maxt]); a path that reaches one ends there (black BSDF: weight   */
+/* 0, volume.py:245-266).  UNPINNED (OptiX does this on the reference's GPU).*/
+/* ------------------------------------------------------------------------ */
+static float or_tri_hit(const float o[3], const float dd[3], const float* v) {
+    float e1[3], e2[3], tv[3];
+    for (int k = 0; k < 3; ++k) {
+        e1[k] = v[3 + k] - v[k];
+        e2[k] = v[6 + k] - v[k];
+        tv[k] = o[k] - v[k];
+    }
+    float pv[3] = {dd[1] * e2[2] - dd[2] * e2[1], dd[2] * e2[0] - dd[0] * e2[2], dd[0] * e2[1] - dd[1] * e2[0]};
+    float inv_det = 1.0f / (e1[0] * pv[0] + e1[1] * pv[1] + e1[2] * pv[2]);
+    float u = (tv[0] * pv[0] + tv[1] * pv[1] + tv[2] * pv[2]) * inv_det;
+    if (!(u >= 0.0f && u <= 1.0f)) return INFINITY;
+    float qv[3] = {tv[1] * e1[2] - tv[2] * e1[1], tv[2] * e1[0] - tv[0] * e1[2], tv[0] * e1[1] - tv[1] * e1[0]};
+    float w = (dd[0] * qv[0] + dd[1] * qv[1] + dd[2] * qv[2]) * inv_det;
+    if (!(w >= 0.0f && u + w <= 1.0f)) return INFINITY;
+    float t = (e2[0] * qv[0] + e2[1] * qv[1] + e2[2] * qv[2]) * inv_det;
+    return t >= 0.0f ? t : INFINITY;
+}
+
+static float or_occ_hit(const tvam_desc* d, const float o[3], const float dd[3]) {
+    float best = INFINITY;
+    for (int i = 0; i < d->n_occluder_tris; ++i) best = fminf(best, or_tri_hit(o, dd, d->occluder_tris + 9 * i));
+    return best;
+}
+
+/* Closed axis-aligned box [-h, h] (Mitsuba 'cube' scaled, geometry.py:186-219):
+   nearest t >= 0 (entry from outside, exit from inside), outward face normal. */
+static float or_box_hit(const float o[3], const float dd[3], const float h[3], float n[3]) {
+    float tn = -INFINITY, tf = INFINITY;
+    int an = -1, af = -1;
+    for (int a = 0; a < 3; ++a) {
+        if (dd[a] == 0.0f) {
+            if (!(o[a] >= -h[a] && o[a] <= h[a])) return INFINITY;
+            continue;
+        }
+        float t0 = (-h[a] - o[a]) / dd[a], t1 = (h[a] - o[a]) / dd[a];
+        float lo = fminf(t0, t1), hi = fmaxf(t0, t1);
+        if (lo > tn) {
+            tn = lo;
+            an = a;
+        }
+        if (hi < tf) {
+            tf = hi;
+            af = a;
+        }
+    }
+    if (!(tn <= tf)) return INFINITY;
+    n[0] = n[1] = n[2] = 0.0f;
+    if (tn >= 0.0f) {
+        n[an] = dd[an] > 0.0f ? -1.0f : 1.0f;
+        return tn;
+    }
+    if (tf >= 0.0f) {
+        n[af] = dd[af] > 0.0f ? 1.0f : -1.0f;
+        return tf;
+    }
+    return INFINITY;
+}
+
 /* In-medium segment of a projector ray: origin o', maxt.  Returns 0 on miss. */
 static int or_segment_index_matched(const or_scene* s, const or_ray* ray, float o2[3], float* maxt) {
     const tvam_desc* d = s->d;
@@ -228,6 +292,7 @@ static int or_segment_index_matched(const or_scene* s, const or_ray* ray, float 
     float t0, t1;
     if (!or_cyl_roots(ray->o, ray->d, d->vial_r, &t0, &t1)) return 0;
     if (!(t0 >= 0.0f)) return 0; /* projector outside the vial: the entry is the near root */
+    if (d->n_occluder_tris && or_occ_hit(d, ray->o, ray->d) < t0) return 0; /* blocked before the vial */
     float p[3];
     for (int k = 0; k < 3; ++k) p[k] = fmaf(ray->d[k], t0, ray->o[k]);
     float rp = sqrtf(p[0] * p[0] + p[1] * p[1]);
@@ -241,6 +306,7 @@ static int or_segment_index_matched(const or_scene* s, const or_ray* ray, float 
     if (!or_cyl_roots(o2, ray->d, d->vial_r, &u0, &u1)) return 0;
     if (!(u1 > 0.0f)) return 0;
     *maxt = u1;
+    if (d->n_occluder_tris) *maxt = fminf(u1, or_occ_hit(d, o2, ray->d)); /* ends on an occluder */
     return 1;
 }
 
@@ -316,6 +382,13 @@ static int or_segment_cylindrical(const or_scene* s, const or_ray* ray, float o2
         float te = or_tube_hit(o, dd, d->vial_r_ext, half), ti = or_tube_hit(o, dd, d->vial_r, half);
         int inner = ti <= te;
         float t = inner ? ti : te;
+        if (d->n_occluder_tris) {
+            float toc = or_occ_hit(d, o, dd);
+            if (toc < t) { /* an occluder: the segment ends there, or the ray dies outside the medium */
+                if (!in_medium) return 0;
+                t = toc;
+            }
+        }
         if (!(t < INFINITY)) return 0;
         if (in_medium) { /* the medium segment [0, t] (volume.py:209-216) */
             for (int k = 0; k < 3; ++k) {
@@ -353,6 +426,81 @@ static int or_segment_cylindrical(const or_scene* s, const or_ray* ray, float o2
 /* DDA declared ahead for the scattering path */
 static double or_dda(const or_scene* s, const float o[3], const float dd[3], float maxt, double em,
                      int mode, double* film, const float* grad, int only_slice, uint64_t* visits);
+
+/* Square vial (geometry.py:186-219): glass cuboids, outer [-w_ext/2, w_ext/2]^2
+   x [-h/2, h/2] (dielectric air|glass), inner [-w_int/2, w_int/2]^2 x
+   [-0.45 h, 0.45 h] (glass|medium, interior = the medium).  Same loop as the
+   tubes; the transmission uses the world-space form of Mitsuba's refract()
+   (wo = -eta_ti wi + (eta_ti cos_i + cos_t) n, frame-independent for the
+   cube's faces). */
+static float or_transmit_world(const float n[3], const float dd[3], float eta, float wo[3]) {
+    float cos_i = -(dd[0] * n[0] + dd[1] * n[1] + dd[2] * n[2]);
+    float cos_t, eta_ti;
+    float r = or_fresnel(cos_i, eta, &cos_t, &eta_ti);
+    float t = 1.0f - r;
+    if (!(t > 0.0f)) return 0.0f;
+    float c = eta_ti * cos_i + cos_t;
+    for (int k = 0; k < 3; ++k) wo[k] = eta_ti * dd[k] + c * n[k];
+    return t * (eta_ti * eta_ti);
+}
+
+static void or_square_extents(const tvam_desc* d, float he[3], float hi[3]) {
+    he[0] = he[1] = d->vial_r_ext;
+    he[2] = 0.5f * d->vial_height;
+    hi[0] = hi[1] = d->vial_r;
+    hi[2] = (float)(0.5 * 0.9 * (double)d->vial_height);
+}
+
+static int or_segment_square(const or_scene* s, const or_ray* ray, float o2[3], float d2[3], float* maxt,
+                             double* weight) {
+    const tvam_desc* d = s->d;
+    float he[3], hi[3];
+    or_square_extents(d, he, hi);
+    float o[3] = {ray->o[0], ray->o[1], ray->o[2]}, dd[3] = {ray->d[0], ray->d[1], ray->d[2]};
+    float att = 1.0f;
+    int in_medium = 0;
+    for (int depth = 0; depth < d->max_depth; ++depth) {
+        float ne[3], ni[3];
+        float te = or_box_hit(o, dd, he, ne), ti = or_box_hit(o, dd, hi, ni);
+        int inner = ti <= te;
+        float t = inner ? ti : te;
+        if (d->n_occluder_tris) {
+            float toc = or_occ_hit(d, o, dd);
+            if (toc < t) {
+                if (!in_medium) return 0;
+                t = toc;
+            }
+        }
+        if (!(t < INFINITY)) return 0;
+        if (in_medium) {
+            for (int k = 0; k < 3; ++k) {
+                o2[k] = o[k];
+                d2[k] = dd[k];
+            }
+            *maxt = t;
+            *weight = (double)att;
+            return 1;
+        }
+        const float* n = inner ? ni : ne;
+        float p[3];
+        for (int k = 0; k < 3; ++k) p[k] = fmaf(dd[k], t, o[k]);
+        float eta = inner ? d->medium_ior / d->vial_ior : d->vial_ior / OR_IOR_AIR;
+        float wo[3];
+        float w = or_transmit_world(n, dd, eta, wo);
+        if (!(w > 0.0f)) return 0;
+        att = att * w;
+        float m = fmaxf(fmaxf(fabsf(p[0]), fabsf(p[1])), fabsf(p[2]));
+        float mag = (1.0f + m) * OR_RAY_EPS;
+        float nwo = n[0] * wo[0] + n[1] * wo[1] + n[2] * wo[2];
+        if (signbit(nwo)) mag = -mag;
+        for (int k = 0; k < 3; ++k) {
+            o[k] = fmaf(mag, n[k], p[k]);
+            dd[k] = wo[k];
+        }
+        in_medium = inner && nwo < 0.0f;
+    }
+    return 0;
+}
 
 /* ------------------------------------------------------------------------ */
 /* Scattering media: the full path loop of volume.py:179-272  */
@@ -436,16 +584,30 @@ static void or_phase_sample(const tvam_desc* d, const float dd[3], float u1, flo
 static float or_container_hit(const or_scene* s, const float o[3], const float dd[3], int* which) {
     const tvam_desc* d = s->d;
     float half = 0.5f * d->vial_height;
-    float ti = or_tube_hit(o, dd, d->vial_r, half);
+    float t;
     *which = 1;
-    if (d->vial_type == TVAM_VIAL_CYLINDRICAL) {
-        float te = or_tube_hit(o, dd, d->vial_r_ext, half);
-        if (!(ti <= te)) {
-            *which = 0;
-            return te;
+    if (d->vial_type == TVAM_VIAL_SQUARE) {
+        float he[3], hi[3], n[3];
+        or_square_extents(d, he, hi);
+        t = or_box_hit(o, dd, hi, n);
+    } else {
+        t = or_tube_hit(o, dd, d->vial_r, half);
+        if (d->vial_type == TVAM_VIAL_CYLINDRICAL) {
+            float te = or_tube_hit(o, dd, d->vial_r_ext, half);
+            if (!(t <= te)) {
+                *which = 0;
+                t = te;
+            }
         }
     }
-    return ti;
+    if (d->n_occluder_tris) {
+        float toc = or_occ_hit(d, o, dd);
+        if (toc < t) {
+            *which = 2;
+            t = toc;
+        }
+    }
+    return t;
 }
 
 /* One scattering path (volume.py:179-272).  The first medium segment is the
@@ -462,8 +624,10 @@ static double or_trace_scatter(const or_scene* s, uint32_t pixel, uint64_t wave_
     float o[3], dd[3], maxt;
     double attd = 1.0;
     int nsurf;
-    if (d->vial_type == TVAM_VIAL_CYLINDRICAL) {
-        if (!or_segment_cylindrical(s, &ray, o, dd, &maxt, &attd)) return 0.0;
+    if (d->vial_type == TVAM_VIAL_CYLINDRICAL || d->vial_type == TVAM_VIAL_SQUARE) {
+        if (!(d->vial_type == TVAM_VIAL_SQUARE ? or_segment_square(s, &ray, o, dd, &maxt, &attd)
+                                               : or_segment_cylindrical(s, &ray, o, dd, &maxt, &attd)))
+            return 0.0;
         nsurf = 2;
     } else {
         if (d->max_depth < 2 || !or_segment_index_matched(s, &ray, o, &maxt)) return 0.0;
@@ -624,7 +788,10 @@ static uint64_t or_stream(const tvam_desc* d, uint32_t pixel) {
 }
 
 static int or_check(const tvam_desc* d) {
-    if (d->vial_type != TVAM_VIAL_INDEX_MATCHED && d->vial_type != TVAM_VIAL_CYLINDRICAL) return TVAM_ERR_UNSUPPORTED;
+    if (d->vial_type != TVAM_VIAL_INDEX_MATCHED && d->vial_type != TVAM_VIAL_CYLINDRICAL &&
+        d->vial_type != TVAM_VIAL_SQUARE)
+        return TVAM_ERR_UNSUPPORTED;
+    if (d->n_occluder_tris < 0 || (d->n_occluder_tris > 0 && !d->occluder_tris)) return TVAM_ERR_INVALID;
     if (d->projector_type != TVAM_PROJECTOR_COLLIMATED) return TVAM_ERR_UNSUPPORTED;
     if (d->film_channels != 1) return TVAM_ERR_UNSUPPORTED;
     if (d->albedo < 0.0f || d->albedo > 1.0f) return TVAM_ERR_INVALID;
@@ -632,7 +799,7 @@ static int or_check(const tvam_desc* d) {
     if (d->phase_type < TVAM_PHASE_ISOTROPIC || d->phase_type > TVAM_PHASE_HG) return TVAM_ERR_INVALID;
     /* Russian roulette (volume.py:182-185, depth > rr_depth) before the medium
        segment (path vertex 1 index matched, 2 behind the glass) is not restated */
-    if (d->rr_depth < (d->vial_type == TVAM_VIAL_CYLINDRICAL ? 2 : 1)) return TVAM_ERR_UNSUPPORTED;
+    if (d->rr_depth < (d->vial_type == TVAM_VIAL_INDEX_MATCHED ? 1 : 2)) return TVAM_ERR_UNSUPPORTED;
     return 0;
 }
 
@@ -645,10 +812,12 @@ static double or_trace(const or_scene* s, uint32_t pixel, uint64_t wave_index, u
     or_ray ray;
     or_gen_ray(s, pixel, wave_index, seed, &ray);
     float o2[3], maxt;
-    if (s->d->vial_type == TVAM_VIAL_CYLINDRICAL) {
+    if (s->d->vial_type == TVAM_VIAL_CYLINDRICAL || s->d->vial_type == TVAM_VIAL_SQUARE) {
         float d2[3];
         double att;
-        if (!or_segment_cylindrical(s, &ray, o2, d2, &maxt, &att)) return 0.0;
+        if (!(s->d->vial_type == TVAM_VIAL_SQUARE ? or_segment_square(s, &ray, o2, d2, &maxt, &att)
+                                                  : or_segment_cylindrical(s, &ray, o2, d2, &maxt, &att)))
+            return 0.0;
         /* the interfaces' attenuation scales every contribution (sensor.py:404) */
         if (mode == 0) return or_dda(s, o2, d2, maxt, em * att, mode, film, grad, only_slice, visits);
         return att * or_dda(s, o2, d2, maxt, em, mode, film, grad, only_slice, visits);
@@ -831,6 +1000,7 @@ int oracle_ray(const tvam_desc* d, uint32_t pixel, uint64_t wave_index, uint32_t
     int hit = 0;
     if (d->vial_type == TVAM_VIAL_INDEX_MATCHED) hit = or_segment_index_matched(&s, &ray, o2, &maxt);
     else if (d->vial_type == TVAM_VIAL_CYLINDRICAL) hit = or_segment_cylindrical(&s, &ray, o2, d2, &maxt, &att);
+    else if (d->vial_type == TVAM_VIAL_SQUARE) hit = or_segment_square(&s, &ray, o2, d2, &maxt, &att);
     out[6] = (float)hit;
     out[7] = o2[0];
     out[8] = o2[1];

@@ -27,20 +27,23 @@ def test_library_exports_every_declared_symbol():
     assert set(names) == set(_abi.EXPORTS), "ctypes signature table out of sync with include/tvam.h"
 
 
-def test_desc_layout_matches_header():
-    # the ctypes mirror must have the same size as the C struct: count fields in the header
-    src = open(HEADER).read()
-    body = src[src.index("typedef struct tvam_desc {"):src.index("} tvam_desc;")]
-    body = re.sub(r"/\*.*?\*/", "", body, flags=re.S)
-    n = 0
-    for line in body.splitlines():
-        m = re.match(r"\s*(int32_t|float)\s+(.*);", line)
-        if not m:
-            continue
-        for decl in m.group(2).split(","):
-            arr = re.search(r"\[(\d+)\]", decl)
-            n += int(arr.group(1)) if arr else 1
-    assert ctypes.sizeof(_abi.TvamDesc) == 4 * n
+def test_desc_layout_matches_header(tmp_path):
+    """The ctypes mirror has the C struct's size and field offsets (compiled with gcc)."""
+    import shutil
+    import subprocess
+    if shutil.which("gcc") is None:
+        pytest.skip("gcc not available")
+    names = [n for n, _ in _abi.TvamDesc._fields_]
+    src = tmp_path / "layout.c"
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "tvam.h"\nint main(void){\n'
+                   'printf("%zu\\n", sizeof(tvam_desc));\n' +
+                   "".join(f'printf("%zu\\n", offsetof(tvam_desc, {n}));\n' for n in names) + "return 0;}\n")
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-I", os.path.dirname(HEADER), str(src), "-o", str(exe)], check=True)
+    vals = [int(x) for x in subprocess.run([str(exe)], check=True, capture_output=True, text=True).stdout.split()]
+    assert ctypes.sizeof(_abi.TvamDesc) == vals[0]
+    for n, off in zip(names, vals[1:]):
+        assert getattr(_abi.TvamDesc, n).offset == off, n
 
 
 def test_desc_defaults_follow_reference():
