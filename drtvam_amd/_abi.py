@@ -120,6 +120,7 @@ EXPORTS = {
     "tvam_axpy_clamp": (ctypes.c_int, [ctypes.c_uint64, _P, ctypes.c_float, _P, ctypes.c_float, _P, _P]),
     "tvam_row_slices": (ctypes.c_int, [ctypes.POINTER(TvamDesc), _P]),
     "tvam_plan_path": (ctypes.c_int, [_P]),
+    "tvam_radon": (ctypes.c_int, [_P, _P, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int32, _P, _P]),
     "tvam_count_visits": (ctypes.c_int, [_P, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]),
     "tvam_plan_stats": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),
     "tvam_loss_threshold": (

@@ -10,5 +10,5 @@ HIPCC="${HIPCC:-/opt/rocm/bin/hipcc}"
   -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -munsafe-fp-atomics \
   -Wall -Wno-unused-function \
   -I"$here/../../include" \
-  "$here/tvam_plan.hip" "$here/tvam_kernels.hip" "$here/tvam_planar.hip" "$here/tvam_vec.hip" "$here/tvam_scatter.hip" \
+  "$here/tvam_plan.hip" "$here/tvam_kernels.hip" "$here/tvam_planar.hip" "$here/tvam_vec.hip" "$here/tvam_scatter.hip" "$here/tvam_radon.hip" \
   -o "$out"

@@ -400,6 +400,108 @@ TVAM_HD bool tvam_segment_cyl(const TvamConsts& k, float ox, float oy, float oz,
     return false;
 }
 
+// Radon filter path (integrators/radon.py:77-106; oracle or_radon_ray): a
+// planar projector ray through the scene (container surfaces, occluders, the
+// target mesh with its null BSDF), summing throughput e^{-st t}(1 - e^{-st
+// si.t}) over the segments inside both the medium and the target (t = the
+// distance travelled so far, from the ray origin).  Target hits toggle
+// inside_target and do not count as depth.  Only L > 0 matters to the filter
+// (optimize.py:143-163).
+TVAM_HD float tvam_radon_ray(const TvamConsts& k, const float* tgt, int ntgt, int max_depth, float ox, float oy,
+                             float oz, float dx, float dy) {
+    float px = ox, py = oy, vx = dx, vy = dy;
+    float thr = 1.0f, L = 0.0f, t = 0.0f;
+    bool in_medium = false, inside = false;
+    int depth = 0;
+    for (int it = 0; it < 4096; ++it) {
+        // nearest surface: container (kind 0 outer glass, 1 medium boundary), occluder (2), target (3)
+        float tb = TVAM_INF, nx = 0.0f, ny = 0.0f;
+        int kind = -1, tri = -1;
+        if (k.vial_type == 2) {
+            float ax, ay, az, bx, by, bz;
+            const float te = tvam_box_hit(px, py, oz, vx, vy, 0.0f, k.vial_r_ext, k.vial_r_ext, k.vial_half_h, ax, ay, az);
+            const float ti = tvam_box_hit(px, py, oz, vx, vy, 0.0f, k.vial_r, k.vial_r, k.vial_hz_int, bx, by, bz);
+            if (ti <= te) {
+                tb = ti;
+                kind = 1;
+                nx = bx;
+                ny = by;
+            } else {
+                tb = te;
+                kind = 0;
+                nx = ax;
+                ny = ay;
+            }
+        } else if (oz >= -k.vial_half_h && oz <= k.vial_half_h) {
+            const float ti = tvam_tube_hit(px, py, vx, vy, k.vial_r);
+            const float te = k.vial_type == 1 ? tvam_tube_hit(px, py, vx, vy, k.vial_r_ext) : TVAM_INF;
+            tb = ti <= te ? ti : te;
+            kind = ti <= te ? 1 : 0;
+        }
+        if (k.n_occ) {
+            const float toc = tvam_occ_hit(k, px, py, oz, vx, vy, 0.0f);
+            if (toc < tb) {
+                tb = toc;
+                kind = 2;
+            }
+        }
+        for (int i = 0; i < ntgt; ++i) {
+            const float tt = tvam_tri_hit(tgt + 9 * i, px, py, oz, vx, vy, 0.0f);
+            if (tt < tb) {
+                tb = tt;
+                kind = 3;
+                tri = i;
+            }
+        }
+        if (!(tb < TVAM_INF)) break;
+        const float contrib = thr * expf(-k.sig_t * t) * (1.0f - expf(-k.sig_t * tb));
+        if (inside && in_medium) L = L + contrib;
+        t = t + tb;
+        const float hx = fmaf(vx, tb, px), hy = fmaf(vy, tb, py);
+        float wx = vx, wy = vy, wz = 0.0f, nz = 0.0f;
+        if (kind == 3) {  // target: null BSDF; geometric normal of the triangle for the spawn offset
+            const float* v = tgt + 9 * tri;
+            const float e1x = v[3] - v[0], e1y = v[4] - v[1], e1z = v[5] - v[2];
+            const float e2x = v[6] - v[0], e2y = v[7] - v[1], e2z = v[8] - v[2];
+            float cx = e1y * e2z - e1z * e2y, cy = e1z * e2x - e1x * e2z, cz = e1x * e2y - e1y * e2x;
+            const float inv = 1.0f / sqrtf(cx * cx + cy * cy + cz * cz);
+            nx = cx * inv;
+            ny = cy * inv;
+            nz = cz * inv;
+            inside = !inside;
+        } else if (kind == 2) {
+            break;  // black occluder: throughput 0 from here on
+        } else {
+            if (k.vial_type == 1 || (k.vial_type == 0)) {  // tubes: outward normal
+                const float rp = sqrtf(hx * hx + hy * hy);
+                nx = hx / rp;
+                ny = hy / rp;
+            }
+            if (k.vial_type != 0) {
+                const float eta = kind == 1 ? k.eta_int : k.eta_ext;
+                const float w = k.vial_type == 2 ? tvam_transmit_world(nx, ny, 0.0f, vx, vy, 0.0f, eta, wx, wy, wz)
+                                                 : tvam_transmit(nx, ny, vx, vy, eta, wx, wy);
+                if (!(w > 0.0f)) break;
+                thr = thr * w;
+            }
+            ++depth;
+        }
+        const float m = fmaxf(fmaxf(fabsf(hx), fabsf(hy)), fabsf(oz));
+        float mag = (1.0f + m) * TVAM_RAY_EPS;
+        const float nwo = nx * wx + ny * wy + nz * wz;
+        if (__builtin_signbit(nwo)) mag = -mag;
+        px = fmaf(mag, nx, hx);
+        py = fmaf(mag, ny, hy);
+        // (the offset's z component moves oz by mag * nz for a tilted target face)
+        oz = fmaf(mag, nz, oz);
+        vx = wx;
+        vy = wy;
+        if (depth >= max_depth) break;
+        if (kind == 1) in_medium = nwo < 0.0f;  // the medium boundary is the only medium transition
+    }
+    return L;
+}
+
 // The medium segment of a planar projector ray for the plan's container.
 TVAM_HD bool tvam_segment(const TvamConsts& k, float ox, float oy, float oz, float dx, float dy, float& o2x,
                           float& o2y, float& d2x, float& d2y, float& maxt, float& weight) {

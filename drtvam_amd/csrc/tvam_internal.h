@@ -74,6 +74,10 @@ hipError_t tvam_launch_scatter_paths(int mode, const TvamConsts& k, const TvamTi
                                      const int32_t* idxmap, const float* gin, float* out,
                                      unsigned long long* counter, hipStream_t stream);
 
+// Radon filter image of the shard's DMD pixels (tvam_radon.hip).
+hipError_t tvam_launch_radon(const TvamConsts& k, const TvamTiles& t, const float* tgt, int ntgt, int max_depth,
+                             float wray, float* radon, hipStream_t stream);
+
 // Per-ray pre-pass: ray generation, vial segment and DDA initialisation of
 // every ray of the shard, stored as the records the tile kernels resume from.
 hipError_t tvam_launch_ray_setup(const TvamConsts& k, const TvamTiles& t, float4* ray_f, int2* ray_i,

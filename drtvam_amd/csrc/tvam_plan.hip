@@ -993,6 +993,38 @@ extern "C" int tvam_count_visits(tvam_plan* p, uint32_t spp, uint32_t seed, uint
     return 0;
 }
 
+extern "C" int tvam_radon(tvam_plan* p, const float* target_tris, int32_t n_target_tris, uint32_t spp, uint32_t seed,
+                          int32_t max_depth, float* radon, void* stream_) {
+    if (!p || !radon || n_target_tris < 0 || (n_target_tris > 0 && !target_tris))
+        return fail(TVAM_ERR_INVALID, "null argument");
+    const tvam_desc& d = p->desc;
+    const uint64_t n = (uint64_t)(p->k.a1 - p->k.a0) * d.crop_y * d.crop_x;
+    TvamConsts k;
+    int rc = call_setup(p, n, nullptr, spp, k);
+    if (rc) return rc;
+    hipStream_t stream = (hipStream_t)stream_;
+    float* dt = nullptr;
+    hipError_t e = hipSuccess;
+    if (n_target_tris > 0) {
+        const size_t bytes = (size_t)n_target_tris * 9 * sizeof(float);
+        if ((e = hipMalloc((void**)&dt, bytes)) != hipSuccess) return hip_fail(e, "hipMalloc (target mesh)");
+        if ((e = hipMemcpy(dt, target_tris, bytes, hipMemcpyHostToDevice)) != hipSuccess) {
+            (void)hipFree(dt);
+            return hip_fail(e, "hipMemcpy (target mesh)");
+        }
+    }
+    // ray weight inv_pdf / n / spp * print_time (projector.py:164-165, common.py:111)
+    const float area = d.pixel_size_x * d.pixel_size_y * (float)n;
+    const float wray = area / (float)(n * (uint64_t)spp) * d.print_time;
+    TvamTiles t = p->tiles;
+    t.spp = spp;
+    t.seed = seed;
+    e = tvam_launch_radon(k, t, dt, n_target_tris, max_depth, wray, radon, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    (void)hipFree(dt);
+    return e == hipSuccess ? 0 : hip_fail(e, "radon launch");
+}
+
 // bit 0: planar adjoint (+ ray-driven planar forward unless bit 1), bit 1: voxel-driven planar forward
 extern "C" int tvam_plan_path(const tvam_plan* p) { return p ? (p->planar ? 1 : 0) | (p->planar_fwd ? 2 : 0) : 0; }
 

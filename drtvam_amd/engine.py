@@ -99,6 +99,18 @@ class Projection:
                 n_active, spp, seed & 0xFFFFFFFF, out.data_ptr(), _stream_ptr(self.device)))
         return out
 
+    def radon(self, target_tris, spp: int = 4, seed: int = 0, max_depth: int = 5) -> torch.Tensor:
+        """Radon filter image of this plan's DMD pixels (dense crop order of its shard):
+        positive where a ray crosses the target inside the medium (radon.py:47-106)."""
+        import numpy as np
+        tris = np.ascontiguousarray(target_tris, dtype=np.float32).reshape(-1, 9)
+        a0, a1 = self.desc.angle_begin, (self.desc.angle_end if self.desc.angle_end >= 0 else self.desc.n_patterns)
+        out = torch.empty((a1 - a0) * self.desc.crop_y * self.desc.crop_x, dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            _abi.check(self.lib.tvam_radon(self._plan, tris.ctypes.data if tris.size else None, tris.shape[0], spp,
+                                           seed & 0xFFFFFFFF, max_depth, out.data_ptr(), _stream_ptr(self.device)))
+        return out
+
     @property
     def planar(self) -> bool:
         """True when the planar fast path (regular sampling) serves this plan's adjoint."""

@@ -129,7 +129,11 @@ class ShardedLoop:
         if not w:
             return None
         v = self.allreduce_((torch.abs(x.detach()) ** lf.M).sum(dtype=torch.float64) * w)
-        return v / self.n_global if lf.reduction_name == 'mean' else v
+        return v / self.n_active_global() if lf.reduction_name == 'mean' else v
+
+    def n_active_global(self):
+        """Entries of projector.active_data (after filter_radon, the pixels that stayed active)."""
+        return getattr(self, 'n_filtered', None) or self.n_global
 
     def sparsity_grad(self, x):
         lf = self.loss_fn
@@ -137,7 +141,7 @@ class ShardedLoop:
         if not w:
             return None
         g = w * lf.M * torch.abs(x.detach()) ** (lf.M - 1) * torch.sign(x.detach())
-        return g / self.n_global if lf.reduction_name == 'mean' else g
+        return g / self.n_active_global() if lf.reduction_name == 'mean' else g
 
     # ---- projections ----------------------------------------------------------
     def forward(self, x, seed):
@@ -228,7 +232,7 @@ class ShardedLoop:
 class TvamProblem(ShardedLoop):
     """Scene + target + loss + optimizer state of one optimisation run (one rank's angle shard)."""
 
-    def __init__(self, config, device=None, target=None, rank=None, world_size=None):
+    def __init__(self, config, device=None, target=None, rank=None, world_size=None, filter_pixels=True):
         self.config = config
         self.dist = _dist()
         self.rank = rank if rank is not None else (self.dist.get_rank() if self.dist else 0)
@@ -325,11 +329,38 @@ class TvamProblem(ShardedLoop):
         self.n_local = (self.a1 - self.a0) * (self.r1 - self.r0) * self.crop_x
         self.x0 = self.local_from_global(p.active_data)
         self.proj = self.integrator.projection(self.scene, self.sensor)
+        self.mask = None
+        if config.get('filter_radon', False) and filter_pixels:
+            self._filter_radon(config)
         self.fused = fusable and self.target.shape[-1] == 1
         self.grad_vol = torch.empty(self.proj.film_shape, dtype=torch.float32, device=dev)
         self.opt = None
         self.loss_hist = []
         self.timing = []
+
+    def _filter_radon(self, config):
+        """Deactivate the pixels whose rays never cross the target inside the medium
+        (optimize.py:143-163): the Radon integrator (max_depth 5, jittered, spp_filter_radon
+        samples) on this rank's pixels; patterns and gradients of the others stay 0, which is
+        the reference's compressed active set in the dense layout."""
+        from .engine import Projection
+        from .utils import target_triangles
+        d = self.proj.desc.copy()
+        d.regular_sampling = 0
+        d.max_depth = 5
+        d.flags |= 4  # TVAM_FLAG_NO_PLANAR: no planar tables needed for a setup pass
+        radon = Projection(d, self.device).radon(target_triangles(self.scene), spp=config.get('spp_filter_radon', 4),
+                                                 seed=0, max_depth=5)
+        self.mask = (radon > 0).to(torch.float32)
+        n = self.mask.sum().to(torch.float64)
+        self.n_filtered = int(self.allreduce_(n).item())
+        if self.n_filtered == 0:
+            raise ValueError("No active pixels found in the Radon transform.")
+        self.x0 = self.x0 * self.mask
+
+    def adjoint(self, grad_vol, seed):
+        g = self.adjoint_local(grad_vol, seed)
+        return g if self.mask is None else g.mul_(self.mask)
 
     def _row_band(self, desc):
         """Crop rows [r0, r1) whose rays lie in this rank's slab (rows outside the grid go to the
@@ -409,7 +440,7 @@ class TvamProblem(ShardedLoop):
 
 def optimize(config, patterns_fwd=None, device=None):
     """Optimise the patterns (optimize.py:81-368).  Returns the final dose volume."""
-    prob = TvamProblem(config, device=device)
+    prob = TvamProblem(config, device=device, filter_pixels=patterns_fwd is None)
     output = config.get('output', '.')
     os.makedirs(output, exist_ok=True)
     if prob.rank == 0:

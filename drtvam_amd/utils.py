@@ -160,6 +160,17 @@ def voxelize_mesh(verts, tris, bbox_min, voxel_size, res):
     return occ
 
 
+def target_triangles(scene):
+    """World-space triangles [n, 3, 3] (float32) of the scene's target mesh (optimize.py:30-65)."""
+    tgt = scene.target
+    if tgt is None or 'filename' not in tgt:
+        raise ValueError("No target shape found in the scene")
+    verts, tris = read_ply(tgt['filename'])
+    m = np.asarray(tgt.get('to_world', np.eye(4)), dtype=np.float64)
+    verts = (verts @ m[:3, :3].T + m[:3, 3]).astype(np.float32)
+    return verts[np.asarray(tris)]
+
+
 def discretize(scene, sensor=0):
     """Binary target occupancy [Z, Y, X, 1] float32 on the sensor grid (utils.py:83-128)."""
     if isinstance(sensor, int):

@@ -175,6 +175,16 @@ int tvam_adjoint(tvam_plan* plan, const float* grad_dose,
    (needs TVAM_FLAG_FWD_STATS). */
 int tvam_plan_stats(tvam_plan* plan, uint64_t* fallback_tiles);
 
+/* Radon filter (integrators/radon.py:47-106, optimize.py:143-163, 'filter_radon'):
+   for every DMD pixel of the plan's shard (dense crop order [angle][row][col],
+   n = shard angles * crop_y * crop_x), the sum over `spp` samples of the ray
+   weight times the absorption on the ray's segments inside both the medium
+   and the target mesh (null BSDF); the optimiser keeps the pixels with a
+   positive value.  target_tris: host array [n_target_tris][3][3] of
+   world-space triangles.  radon: device, n floats, overwritten.  Synchronous. */
+int tvam_radon(tvam_plan* plan, const float* target_tris, int32_t n_target_tris, uint32_t spp, uint32_t seed,
+               int32_t max_depth, float* radon, void* stream);
+
 /* Which kernels serve this plan (bit mask; 0 = per-ray tile kernels):
    bit 0 = planar adjoint (regular sampling: one ray record per (angle,
    column), Z-slice-sharing adjoint); bit 1 = voxel-driven planar forward

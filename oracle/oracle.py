@@ -44,6 +44,8 @@ def lib():
         L.oracle_forward_part.argtypes = L.oracle_forward.argtypes + [ctypes.c_int]
         L.oracle_phase.restype = ctypes.c_int
         L.oracle_phase.argtypes = [D, P, ctypes.c_float, ctypes.c_float, P]
+        L.oracle_radon.restype = ctypes.c_int
+        L.oracle_radon.argtypes = [D, P, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, P, ctypes.c_int]
         L.oracle_dda_ray.restype = ctypes.c_int
         L.oracle_dda_ray.argtypes = [D, P, P, ctypes.c_float, ctypes.c_double, P, P]
         _lib = L
@@ -94,6 +96,16 @@ def ray(desc, pixel, wave_index=0, seed=0):
     lib().oracle_ray(ctypes.byref(desc), pixel, wave_index, seed, _ptr(out))
     return {"o": out[0:3].copy(), "d": out[3:6].copy(), "hit": bool(out[6]), "o2": out[7:10].copy(),
             "maxt": float(out[10]), "d2": out[11:14].copy(), "weight": float(out[14])}
+
+
+def radon(desc, target_tris, spp=4, seed=0, max_depth=5, nthreads=1):
+    """Radon filter image (float64, dense crop order) for world-space target triangles [n, 3, 3]."""
+    tris = np.ascontiguousarray(target_tris, dtype=np.float32).reshape(-1, 9)
+    out = np.zeros(desc.n_patterns * desc.crop_y * desc.crop_x, dtype=np.float64)
+    rc = lib().oracle_radon(ctypes.byref(desc), _ptr(tris), tris.shape[0], spp, seed, max_depth, _ptr(out), nthreads)
+    if rc:
+        raise ValueError(f"oracle_radon failed ({rc})")
+    return out
 
 
 def phase(desc, d, u1, u2):

@@ -828,6 +828,134 @@ static double or_trace(const or_scene* s, uint32_t pixel, uint64_t wave_index, u
 }
 
 /* ------------------------------------------------------------------------ */
+/* Radon filter (integrators/radon.py:47-106, optimize.py:143-163; SURVEY    */
+/* 8f-f4): per DMD pixel, the sum over samples of the ray's weighted         */
+/* absorption on the segments inside both the medium and the target mesh     */
+/* (null BSDF; t counts from the ray origin).  Pixels with radon > 0 stay    */
+/* active under 'filter_radon'.  Draw order: sample_rays only (the BSDF      */
+/* draws of the loop do not change transmission-only / null outcomes).      */
+/* ------------------------------------------------------------------------ */
+static double or_radon_ray(const or_scene* s, const or_ray* ray, const float* tgt, int ntgt, int max_depth) {
+    const tvam_desc* d = s->d;
+    float o[3] = {ray->o[0], ray->o[1], ray->o[2]}, dd[3] = {ray->d[0], ray->d[1], ray->d[2]};
+    const float half = 0.5f * d->vial_height;
+    float thr = 1.0f, L = 0.0f, t = 0.0f;
+    int in_medium = 0, inside = 0, depth = 0;
+    float he[3], hi[3];
+    or_square_extents(d, he, hi);
+    for (int it = 0; it < 4096; ++it) {
+        float tb = INFINITY, n[3] = {0.0f, 0.0f, 0.0f};
+        int kind = -1, tri = -1;
+        if (d->vial_type == TVAM_VIAL_SQUARE) {
+            float ne[3], ni[3];
+            float te = or_box_hit(o, dd, he, ne), ti = or_box_hit(o, dd, hi, ni);
+            if (ti <= te) {
+                tb = ti;
+                kind = 1;
+                memcpy(n, ni, sizeof(n));
+            } else {
+                tb = te;
+                kind = 0;
+                memcpy(n, ne, sizeof(n));
+            }
+        } else if (o[2] >= -half && o[2] <= half) {
+            float t0, t1, ti = INFINITY, te = INFINITY;
+            if (or_cyl_roots(o, dd, d->vial_r, &t0, &t1) && t1 >= 0.0f) ti = t0 >= 0.0f ? t0 : t1;
+            if (d->vial_type == TVAM_VIAL_CYLINDRICAL && or_cyl_roots(o, dd, d->vial_r_ext, &t0, &t1) && t1 >= 0.0f)
+                te = t0 >= 0.0f ? t0 : t1;
+            tb = ti <= te ? ti : te;
+            kind = ti <= te ? 1 : 0;
+        }
+        if (d->n_occluder_tris) {
+            float toc = or_occ_hit(d, o, dd);
+            if (toc < tb) {
+                tb = toc;
+                kind = 2;
+            }
+        }
+        for (int i = 0; i < ntgt; ++i) {
+            float tt = or_tri_hit(o, dd, tgt + 9 * i);
+            if (tt < tb) {
+                tb = tt;
+                kind = 3;
+                tri = i;
+            }
+        }
+        if (!(tb < INFINITY)) break;
+        float contrib = thr * expf(-d->sigma_t * t) * (1.0f - expf(-d->sigma_t * tb));
+        if (inside && in_medium) L = L + contrib;
+        t = t + tb;
+        float p[3];
+        for (int k = 0; k < 3; ++k) p[k] = fmaf(dd[k], tb, o[k]);
+        float wo[3] = {dd[0], dd[1], dd[2]};
+        if (kind == 3) {
+            const float* v = tgt + 9 * tri;
+            float e1[3] = {v[3] - v[0], v[4] - v[1], v[5] - v[2]}, e2[3] = {v[6] - v[0], v[7] - v[1], v[8] - v[2]};
+            float c[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+            float inv = 1.0f / sqrtf(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+            for (int k = 0; k < 3; ++k) n[k] = c[k] * inv;
+            inside = !inside;
+        } else if (kind == 2) {
+            break;
+        } else {
+            if (d->vial_type != TVAM_VIAL_SQUARE) {
+                float rp = sqrtf(p[0] * p[0] + p[1] * p[1]);
+                n[0] = p[0] / rp;
+                n[1] = p[1] / rp;
+                n[2] = 0.0f;
+            }
+            if (d->vial_type != TVAM_VIAL_INDEX_MATCHED) {
+                float eta = kind == 1 ? d->medium_ior / d->vial_ior : d->vial_ior / OR_IOR_AIR;
+                float w = d->vial_type == TVAM_VIAL_SQUARE ? or_transmit_world(n, dd, eta, wo) : or_transmit(n, dd, eta, wo);
+                if (!(w > 0.0f)) break;
+                thr = thr * w;
+            }
+            ++depth;
+        }
+        float m = fmaxf(fmaxf(fabsf(p[0]), fabsf(p[1])), fabsf(p[2]));
+        float mag = (1.0f + m) * OR_RAY_EPS;
+        float nwo = n[0] * wo[0] + n[1] * wo[1] + n[2] * wo[2];
+        if (signbit(nwo)) mag = -mag;
+        for (int k = 0; k < 3; ++k) {
+            o[k] = fmaf(mag, n[k], p[k]);
+            dd[k] = wo[k];
+        }
+        if (depth >= max_depth) break;
+        if (kind == 1) in_medium = nwo < 0.0f;
+    }
+    return (double)L;
+}
+
+/* radon[i] for every pixel of the dense crop (angle, row, col): sum over spp samples of
+   ray weight * L (radon.py:72-78: imgs[idx] += L * weight). */
+int oracle_radon(const tvam_desc* d, const float* tgt, int ntgt, uint32_t spp, uint32_t seed, int max_depth,
+                 double* radon, int nthreads) {
+    int rc = or_check(d);
+    if (rc) return rc;
+    if (d->regular_sampling) spp = 1;
+    or_scene s;
+    or_scene_init(&s, d);
+    const uint64_t n = (uint64_t)d->n_patterns * d->crop_y * d->crop_x;
+    const double wr = or_ray_weight(d, n, spp);
+    if (nthreads < 1) nthreads = 1;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 256) num_threads(nthreads)
+#endif
+    for (int64_t i = 0; i < (int64_t)n; ++i) {
+        uint32_t pixel = or_pixel(d, NULL, (uint64_t)i);
+        uint64_t st = or_stream(d, pixel);
+        double acc = 0.0;
+        for (uint32_t k = 0; k < spp; ++k) {
+            or_ray ray;
+            or_gen_ray(&s, pixel, st * spp + k, seed, &ray);
+            acc += or_radon_ray(&s, &ray, tgt, ntgt, max_depth);
+        }
+        radon[i] = wr * acc;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------ */
 /* Public oracle entry points (called from tests/ and bench.py via ctypes)   */
 /* ------------------------------------------------------------------------ */
 int oracle_forward_part(const tvam_desc* d, const float* active_data, const uint32_t* active_pixels,

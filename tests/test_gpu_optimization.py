@@ -72,10 +72,9 @@ def test_box_hole_square_optimization(tmp_path):
 
 
 def test_box_hole_scattering_optimization(tmp_path):
-    """tests/files/box_hole_scattering.json (square vial, albedo 0.9); bar 99.0 % (test_optimization.py:149-151)."""
-    cfg = copy.deepcopy(BOX_HOLE_SCATTERING)
-    cfg.pop("filter_radon")  # filter_radon (SURVEY 8f-f4) is not on the GPU path yet
-    cfg, vol = _run(cfg, tmp_path)
+    """tests/files/box_hole_scattering.json (square vial, albedo 0.9, filter_radon); bar 99.0 %
+    (test_optimization.py:149-151)."""
+    cfg, vol = _run(BOX_HOLE_SCATTERING, tmp_path)  # as given: filter_radon, spp 4 / spp_grad 16 / spp_ref 16
     th = (cfg["loss"]["tl"] + cfg["loss"]["tu"]) / 2
     correct = np.mean(np.isclose(box_hole_reference(), vol > th)) * 100
     print("percentage correct", correct)
