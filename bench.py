@@ -10,7 +10,8 @@ not available).  Every ray is marched (zero-pattern skipping disabled).
 
 --config 3 runs BASELINE.json configs[2] instead: the same scene behind a
 cylindrical glass vial (two refracting interfaces per ray); --config 4 runs
-configs[3]: that vial around a scattering resin, 16 jittered rays per pixel.
+configs[3]: that vial around a scattering resin, 16 jittered rays per pixel;
+--config 5 --n 800 runs configs[4]: a square vial with an occluder mesh.
 
 Multi-GPU: one process per GPU (torch.distributed.run), angles sharded in
 contiguous blocks, dose all-reduced over RCCL twice per iteration, L-BFGS
@@ -33,8 +34,9 @@ def log(*a):
 
 
 def scene_config(config, N, A):
-    from drtvam_amd.configs import benchy_index_matched, cylindrical_refraction, cylindrical_scattering
-    return {2: benchy_index_matched, 3: cylindrical_refraction, 4: cylindrical_scattering}[config](N=N, angles=A)
+    from drtvam_amd.configs import benchy_index_matched, cylindrical_refraction, cylindrical_scattering, square_occluded
+    return {2: benchy_index_matched, 3: cylindrical_refraction, 4: cylindrical_scattering,
+            5: square_occluded}[config](N=N, angles=A)
 
 
 def cpu_baseline(config, N, seconds, threads):
@@ -77,10 +79,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--config", type=int, choices=[2, 3, 4], default=2,
+    ap.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=2,
                     help="BASELINE.json configs[1] (2: index-matched, the metric's workload), configs[2] "
                          "(3: cylindrical vial, refraction) or configs[3] (4: cylindrical vial, scattering "
-                         "resin, 16 jittered rays per pixel)")
+                         "resin, 16 jittered rays per pixel) or configs[4] (5: square vial + occluder mesh, 4 jittered rays per "
+                         "pixel; use --n 800)")
     ap.add_argument("--n", type=int, default=400, help="voxels per axis = DMD pixels per axis = angles")
     ap.add_argument("--angles", type=int, default=None)
     ap.add_argument("--tile", type=int, default=0)
@@ -213,7 +216,9 @@ def main():
                          f"config3: cylindrical vial (glass r 8/9 mm, n 1.54 | resin n 1.40), {N}^3 voxels, {A} angles, "
                          f"{N}x{N} DMD, 1 ray/px, regular sampling" if args.config == 3 else
                          f"config4: cylindrical vial, scattering resin (sigma_t 0.1/mm, albedo 0.5, Rayleigh), "
-                         f"{N}^3 voxels, {A} angles, {N}x{N} DMD, {prob.spp} jittered rays/px"),
+                         f"{N}^3 voxels, {A} angles, {N}x{N} DMD, {prob.spp} jittered rays/px" if args.config == 4 else
+                         f"config5: square vial + occluder mesh (box_hole_occlusion scene), {N}^3 voxels, {A} angles, "
+                         f"{N}x{N} DMD, {prob.spp} jittered rays/px"),
             "voxels": N ** 3, "angles": A, "dmd": [N, N], "spp": prob.spp, "sigma_t": cfg["vial"]["medium"]["extinction"],
             "parallelism": ("single GPU" if world == 1 else
                             f"z-slab x{world} (film slabs + DMD row bands, scalar all-reduces only)"

@@ -199,9 +199,11 @@ def analytic_target(res, bbox_min, bbox_max, kind='box_hole'):
     x = bmin[0] + (0.5 + np.arange(rx)) * h[0]
     y = bmin[1] + (0.5 + np.arange(ry)) * h[1]
     z = bmin[2] + (0.5 + np.arange(rz)) * h[2]
-    Z, Y, X = np.meshgrid(z, y, x, indexing='ij')
     ext = bmax - bmin
-    u, v, w = (X - bmin[0]) / ext[0], (Y - bmin[1]) / ext[1], (Z - bmin[2]) / ext[2]
+    # broadcast [Z, 1, 1] / [1, Y, 1] / [1, 1, X] (no full-size coordinate grids at 800^3)
+    u = ((x - bmin[0]) / ext[0])[None, None, :]
+    v = ((y - bmin[1]) / ext[1])[None, :, None]
+    w = ((z - bmin[2]) / ext[2])[:, None, None]
     if kind == 'sphere':
         occ = (u - 0.5) ** 2 + (v - 0.5) ** 2 + (w - 0.5) ** 2 < 0.4 ** 2
     else:
