@@ -493,44 +493,68 @@ void mark_tiles(const TileGrid& g, const CylChord& ch, double m, F&& mark) {
 }  // namespace
 
 // Fixed-point bound behind a refracting vial (replaces TvamConsts::rays_per_voxel):
-// the beam converges, so more than one ray per pixel pitch of one angle may
-// cross a voxel.  From the chords of one angle (the optics are rotation
-// invariant) at 1 (regular) or 8 (jittered) positions per column: the least
-// perpendicular spacing of neighbouring chords per column, s_min (the distance
-// of a point moving along one chord to the other's line is linear, so its
-// minimum is at an end point), and the largest interface weight.  At most
-// ceil(sqrt2 h / s_min) + 2 columns' rays cross a voxel; a factor 2 covers the
-// approximation.  Chords that cross (or touch) inside the medium: infinite
-// (the kernels then add in float).
+// the beam converges, and a cuboid splits it into sub-beams that cross, so
+// more than one ray per pixel pitch of one angle may cross a voxel.  From the
+// chords of an angle at 1 (regular) or 8 (jittered) positions per column, in
+// column order, split into runs of neighbours that keep one side of each
+// other along the whole chord (the distance of a point moving along one chord
+// to the other's line is linear, so checking both end points suffices; a miss,
+// a crossing or a change of side starts a new run).  A run whose least
+// neighbour spacing is s contributes at most ceil(sqrt2 h / s) + 2 columns'
+// rays to a voxel (a factor 2 covers the approximation); the runs add up.
+// The largest interface weight scales the bound.  A tube is rotation
+// invariant (one angle); a cuboid is not (every angle, the largest sum).
 static float cyl_rays_per_voxel(const tvam_desc& d, const TvamConsts& k, const std::vector<float2>& cs) {
     const int sub = d.regular_sampling ? 1 : 8;
     const int ns = (int)cs.size();
-    // a tube is rotation invariant (one angle); a cuboid is not (every angle)
     const int nang = d.vial_type == TVAM_VIAL_SQUARE ? ns : std::min(ns, 1);
-    double smin = INFINITY, wmax = 1.0;
+    const double hxy = std::max((double)k.h[0], (double)k.h[1]);
+    const double D = 2.0 * std::sqrt(2.0) * hxy;
+    double wmax = 1.0, worst = 0.0;
     std::vector<CylChord> ch;
     for (int ai = 0; ai < nang; ++ai) {
-    const float c = d.vial_type == TVAM_VIAL_SQUARE ? cs[ai].x : 1.0f, sn = d.vial_type == TVAM_VIAL_SQUARE ? cs[ai].y : 0.0f;
-    ch.clear();
-    for (int col = 0; col < d.crop_x; ++col)
-        for (int j = 0; j < sub; ++j)
-            ch.push_back(cyl_chord(k, c, sn, d.crop_offset_x + col, ((float)j + 0.5f) / (float)sub));
-    for (size_t i = 0; i < ch.size(); ++i) {
-        if (!ch[i].hit) continue;
-        wmax = std::max(wmax, (double)ch[i].w);
-        if (i + 1 == ch.size() || !ch[i + 1].hit) continue;
-        const double dx = ch[i].bx - ch[i].ax, dy = ch[i].by - ch[i].ay, L = std::hypot(dx, dy);
-        if (!(L > 1e-12)) continue;
-        const double nx = -dy / L, ny = dx / L;
-        const double da = (ch[i + 1].ax - ch[i].ax) * nx + (ch[i + 1].ay - ch[i].ay) * ny;
-        const double db = (ch[i + 1].bx - ch[i].ax) * nx + (ch[i + 1].by - ch[i].ay) * ny;
-        if (!(da * db > 0.0)) return INFINITY;
-        smin = std::min(smin, std::min(std::fabs(da), std::fabs(db)) * sub);
+        const bool sq = d.vial_type == TVAM_VIAL_SQUARE;
+        const float c = sq ? cs[ai].x : 1.0f, sn = sq ? cs[ai].y : 0.0f;
+        ch.clear();
+        for (int col = 0; col < d.crop_x; ++col)
+            for (int j = 0; j < sub; ++j)
+                ch.push_back(cyl_chord(k, c, sn, d.crop_offset_x + col, ((float)j + 0.5f) / (float)sub));
+        double total = 0.0, run_s = INFINITY;
+        int run_sign = 0;
+        bool in_run = false;
+        auto close_run = [&]() {
+            if (in_run) total += (run_s < INFINITY ? std::ceil(D / run_s) : 0.0) + 2.0;
+            in_run = false;
+            run_s = INFINITY;
+            run_sign = 0;
+        };
+        for (size_t i = 0; i < ch.size(); ++i) {
+            if (!ch[i].hit) {
+                close_run();
+                continue;
+            }
+            wmax = std::max(wmax, (double)ch[i].w);
+            in_run = true;
+            if (i + 1 == ch.size() || !ch[i + 1].hit) continue;
+            const double dx = ch[i].bx - ch[i].ax, dy = ch[i].by - ch[i].ay, L = std::hypot(dx, dy);
+            if (!(L > 1e-12)) continue;
+            const double nx = -dy / L, ny = dx / L;
+            const double da = (ch[i + 1].ax - ch[i].ax) * nx + (ch[i + 1].ay - ch[i].ay) * ny;
+            const double db = (ch[i + 1].bx - ch[i].ax) * nx + (ch[i + 1].by - ch[i].ay) * ny;
+            const int sg = da > 0.0 ? 1 : -1;
+            if (!(da * db > 0.0) || (run_sign != 0 && sg != run_sign)) {
+                close_run();  // the next chord crosses (or turns): a new run starts with it
+                in_run = false;
+                continue;
+            }
+            run_sign = sg;
+            run_s = std::min(run_s, std::min(std::fabs(da), std::fabs(db)) * sub);
+        }
+        close_run();
+        worst = std::max(worst, total);
     }
-    }
-    if (!(smin < INFINITY)) return k.rays_per_voxel;  // fewer than two chords: the straight-ray bound
-    const double hxy = std::max((double)k.h[0], (double)k.h[1]);
-    return (float)((double)ns * (std::ceil(2.0 * std::sqrt(2.0) * hxy / smin) + 2.0) * wmax * 1.01);
+    if (!(worst > 0.0)) return k.rays_per_voxel;  // no chord: the straight-ray bound
+    return (float)((double)ns * worst * wmax * 1.01);
 }
 
 static void cyl_slot_lists(const tvam_desc& d, const TvamConsts& k, const std::vector<float2>& cs, int tsx, int tsy,
