@@ -33,6 +33,7 @@ FLAG_NO_ZERO_SKIP = 1
 FLAG_FWD_STATS = 2
 FLAG_NO_PLANAR = 4
 FLAG_RAY_FWD = 8
+FLAG_SCATTER_ATOMIC = 16
 LBFGS_WORK_DOUBLES = 512 * 64
 
 

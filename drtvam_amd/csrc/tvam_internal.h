@@ -62,7 +62,39 @@ hipError_t tvam_launch_fwd_rays_planar(const TvamConsts& k, const TvamPlanar& pl
                                        const float* pat, unsigned* amax, float* scale, float* dose,
                                        hipStream_t stream);
 
-enum TvamMode { TVAM_MODE_FWD = 0, TVAM_MODE_ADJ = 1, TVAM_MODE_COUNT = 2 };
+enum TvamMode { TVAM_MODE_FWD = 0, TVAM_MODE_ADJ = 1, TVAM_MODE_COUNT = 2, TVAM_MODE_EMIT = 3 };
+
+// Brick of the binned scattered-segment forward (LDS int64 tile: 128 KB)
+#define TVAM_BX 32
+#define TVAM_BY 32
+#define TVAM_BZ 16
+
+// Scattered segments of paths [p0, p1): `slots` records per path
+// (a = {t_start, tau_end, dtm0_x, dtm0_y}, b = {dtm0_z, +-ts_x, +-ts_y, +-ts_z},
+// c = {start voxel x | y << 11 | z << 22, weight bits}), m = bricks crossed (0: empty).
+struct TvamSegBuf {
+    int64_t p0, p1;
+    int32_t slots;
+    float4* a;
+    float4* b;
+    int2* c;
+    uint32_t* m;
+};
+
+// Scratch of the binned forward (owned by the plan, grown on demand).
+struct TvamBinScratch {
+    TvamSegBuf sb;
+    int64_t cap_slots = 0;
+    uint32_t* off = nullptr;      // [cap_slots + 1] exclusive scan of m
+    uint32_t* keys[2] = {nullptr, nullptr};
+    uint32_t* vals[2] = {nullptr, nullptr};
+    int64_t cap_entries = 0;
+    uint32_t* bstart = nullptr;   // [nbricks + 1]
+    int32_t cap_bricks = 0;
+    void* temp = nullptr;
+    size_t temp_bytes = 0;
+    int acc_float = 0;            // 1: float LDS adds instead of int64 fixed point (TVAM_BIN_FLOAT)
+};
 
 hipError_t tvam_launch_tiles(int mode, const TvamConsts& k, const TvamTiles& t, size_t lds_bytes,
                              const float* pat, const int32_t* idxmap, const float* gin, float* out,
@@ -73,6 +105,12 @@ hipError_t tvam_launch_tiles(int mode, const TvamConsts& k, const TvamTiles& t, 
 hipError_t tvam_launch_scatter_paths(int mode, const TvamConsts& k, const TvamTiles& t, const float* pat,
                                      const int32_t* idxmap, const float* gin, float* out,
                                      unsigned long long* counter, hipStream_t stream);
+// Forward of the scattered segments through brick bins (chunks of paths; host
+// syncs once per chunk to size the bins).  Returns hipErrorNotSupported when
+// the grid is too large for the packed records (callers then use the atomics).
+hipError_t tvam_scatter_forward_binned(const TvamConsts& k, const TvamTiles& t, const float* pat, float* dose,
+                                       TvamBinScratch& s, hipStream_t stream);
+void tvam_bin_scratch_free(TvamBinScratch& s);
 
 // Radon filter image of the shard's DMD pixels (tvam_radon.hip).
 hipError_t tvam_launch_radon(const TvamConsts& k, const TvamTiles& t, const float* tgt, int ntgt, int max_depth,

@@ -75,6 +75,7 @@ struct tvam_plan {
     unsigned* d_amax = nullptr;  // ray-driven forward: per-angle max |pattern|, fixed-point scale
     float* d_fscale = nullptr;
     int32_t planar_rz = 4;
+    TvamBinScratch bins;  // scattering media: brick-binned forward scratch
     std::vector<float4> fwd_ang_h;  // host staging of the forward tables (plan creation only)
     std::vector<int32_t> fwd_cb_h;
     // sparse scratch (dense crop layout), allocated on first sparse call
@@ -144,6 +145,7 @@ static void plan_free(tvam_plan* p) {
     (void)hipFree(p->d_pl_rec_g);
     (void)hipFree(p->d_amax);
     (void)hipFree(p->d_occ);
+    tvam_bin_scratch_free(p->bins);
     (void)hipFree(p->d_fscale);
     delete p;
 }
@@ -937,7 +939,11 @@ extern "C" int tvam_forward(tvam_plan* p, const float* active_data, const uint32
         TvamTiles t = p->tiles;
         t.spp = spp;
         t.seed = seed;
-        e = tvam_launch_scatter_paths(TVAM_MODE_FWD, kc, t, pat, idxmap, nullptr, dose, nullptr, stream);
+        e = hipErrorNotSupported;
+        p->bins.acc_float = env_int("TVAM_BIN_FLOAT", 0);
+        if (!(p->desc.flags & TVAM_FLAG_SCATTER_ATOMIC)) e = tvam_scatter_forward_binned(kc, t, pat, dose, p->bins, stream);
+        if (e == hipErrorNotSupported)
+            e = tvam_launch_scatter_paths(TVAM_MODE_FWD, kc, t, pat, idxmap, nullptr, dose, nullptr, stream);
         if (e != hipSuccess) return hip_fail(e, "scatter forward launch");
     }
     return 0;

@@ -110,13 +110,23 @@ __device__ __forceinline__ void sc_phase(const TvamConsts& k, float dx, float dy
     wz = sz * lx + tz * ly + nz * lz;
 }
 
-// One medium segment's 3-D DDA (sensor.py:327-438, op for op like the oracle's
-// or_dda): MODE FWD adds em * (e^{-st t} - e^{-st (t + dt)}) * inv_vol into the
-// dose, ADJ returns sum (...) * grad * inv_vol, COUNT counts visits.
-template <int MODE>
-__device__ float sc_dda(const TvamConsts& k, float ox, float oy, float oz, float dx, float dy, float dz, float maxt,
-                        float em, float* __restrict__ dose, const float* __restrict__ gin, uint64_t& nvis) {
-    const float o[3] = {ox, oy, oz}, d[3] = {dx, dy, dz};
+// ---------------------------------------------------------------------------
+// Brick-binned forward of the scattered segments.  A segment's DDA state after
+// the box clip and initialisation (sensor.py:327-365) is stored as a record;
+// its visits inside a brick of TVAM_BX x TVAM_BY x TVAM_BZ voxels follow in
+// closed form from the per-axis crossing times t_a(k) = dtm0_a + (k - 1) ts_a
+// (relative to t_start; the resume of the tile kernels, in 3-D), so each brick
+// workgroup marches only its part of every segment crossing it, adding into an
+// LDS tile, and writes the tile once.
+// ---------------------------------------------------------------------------
+struct SegDda {
+    float t_start, tau_end;
+    float dtm0[3], ts[3];  // ts > 0; step sign separate
+    int sv[3], step[3];
+};
+
+__device__ __forceinline__ bool sc_dda_init(const TvamConsts& k, const float o[3], const float d[3], float maxt,
+                                            SegDda& q) {
     float lo[3], hi[3];
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
@@ -127,52 +137,134 @@ __device__ float sc_dda(const TvamConsts& k, float ox, float oy, float oz, float
     }
     const float t_start = fmaxf(fmaxf(fmaxf(fmaxf(lo[0], lo[1]), lo[2]), 0.0f), 0.0f);
     const float t_end = fminf(fminf(fminf(hi[0], hi[1]), hi[2]), maxt);
-    if (!(isfinite(t_start) && isfinite(t_end) && t_start < t_end)) return 0.0f;
-    int cur[3], endv[3], step[3];
-    float dtmax[3], tstep[3];
+    if (!(isfinite(t_start) && isfinite(t_end) && t_start < t_end)) return false;
+    q.t_start = t_start;
+    q.tau_end = t_end - t_start;
 #pragma unroll
     for (int a = 0; a < 3; ++a) {
         const float gs = fmaf(d[a], t_start, o[a]);
-        const float ge = fmaf(d[a], t_end, o[a]);
-        step[a] = d[a] > 0.0f ? 1 : -1;
+        q.step[a] = d[a] > 0.0f ? 1 : -1;
         int sv = (int)((gs - k.bmin[a]) / k.h[a]);
-        int ev = (int)((ge - k.bmin[a]) / k.h[a]);
         sv = sv < 0 ? 0 : (sv > k.res[a] - 1 ? k.res[a] - 1 : sv);
-        ev = ev < 0 ? 0 : (ev > k.res[a] - 1 ? k.res[a] - 1 : ev);
-        cur[a] = sv;
-        endv[a] = ev;
-        float next = k.bmin[a] + (float)(sv + step[a]) * k.h[a];
+        q.sv[a] = sv;
+        float next = k.bmin[a] + (float)(sv + q.step[a]) * k.h[a];
         if (d[a] < 0.0f) next = next + k.h[a];
         const bool valid = fabsf(d[a]) > 1e-8f;
         float dtm = valid ? (next - gs) / d[a] : TVAM_INF;
         if (dtm < 0.0f) dtm = TVAM_INF;
-        dtmax[a] = dtm;
-        tstep[a] = valid ? (k.h[a] / d[a]) * (float)step[a] : TVAM_INF;
+        q.dtm0[a] = dtm;
+        q.ts[a] = valid ? (k.h[a] / d[a]) * (float)q.step[a] : TVAM_INF;
     }
-    float t = t_start, remaining = t_end - t_start;
-    float e0 = sc_exp2(k.nsig2 * t);
-    float acc = 0.0f;
-    const int64_t sx = 1, sy = k.res[0], sz = (int64_t)k.res[0] * k.res[1];
-    for (;;) {
-        const float dt = fminf(fminf(fminf(dtmax[0], dtmax[1]), dtmax[2]), remaining);
-        remaining = remaining - dt;
-        const float e1 = sc_exp2(k.nsig2 * (t + fmaxf(dt, 0.0f)));
-        const int64_t idx = cur[0] * sx + cur[1] * sy + cur[2] * sz;
-        if (MODE == TVAM_MODE_FWD) atomicAdd(&dose[idx], em * (e0 - e1));
-        else if (MODE == TVAM_MODE_ADJ) acc = fmaf(e0 - e1, gin[idx] * k.inv_vol, acc);
-        ++nvis;
-        if (!((cur[0] != endv[0] || cur[1] != endv[1] || cur[2] != endv[2]) && remaining > 1e-6f)) break;
+    return true;
+}
+
+__device__ __forceinline__ int sc_nbr(const TvamConsts& k, int a) {
+    const int B = a == 0 ? TVAM_BX : (a == 1 ? TVAM_BY : TVAM_BZ);
+    return (k.res[a] + B - 1) / B;
+}
+
+// Bricks a segment's DDA visits, in time order: each axis' brick windows
+// partition time exactly (tvam_axis_window on brick bounds), so stepping the
+// axis whose window closes first walks the same sequence the brick kernel
+// resumes from.  F(brick id) per brick; returns the count.
+template <typename F>
+__device__ __forceinline__ int sc_walk_bricks(const TvamConsts& k, const SegDda& q, F&& f) {
+    const int B[3] = {TVAM_BX, TVAM_BY, TVAM_BZ};
+    const int nb[3] = {sc_nbr(k, 0), sc_nbr(k, 1), sc_nbr(k, 2)};
+    int b[3] = {q.sv[0] / B[0], q.sv[1] / B[1], q.sv[2] / B[2]};
+    int cnt = 0;
+    for (int guard = 0; guard < 4096; ++guard) {
+        f((b[2] * nb[1] + b[1]) * nb[0] + b[0]);
+        ++cnt;
+        float tout[3];
 #pragma unroll
         for (int a = 0; a < 3; ++a) {
-            const bool m = dtmax[a] == dt;
-            dtmax[a] = m ? tstep[a] : dtmax[a] - dt;
-            cur[a] += m ? step[a] : 0;
+            float tin;
+            int nin, nout;
+            const int lo = b[a] * B[a], hi = min(lo + B[a], k.res[a]);
+            tvam_axis_window(q.sv[a], q.step[a], q.dtm0[a], q.ts[a], lo, hi, tin, tout[a], nin, nout);
         }
-        if (cur[0] < 0 || cur[1] < 0 || cur[2] < 0 || cur[0] >= k.res[0] || cur[1] >= k.res[1] || cur[2] >= k.res[2])
-            break;
-        t = t + dt;
-        e0 = e1;
+        int am = 0;
+        if (tout[1] < tout[am]) am = 1;
+        if (tout[2] < tout[am]) am = 2;
+        if (!(tout[am] < q.tau_end)) break;
+        b[am] += q.step[am];
+        if (b[am] < 0 || b[am] >= nb[am]) break;
     }
+    return cnt;
+}
+
+// The visits of a segment inside the voxel box [lo, hi) (a brick), resumed in
+// closed form at the box entry: per axis the step count n at the entry time,
+// the next crossing at t = dtm0 + n ts (fmaf from the count, so a visit splits
+// at a brick face exactly where the neighbouring brick resumes), one axis per
+// visit.  F(local voxel x, y, z, weight e^{-st t0} - e^{-st t1}).
+template <typename F>
+__device__ __forceinline__ void sc_box_march(const TvamConsts& k, const SegDda& q, const int lo[3], const int hi[3],
+                                             F&& f) {
+    float tin[3], tout[3];
+    int nin[3], nout[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+        tvam_axis_window(q.sv[a], q.step[a], q.dtm0[a], q.ts[a], lo[a], hi[a], tin[a], tout[a], nin[a], nout[a]);
+    const float tau_e = fmaxf(fmaxf(fmaxf(tin[0], tin[1]), tin[2]), 0.0f);
+    const float tau_x = fminf(fminf(fminf(tout[0], tout[1]), tout[2]), q.tau_end);
+    if (!(tau_e < tau_x)) return;
+    int v[3], n[3];
+    float T[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a) {
+        n[a] = tvam_axis_steps(tau_e, q.dtm0[a], q.ts[a], nin[a], nout[a]);
+        v[a] = q.sv[a] + q.step[a] * n[a] - lo[a];
+        T[a] = q.dtm0[a] < TVAM_INF ? fmaf((float)n[a], q.ts[a], q.dtm0[a]) : TVAM_INF;
+    }
+    const float stop = tau_x - 1e-6f;
+    float ea = sc_exp2(k.nsig2 * (q.t_start + tau_e));
+    for (int guard = 0; guard < 3 * 4096; ++guard) {
+        int am = 0;
+        if (T[1] < T[am]) am = 1;
+        if (T[2] < T[am]) am = 2;
+        const float tn = fminf(T[am], tau_x);
+        const float eb = sc_exp2(k.nsig2 * (q.t_start + tn));
+        f(v[0], v[1], v[2], ea - eb);
+        if (!(tn < stop)) break;
+        v[am] += q.step[am];
+        ++n[am];
+        T[am] = fmaf((float)n[am], q.ts[am], q.dtm0[am]);
+        ea = eb;
+    }
+}
+
+// The whole segment, brick by brick (the binned forward's visits exactly).
+template <typename F>
+__device__ __forceinline__ void sc_seg_march(const TvamConsts& k, const SegDda& q, F&& f) {
+    const int B[3] = {TVAM_BX, TVAM_BY, TVAM_BZ};
+    const int nb[3] = {sc_nbr(k, 0), sc_nbr(k, 1), sc_nbr(k, 2)};
+    sc_walk_bricks(k, q, [&](int bid) {
+        const int bx = bid % nb[0], by = (bid / nb[0]) % nb[1], bz = bid / (nb[0] * nb[1]);
+        const int lo[3] = {bx * B[0], by * B[1], bz * B[2]};
+        const int hi[3] = {min(lo[0] + B[0], k.res[0]), min(lo[1] + B[1], k.res[1]), min(lo[2] + B[2], k.res[2])};
+        sc_box_march(k, q, lo, hi, [&](int x, int y, int z, float c) { f(lo[0] + x, lo[1] + y, lo[2] + z, c); });
+    });
+}
+
+// One medium segment's 3-D DDA (sensor.py:327-438, op for op like the oracle's
+// or_dda): MODE FWD adds em * (e^{-st t} - e^{-st (t + dt)}) * inv_vol into the
+// dose, ADJ returns sum (...) * grad * inv_vol, COUNT counts visits.
+template <int MODE>
+__device__ float sc_dda(const TvamConsts& k, float ox, float oy, float oz, float dx, float dy, float dz, float maxt,
+                        float em, float* __restrict__ dose, const float* __restrict__ gin, uint64_t& nvis) {
+    const float o[3] = {ox, oy, oz}, d[3] = {dx, dy, dz};
+    SegDda q;
+    if (!sc_dda_init(k, o, d, maxt, q)) return 0.0f;
+    float acc = 0.0f;
+    const int64_t sy = k.res[0], sz = (int64_t)k.res[0] * k.res[1];
+    sc_seg_march(k, q, [&](int x, int y, int z, float c) {
+        const int64_t idx = x + y * sy + z * sz;
+        if (MODE == TVAM_MODE_FWD) atomicAdd(&dose[idx], em * c);
+        else if (MODE == TVAM_MODE_ADJ) acc = fmaf(c, gin[idx] * k.inv_vol, acc);
+        ++nvis;
+    });
     return acc;
 }
 
@@ -180,19 +272,20 @@ template <int MODE>
 __global__ __launch_bounds__(256) void tvam_scatter_kernel(TvamConsts k, TvamTiles tp, const float* __restrict__ pat,
                                                            const int32_t* __restrict__ idxmap,
                                                            const float* __restrict__ gin, float* __restrict__ out,
-                                                           unsigned long long* __restrict__ counter) {
+                                                           unsigned long long* __restrict__ counter, TvamSegBuf sb) {
     const int spp = (int)tp.spp;
     const int64_t per_angle = (int64_t)k.crop_y * k.crop_x;
-    const int64_t n = (int64_t)tp.n_shard * per_angle * spp;
+    const int64_t n = MODE == TVAM_MODE_EMIT ? sb.p1 : (int64_t)tp.n_shard * per_angle * spp;
+    const int64_t i0 = MODE == TVAM_MODE_EMIT ? sb.p0 : 0;
     const float st = k.sig_t, ss = k.sig_s;
     const int nsurf = k.vial_type == 0 ? 1 : 2;  // glass vials: two surfaces before the medium
     uint64_t nvis = 0;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    for (int64_t i = i0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t local = i / spp;
         const int smp = (int)(i - local * spp);
         float em = 1.0f;
         int64_t act = local;
-        if (MODE == TVAM_MODE_FWD) {
+        if (MODE == TVAM_MODE_FWD || MODE == TVAM_MODE_EMIT) {
             const float p = pat[local];
             if (p == 0.0f && k.skip_zero) continue;
             em = p * k.wscale * k.inv_vol;
@@ -239,7 +332,18 @@ __global__ __launch_bounds__(256) void tvam_scatter_kernel(TvamConsts k, TvamTil
             }
             const float u_m = rng.next_float();
             const float tmi = -logf(1.0f - u_m) / st;
-            if (seg > 0) {
+            if (seg > 0 && MODE == TVAM_MODE_EMIT) {
+                const float o[3] = {px, py, pz}, dv[3] = {vx, vy, vz};
+                SegDda q;
+                if (seg <= sb.slots && sc_dda_init(k, o, dv, tsi, q)) {
+                    const int64_t slot = (i - sb.p0) * sb.slots + (seg - 1);
+                    sb.a[slot] = make_float4(q.t_start, q.tau_end, q.dtm0[0], q.dtm0[1]);
+                    sb.b[slot] = make_float4(q.dtm0[2], q.ts[0] * (float)q.step[0], q.ts[1] * (float)q.step[1],
+                                             q.ts[2] * (float)q.step[2]);
+                    sb.c[slot] = make_int2(q.sv[0] | (q.sv[1] << 11) | (q.sv[2] << 22), __float_as_int(em * att));
+                    sb.m[slot] = (uint32_t)sc_walk_bricks(k, q, [](int) {});
+                }
+            } else if (seg > 0) {
                 const float r = sc_dda<MODE>(k, px, py, pz, vx, vy, vz, tsi, em * att, out, gin, nvis);
                 if (MODE == TVAM_MODE_ADJ) acc = fmaf(att, r, acc);
             }
@@ -280,18 +384,285 @@ hipError_t tvam_launch_scatter_paths(int mode, const TvamConsts& k, const TvamTi
     int64_t g = (n + 255) / 256;
     if (g > 262144) g = 262144;
     if (g < 1) g = 1;
+    const TvamSegBuf none{};
     switch (mode) {
         case TVAM_MODE_FWD:
             hipLaunchKernelGGL(tvam_scatter_kernel<TVAM_MODE_FWD>, dim3((unsigned)g), dim3(256), 0, stream, k, t, pat,
-                               idxmap, gin, out, counter);
+                               idxmap, gin, out, counter, none);
             break;
         case TVAM_MODE_ADJ:
             hipLaunchKernelGGL(tvam_scatter_kernel<TVAM_MODE_ADJ>, dim3((unsigned)g), dim3(256), 0, stream, k, t, pat,
-                               idxmap, gin, out, counter);
+                               idxmap, gin, out, counter, none);
             break;
         default:
             hipLaunchKernelGGL(tvam_scatter_kernel<TVAM_MODE_COUNT>, dim3((unsigned)g), dim3(256), 0, stream, k, t,
-                               pat, idxmap, gin, out, counter);
+                               pat, idxmap, gin, out, counter, none);
     }
     return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// Brick bins: fill (segment, brick) pairs, sort by brick, march per brick.
+// ---------------------------------------------------------------------------
+#include <hipcub/hipcub.hpp>
+
+namespace {
+
+__device__ __forceinline__ void sc_unpack(const float4 a, const float4 b, const int2 c, SegDda& q, float& w) {
+    q.t_start = a.x;
+    q.tau_end = a.y;
+    q.dtm0[0] = a.z;
+    q.dtm0[1] = a.w;
+    q.dtm0[2] = b.x;
+    const float tsv[3] = {b.y, b.z, b.w};
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        q.step[i] = tsv[i] < 0.0f ? -1 : 1;
+        q.ts[i] = fabsf(tsv[i]);
+    }
+    q.sv[0] = c.x & 0x7ff;
+    q.sv[1] = (c.x >> 11) & 0x7ff;
+    q.sv[2] = (c.x >> 22) & 0x3ff;
+    w = __int_as_float(c.y);
+}
+
+__global__ __launch_bounds__(256) void tvam_bin_fill_kernel(TvamConsts k, TvamSegBuf sb, const uint32_t* __restrict__ off,
+                                                            int64_t nslots, uint32_t* __restrict__ keys,
+                                                            uint32_t* __restrict__ vals) {
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nslots; s += (int64_t)gridDim.x * blockDim.x) {
+        if (sb.m[s] == 0) continue;
+        SegDda q;
+        float w;
+        sc_unpack(sb.a[s], sb.b[s], sb.c[s], q, w);
+        uint32_t o = off[s];
+        sc_walk_bricks(k, q, [&](int bid) {
+            keys[o] = (uint32_t)bid;
+            vals[o] = (uint32_t)s;
+            ++o;
+        });
+    }
+}
+
+__global__ void tvam_bin_start_kernel(const uint32_t* __restrict__ keys, int64_t n, int nbricks,
+                                      uint32_t* __restrict__ bstart) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int kc = i < n ? (int)keys[i] : nbricks;
+        const int kp = i > 0 ? (int)keys[i - 1] : -1;
+        for (int b = kp + 1; b <= kc; ++b) bstart[b] = (uint32_t)i;  // bricks (kp, kc] start here
+    }
+}
+
+// One workgroup per brick: the brick's visits added in LDS, then dose += tile
+// (the brick is this launch's alone).  ACC 0: exact int64 fixed point with a
+// per-brick scale 2^e from sum |w| * the largest per-visit weight
+// min(1, st sqrt3 h) (a line crosses a voxel once; 2^62 headroom keeps the
+// quantisation ~1e-13 of the bound); ACC 1: float LDS adds.
+template <int ACC>
+__global__ __launch_bounds__(512) void tvam_bin_march_kernel(TvamConsts k, TvamSegBuf sb,
+                                                             const uint32_t* __restrict__ vals,
+                                                             const uint32_t* __restrict__ bstart,
+                                                             float* __restrict__ dose) {
+    constexpr int NV = TVAM_BX * TVAM_BY * TVAM_BZ;
+    __shared__ __attribute__((aligned(16))) unsigned char smem[NV * (ACC == 0 ? 8 : 4)];
+    __shared__ float red[8];
+    long long* ltile = reinterpret_cast<long long*>(smem);
+    float* ftile = reinterpret_cast<float*>(smem);
+    const int nbx = sc_nbr(k, 0), nby = sc_nbr(k, 1);
+    const int bid = blockIdx.x;
+    const uint32_t e0 = bstart[bid], e1 = bstart[bid + 1];
+    if (e0 == e1) return;
+    const int bx = bid % nbx, by = (bid / nbx) % nby, bz = bid / (nbx * nby);
+    const int lo[3] = {bx * TVAM_BX, by * TVAM_BY, bz * TVAM_BZ};
+    const int hi[3] = {min(lo[0] + TVAM_BX, k.res[0]), min(lo[1] + TVAM_BY, k.res[1]), min(lo[2] + TVAM_BZ, k.res[2])};
+    float scale = 1.0f;
+    if (ACC == 0) {
+        float sw = 0.0f;
+        for (uint32_t e = e0 + threadIdx.x; e < e1; e += 512) sw += fabsf(__int_as_float(sb.c[vals[e]].y));
+        for (int o = 32; o > 0; o >>= 1) sw += __shfl_xor(sw, o, 64);
+        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sw;
+        for (int i = threadIdx.x; i < NV; i += 512) ltile[i] = 0;
+        __syncthreads();
+        float tot = 0.0f;
+        for (int w = 0; w < 8; ++w) tot += red[w];
+        const float hmax = fmaxf(fmaxf(k.h[0], k.h[1]), k.h[2]);
+        const float bound = tot * fminf(1.0f, k.sig_t * 1.7320508f * hmax) * 1.001f;
+        if (bound > 0.0f && isfinite(bound)) {
+            int ex;
+            frexpf(bound, &ex);
+            ex = 61 - ex;
+            ex = ex > 126 ? 126 : (ex < -126 ? -126 : ex);
+            scale = ldexpf(1.0f, ex);
+        }
+    } else {
+        for (int i = threadIdx.x; i < NV; i += 512) ftile[i] = 0.0f;
+        __syncthreads();
+    }
+    const int sy = TVAM_BX, sz = TVAM_BX * TVAM_BY;
+    for (uint32_t e = e0 + threadIdx.x; e < e1; e += 512) {
+        const uint32_t s = vals[e];
+        SegDda q;
+        float w;
+        sc_unpack(sb.a[s], sb.b[s], sb.c[s], q, w);
+        const float ws = w * scale;
+        sc_box_march(k, q, lo, hi, [&](int x, int y, int z, float c) {
+            const int li = z * sz + y * sy + x;
+            if (ACC == 0)
+                __hip_atomic_fetch_add(&ltile[li], (long long)__float2ll_rn(ws * c), __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_WORKGROUP);
+            else
+                __hip_atomic_fetch_add(&ftile[li], w * c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        });
+    }
+    __syncthreads();
+    const float inv = 1.0f / scale;
+    const int wx = hi[0] - lo[0], wy = hi[1] - lo[1], wz = hi[2] - lo[2];
+    for (int i = threadIdx.x; i < wx * wy * wz; i += 512) {
+        const int x = i % wx, y = (i / wx) % wy, z = i / (wx * wy);
+        const int li = z * sz + y * sy + x;
+        const float v = ACC == 0 ? (float)ltile[li] * inv : ftile[li];
+        if (v != 0.0f) {
+            const size_t g = ((size_t)(lo[2] + z) * k.res[1] + (lo[1] + y)) * k.res[0] + (lo[0] + x);
+            dose[g] += v;
+        }
+    }
+}
+
+template <typename T>
+hipError_t grow(T** p, int64_t& cap, int64_t need) {
+    if (need <= cap) return hipSuccess;
+    (void)hipFree(*p);
+    *p = nullptr;
+    cap = 0;
+    hipError_t e = hipMalloc((void**)p, (size_t)need * sizeof(T));
+    if (e == hipSuccess) cap = need;
+    return e;
+}
+
+}  // namespace
+
+void tvam_bin_scratch_free(TvamBinScratch& s) {
+    (void)hipFree(s.sb.a);
+    (void)hipFree(s.sb.b);
+    (void)hipFree(s.sb.c);
+    (void)hipFree(s.sb.m);
+    (void)hipFree(s.off);
+    for (int i = 0; i < 2; ++i) {
+        (void)hipFree(s.keys[i]);
+        (void)hipFree(s.vals[i]);
+    }
+    (void)hipFree(s.bstart);
+    (void)hipFree(s.temp);
+    s = TvamBinScratch{};
+}
+
+hipError_t tvam_scatter_forward_binned(const TvamConsts& k, const TvamTiles& t, const float* pat, float* dose,
+                                       TvamBinScratch& s, hipStream_t stream) {
+    const int nsurf = k.vial_type == 0 ? 1 : 2;
+    const int slots = k.max_depth - nsurf - 1;  // later medium segments per path
+    if (slots <= 0) return hipSuccess;
+    if (k.res[0] > 2048 || k.res[1] > 2048 || k.res[2] > 1024) return hipErrorNotSupported;
+    const int nbx = (k.res[0] + TVAM_BX - 1) / TVAM_BX, nby = (k.res[1] + TVAM_BY - 1) / TVAM_BY,
+              nbz = (k.res[2] + TVAM_BZ - 1) / TVAM_BZ;
+    const int nbricks = nbx * nby * nbz;
+    int bits = 1;
+    while ((1 << bits) < nbricks) ++bits;
+    const int64_t npaths = (int64_t)t.n_shard * k.crop_y * k.crop_x * t.spp;
+    const int64_t chunk = std::min<int64_t>(npaths, std::max<int64_t>(1, (int64_t)(1 << 27) / slots));  // 128M slots
+    const int64_t nsl = chunk * slots;
+    hipError_t e;
+    int64_t capa = s.cap_slots;
+    if (nsl > s.cap_slots) {
+        tvam_bin_scratch_free(s);
+        if ((e = hipMalloc((void**)&s.sb.a, nsl * sizeof(float4))) != hipSuccess ||
+            (e = hipMalloc((void**)&s.sb.b, nsl * sizeof(float4))) != hipSuccess ||
+            (e = hipMalloc((void**)&s.sb.c, nsl * sizeof(int2))) != hipSuccess ||
+            (e = hipMalloc((void**)&s.sb.m, (nsl + 1) * sizeof(uint32_t))) != hipSuccess ||
+            (e = hipMalloc((void**)&s.off, (nsl + 1) * sizeof(uint32_t))) != hipSuccess)
+            return e;
+        s.cap_slots = nsl;
+        capa = nsl;
+    }
+    (void)capa;
+    int64_t capb = s.cap_bricks;
+    if ((e = grow(&s.bstart, capb, (int64_t)nbricks + 1)) != hipSuccess) return e;
+    s.cap_bricks = (int32_t)capb;
+    for (int64_t p0 = 0; p0 < npaths; p0 += chunk) {
+        const int64_t p1 = std::min(npaths, p0 + chunk);
+        const int64_t ns = (p1 - p0) * slots;
+        TvamSegBuf sb = s.sb;
+        sb.p0 = p0;
+        sb.p1 = p1;
+        sb.slots = slots;
+        if ((e = hipMemsetAsync(sb.m, 0, (ns + 1) * sizeof(uint32_t), stream)) != hipSuccess) return e;
+        int64_t g = std::min<int64_t>((p1 - p0 + 255) / 256, 262144);
+        hipLaunchKernelGGL(tvam_scatter_kernel<TVAM_MODE_EMIT>, dim3((unsigned)g), dim3(256), 0, stream, k, t, pat,
+                           nullptr, nullptr, nullptr, nullptr, sb);
+        // exclusive scan of the brick counts (ns + 1 entries: the last gives the total)
+        size_t tb = 0;
+        if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, sb.m, s.off, (int)(ns + 1), stream)) != hipSuccess)
+            return e;
+        size_t tb2 = 0;
+        if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                                    (uint32_t*)nullptr, (uint32_t*)nullptr,
+                                                    (int)std::max<int64_t>(s.cap_entries, 1), 0, bits, stream)) !=
+            hipSuccess)
+            return e;
+        if (std::max(tb, tb2) > s.temp_bytes) {
+            (void)hipFree(s.temp);
+            s.temp = nullptr;
+            s.temp_bytes = 0;
+            if ((e = hipMalloc(&s.temp, std::max(tb, tb2))) != hipSuccess) return e;
+            s.temp_bytes = std::max(tb, tb2);
+        }
+        if ((e = hipcub::DeviceScan::ExclusiveSum(s.temp, tb, sb.m, s.off, (int)(ns + 1), stream)) != hipSuccess)
+            return e;
+        uint32_t total = 0;
+        if ((e = hipMemcpyAsync(&total, s.off + ns, sizeof(uint32_t), hipMemcpyDeviceToHost, stream)) != hipSuccess)
+            return e;
+        if ((e = hipStreamSynchronize(stream)) != hipSuccess) return e;
+        if (total == 0) continue;
+        if ((int64_t)total > s.cap_entries) {
+            for (int i = 0; i < 2; ++i) {
+                (void)hipFree(s.keys[i]);
+                (void)hipFree(s.vals[i]);
+                s.keys[i] = s.vals[i] = nullptr;
+            }
+            s.cap_entries = 0;
+            const int64_t cap = (int64_t)total + total / 4;
+            for (int i = 0; i < 2; ++i)
+                if ((e = hipMalloc((void**)&s.keys[i], cap * sizeof(uint32_t))) != hipSuccess ||
+                    (e = hipMalloc((void**)&s.vals[i], cap * sizeof(uint32_t))) != hipSuccess)
+                    return e;
+            s.cap_entries = cap;
+            tb2 = 0;
+            if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, s.keys[0], s.keys[1], s.vals[0], s.vals[1],
+                                                        (int)cap, 0, bits, stream)) != hipSuccess)
+                return e;
+            if (tb2 > s.temp_bytes) {
+                (void)hipFree(s.temp);
+                s.temp = nullptr;
+                s.temp_bytes = 0;
+                if ((e = hipMalloc(&s.temp, tb2)) != hipSuccess) return e;
+                s.temp_bytes = tb2;
+            }
+        }
+        g = std::min<int64_t>((ns + 255) / 256, 262144);
+        hipLaunchKernelGGL(tvam_bin_fill_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, sb, s.off, ns, s.keys[0],
+                           s.vals[0]);
+        size_t tb3 = s.temp_bytes;
+        if ((e = hipcub::DeviceRadixSort::SortPairs(s.temp, tb3, s.keys[0], s.keys[1], s.vals[0], s.vals[1],
+                                                    (int)total, 0, bits, stream)) != hipSuccess)
+            return e;
+        g = std::min<int64_t>(((int64_t)total + 256) / 256, 65536);
+        hipLaunchKernelGGL(tvam_bin_start_kernel, dim3((unsigned)g), dim3(256), 0, stream, s.keys[1], (int64_t)total,
+                           nbricks, s.bstart);
+        if (s.acc_float)
+            hipLaunchKernelGGL(tvam_bin_march_kernel<1>, dim3((unsigned)nbricks), dim3(512), 0, stream, k, sb,
+                               s.vals[1], s.bstart, dose);
+        else
+            hipLaunchKernelGGL(tvam_bin_march_kernel<0>, dim3((unsigned)nbricks), dim3(512), 0, stream, k, sb,
+                               s.vals[1], s.bstart, dose);
+        if ((e = hipGetLastError()) != hipSuccess) return e;
+    }
+    return hipSuccess;
 }
