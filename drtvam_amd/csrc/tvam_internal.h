@@ -75,6 +75,7 @@ enum TvamMode { TVAM_MODE_FWD = 0, TVAM_MODE_ADJ = 1, TVAM_MODE_COUNT = 2, TVAM_
 struct TvamSegBuf {
     int64_t p0, p1;
     int32_t slots;
+    int32_t adj;                  // records for the adjoint (weight att * wscale)
     float4* a;
     float4* b;
     int2* c;
@@ -94,6 +95,8 @@ struct TvamBinScratch {
     void* temp = nullptr;
     size_t temp_bytes = 0;
     int acc_float = 0;            // 1: float LDS adds instead of int64 fixed point (TVAM_BIN_FLOAT)
+    uint32_t* slot_of = nullptr;  // [cap_entries] segment slot of each (segment, brick) entry
+    float* part = nullptr;        // [cap_entries] adjoint partial of each entry
 };
 
 hipError_t tvam_launch_tiles(int mode, const TvamConsts& k, const TvamTiles& t, size_t lds_bytes,
@@ -108,8 +111,9 @@ hipError_t tvam_launch_scatter_paths(int mode, const TvamConsts& k, const TvamTi
 // Forward of the scattered segments through brick bins (chunks of paths; host
 // syncs once per chunk to size the bins).  Returns hipErrorNotSupported when
 // the grid is too large for the packed records (callers then use the atomics).
-hipError_t tvam_scatter_forward_binned(const TvamConsts& k, const TvamTiles& t, const float* pat, float* dose,
-                                       TvamBinScratch& s, hipStream_t stream);
+hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t, const float* pat,
+                               const int32_t* idxmap, const float* gin, float* out, TvamBinScratch& s,
+                               hipStream_t stream);
 void tvam_bin_scratch_free(TvamBinScratch& s);
 
 // Radon filter image of the shard's DMD pixels (tvam_radon.hip).

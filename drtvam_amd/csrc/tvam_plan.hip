@@ -941,7 +941,8 @@ extern "C" int tvam_forward(tvam_plan* p, const float* active_data, const uint32
         t.seed = seed;
         e = hipErrorNotSupported;
         p->bins.acc_float = env_int("TVAM_BIN_FLOAT", 0);
-        if (!(p->desc.flags & TVAM_FLAG_SCATTER_ATOMIC)) e = tvam_scatter_forward_binned(kc, t, pat, dose, p->bins, stream);
+        if (!(p->desc.flags & TVAM_FLAG_SCATTER_ATOMIC))
+            e = tvam_scatter_binned(TVAM_MODE_FWD, kc, t, pat, idxmap, nullptr, dose, p->bins, stream);
         if (e == hipErrorNotSupported)
             e = tvam_launch_scatter_paths(TVAM_MODE_FWD, kc, t, pat, idxmap, nullptr, dose, nullptr, stream);
         if (e != hipSuccess) return hip_fail(e, "scatter forward launch");
@@ -988,7 +989,11 @@ extern "C" int tvam_adjoint(tvam_plan* p, const float* grad_dose, const uint32_t
         TvamTiles t = p->tiles;
         t.spp = spp;
         t.seed = seed;
-        e = tvam_launch_scatter_paths(TVAM_MODE_ADJ, k, t, nullptr, idxmap, grad_dose, grad_active, nullptr, stream);
+        e = hipErrorNotSupported;
+        if (!(p->desc.flags & TVAM_FLAG_SCATTER_ATOMIC))
+            e = tvam_scatter_binned(TVAM_MODE_ADJ, k, t, nullptr, idxmap, grad_dose, grad_active, p->bins, stream);
+        if (e == hipErrorNotSupported)
+            e = tvam_launch_scatter_paths(TVAM_MODE_ADJ, k, t, nullptr, idxmap, grad_dose, grad_active, nullptr, stream);
         if (e != hipSuccess) return hip_fail(e, "scatter adjoint launch");
     }
     return 0;

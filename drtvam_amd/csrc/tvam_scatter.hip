@@ -285,10 +285,13 @@ __global__ __launch_bounds__(256) void tvam_scatter_kernel(TvamConsts k, TvamTil
         const int smp = (int)(i - local * spp);
         float em = 1.0f;
         int64_t act = local;
-        if (MODE == TVAM_MODE_FWD || MODE == TVAM_MODE_EMIT) {
+        if (MODE == TVAM_MODE_FWD || (MODE == TVAM_MODE_EMIT && !sb.adj)) {
             const float p = pat[local];
             if (p == 0.0f && k.skip_zero) continue;
             em = p * k.wscale * k.inv_vol;
+        } else if (MODE == TVAM_MODE_EMIT) {  // adjoint records: weight att * wscale (grad * inv_vol gathered)
+            em = k.wscale;
+            if (idxmap && idxmap[local] < 0) continue;
         } else if (idxmap) {
             act = idxmap[local];
             if (act < 0) continue;
@@ -426,9 +429,12 @@ __device__ __forceinline__ void sc_unpack(const float4 a, const float4 b, const 
     w = __int_as_float(c.y);
 }
 
+// (brick, entry) pairs; an entry is one (segment, brick) crossing, entries of
+// a segment are contiguous from off[slot] (slot_of maps them back).
 __global__ __launch_bounds__(256) void tvam_bin_fill_kernel(TvamConsts k, TvamSegBuf sb, const uint32_t* __restrict__ off,
                                                             int64_t nslots, uint32_t* __restrict__ keys,
-                                                            uint32_t* __restrict__ vals) {
+                                                            uint32_t* __restrict__ vals,
+                                                            uint32_t* __restrict__ slot_of) {
     for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nslots; s += (int64_t)gridDim.x * blockDim.x) {
         if (sb.m[s] == 0) continue;
         SegDda q;
@@ -437,7 +443,8 @@ __global__ __launch_bounds__(256) void tvam_bin_fill_kernel(TvamConsts k, TvamSe
         uint32_t o = off[s];
         sc_walk_bricks(k, q, [&](int bid) {
             keys[o] = (uint32_t)bid;
-            vals[o] = (uint32_t)s;
+            vals[o] = o;
+            slot_of[o] = (uint32_t)s;
             ++o;
         });
     }
@@ -452,16 +459,20 @@ __global__ void tvam_bin_start_kernel(const uint32_t* __restrict__ keys, int64_t
     }
 }
 
-// One workgroup per brick: the brick's visits added in LDS, then dose += tile
-// (the brick is this launch's alone).  ACC 0: exact int64 fixed point with a
+// One workgroup per brick.  Forward (ACC 0: exact int64 fixed point with a
 // per-brick scale 2^e from sum |w| * the largest per-visit weight
-// min(1, st sqrt3 h) (a line crosses a voxel once; 2^62 headroom keeps the
-// quantisation ~1e-13 of the bound); ACC 1: float LDS adds.
+// min(1, st sqrt3 h) -- a line crosses a voxel once; 2^61 headroom keeps the
+// quantisation ~1e-13 of the bound; ACC 1: float adds): the brick's visits
+// added in LDS, then dose += tile (the brick is this launch's alone).
+// Adjoint (ACC 2): the brick's grad * inv_vol staged in LDS, each entry's
+// weighted gather written to part[entry] (no atomics; summed per path later).
 template <int ACC>
 __global__ __launch_bounds__(512) void tvam_bin_march_kernel(TvamConsts k, TvamSegBuf sb,
                                                              const uint32_t* __restrict__ vals,
+                                                             const uint32_t* __restrict__ slot_of,
                                                              const uint32_t* __restrict__ bstart,
-                                                             float* __restrict__ dose) {
+                                                             float* __restrict__ dose, const float* __restrict__ gin,
+                                                             float* __restrict__ part) {
     constexpr int NV = TVAM_BX * TVAM_BY * TVAM_BZ;
     __shared__ __attribute__((aligned(16))) unsigned char smem[NV * (ACC == 0 ? 8 : 4)];
     __shared__ float red[8];
@@ -474,10 +485,12 @@ __global__ __launch_bounds__(512) void tvam_bin_march_kernel(TvamConsts k, TvamS
     const int bx = bid % nbx, by = (bid / nbx) % nby, bz = bid / (nbx * nby);
     const int lo[3] = {bx * TVAM_BX, by * TVAM_BY, bz * TVAM_BZ};
     const int hi[3] = {min(lo[0] + TVAM_BX, k.res[0]), min(lo[1] + TVAM_BY, k.res[1]), min(lo[2] + TVAM_BZ, k.res[2])};
+    const int wx = hi[0] - lo[0], wy = hi[1] - lo[1], wz = hi[2] - lo[2];
+    const int sy = TVAM_BX, sz = TVAM_BX * TVAM_BY;
     float scale = 1.0f;
     if (ACC == 0) {
         float sw = 0.0f;
-        for (uint32_t e = e0 + threadIdx.x; e < e1; e += 512) sw += fabsf(__int_as_float(sb.c[vals[e]].y));
+        for (uint32_t e = e0 + threadIdx.x; e < e1; e += 512) sw += fabsf(__int_as_float(sb.c[slot_of[vals[e]]].y));
         for (int o = 32; o > 0; o >>= 1) sw += __shfl_xor(sw, o, 64);
         if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sw;
         for (int i = threadIdx.x; i < NV; i += 512) ltile[i] = 0;
@@ -493,29 +506,40 @@ __global__ __launch_bounds__(512) void tvam_bin_march_kernel(TvamConsts k, TvamS
             ex = ex > 126 ? 126 : (ex < -126 ? -126 : ex);
             scale = ldexpf(1.0f, ex);
         }
-    } else {
+    } else if (ACC == 1) {
         for (int i = threadIdx.x; i < NV; i += 512) ftile[i] = 0.0f;
         __syncthreads();
+    } else {
+        for (int i = threadIdx.x; i < wx * wy * wz; i += 512) {
+            const int x = i % wx, y = (i / wx) % wy, z = i / (wx * wy);
+            const size_t g = ((size_t)(lo[2] + z) * k.res[1] + (lo[1] + y)) * k.res[0] + (lo[0] + x);
+            ftile[z * sz + y * sy + x] = gin[g] * k.inv_vol;  // volume.py:130
+        }
+        __syncthreads();
     }
-    const int sy = TVAM_BX, sz = TVAM_BX * TVAM_BY;
     for (uint32_t e = e0 + threadIdx.x; e < e1; e += 512) {
-        const uint32_t s = vals[e];
+        const uint32_t ent = vals[e];
+        const uint32_t s = slot_of[ent];
         SegDda q;
         float w;
         sc_unpack(sb.a[s], sb.b[s], sb.c[s], q, w);
         const float ws = w * scale;
+        float acc = 0.0f;
         sc_box_march(k, q, lo, hi, [&](int x, int y, int z, float c) {
             const int li = z * sz + y * sy + x;
             if (ACC == 0)
                 __hip_atomic_fetch_add(&ltile[li], (long long)__float2ll_rn(ws * c), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
-            else
+            else if (ACC == 1)
                 __hip_atomic_fetch_add(&ftile[li], w * c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            else
+                acc = fmaf(c, ftile[li], acc);
         });
+        if (ACC == 2) part[ent] = w * acc;
     }
+    if (ACC == 2) return;
     __syncthreads();
     const float inv = 1.0f / scale;
-    const int wx = hi[0] - lo[0], wy = hi[1] - lo[1], wz = hi[2] - lo[2];
     for (int i = threadIdx.x; i < wx * wy * wz; i += 512) {
         const int x = i % wx, y = (i / wx) % wy, z = i / (wx * wy);
         const int li = z * sz + y * sy + x;
@@ -524,6 +548,31 @@ __global__ __launch_bounds__(512) void tvam_bin_march_kernel(TvamConsts k, TvamS
             const size_t g = ((size_t)(lo[2] + z) * k.res[1] + (lo[1] + y)) * k.res[0] + (lo[0] + x);
             dose[g] += v;
         }
+    }
+}
+
+// Adjoint: per DMD pixel of the chunk, the sum of its samples' segment-brick
+// partials (contiguous from off[first slot]), added to the pattern gradient
+// after the first-segment kernels (same stream, one writer per entry).
+__global__ __launch_bounds__(256) void tvam_bin_reduce_kernel(TvamConsts k, TvamSegBuf sb, int spp,
+                                                              const uint32_t* __restrict__ off,
+                                                              const float* __restrict__ part,
+                                                              const int32_t* __restrict__ idxmap,
+                                                              float* __restrict__ grad) {
+    const int64_t l0 = sb.p0 / spp, l1 = sb.p1 / spp;
+    for (int64_t local = l0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; local < l1;
+         local += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t s0 = (local * spp - sb.p0) * sb.slots, s1 = s0 + (int64_t)spp * sb.slots;
+        const uint32_t a = off[s0], b = off[s1];
+        if (a == b) continue;
+        float acc = 0.0f;
+        for (uint32_t e = a; e < b; ++e) acc += part[e];
+        int64_t act = local;
+        if (idxmap) {
+            act = idxmap[local];
+            if (act < 0) continue;
+        }
+        grad[act] += acc;
     }
 }
 
@@ -552,27 +601,36 @@ void tvam_bin_scratch_free(TvamBinScratch& s) {
     }
     (void)hipFree(s.bstart);
     (void)hipFree(s.temp);
+    (void)hipFree(s.slot_of);
+    (void)hipFree(s.part);
     s = TvamBinScratch{};
 }
 
-hipError_t tvam_scatter_forward_binned(const TvamConsts& k, const TvamTiles& t, const float* pat, float* dose,
-                                       TvamBinScratch& s, hipStream_t stream) {
+hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t, const float* pat,
+                               const int32_t* idxmap, const float* gin, float* out, TvamBinScratch& s,
+                               hipStream_t stream) {
     const int nsurf = k.vial_type == 0 ? 1 : 2;
     const int slots = k.max_depth - nsurf - 1;  // later medium segments per path
     if (slots <= 0) return hipSuccess;
     if (k.res[0] > 2048 || k.res[1] > 2048 || k.res[2] > 1024) return hipErrorNotSupported;
+    const bool adj = mode == TVAM_MODE_ADJ;
     const int nbx = (k.res[0] + TVAM_BX - 1) / TVAM_BX, nby = (k.res[1] + TVAM_BY - 1) / TVAM_BY,
               nbz = (k.res[2] + TVAM_BZ - 1) / TVAM_BZ;
     const int nbricks = nbx * nby * nbz;
     int bits = 1;
     while ((1 << bits) < nbricks) ++bits;
-    const int64_t npaths = (int64_t)t.n_shard * k.crop_y * k.crop_x * t.spp;
-    const int64_t chunk = std::min<int64_t>(npaths, std::max<int64_t>(1, (int64_t)(1 << 27) / slots));  // 128M slots
+    const int spp = (int)t.spp;
+    const int64_t npaths = (int64_t)t.n_shard * k.crop_y * k.crop_x * spp;
+    // chunk of paths: a whole number of pixels (the adjoint reduces a pixel's samples together)
+    int64_t chunk = std::max<int64_t>(1, (int64_t)(1 << 27) / slots);  // 128M slots
+    chunk = std::max<int64_t>(spp, chunk / spp * spp);
+    chunk = std::min(npaths, chunk);
     const int64_t nsl = chunk * slots;
     hipError_t e;
-    int64_t capa = s.cap_slots;
     if (nsl > s.cap_slots) {
+        const int keep_float = s.acc_float;
         tvam_bin_scratch_free(s);
+        s.acc_float = keep_float;
         if ((e = hipMalloc((void**)&s.sb.a, nsl * sizeof(float4))) != hipSuccess ||
             (e = hipMalloc((void**)&s.sb.b, nsl * sizeof(float4))) != hipSuccess ||
             (e = hipMalloc((void**)&s.sb.c, nsl * sizeof(int2))) != hipSuccess ||
@@ -580,9 +638,7 @@ hipError_t tvam_scatter_forward_binned(const TvamConsts& k, const TvamTiles& t, 
             (e = hipMalloc((void**)&s.off, (nsl + 1) * sizeof(uint32_t))) != hipSuccess)
             return e;
         s.cap_slots = nsl;
-        capa = nsl;
     }
-    (void)capa;
     int64_t capb = s.cap_bricks;
     if ((e = grow(&s.bstart, capb, (int64_t)nbricks + 1)) != hipSuccess) return e;
     s.cap_bricks = (int32_t)capb;
@@ -593,26 +649,21 @@ hipError_t tvam_scatter_forward_binned(const TvamConsts& k, const TvamTiles& t, 
         sb.p0 = p0;
         sb.p1 = p1;
         sb.slots = slots;
+        sb.adj = adj ? 1 : 0;
         if ((e = hipMemsetAsync(sb.m, 0, (ns + 1) * sizeof(uint32_t), stream)) != hipSuccess) return e;
         int64_t g = std::min<int64_t>((p1 - p0 + 255) / 256, 262144);
         hipLaunchKernelGGL(tvam_scatter_kernel<TVAM_MODE_EMIT>, dim3((unsigned)g), dim3(256), 0, stream, k, t, pat,
-                           nullptr, nullptr, nullptr, nullptr, sb);
+                           idxmap, nullptr, nullptr, nullptr, sb);
         // exclusive scan of the brick counts (ns + 1 entries: the last gives the total)
         size_t tb = 0;
         if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, sb.m, s.off, (int)(ns + 1), stream)) != hipSuccess)
             return e;
-        size_t tb2 = 0;
-        if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                                    (uint32_t*)nullptr, (uint32_t*)nullptr,
-                                                    (int)std::max<int64_t>(s.cap_entries, 1), 0, bits, stream)) !=
-            hipSuccess)
-            return e;
-        if (std::max(tb, tb2) > s.temp_bytes) {
+        if (tb > s.temp_bytes) {
             (void)hipFree(s.temp);
             s.temp = nullptr;
             s.temp_bytes = 0;
-            if ((e = hipMalloc(&s.temp, std::max(tb, tb2))) != hipSuccess) return e;
-            s.temp_bytes = std::max(tb, tb2);
+            if ((e = hipMalloc(&s.temp, tb)) != hipSuccess) return e;
+            s.temp_bytes = tb;
         }
         if ((e = hipcub::DeviceScan::ExclusiveSum(s.temp, tb, sb.m, s.off, (int)(ns + 1), stream)) != hipSuccess)
             return e;
@@ -627,41 +678,55 @@ hipError_t tvam_scatter_forward_binned(const TvamConsts& k, const TvamTiles& t, 
                 (void)hipFree(s.vals[i]);
                 s.keys[i] = s.vals[i] = nullptr;
             }
+            (void)hipFree(s.slot_of);
+            (void)hipFree(s.part);
+            s.slot_of = nullptr;
+            s.part = nullptr;
             s.cap_entries = 0;
             const int64_t cap = (int64_t)total + total / 4;
             for (int i = 0; i < 2; ++i)
                 if ((e = hipMalloc((void**)&s.keys[i], cap * sizeof(uint32_t))) != hipSuccess ||
                     (e = hipMalloc((void**)&s.vals[i], cap * sizeof(uint32_t))) != hipSuccess)
                     return e;
-            s.cap_entries = cap;
-            tb2 = 0;
-            if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, s.keys[0], s.keys[1], s.vals[0], s.vals[1],
-                                                        (int)cap, 0, bits, stream)) != hipSuccess)
+            if ((e = hipMalloc((void**)&s.slot_of, cap * sizeof(uint32_t))) != hipSuccess ||
+                (e = hipMalloc((void**)&s.part, cap * sizeof(float))) != hipSuccess)
                 return e;
-            if (tb2 > s.temp_bytes) {
-                (void)hipFree(s.temp);
-                s.temp = nullptr;
-                s.temp_bytes = 0;
-                if ((e = hipMalloc(&s.temp, tb2)) != hipSuccess) return e;
-                s.temp_bytes = tb2;
-            }
+            s.cap_entries = cap;
+        }
+        size_t tb2 = 0;
+        if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, s.keys[0], s.keys[1], s.vals[0], s.vals[1],
+                                                    (int)total, 0, bits, stream)) != hipSuccess)
+            return e;
+        if (tb2 > s.temp_bytes) {
+            (void)hipFree(s.temp);
+            s.temp = nullptr;
+            s.temp_bytes = 0;
+            if ((e = hipMalloc(&s.temp, tb2)) != hipSuccess) return e;
+            s.temp_bytes = tb2;
         }
         g = std::min<int64_t>((ns + 255) / 256, 262144);
         hipLaunchKernelGGL(tvam_bin_fill_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, sb, s.off, ns, s.keys[0],
-                           s.vals[0]);
-        size_t tb3 = s.temp_bytes;
-        if ((e = hipcub::DeviceRadixSort::SortPairs(s.temp, tb3, s.keys[0], s.keys[1], s.vals[0], s.vals[1],
+                           s.vals[0], s.slot_of);
+        if ((e = hipcub::DeviceRadixSort::SortPairs(s.temp, tb2, s.keys[0], s.keys[1], s.vals[0], s.vals[1],
                                                     (int)total, 0, bits, stream)) != hipSuccess)
             return e;
         g = std::min<int64_t>(((int64_t)total + 256) / 256, 65536);
         hipLaunchKernelGGL(tvam_bin_start_kernel, dim3((unsigned)g), dim3(256), 0, stream, s.keys[1], (int64_t)total,
                            nbricks, s.bstart);
-        if (s.acc_float)
+        if (adj) {
+            hipLaunchKernelGGL(tvam_bin_march_kernel<2>, dim3((unsigned)nbricks), dim3(512), 0, stream, k, sb,
+                               s.vals[1], s.slot_of, s.bstart, nullptr, gin, s.part);
+            const int64_t npix = (p1 - p0) / spp;
+            g = std::min<int64_t>((npix + 255) / 256, 65536);
+            hipLaunchKernelGGL(tvam_bin_reduce_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, sb, spp, s.off,
+                               s.part, idxmap, out);
+        } else if (s.acc_float) {
             hipLaunchKernelGGL(tvam_bin_march_kernel<1>, dim3((unsigned)nbricks), dim3(512), 0, stream, k, sb,
-                               s.vals[1], s.bstart, dose);
-        else
+                               s.vals[1], s.slot_of, s.bstart, out, nullptr, nullptr);
+        } else {
             hipLaunchKernelGGL(tvam_bin_march_kernel<0>, dim3((unsigned)nbricks), dim3(512), 0, stream, k, sb,
-                               s.vals[1], s.bstart, dose);
+                               s.vals[1], s.slot_of, s.bstart, out, nullptr, nullptr);
+        }
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
     return hipSuccess;

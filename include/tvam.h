@@ -135,7 +135,7 @@ typedef struct tvam_desc {
 #define TVAM_FLAG_FWD_STATS    2  /* forward: count tiles that fell back to float LDS atomics */
 #define TVAM_FLAG_NO_PLANAR    4  /* use the per-ray tile kernels even where the planar path applies */
 #define TVAM_FLAG_RAY_FWD      8  /* planar path: ray-driven forward instead of the voxel-driven one */
-#define TVAM_FLAG_SCATTER_ATOMIC 16 /* scattering media: global atomics instead of brick bins (forward) */
+#define TVAM_FLAG_SCATTER_ATOMIC 16 /* scattering media: per-path global atomics / gathers instead of brick bins */
 
 typedef struct tvam_plan tvam_plan;
 

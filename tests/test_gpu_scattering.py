@@ -143,8 +143,9 @@ def test_slab_refused():
 
 @pytest.mark.parametrize("case", [dict(), dict(vial="cylindrical", regular=False, spp=2), dict(N=40, A=8, albedo=0.9)],
                          ids=_id)
-def test_binned_forward_matches_atomics(case):
-    """Brick-binned scattered forward (LDS fixed point) == the per-path global-atomic forward."""
+def test_binned_matches_per_path(case):
+    """Brick-binned scattered forward (LDS fixed point) and adjoint (LDS-staged gathers, per-entry
+    partials) == the per-path global-atomic / global-gather kernels."""
     spp = case.get("spp", 1)
     d = make(**case)
     n = d.n_patterns * d.crop_y * d.crop_x
@@ -154,3 +155,7 @@ def test_binned_forward_matches_atomics(case):
     d2.flags |= _abi.FLAG_SCATTER_ATOMIC
     b = Projection(d2, "cuda:0").forward(p, None, spp, 3)
     assert float(torch.linalg.norm(a - b) / torch.linalg.norm(b)) < 1e-5
+    G = torch.as_tensor(np.random.default_rng(5).uniform(-1, 1, a.shape[:3]).astype(np.float32), device="cuda:0")
+    ga = Projection(d, "cuda:0").adjoint(G, n, None, spp, 7)
+    gb = Projection(d2, "cuda:0").adjoint(G, n, None, spp, 7)
+    assert float(torch.linalg.norm(ga - gb) / torch.linalg.norm(gb)) < 1e-5
