@@ -169,27 +169,34 @@ __device__ __forceinline__ int sc_nbr(const TvamConsts& k, int a) {
 // resumes from.  F(brick id) per brick; returns the count.
 template <typename F>
 __device__ __forceinline__ int sc_walk_bricks(const TvamConsts& k, const SegDda& q, F&& f) {
-    const int B[3] = {TVAM_BX, TVAM_BY, TVAM_BZ};
-    const int nb[3] = {sc_nbr(k, 0), sc_nbr(k, 1), sc_nbr(k, 2)};
-    int b[3] = {q.sv[0] / B[0], q.sv[1] / B[1], q.sv[2] / B[2]};
+    const int nb0 = sc_nbr(k, 0), nb1 = sc_nbr(k, 1), nb2 = sc_nbr(k, 2);
+    int b0 = q.sv[0] / TVAM_BX, b1 = q.sv[1] / TVAM_BY, b2 = q.sv[2] / TVAM_BZ;
     int cnt = 0;
     for (int guard = 0; guard < 4096; ++guard) {
-        f((b[2] * nb[1] + b[1]) * nb[0] + b[0]);
+        f((b2 * nb1 + b1) * nb0 + b0);
         ++cnt;
-        float tout[3];
-#pragma unroll
-        for (int a = 0; a < 3; ++a) {
-            float tin;
-            int nin, nout;
-            const int lo = b[a] * B[a], hi = min(lo + B[a], k.res[a]);
-            tvam_axis_window(q.sv[a], q.step[a], q.dtm0[a], q.ts[a], lo, hi, tin, tout[a], nin, nout);
+        float tin, t0, t1, t2;
+        int nin, nout;
+        tvam_axis_window(q.sv[0], q.step[0], q.dtm0[0], q.ts[0], b0 * TVAM_BX, min(b0 * TVAM_BX + TVAM_BX, k.res[0]),
+                         tin, t0, nin, nout);
+        tvam_axis_window(q.sv[1], q.step[1], q.dtm0[1], q.ts[1], b1 * TVAM_BY, min(b1 * TVAM_BY + TVAM_BY, k.res[1]),
+                         tin, t1, nin, nout);
+        tvam_axis_window(q.sv[2], q.step[2], q.dtm0[2], q.ts[2], b2 * TVAM_BZ, min(b2 * TVAM_BZ + TVAM_BZ, k.res[2]),
+                         tin, t2, nin, nout);
+        const bool m0 = t0 <= t1 && t0 <= t2;
+        const bool m1 = !m0 && t1 <= t2;
+        const float tm = m0 ? t0 : (m1 ? t1 : t2);
+        if (!(tm < q.tau_end)) break;
+        if (m0) {
+            b0 += q.step[0];
+            if (b0 < 0 || b0 >= nb0) break;
+        } else if (m1) {
+            b1 += q.step[1];
+            if (b1 < 0 || b1 >= nb1) break;
+        } else {
+            b2 += q.step[2];
+            if (b2 < 0 || b2 >= nb2) break;
         }
-        int am = 0;
-        if (tout[1] < tout[am]) am = 1;
-        if (tout[2] < tout[am]) am = 2;
-        if (!(tout[am] < q.tau_end)) break;
-        b[am] += q.step[am];
-        if (b[am] < 0 || b[am] >= nb[am]) break;
     }
     return cnt;
 }
@@ -198,7 +205,9 @@ __device__ __forceinline__ int sc_walk_bricks(const TvamConsts& k, const SegDda&
 // closed form at the box entry: per axis the step count n at the entry time,
 // the next crossing at t = dtm0 + n ts (fmaf from the count, so a visit splits
 // at a brick face exactly where the neighbouring brick resumes), one axis per
-// visit.  F(local voxel x, y, z, weight e^{-st t0} - e^{-st t1}).
+// visit (ties: x before y before z).  Axes are kept in scalars (dynamically
+// indexed arrays would be promoted to LDS).  F(local x, y, z, weight
+// e^{-st t0} - e^{-st t1}).
 template <typename F>
 __device__ __forceinline__ void sc_box_march(const TvamConsts& k, const SegDda& q, const int lo[3], const int hi[3],
                                              F&& f) {
@@ -210,27 +219,42 @@ __device__ __forceinline__ void sc_box_march(const TvamConsts& k, const SegDda& 
     const float tau_e = fmaxf(fmaxf(fmaxf(tin[0], tin[1]), tin[2]), 0.0f);
     const float tau_x = fminf(fminf(fminf(tout[0], tout[1]), tout[2]), q.tau_end);
     if (!(tau_e < tau_x)) return;
-    int v[3], n[3];
-    float T[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        n[a] = tvam_axis_steps(tau_e, q.dtm0[a], q.ts[a], nin[a], nout[a]);
-        v[a] = q.sv[a] + q.step[a] * n[a] - lo[a];
-        T[a] = q.dtm0[a] < TVAM_INF ? fmaf((float)n[a], q.ts[a], q.dtm0[a]) : TVAM_INF;
-    }
+    int n0 = tvam_axis_steps(tau_e, q.dtm0[0], q.ts[0], nin[0], nout[0]);
+    int n1 = tvam_axis_steps(tau_e, q.dtm0[1], q.ts[1], nin[1], nout[1]);
+    int n2 = tvam_axis_steps(tau_e, q.dtm0[2], q.ts[2], nin[2], nout[2]);
+    int x = q.sv[0] + q.step[0] * n0 - lo[0];
+    int y = q.sv[1] + q.step[1] * n1 - lo[1];
+    int z = q.sv[2] + q.step[2] * n2 - lo[2];
+    const float ts0 = q.ts[0], ts1 = q.ts[1], ts2 = q.ts[2];
+    const float d0 = q.dtm0[0], d1 = q.dtm0[1], d2 = q.dtm0[2];
+    float T0 = d0 < TVAM_INF ? fmaf((float)n0, ts0, d0) : TVAM_INF;
+    float T1 = d1 < TVAM_INF ? fmaf((float)n1, ts1, d1) : TVAM_INF;
+    float T2 = d2 < TVAM_INF ? fmaf((float)n2, ts2, d2) : TVAM_INF;
+    const int s0 = q.step[0], s1 = q.step[1], s2 = q.step[2];
     const float stop = tau_x - 1e-6f;
-    float ea = sc_exp2(k.nsig2 * (q.t_start + tau_e));
+    const float base = k.nsig2 * q.t_start;
+    float ea = sc_exp2(fmaf(k.nsig2, tau_e, base));
     for (int guard = 0; guard < 3 * 4096; ++guard) {
-        int am = 0;
-        if (T[1] < T[am]) am = 1;
-        if (T[2] < T[am]) am = 2;
-        const float tn = fminf(T[am], tau_x);
-        const float eb = sc_exp2(k.nsig2 * (q.t_start + tn));
-        f(v[0], v[1], v[2], ea - eb);
+        const bool m0 = T0 <= T1 && T0 <= T2;
+        const bool m1 = !m0 && T1 <= T2;
+        const float tmin = m0 ? T0 : (m1 ? T1 : T2);
+        const float tn = tmin < tau_x ? tmin : tau_x;
+        const float eb = sc_exp2(fmaf(k.nsig2, tn, base));
+        f(x, y, z, ea - eb);
         if (!(tn < stop)) break;
-        v[am] += q.step[am];
-        ++n[am];
-        T[am] = fmaf((float)n[am], q.ts[am], q.dtm0[am]);
+        if (m0) {
+            x += s0;
+            ++n0;
+            T0 = fmaf((float)n0, ts0, d0);
+        } else if (m1) {
+            y += s1;
+            ++n1;
+            T1 = fmaf((float)n1, ts1, d1);
+        } else {
+            z += s2;
+            ++n2;
+            T2 = fmaf((float)n2, ts2, d2);
+        }
         ea = eb;
     }
 }
@@ -459,10 +483,10 @@ __global__ void tvam_bin_start_kernel(const uint32_t* __restrict__ keys, int64_t
     }
 }
 
-// One workgroup per brick.  Forward (ACC 0: exact int64 fixed point with a
-// per-brick scale 2^e from sum |w| * the largest per-visit weight
-// min(1, st sqrt3 h) -- a line crosses a voxel once; 2^61 headroom keeps the
-// quantisation ~1e-13 of the bound; ACC 1: float adds): the brick's visits
+// One workgroup per brick.  Forward (ACC 0: exact int64 fixed point; every add
+// rounds to int32 with a per-brick scale 2^e from max |w| * the largest
+// per-visit weight min(1, st sqrt3 h), so the step is 2^-30 of the largest
+// single add and the int64 sums cannot overflow; ACC 1: float adds): the brick's visits
 // added in LDS, then dose += tile (the brick is this launch's alone).
 // Adjoint (ACC 2): the brick's grad * inv_vol staged in LDS, each entry's
 // weighted gather written to part[entry] (no atomics; summed per path later).
@@ -489,20 +513,21 @@ __global__ __launch_bounds__(512) void tvam_bin_march_kernel(TvamConsts k, TvamS
     const int sy = TVAM_BX, sz = TVAM_BX * TVAM_BY;
     float scale = 1.0f;
     if (ACC == 0) {
+        // per-add bound: each add rounds to int32 (one v_cvt), the int64 sums cannot overflow
         float sw = 0.0f;
-        for (uint32_t e = e0 + threadIdx.x; e < e1; e += 512) sw += fabsf(__int_as_float(sb.c[slot_of[vals[e]]].y));
-        for (int o = 32; o > 0; o >>= 1) sw += __shfl_xor(sw, o, 64);
+        for (uint32_t e = e0 + threadIdx.x; e < e1; e += 512) sw = fmaxf(sw, fabsf(__int_as_float(sb.c[slot_of[vals[e]]].y)));
+        for (int o = 32; o > 0; o >>= 1) sw = fmaxf(sw, __shfl_xor(sw, o, 64));
         if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sw;
         for (int i = threadIdx.x; i < NV; i += 512) ltile[i] = 0;
         __syncthreads();
         float tot = 0.0f;
-        for (int w = 0; w < 8; ++w) tot += red[w];
+        for (int w = 0; w < 8; ++w) tot = fmaxf(tot, red[w]);
         const float hmax = fmaxf(fmaxf(k.h[0], k.h[1]), k.h[2]);
         const float bound = tot * fminf(1.0f, k.sig_t * 1.7320508f * hmax) * 1.001f;
         if (bound > 0.0f && isfinite(bound)) {
             int ex;
             frexpf(bound, &ex);
-            ex = 61 - ex;
+            ex = 30 - ex;
             ex = ex > 126 ? 126 : (ex < -126 ? -126 : ex);
             scale = ldexpf(1.0f, ex);
         }
@@ -528,7 +553,7 @@ __global__ __launch_bounds__(512) void tvam_bin_march_kernel(TvamConsts k, TvamS
         sc_box_march(k, q, lo, hi, [&](int x, int y, int z, float c) {
             const int li = z * sz + y * sy + x;
             if (ACC == 0)
-                __hip_atomic_fetch_add(&ltile[li], (long long)__float2ll_rn(ws * c), __ATOMIC_RELAXED,
+                __hip_atomic_fetch_add(&ltile[li], (long long)__float2int_rn(ws * c), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
             else if (ACC == 1)
                 __hip_atomic_fetch_add(&ftile[li], w * c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
