@@ -94,6 +94,9 @@ def main():
     ap.add_argument("--shard", choices=["auto", "angle", "slab"], default="auto",
                     help="multi-GPU partition: z-slabs of the film + DMD row bands (planar scenes, no dose "
                          "all-reduce; auto) or angle blocks + RCCL dose all-reduce")
+    ap.add_argument("--emulate", type=str, default=None, metavar="RANK/WORLD",
+                    help="time one rank's shard of a WORLD-rank run on this single GPU (no collectives; "
+                         "scaling study only, never the bench line)")
     args = ap.parse_args()
 
     import torch
@@ -117,7 +120,12 @@ def main():
     cfg["shard"] = args.shard
     cfg["flags"] = (0 if args.zero_skip else _abi.FLAG_NO_ZERO_SKIP) | (_abi.FLAG_FWD_STATS if args.stats else 0)
     t_setup = time.perf_counter()
-    prob = TvamProblem(cfg, device=dev)
+    if args.emulate:
+        er, ew = (int(v) for v in args.emulate.split("/"))
+        prob = TvamProblem(cfg, device=dev, rank=er, world_size=ew)
+        rank = er
+    else:
+        prob = TvamProblem(cfg, device=dev)
     g = torch.Generator().manual_seed(0)
     full = torch.rand(prob.n_global, generator=g) * 0.1
     prob.x0 = prob.local_from_global(full)
@@ -178,6 +186,12 @@ def main():
     log(f"[rank {rank}] {args.steps} iterations in {elapsed:.3f}s; fwd {fwd_avg * 1e3:.2f} ms, adj {adj_avg * 1e3:.2f} ms, "
         f"last loss {prob.loss_hist[-1]:.6e}")
 
+    if args.emulate:
+        print(json.dumps({"emulate": args.emulate, "shard": prob.shard, "ms_per_step": elapsed / args.steps * 1e3,
+                          "fwd_ms": fwd_avg * 1e3, "adj_ms": adj_avg * 1e3, "visits_per_pass": visits,
+                          "slices": [prob.z0, prob.z1], "rows": [prob.r0, prob.r1],
+                          "angles": [prob.a0, prob.a1]}), flush=True)
+        return
     if rank != 0:
         if dist:
             dist.barrier()

@@ -72,6 +72,7 @@ struct tvam_plan {
     float4* d_pl_rec_f = nullptr;
     int32_t* d_pl_rec_i = nullptr;
     float4* d_pl_rec_g = nullptr;
+    float* d_pl_part = nullptr;  // voxel-driven forward: partial doses of the angle parts
     unsigned* d_amax = nullptr;  // ray-driven forward: per-angle max |pattern|, fixed-point scale
     float* d_fscale = nullptr;
     int32_t planar_rz = 4;
@@ -143,6 +144,7 @@ static void plan_free(tvam_plan* p) {
     (void)hipFree(p->d_pl_rec_f);
     (void)hipFree(p->d_pl_rec_i);
     (void)hipFree(p->d_pl_rec_g);
+    (void)hipFree(p->d_pl_part);
     (void)hipFree(p->d_amax);
     (void)hipFree(p->d_occ);
     tvam_bin_scratch_free(p->bins);
@@ -304,9 +306,10 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
         rows.insert(rows.end(), rows_of[s].begin(), rows_of[s].end());
     }
     off[k.nz] = (int32_t)rows.size();
-    p->planar_fz = env_int("TVAM_PLANAR_FWD_Z", 32);
+    p->planar_fz = env_int("TVAM_PLANAR_FWD_Z", 0);  // 0: chosen from the slab depth (planar_fwd_setup)
     p->planar_az = env_int("TVAM_PLANAR_ADJ_Z", 4);
-    if (p->planar_fz != 8 && p->planar_fz != 16 && p->planar_fz != 32) p->planar_fz = 32;
+    if (p->planar_fz != 8 && p->planar_fz != 16 && p->planar_fz != 24 && p->planar_fz != 28 && p->planar_fz != 32)
+        p->planar_fz = 0;
     if (p->planar_az != 4 && p->planar_az != 8) p->planar_az = 4;
     const int ns = (int)cs.size();
     int32_t mrc = 0;
@@ -328,6 +331,15 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     if (p->planar_fwd && !planar_fwd_setup(p, cs, off)) p->planar_fwd = false;
     if (tvam_planar_adj_lds(p->pl, p->tiles, p->planar_az) > 160 * 1024) p->planar_az = 4;
     if (tvam_planar_adj_lds(p->pl, p->tiles, p->planar_az) > 160 * 1024) return 0;  // tile too large: general path
+    {
+        // a thin slab (z-slab sharding) leaves few (tile, chunk) workgroups for 256
+        // CUs: split each tile's ray list over up to 8 workgroups (>= ~4096 in all)
+        const int64_t nwg = (int64_t)p->tiles.ntx * p->tiles.nty * ((k.nz + p->planar_az - 1) / p->planar_az);
+        int split = (int)std::min<int64_t>(8, std::max<int64_t>(1, (4096 + nwg - 1) / std::max<int64_t>(nwg, 1)));
+        const int es = env_int("TVAM_ADJ_SPLIT", 0);
+        if (es >= 1 && es <= 64) split = es;
+        p->pl.adj_split = split;
+    }
     if (tvam_planar_rayfwd_lds(p->pl, p->tiles, p->planar_rz) > 160 * 1024) p->planar_rz = 4;
     if (tvam_planar_rayfwd_lds(p->pl, p->tiles, p->planar_rz) > 160 * 1024) return 0;
     int rc;
@@ -341,6 +353,25 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     }
     p->fwd_ang_h.clear();
     p->fwd_cb_h.clear();
+    p->pl.fwd_parts = 1;
+    if (p->planar_fwd) {
+        // A thin slab leaves few (16x16 tile, slice chunk) workgroups, each running
+        // every angle: at 3 resident workgroups per CU, 1250 of them (400^2 film,
+        // 50 slices) fill 1.6 rounds of the 768 slots.  Split the angles into parts
+        // until >= 4 rounds; the partial doses are summed in fixed order.
+        const int64_t nwg = (int64_t)((k.res[0] + 15) / 16) * ((k.res[1] + 15) / 16) *
+                            ((k.nz + p->planar_fz - 1) / p->planar_fz);
+        int parts = (int)std::min<int64_t>(4, std::max<int64_t>(1, (4 * 768 + nwg - 1) / std::max<int64_t>(nwg, 1)));
+        const int ep = env_int("TVAM_FWD_PARTS", 0);
+        if (ep >= 1 && ep <= 16) parts = ep;
+        parts = std::max(1, std::min(parts, ns));
+        if (parts > 1) {
+            const size_t bytes = (size_t)parts * k.nz * k.res[0] * k.res[1] * sizeof(float);
+            if ((e = hipMalloc((void**)&p->d_pl_part, bytes)) != hipSuccess) return hip_fail(e, "hipMalloc (forward parts)");
+            p->pl.fwd_part = p->d_pl_part;
+        }
+        p->pl.fwd_parts = parts;
+    }
     if ((e = hipMalloc((void**)&p->d_pl_vox, nrec * sizeof(float4))) != hipSuccess ||
         (e = hipMalloc((void**)&p->d_pl_rec_f, nrec * sizeof(float4))) != hipSuccess ||
         (e = hipMalloc((void**)&p->d_pl_rec_i, nrec * sizeof(int32_t))) != hipSuccess ||
@@ -418,6 +449,18 @@ static bool planar_fwd_setup(tvam_plan* p, const std::vector<float2>& cs, const 
         bool multi = false;
         for (int z = 0; z < k.nz; ++z) multi |= off[z + 1] - off[z] > 1;
         p->pl.fwd_multi = multi ? 1 : 0;
+    }
+    if (p->planar_fz == 0) {
+        // slices per workgroup: the fewest padded slice-passes ceil(nz / Z) * (Z + 4)
+        // (the +4 prices the per-angle candidate geometry shared by the Z slices)
+        int best = 8;
+        int64_t bcost = INT64_MAX;
+        for (int Z : {32, 28, 24, 16, 8}) {
+            if (!tvam_planar_fwd_fits(p->pl, Z)) continue;
+            const int64_t cost = (int64_t)((k.nz + Z - 1) / Z) * (Z + 4);
+            if (cost < bcost) bcost = cost, best = Z;
+        }
+        p->planar_fz = best;
     }
     while (p->planar_fz > 8 && !tvam_planar_fwd_fits(p->pl, p->planar_fz)) p->planar_fz /= 2;
     p->pl.fwd_pf = (p->pl.ncmax * p->planar_fz + 255) / 256 <= 2 ? 2 : 4;

@@ -98,10 +98,10 @@ hipError_t tvam_launch_planar_rays(const TvamConsts& k, const TvamPlanar& pl, hi
 // the DDA forms, up to fp32 rounding of the crossing times.
 // ---------------------------------------------------------------------------
 #define TVAM_PF 4     // most staged pattern values per thread and angle (host: ncmax * Z <= TVAM_PF * TVAM_PB)
+// slab row stride (words) of Z slices: an odd number of 16-byte groups, so 16
+// consecutive columns' ds_read_b128 hit 16 different bank groups
+__host__ __device__ constexpr int tvam_fwd_zs(int Z) { return ((Z + 4) / 4) % 2 ? Z + 4 : Z + 8; }
 #define TVAM_ACH 256  // angles per LDS chunk of per-angle constants
-#ifndef TVAM_FWD_DEPTH
-#define TVAM_FWD_DEPTH 1  // angles of global-load look-ahead in the forward
-#endif
 
 // Z: slices per thread; NC: candidate DMD columns per (voxel, angle), a
 // bound the plan derives from the voxel's lateral width in columns; MULTI:
@@ -112,9 +112,8 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
                                                                   float* __restrict__ dose) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int ncm = pl.ncmax;
-    // [2][ncm][Z + 4] (double buffer); the +4 pad puts 16 consecutive columns'
-    // 16-byte reads in 16 different bank groups
-    constexpr int ZS = Z + 4;
+    // [2][ncm][ZS] (double buffer), ZS = tvam_fwd_zs(Z)
+    constexpr int ZS = tvam_fwd_zs(Z);
     float* s_p = reinterpret_cast<float*>(smem);
     float4* s_r = reinterpret_cast<float4*>(s_p + 2 * ncm * ZS);  // [2][ncm]
     // per-angle constants of TVAM_ACH (+2 look-ahead) angles, copied to LDS so the
@@ -125,7 +124,8 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
     int* s_row = s_cb + (TVAM_ACH + 2);                            // [Z]: the slice's row, -1 none, -2 several
 
     const int ntx = (k.res[0] + 15) >> 4, nty = (k.res[1] + 15) >> 4;
-    const int ntiles = ntx * nty, nwg = ntiles * ((k.nz + Z - 1) / Z);
+    const int ntiles = ntx * nty, nwg1 = ntiles * ((k.nz + Z - 1) / Z);
+    const int parts = pl.fwd_parts > 1 ? pl.fwd_parts : 1, nwg = nwg1 * parts;
     // XCD-aware order: workgroup b runs on XCD b % 8; give each XCD a contiguous
     // run of (z-chunk, tile) pairs so the tiles sharing a z-chunk's pattern rows
     // share that XCD's L2
@@ -135,6 +135,11 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
         L = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
     }
     if (L >= nwg) return;
+    // angle part [ab, ae) of this workgroup (thin slabs: parts > 1 workgroups per
+    // (tile, chunk), partial doses summed in fixed order by tvam_fwd_parts_kernel)
+    const int part = L / nwg1;
+    L -= part * nwg1;
+    const int ab = (int)(((int64_t)pl.ns * part) / parts), ae = (int)(((int64_t)pl.ns * (part + 1)) / parts);
     const int tile = L % ntiles;
     const int bx = tile % ntx, by = tile / ntx;
     const int ix = bx * 16 + (threadIdx.x & 15), iy = by * 16 + (threadIdx.x >> 4);
@@ -157,7 +162,7 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
         s_row[threadIdx.x] = r;
     }
     const int ns = pl.ns;
-    int tbase = 0;
+    int tbase = ab;
     auto load_table = [&](int base) {
         for (int i = threadIdx.x; i < TVAM_ACH + 2; i += TVAM_PB) {
             const int a = base + i;
@@ -168,7 +173,7 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
             }
         }
     };
-    load_table(0);
+    load_table(ab);
     __syncthreads();
 
     // This thread's staging slots i = tid + q * 256 of the [Z][ncm] slab are
@@ -277,62 +282,48 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
         }
     };
 
-#if TVAM_FWD_DEPTH == 2
-    // Software pipeline over angles: angle a is computed from LDS buffer a & 1
-    // while the loads of angle a + 1 (issued one step earlier) and a + 2 are in
-    // flight in the register stages SB / SA.
-    Stage SA, SB;
-    fetch(0, SA);
-    store(0, SA);
-    if (ns > 1) fetch(1, SB);
-    __syncthreads();
-    for (int al = 0; al < ns; al += 2) {
-        if (al > 0 && (al & (TVAM_ACH - 1)) == 0) {  // next chunk of per-angle constants
-            tbase = al;
-            load_table(al);
-            __syncthreads();
-        }
-        if (al + 2 < ns) fetch(al + 2, SA);
-        compute(al, 0);
-        if (al + 1 < ns) store(1, SB);
-        __syncthreads();
-        if (al + 1 >= ns) break;
-        if (al + 3 < ns) fetch(al + 3, SB);
-        compute(al + 1, 1);
-        if (al + 2 < ns) store(0, SA);
-        __syncthreads();
-    }
-#else
     // Software pipeline over angles: angle a is computed from LDS buffer a & 1
     // while the loads of angle a + 1 are in flight in registers.
-    Stage S;
-    fetch(0, S);
-    store(0, S);
-    __syncthreads();
-    for (int al = 0; al < ns; ++al) {
-        if (al > 0 && (al & (TVAM_ACH - 1)) == 0) {  // next chunk of per-angle constants
-            tbase = al;
-            load_table(al);
+    if (ab < ae) {
+        Stage S;
+        fetch(ab, S);
+        store(0, S);
+        __syncthreads();
+        for (int al = ab; al < ae; ++al) {
+            if (al - tbase == TVAM_ACH) {  // next chunk of per-angle constants
+                tbase = al;
+                load_table(al);
+                __syncthreads();
+            }
+            if (al + 1 < ae) fetch(al + 1, S);
+            compute(al, (al - ab) & 1);
+            if (al + 1 < ae) store((al + 1 - ab) & 1, S);
             __syncthreads();
         }
-        if (al + 1 < ns) fetch(al + 1, S);
-        compute(al, al & 1);
-        if (al + 1 < ns) store((al + 1) & 1, S);
-        __syncthreads();
     }
-#endif
 
     if (ix < k.res[0] && iy < k.res[1]) {
         const float scale = k.wscale * k.inv_vol;  // Le * weight (common.py:108-111) / voxel volume (volume.py:41-42)
         const size_t plane = (size_t)k.res[0] * k.res[1];
+        float* out = parts > 1 ? pl.fwd_part + (size_t)part * k.nz * plane : dose;
 #pragma unroll
         for (int z = 0; z < Z; ++z)
-            if (z0 + z < k.nz) dose[(size_t)(z0 + z) * plane + (size_t)iy * k.res[0] + ix] = acc[z] * scale;
+            if (z0 + z < k.nz) out[(size_t)(z0 + z) * plane + (size_t)iy * k.res[0] + ix] = acc[z] * scale;
+    }
+}
+
+// dose = sum of the angle parts' partial doses, in part order (deterministic)
+__global__ __launch_bounds__(256) void tvam_fwd_parts_kernel(int64_t n, int parts, const float* __restrict__ part,
+                                                             float* __restrict__ dose) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        float v = part[i];
+        for (int q = 1; q < parts; ++q) v += part[(size_t)q * n + i];
+        dose[i] = v;
     }
 }
 
 size_t tvam_planar_fwd_lds(const TvamPlanar& pl, int Z) {
-    return 2 * ((size_t)pl.ncmax * (Z + 4) * sizeof(float) + (size_t)pl.ncmax * sizeof(float4)) +
+    return 2 * ((size_t)pl.ncmax * tvam_fwd_zs(Z) * sizeof(float) + (size_t)pl.ncmax * sizeof(float4)) +
            (size_t)(TVAM_ACH + 2) * (2 * sizeof(float4) + sizeof(int)) + (size_t)Z * sizeof(int);
 }
 
@@ -365,15 +356,32 @@ static hipError_t launch_fwd_z(dim3 grid, size_t lds, hipStream_t stream, const 
     return hipGetLastError();
 }
 
+static hipError_t tvam_launch_fwd_planar_z(dim3 grid, size_t lds, hipStream_t stream, const TvamConsts& k,
+                                           const TvamPlanar& pl, int Z, const float* pat, float* dose);
+
 hipError_t tvam_launch_fwd_planar(const TvamConsts& k, const TvamPlanar& pl, int Z, const float* pat, float* dose,
                                   hipStream_t stream) {
     const int ntx = (k.res[0] + 15) / 16, nty = (k.res[1] + 15) / 16;
-    const unsigned nwg = (unsigned)(ntx * nty) * (unsigned)((k.nz + Z - 1) / Z);
+    const int parts = pl.fwd_parts > 1 ? pl.fwd_parts : 1;
+    if (parts > 1 && !pl.fwd_part) return hipErrorInvalidValue;
+    const unsigned nwg = (unsigned)(ntx * nty) * (unsigned)((k.nz + Z - 1) / Z) * (unsigned)parts;
     dim3 grid(pl.xcd_remap ? (nwg + 7) / 8 * 8 : nwg);
     const size_t lds = tvam_planar_fwd_lds(pl, Z);
+    hipError_t e = tvam_launch_fwd_planar_z(grid, lds, stream, k, pl, Z, pat, dose);
+    if (e != hipSuccess || parts == 1) return e;
+    const int64_t n = (int64_t)k.nz * k.res[0] * k.res[1];
+    const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
+    hipLaunchKernelGGL(tvam_fwd_parts_kernel, dim3(g), dim3(256), 0, stream, n, parts, pl.fwd_part, dose);
+    return hipGetLastError();
+}
+
+static hipError_t tvam_launch_fwd_planar_z(dim3 grid, size_t lds, hipStream_t stream, const TvamConsts& k,
+                                           const TvamPlanar& pl, int Z, const float* pat, float* dose) {
     switch (Z) {
         case 8: return launch_fwd_z<8>(grid, lds, stream, k, pl, pat, dose);
         case 16: return launch_fwd_z<16>(grid, lds, stream, k, pl, pat, dose);
+        case 24: return launch_fwd_z<24>(grid, lds, stream, k, pl, pat, dose);
+        case 28: return launch_fwd_z<28>(grid, lds, stream, k, pl, pat, dose);
         case 32: return launch_fwd_z<32>(grid, lds, stream, k, pl, pat, dose);
         default: return hipErrorInvalidValue;
     }
@@ -426,9 +434,13 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_adj_planar_kernel(TvamConsts k, 
     __syncthreads();
     if (s_roff[Z] == 0) return;  // no DMD row lies in these slices
 
+    // this workgroup's part of the tile's ray list (a thin slab has few slice
+    // chunks: several workgroups then share one tile's rays, each ray once)
     const uint32_t* slots = tp.slots + tp.slot_off[tile_id];
-    const int nrt = (int)(tp.slot_off[tile_id + 1] - tp.slot_off[tile_id]);
-    for (int g = threadIdx.x; g < nrt; g += TVAM_PB) {
+    const int nall = (int)(tp.slot_off[tile_id + 1] - tp.slot_off[tile_id]);
+    const int gb = (int)(((int64_t)nall * blockIdx.z) / gridDim.z);
+    const int nrt = (int)(((int64_t)nall * (blockIdx.z + 1)) / gridDim.z);
+    for (int g = gb + (int)threadIdx.x; g < nrt; g += TVAM_PB) {
         const uint32_t e = slots[g];
         const int al = (int)(e >> 16), colc = (int)(e & 0xffffu);
         const int ri = pl.rec_i[(size_t)al * k.crop_x + colc];
@@ -512,7 +524,7 @@ size_t tvam_planar_adj_lds(const TvamPlanar& pl, const TvamTiles& t, int Z) {
 
 hipError_t tvam_launch_adj_planar(const TvamConsts& k, const TvamPlanar& pl, const TvamTiles& t, int Z,
                                   const int32_t* idxmap, const float* gin, float* out, hipStream_t stream) {
-    dim3 grid((unsigned)(t.ntx * t.nty), (unsigned)((k.nz + Z - 1) / Z));
+    dim3 grid((unsigned)(t.ntx * t.nty), (unsigned)((k.nz + Z - 1) / Z), (unsigned)std::max(pl.adj_split, 1));
     const size_t lds = tvam_planar_adj_lds(pl, t, Z);
     switch (Z) {
         case 4:
