@@ -34,7 +34,7 @@ from .integrators import VolumeIntegrator
 from .lbfgs import FusedLinearLBFGS, LinearLBFGS
 from .loss import losses, ThresholdedLoss
 from .scene import load_dict
-from .utils import discretize, analytic_target, mesh_bbox, target_transform, save_vol
+from .utils import discretize, analytic_target, mesh_bbox, target_transform, save_vol, save_img
 
 
 def load_scene(config):
@@ -307,6 +307,7 @@ class TvamProblem(ShardedLoop):
             self.a0, self.a1 = angle_shard(A, self.rank, self.world)
             self.z0, self.z1, self.r0, self.r1 = 0, self.res_z, 0, self.crop_y
             shard_props = {'angle_range': (self.a0, self.a1)}
+        self.base_props = dict(base)
         iprops = base | shard_props
         self.integrator = VolumeIntegrator(iprops)
         self.final_integrator = VolumeIntegrator(iprops | {'max_depth': config.get('max_depth_ref', 16),
@@ -444,10 +445,19 @@ def optimize(config, patterns_fwd=None, device=None):
     output = config.get('output', '.')
     os.makedirs(output, exist_ok=True)
     if prob.rank == 0:
-        np.save(os.path.join(output, "target.npy"), prob.target_full.cpu().numpy())
+        tgt = prob.target_full.cpu().numpy()
+        save_vol(tgt, os.path.join(output, "target.exr"))
+        np.save(os.path.join(output, "target.npy"), tgt)
+    p = prob.scene.projector
     if patterns_fwd is not None:
         print("Using provided patterns for forward mode.")
-        prob.x0 = prob.local_from_global(np.asarray(patterns_fwd, dtype=np.float32).reshape(-1))
+        pf = np.asarray(patterns_fwd, dtype=np.float32)
+        if pf.ndim == 3 and tuple(pf.shape[1:]) == (p.res[1], p.res[0]) and tuple(p.crop) != tuple(p.res):
+            ox, oy = p.crop_offset  # full-DMD patterns (patterns.npz): keep the crop
+            pf = pf[:, oy:oy + p.crop[1], ox:ox + p.crop[0]]
+        prob.x0 = prob.local_from_global(pf.reshape(-1))
+    elif "psf_analysis" in config:
+        return psf_analysis(prob, config, output)
     else:
         print("Optimizing patterns...")
         for i in range(prob.n_steps):
@@ -460,20 +470,73 @@ def optimize(config, patterns_fwd=None, device=None):
                 break
     print("Rendering final state...")
     vol_final = prob.final_render()
-    if prob.rank == 0:
-        np.save(os.path.join(output, "final.npy"), vol_final.cpu().numpy())
-        np.save(os.path.join(output, "loss.npy"), np.asarray(prob.loss_hist))
-        np.save(os.path.join(output, "timing.npy"), np.asarray(prob.timing))
     pats = prob.gather_patterns(prob.patterns_local().float())
     if prob.rank == 0:
-        p = prob.scene.projector
-        full = pats.cpu().numpy().reshape(-1, p.crop[1], p.crop[0])
-        np.savez_compressed(os.path.join(output, "patterns.npz"), patterns=full)
-        mx = float(full.max()) if full.size else 0.0
-        if mx > 0:
-            np.savez_compressed(os.path.join(output, "patterns_normalized_uint8.npz"),
-                                patterns=(full / mx * 255).astype(np.uint8))
+        crop = pats.cpu().numpy().reshape(-1, p.crop[1], p.crop[0])
+        _save_outputs(output, prob, vol_final, full_dmd(p, crop))
     return vol_final
+
+
+def full_dmd(p, crop):
+    """The full DMD stack [n, res_y, res_x] of crop-order patterns (projector.patterns(),
+    projector.py:125-129: zeros outside the crop)."""
+    full = np.zeros((crop.shape[0], p.res[1], p.res[0]), dtype=np.float32)
+    ox, oy = p.crop_offset
+    full[:, oy:oy + p.crop[1], ox:ox + p.crop[0]] = crop
+    return full
+
+
+def _save_outputs(output, prob, vol_final, full):
+    """final.npy / final.exr, loss / timing, patterns/NNNN.exr and patterns(.npz, _normalized_uint8.npz)
+    (optimize.py:330-353)."""
+    vf = vol_final.cpu().numpy()
+    np.save(os.path.join(output, "final.npy"), vf)
+    save_vol(vf, os.path.join(output, "final.exr"))
+    np.save(os.path.join(output, "loss.npy"), np.asarray(prob.loss_hist))
+    np.save(os.path.join(output, "timing.npy"), np.asarray(prob.timing))
+    print("Saving images...")
+    os.makedirs(os.path.join(output, "patterns"), exist_ok=True)
+    for i in range(full.shape[0]):
+        save_img(full[i], os.path.join(output, "patterns", f"{i:04d}.exr"))
+    np.savez_compressed(os.path.join(output, "patterns.npz"), patterns=full)
+    mx = float(full.max()) if full.size else 0.0
+    if mx > 0:
+        np.savez_compressed(os.path.join(output, "patterns_normalized_uint8.npz"),
+                            patterns=(full / mx * 255).astype(np.uint8))
+        print("Pattern efficiency {:.4f}".format(float(np.sum(full / mx / full.size))))
+
+
+def psf_analysis(prob, config, output):
+    """Dose of single DMD pixels (optimize.py:245-283): the active set is the listed pixels
+    (index_pattern, y, x) on the full DMD with their intensities; one render with the
+    reference integrator settings on the final sensor."""
+    p = prob.scene.projector
+    xres, yres = config["projector"]["resx"], config["projector"]["resy"]
+    entries = config["psf_analysis"]
+    print("\nPSF analysis enabled.")
+    print("Number of traced pixels:", len(entries))
+    pix = np.zeros(len(entries), dtype=np.int64)
+    data = np.ones(len(entries), dtype=np.float32)
+    for i, e in enumerate(entries):
+        assert e["x"] < xres, "Invalid entry in psf_analysis: x out of bounds. Please check the configuration file."
+        assert e["y"] < yres, "Invalid entry in psf_analysis: y out of bounds. Please check the configuration file."
+        assert e["index_pattern"] < config["projector"]["n_patterns"], \
+            "Invalid entry in psf_analysis: index_pattern out of bounds. Please check the configuration file."
+        pix[i] = xres * yres * e["index_pattern"] + xres * e["y"] + e["x"]
+        data[i] *= e["intensity"]
+    if prob.world > 1:
+        raise NotImplementedError("psf_analysis runs on one rank")
+    integ = VolumeIntegrator(prob.base_props | {'max_depth': config.get('max_depth_ref', 16),
+                                                'rr_depth': config.get('rr_depth_ref', 8)})
+    proj = integ.projection(prob.scene, prob.final_sensor)
+    dev = prob.device
+    print("Rendering final state...")
+    vol = proj.forward(torch.as_tensor(data, device=dev), torch.as_tensor(pix.astype(np.int32), device=dev),
+                       prob.spp_ref, 0)
+    full = np.zeros((p.n_patterns, yres, xres), dtype=np.float32)
+    full.reshape(-1)[pix] = data
+    _save_outputs(output, prob, vol, full)
+    return vol
 
 
 class OverrideAction(argparse.Action):

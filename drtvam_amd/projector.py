@@ -23,7 +23,7 @@ def default_device() -> torch.device:
 
 
 def load_patterns(filepath):
-    """.npy / .npz pattern stacks (projector.py:8-39).  EXR directories need Mitsuba's Bitmap and are not supported."""
+    """.npy / .npz pattern stacks or a directory of EXR images (projector.py:8-39)."""
     if os.path.isfile(filepath):
         if filepath.endswith(".npy"):
             patterns = np.load(filepath)
@@ -37,7 +37,24 @@ def load_patterns(filepath):
         if len(patterns.shape) != 3:
             raise ValueError(f"Patterns must be 3D, but got a tensor of shape {patterns.shape}.")
         return np.ascontiguousarray(patterns, dtype=np.float32)
-    raise ValueError("No patterns found in the specified path. EXR pattern directories are not supported; use .npy/.npz.")
+    import glob
+    from .exr import read_exr
+    filenames = glob.glob(os.path.join(filepath, "*.exr"))
+    if len(filenames) == 0:
+        raise ValueError("No patterns found in the specified directory. Please make sure the patterns are in EXR format.")
+    imgs = None
+    for i, fn in enumerate(sorted(filenames)):
+        img = read_exr(fn)
+        if i == 0:
+            h, w, _ = img.shape
+            imgs = np.empty((len(filenames), h, w), dtype=np.float32)
+        elif img.shape[:2] != (h, w):
+            raise ValueError(f"File '{fn}' has a different resolution ({img.shape[0]}x{img.shape[1]}) than the previous "
+                             f"files ({h}x{w}). All patterns are expected to have the same resolution.")
+        # mi.TensorXf(Bitmap).array scattered over h*w entries: the first h*w values of the
+        # interleaved [h, w, c] image (projector.py:34-35)
+        imgs[i] = img.reshape(-1)[:h * w].reshape(h, w)
+    return imgs
 
 
 class TVAMProjector:

@@ -213,8 +213,37 @@ def analytic_target(res, bbox_min, bbox_max, kind='box_hole'):
     return torch.from_numpy(occ.astype(np.float32)[..., None])
 
 
+def reshape_grid(array):
+    """Tiles a stack [n, h, w(, c)] into one square mosaic [rows*h, rows*w, c] (utils.py:13-27)."""
+    if len(array.shape) == 3:
+        n, h, w = array.shape
+        c = 1
+    elif len(array.shape) == 4:
+        n, h, w, c = array.shape
+    else:
+        raise ValueError(f"Invalid array shape: {array.shape}")
+    rows = int(np.ceil(np.sqrt(n)))
+    array_new = np.zeros((rows ** 2, h, w, c))
+    array_new[:n] = np.asarray(array).reshape(n, h, w, c)
+    return array_new.reshape((rows, rows, h, w, c)).swapaxes(1, 2).reshape((rows * h, rows * w, c))
+
+
+def save_img(img, path):
+    """One image [h, w] or [h, w, c] as an EXR (utils.py:29-37, Bitmap.write)."""
+    from .exr import write_exr
+    if isinstance(img, torch.Tensor):
+        img = img.detach().cpu().numpy()
+    img = np.asarray(img, dtype=np.float32)
+    if img.ndim not in (2, 3):
+        raise ValueError("Invalid image shape")
+    write_exr(path, img)
+
+
 def save_vol(vol, path):
-    """Saves the volume as .npy (EXR output needs Mitsuba's Bitmap and is not provided)."""
+    """A volume [Z, Y, X(, C)] as an EXR mosaic of its slices (utils.py:39-46)."""
+    from .exr import write_exr
     if isinstance(vol, torch.Tensor):
         vol = vol.detach().cpu().numpy()
-    np.save(os.path.splitext(path)[0] + '.npy', vol)
+    elif not isinstance(vol, np.ndarray):
+        raise ValueError(f"Invalid volume type: '{type(vol)}'")
+    write_exr(path, reshape_grid(vol).astype(np.float32))

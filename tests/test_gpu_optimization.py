@@ -96,3 +96,29 @@ def test_box_hole_occlusion_optimization(tmp_path):
     correct = np.mean(np.isclose(ref, vol > th)) * 100
     print("percentage correct", correct)
     assert correct > 97.0
+
+
+def test_psf_analysis_matches_oracle(tmp_path):
+    """psf_analysis (optimize.py:245-283): the dose of the listed DMD pixels (full-DMD indices,
+    intensities) rendered with spp_ref jittered rays on the final sensor, vs the oracle."""
+    from oracle import oracle
+    from drtvam_amd.integrators import VolumeIntegrator
+    from drtvam_amd.optimize import TvamProblem
+    cfg = copy.deepcopy(BOX_HOLE_INDEX_MATCHED)
+    cfg["target"]["filename"] = os.path.join(GOLDEN, "box_hole.ply")
+    cfg["output"] = str(tmp_path)
+    cfg["spp_ref"] = 3
+    cfg["psf_analysis"] = [{"index_pattern": 0, "x": 100, "y": 10, "intensity": 2.0},
+                           {"index_pattern": 57, "x": 80, "y": 3, "intensity": 0.5},
+                           {"index_pattern": 199, "x": 120, "y": 15, "intensity": 1.0}]
+    vol = optimize(cfg, device="cuda:0").cpu().numpy()[..., 0]
+    prob = TvamProblem(copy.deepcopy(cfg), device="cuda:0")
+    desc = VolumeIntegrator(prob.base_props | {"max_depth": 16, "rr_depth": 8}).desc(prob.scene, prob.final_sensor)
+    pix = np.array([200 * 20 * e["index_pattern"] + 200 * e["y"] + e["x"] for e in cfg["psf_analysis"]], np.uint32)
+    data = np.array([e["intensity"] for e in cfg["psf_analysis"]], np.float32)
+    ref, _ = oracle.forward(desc, data, active_pixels=pix, spp=3, seed=0, nthreads=8)
+    assert np.abs(ref).max() > 0
+    assert np.linalg.norm(vol - ref) / np.linalg.norm(ref) < 1e-4
+    pats = np.load(tmp_path / "patterns.npz")["patterns"]
+    assert pats.shape == (200, 20, 200) and pats[57, 3, 80] == np.float32(0.5)
+    assert (tmp_path / "final.exr").exists() and (tmp_path / "patterns" / "0199.exr").exists()
