@@ -12,7 +12,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libtvam.so")
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 
 TVAM_OK = 0
 TVAM_ERR_INVALID = -1
@@ -81,14 +81,25 @@ class TvamDesc(ctypes.Structure):
         ("phase_g", ctypes.c_float),
         ("occluder_tris", ctypes.c_void_p),
         ("n_occluder_tris", ctypes.c_int32),
+        ("target_tris", ctypes.c_void_p),
+        ("n_target_tris", ctypes.c_int32),
     ]
 
     def copy(self) -> "TvamDesc":
         d = TvamDesc()
         ctypes.pointer(d)[0] = self
-        if hasattr(self, "_occluders"):  # keep the occluder triangle array alive with the copy
-            d._occluders = self._occluders
+        for keep in ("_occluders", "_targets"):  # keep the triangle arrays alive with the copy
+            if hasattr(self, keep):
+                setattr(d, keep, getattr(self, keep))
         return d
+
+    def set_target(self, tris) -> None:
+        """Target mesh triangles [n][3][3] (float32, host, world space) for surface-aware films."""
+        import numpy as np
+        t = np.ascontiguousarray(tris, dtype=np.float32).reshape(-1, 3, 3)
+        self._targets = t
+        self.target_tris = t.ctypes.data if t.size else None
+        self.n_target_tris = int(t.shape[0])
 
     def set_occluders(self, tris) -> None:
         """Occluder triangles [n][3][3] (float32, host); the desc keeps the array alive."""
@@ -121,6 +132,8 @@ EXPORTS = {
     "tvam_axpy_clamp": (ctypes.c_int, [ctypes.c_uint64, _P, ctypes.c_float, _P, ctypes.c_float, _P, _P]),
     "tvam_row_slices": (ctypes.c_int, [ctypes.POINTER(TvamDesc), _P]),
     "tvam_plan_path": (ctypes.c_int, [_P]),
+    "tvam_compute_volume": (ctypes.c_int, [_P, ctypes.c_uint32, _P, _P]),
+    "tvam_plan_set_volumes": (ctypes.c_int, [_P, _P]),
     "tvam_radon": (ctypes.c_int, [_P, _P, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int32, _P, _P]),
     "tvam_count_visits": (ctypes.c_int, [_P, ctypes.c_uint32, ctypes.c_uint32, ctypes.POINTER(ctypes.c_uint64)]),
     "tvam_plan_stats": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),

@@ -47,6 +47,8 @@ struct TvamConsts {
     float vial_hz_int;   // square: half height of the inner cuboid (0.45 height, geometry.py:207)
     const float* occ;    // occluder triangles [n_occ][3][3] (device; geometry.py:55-72), nullptr if none
     int32_t n_occ;
+    const float* tgt;    // surface-aware films: target mesh triangles [n_tgt][3][3] (device), else nullptr
+    int32_t n_tgt;
     float eta_ext, eta_int;     // cylindrical: int/ext IOR of the outer (glass/air) and inner (medium/glass) surface
     // medium / weights
     float sig_t, sig_s;  // scattering media: sigma_t, sigma_s = albedo * sigma_t (fp32, Mitsuba homogeneous)

@@ -119,6 +119,17 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
                                hipStream_t stream);
 void tvam_bin_scratch_free(TvamBinScratch& s);
 
+// Surface-aware films (film_channels 2): every path's medium segment cut at the
+// target mesh, channel 0 inside / 1 outside, global atomics / gathers; vols =
+// the per-(voxel, channel) volumes (tvam_scatter.hip).  The forward adds the
+// unscaled film (caller zeroes `out`) and tvam_launch_scale_volumes divides it.
+hipError_t tvam_launch_surface_paths(int mode, const TvamConsts& k, const TvamTiles& t, const float* pat,
+                                     const int32_t* idxmap, const float* gin, const float* vols, float* out,
+                                     unsigned long long* counter, hipStream_t stream);
+hipError_t tvam_launch_scale_volumes(int64_t n, const float* vols, float* dose, hipStream_t stream);
+// compute_volume (sensor.py:47-110): volumes [res z][y][x][2]
+hipError_t tvam_launch_volumes(const TvamConsts& k, uint32_t sample_count, float* volumes, hipStream_t stream);
+
 // Radon filter image of the shard's DMD pixels (tvam_radon.hip).
 hipError_t tvam_launch_radon(const TvamConsts& k, const TvamTiles& t, const float* tgt, int ntgt, int max_depth,
                              float wray, float* radon, hipStream_t stream);

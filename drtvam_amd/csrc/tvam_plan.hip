@@ -41,6 +41,9 @@ struct tvam_plan {
     int32_t max_rows_per_slice;
     bool empty;  // max_depth too small for any ray to reach the medium
     bool cyl;    // refracting (cylindrical / square) vial: per-ray directions and weights
+    bool surface = false;    // surface-aware film (2 channels): per-path kernels cut at the target mesh
+    float* d_tgt = nullptr;  // target mesh triangles (surface-aware films)
+    const float* vols = nullptr;  // caller's compute_volume() output (tvam_plan_set_volumes)
     float* d_occ = nullptr;  // occluder triangles
     // device tables
     float2* d_cs = nullptr;
@@ -147,6 +150,7 @@ static void plan_free(tvam_plan* p) {
     (void)hipFree(p->d_pl_part);
     (void)hipFree(p->d_amax);
     (void)hipFree(p->d_occ);
+    (void)hipFree(p->d_tgt);
     tvam_bin_scratch_free(p->bins);
     (void)hipFree(p->d_fscale);
     delete p;
@@ -171,7 +175,15 @@ static int validate(const tvam_desc& d) {
         return fail(TVAM_ERR_UNSUPPORTED, "only the 'index_matched', 'cylindrical' and 'square' containers are implemented on the GPU path");
     if (d.n_occluder_tris < 0 || (d.n_occluder_tris > 0 && !d.occluder_tris))
         return fail(TVAM_ERR_INVALID, "occluder_tris is null");
-    if (d.film_channels != 1) return fail(TVAM_ERR_UNSUPPORTED, "surface-aware films (2 channels) are not implemented");
+    if (d.film_channels != 1 && d.film_channels != 2) return fail(TVAM_ERR_INVALID, "film_channels must be 1 or 2");
+    if (d.film_channels == 2) {
+        if (d.n_target_tris <= 0 || !d.target_tris)
+            return fail(TVAM_ERR_INVALID, "No target shape found in the scene");  // sensor.py:60-61
+        if (d.albedo != 0.0f)
+            return fail(TVAM_ERR_UNSUPPORTED, "surface-aware films are implemented for non-scattering media");
+        if (d.slab_begin != 0 || (d.slab_end >= 0 && d.slab_end != d.film_res[2]))
+            return fail(TVAM_ERR_UNSUPPORTED, "surface-aware films cannot be split into slabs");
+    }
     if (!(d.albedo >= 0.0f && d.albedo <= 1.0f)) return fail(TVAM_ERR_INVALID, "medium albedo must lie in [0, 1]");
     if (d.albedo != 0.0f) {
         if (!(d.sigma_t > 0.0f)) return fail(TVAM_ERR_INVALID, "scattering medium: extinction must be positive");
@@ -675,6 +687,16 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
     // index matched: entry bounce + medium segment; glass vials: two glass
     // surfaces + medium segment (volume.py:179, :271-272)
     p->empty = d.max_depth < (p->cyl ? 3 : 2);
+    p->surface = d.film_channels == 2;
+    if (p->surface) {  // target mesh to the device (TvamConsts::tgt)
+        std::vector<float> tri(d.target_tris, d.target_tris + 9 * (size_t)d.n_target_tris);
+        if ((rc = upload(&p->d_tgt, tri))) {
+            plan_free(p);
+            return rc;
+        }
+        p->k.tgt = p->d_tgt;
+        p->k.n_tgt = d.n_target_tris;
+    }
     if (d.n_occluder_tris > 0) {  // occluder triangles to the device (TvamConsts::occ)
         std::vector<float> tri(d.occluder_tris, d.occluder_tris + 9 * (size_t)d.n_occluder_tris);
         if ((rc = upload(&p->d_occ, tri))) {
@@ -845,7 +867,7 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
     p->tiles.tsx = tsx;
     p->tiles.tsy = tsy;
     p->tiles.n_shard = ns;
-    if ((rc = planar_setup(p, cs))) {
+    if (!p->surface && (rc = planar_setup(p, cs))) {
         plan_free(p);
         return rc;
     }
@@ -935,11 +957,13 @@ extern "C" int tvam_forward(tvam_plan* p, const float* active_data, const uint32
     int rc = call_setup(p, n_active, active_pixels, spp, k);
     if (rc) return rc;
     const TvamConsts& kc = k;
-    size_t V = (size_t)kc.res[0] * kc.res[1] * kc.nz;
+    size_t V = (size_t)kc.res[0] * kc.res[1] * kc.nz * (p->surface ? 2 : 1);
     hipError_t e;
-    if (p->empty || n_active == 0) {
+    if (p->surface && !p->vols) return fail(TVAM_ERR_INVALID, "surface-aware film: call tvam_plan_set_volumes first");
+    if (p->empty || n_active == 0 || p->surface) {
         e = hipMemsetAsync(dose, 0, V * sizeof(float), stream);
-        return e == hipSuccess ? 0 : hip_fail(e, "hipMemsetAsync");
+        if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
+        if (p->empty || n_active == 0) return 0;
     }
     const float* pat = active_data;
     const int32_t* idxmap = nullptr;
@@ -953,6 +977,14 @@ extern "C" int tvam_forward(tvam_plan* p, const float* active_data, const uint32
             return hip_fail(e, "scatter launch");
         pat = p->d_dense;
         idxmap = p->d_idxmap;
+    }
+    if (p->surface) {
+        TvamTiles t = p->tiles;
+        t.spp = spp;
+        t.seed = seed;
+        e = tvam_launch_surface_paths(TVAM_MODE_FWD, kc, t, pat, idxmap, nullptr, p->vols, dose, nullptr, stream);
+        if (e == hipSuccess) e = tvam_launch_scale_volumes((int64_t)V, p->vols, dose, stream);
+        return e == hipSuccess ? 0 : hip_fail(e, "surface-aware forward launch");
     }
     if (p->planar_fwd) {
         if (p->desc.flags & TVAM_FLAG_FWD_STATS) {
@@ -1016,6 +1048,16 @@ extern "C" int tvam_adjoint(tvam_plan* p, const float* grad_dose, const uint32_t
     }
     if ((e = hipMemsetAsync(grad_active, 0, n_active * sizeof(float), stream)) != hipSuccess)
         return hip_fail(e, "hipMemsetAsync");
+    if (p->surface) {
+        if (!p->vols) return fail(TVAM_ERR_INVALID, "surface-aware film: call tvam_plan_set_volumes first");
+        if (p->empty) return 0;
+        TvamTiles t = p->tiles;
+        t.spp = spp;
+        t.seed = seed;
+        e = tvam_launch_surface_paths(TVAM_MODE_ADJ, k, t, nullptr, idxmap, grad_dose, p->vols, grad_active, nullptr,
+                                      stream);
+        return e == hipSuccess ? 0 : hip_fail(e, "surface-aware adjoint launch");
+    }
     if (p->planar) {
         e = tvam_launch_adj_planar(k, p->pl, p->tiles, p->planar_az, idxmap, grad_dose, grad_active, stream);
         if (e != hipSuccess) return hip_fail(e, "planar adjoint launch");
@@ -1056,9 +1098,14 @@ extern "C" int tvam_count_visits(tvam_plan* p, uint32_t spp, uint32_t seed, uint
     TvamTiles t = p->tiles;
     t.spp = spp;
     t.seed = seed;
-    if ((rc = ensure_rays(p, k, t, nullptr))) return rc;
-    e = tvam_launch_tiles(TVAM_MODE_COUNT, k, t, p->lds_bytes, nullptr, nullptr, nullptr, nullptr, p->d_counter,
-                          nullptr);
+    if (p->surface) {
+        e = tvam_launch_surface_paths(TVAM_MODE_COUNT, k, t, nullptr, nullptr, nullptr, nullptr, nullptr, p->d_counter,
+                                      nullptr);
+    } else {
+        if ((rc = ensure_rays(p, k, t, nullptr))) return rc;
+        e = tvam_launch_tiles(TVAM_MODE_COUNT, k, t, p->lds_bytes, nullptr, nullptr, nullptr, nullptr, p->d_counter,
+                              nullptr);
+    }
     if (e != hipSuccess) return hip_fail(e, "count launch");
     if (p->desc.albedo != 0.0f) {
         e = tvam_launch_scatter_paths(TVAM_MODE_COUNT, k, t, nullptr, nullptr, nullptr, nullptr, p->d_counter, nullptr);
@@ -1101,6 +1148,25 @@ extern "C" int tvam_radon(tvam_plan* p, const float* target_tris, int32_t n_targ
     if (e == hipSuccess) e = hipStreamSynchronize(stream);
     (void)hipFree(dt);
     return e == hipSuccess ? 0 : hip_fail(e, "radon launch");
+}
+
+extern "C" int tvam_compute_volume(tvam_plan* p, uint32_t sample_count, float* volumes, void* stream_) {
+    if (!p || !volumes) return fail(TVAM_ERR_INVALID, "null argument");
+    if (!p->surface) return fail(TVAM_ERR_INVALID, "compute_volume needs a surface-aware film (film_channels 2)");
+    if (sample_count == 0) return fail(TVAM_ERR_INVALID, "sample_count must be positive");
+    hipError_t e = hipSetDevice(p->device);
+    if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+    hipStream_t stream = (hipStream_t)stream_;
+    e = tvam_launch_volumes(p->k, sample_count, volumes, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "compute_volume launch");
+}
+
+extern "C" int tvam_plan_set_volumes(tvam_plan* p, const float* volumes) {
+    if (!p) return fail(TVAM_ERR_INVALID, "null argument");
+    if (!p->surface) return fail(TVAM_ERR_INVALID, "volumes apply to surface-aware films (film_channels 2)");
+    p->vols = volumes;
+    return 0;
 }
 
 // bit 0: planar adjoint (+ ray-driven planar forward unless bit 1), bit 1: voxel-driven planar forward

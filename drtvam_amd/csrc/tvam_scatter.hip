@@ -22,6 +22,9 @@
 // BSDF next_1d + next_2d on surfaces, phase next_1d + next_2d on scattering.
 #include "tvam_internal.h"
 
+#include <algorithm>
+#include <vector>
+
 namespace {
 
 __device__ __forceinline__ float sc_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
@@ -66,10 +69,10 @@ __device__ __forceinline__ float sc_container_hit(const TvamConsts& k, float ox,
 __device__ __forceinline__ void sc_phase(const TvamConsts& k, float dx, float dy, float dz, float u1, float u2,
                                          float& wx, float& wy, float& wz) {
     float lx, ly, lz;
-    if (k.phase_type == TVAM_PHASE_ISOTROPIC) {
-        const float z = 1.0f - 2.0f * u1;
+    if (k.phase_type == TVAM_PHASE_ISOTROPIC) {  // square_to_uniform_sphere(u): z = 1 - 2 u.y, phi = 2 pi u.x
+        const float z = 1.0f - 2.0f * u2;
         const float r = sqrtf(fmaxf(1.0f - z * z, 0.0f));
-        const float sp = sinf(TVAM_TWO_PI * u2), cp = cosf(TVAM_TWO_PI * u2);
+        const float sp = sinf(TVAM_TWO_PI * u1), cp = cosf(TVAM_TWO_PI * u1);
         wx = r * cp;
         wy = r * sp;
         wz = z;
@@ -402,7 +405,272 @@ __global__ __launch_bounds__(256) void tvam_scatter_kernel(TvamConsts k, TvamTil
     }
 }
 
+// ---------------------------------------------------------------------------
+// Surface-aware films (film.py:16-21, sensor.py:405-409, volume.py:175-218):
+// the target mesh stays in the scene with a null BSDF, so a path's medium
+// segment is cut at every target hit; each piece restarts its DDA from the
+// spawned origin (offset_p along the face normal), deposits into channel 0
+// while inside the target and 1 outside, and the attenuation picks up
+// e^{-st si.t} per piece (volume.py:263).  Non-scattering media; one thread
+// per (ray, sample); restated op for op in oracle or_trace_surface.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float sf_target_hit(const TvamConsts& k, float ox, float oy, float oz, float dx, float dy,
+                                               float dz, int& tri) {
+    float best = TVAM_INF;
+    tri = -1;
+    for (int i = 0; i < k.n_tgt; ++i) {
+        const float t = tvam_tri_hit(k.tgt + 9 * i, ox, oy, oz, dx, dy, dz);
+        if (t < best) {
+            best = t;
+            tri = i;
+        }
+    }
+    return best;
+}
+
+// sc_dda with the film index x + y res.x + z res.x res.y times 2 plus the channel;
+// FWD adds em * c (unscaled film), ADJ gathers grad / volume of the channel.
+template <int MODE>
+__device__ float sf_dda(const TvamConsts& k, float ox, float oy, float oz, float dx, float dy, float dz, float maxt,
+                        float em, int ch, float* __restrict__ film, const float* __restrict__ gin,
+                        const float* __restrict__ vols, uint64_t& nvis) {
+    const float o[3] = {ox, oy, oz}, d[3] = {dx, dy, dz};
+    SegDda q;
+    if (!sc_dda_init(k, o, d, maxt, q)) return 0.0f;
+    float acc = 0.0f;
+    const int64_t sy = k.res[0], sz = (int64_t)k.res[0] * k.res[1];
+    sc_seg_march(k, q, [&](int x, int y, int z, float c) {
+        const int64_t idx = 2 * (x + y * sy + z * sz) + ch;
+        if (MODE == TVAM_MODE_FWD) atomicAdd(&film[idx], em * c);
+        else if (MODE == TVAM_MODE_ADJ) {
+            const float v = vols[idx];
+            const float iv = v != 0.0f ? 1.0f / v : 0.0f;  // volume.py:41-42
+            acc = fmaf(c, gin[idx] * iv, acc);
+        }
+        ++nvis;
+    });
+    return acc;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void tvam_surface_kernel(TvamConsts k, TvamTiles tp, const float* __restrict__ pat,
+                                                           const int32_t* __restrict__ idxmap,
+                                                           const float* __restrict__ gin,
+                                                           const float* __restrict__ vols, float* __restrict__ out,
+                                                           unsigned long long* __restrict__ counter) {
+    const int spp = (int)tp.spp;
+    const int64_t per_angle = (int64_t)k.crop_y * k.crop_x;
+    const int64_t n = (int64_t)tp.n_shard * per_angle * spp;
+    uint64_t nvis = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t local = i / spp;
+        const int smp = (int)(i - local * spp);
+        float em = 1.0f;
+        int64_t act = local;
+        if (MODE == TVAM_MODE_FWD) {
+            const float p = pat[local];
+            if (p == 0.0f && k.skip_zero) continue;
+            em = p * k.wscale;
+        } else if (idxmap) {
+            act = idxmap[local];
+            if (act < 0) continue;
+        }
+        const int al = (int)(local / per_angle);
+        const int64_t pix = local - (int64_t)al * per_angle;
+        const int rowc = (int)(pix / k.crop_x), colc = (int)(pix - (int64_t)rowc * k.crop_x);
+        const int64_t dense = local + k.shard_base;
+        float jx = 0.5f, jy = 0.5f;
+        if (!k.regular) {
+            TvamPcg rng;
+            rng.seed(tp.seed, (uint64_t)dense * (uint64_t)spp + (uint64_t)smp);
+            jx = rng.next_float();
+            jy = rng.next_float();
+        }
+        const float2 csv = tp.cs[al];
+        float xc, yc, ox, oy, oz, dx, dy;
+        tvam_ray_camera(k, k.crop_off_x + colc, k.crop_off_y + rowc, jx, jy, xc, yc);
+        tvam_ray_world(k, csv.x, csv.y, xc, yc, ox, oy, oz, dx, dy);
+        float o2x, o2y, d2x, d2y, maxt, wgt;
+        if (!tvam_segment(k, ox, oy, oz, dx, dy, o2x, o2y, d2x, d2y, maxt, wgt)) continue;
+        float px = o2x, py = o2y, pz = oz;
+        const float vx = d2x, vy = d2y, vz = 0.0f;
+        float att = wgt, tcont = maxt, acc = 0.0f;
+        int inside = 0;
+        for (int it = 0; it < 4096; ++it) {
+            int tri;
+            const float tt = sf_target_hit(k, px, py, pz, vx, vy, vz, tri);
+            const bool hit = tt < tcont;
+            const float tsi = hit ? tt : tcont;
+            const float r = sf_dda<MODE>(k, px, py, pz, vx, vy, vz, tsi, em * att, inside ? 0 : 1, out, gin, vols, nvis);
+            if (MODE == TVAM_MODE_ADJ) acc = fmaf(att, r, acc);
+            att = att * expf(-k.sig_t * tsi);
+            if (!hit) break;
+            inside ^= 1;
+            // spawn_ray at the target hit: offset_p along the geometric normal (oracle or_trace_surface)
+            const float* v = k.tgt + 9 * tri;
+            const float e1x = v[3] - v[0], e1y = v[4] - v[1], e1z = v[5] - v[2];
+            const float e2x = v[6] - v[0], e2y = v[7] - v[1], e2z = v[8] - v[2];
+            const float cx = e1y * e2z - e1z * e2y, cy = e1z * e2x - e1x * e2z, cz = e1x * e2y - e1y * e2x;
+            const float inv = 1.0f / sqrtf(cx * cx + cy * cy + cz * cz);
+            const float nx = cx * inv, ny = cy * inv, nz = cz * inv;
+            const float hx = fmaf(vx, tt, px), hy = fmaf(vy, tt, py), hz = fmaf(vz, tt, pz);
+            const float m = fmaxf(fmaxf(fabsf(hx), fabsf(hy)), fabsf(hz));
+            float mag = (1.0f + m) * TVAM_RAY_EPS;
+            if (__builtin_signbit(nx * vx + ny * vy + nz * vz)) mag = -mag;
+            px = fmaf(mag, nx, hx);
+            py = fmaf(mag, ny, hy);
+            pz = fmaf(mag, nz, hz);
+            tcont = sc_container_hit(k, px, py, pz, vx, vy, vz);
+            if (!(tcont < TVAM_INF)) break;
+        }
+        if (MODE == TVAM_MODE_ADJ && acc != 0.0f) atomicAdd(&out[act], acc * k.wscale);
+    }
+    if (MODE == TVAM_MODE_COUNT) {
+        for (int off = 32; off > 0; off >>= 1) nvis += __shfl_down(nvis, off, 64);
+        if ((threadIdx.x & 63) == 0 && nvis) atomicAdd(counter, (unsigned long long)nvis);
+    }
+}
+
+__global__ __launch_bounds__(256) void tvam_scale_volumes_kernel(int64_t n, const float* __restrict__ vols,
+                                                                 float* __restrict__ dose) {
+    for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
+        const float v = vols[i];
+        dose[i] = dose[i] * (v != 0.0f ? 1.0f / v : 0.0f);
+    }
+}
+
+// One compute_volume sample (sensor.py:89-104): 1 = inside the target mesh.
+__device__ __forceinline__ int sf_volume_sample(const TvamConsts& k, TvamPcg& rng, int vx, int vy, int vz,
+                                                const float3 mb0, const float3 mb1) {
+    const float fx = rng.next_float(), fy = rng.next_float(), fz = rng.next_float();
+    const float sx = rng.next_float(), sy = rng.next_float();
+    const float ox = k.bmin[0] + k.h[0] * ((float)vx + fx);
+    const float oy = k.bmin[1] + k.h[1] * ((float)vy + fy);
+    const float oz = k.bmin[2] + k.h[2] * ((float)vz + fz);
+    if (!(ox > mb0.x && oy > mb0.y && oz > mb0.z && ox < mb1.x && oy < mb1.y && oz < mb1.z)) return 0;
+    // warp::square_to_uniform_sphere(sample): z = 1 - 2 y, phi = 2 pi x
+    const float dz = 1.0f - 2.0f * sy, r = sqrtf(fmaxf(1.0f - dz * dz, 0.0f));
+    const float dx = r * cosf(TVAM_TWO_PI * sx), dy = r * sinf(TVAM_TWO_PI * sx);
+    int tri;
+    const float t = sf_target_hit(k, ox, oy, oz, dx, dy, dz, tri);
+    if (!(t < TVAM_INF)) return 0;
+    const float* p = k.tgt + 9 * tri;
+    const float e1x = p[3] - p[0], e1y = p[4] - p[1], e1z = p[5] - p[2];
+    const float e2x = p[6] - p[0], e2y = p[7] - p[1], e2z = p[8] - p[2];
+    const float cx = e1y * e2z - e1z * e2y, cy = e1z * e2x - e1x * e2z, cz = e1x * e2y - e1y * e2x;
+    return cx * dx + cy * dy + cz * dz > 0.0f ? 1 : 0;
+}
+
+// compute_volume (sensor.py:47-110): one thread per voxel, sample_count points.
+// A voxel whose box misses the open mesh bbox has every point outside; one whose
+// box meets no triangle's bounding box lies on one side of the (closed) mesh, so
+// every one of its points gets the same answer: its first three samples decide
+// (majority, against a ray grazing an edge).  The others run every sample.
+__global__ __launch_bounds__(256) void tvam_volume_kernel(TvamConsts k, float3 mb0, float3 mb1, uint32_t sample_count,
+                                                          const float* __restrict__ tri_box,
+                                                          float* __restrict__ volumes) {
+    const int64_t V = (int64_t)k.res[0] * k.res[1] * k.res[2];
+    const float vvol = k.h[0] * k.h[1] * k.h[2];
+    for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < V; v += (int64_t)gridDim.x * 256) {
+        const int vx = (int)(v % k.res[0]), vy = (int)((v / k.res[0]) % k.res[1]);
+        const int vz = (int)(v / ((int64_t)k.res[0] * k.res[1]));
+        uint32_t cin = 0;
+        const float x0 = k.bmin[0] + k.h[0] * (float)vx, x1 = k.bmin[0] + k.h[0] * ((float)vx + 1.0f);
+        const float y0 = k.bmin[1] + k.h[1] * (float)vy, y1 = k.bmin[1] + k.h[1] * ((float)vy + 1.0f);
+        const float z0 = k.bmin[2] + k.h[2] * (float)vz, z1 = k.bmin[2] + k.h[2] * ((float)vz + 1.0f);
+        const bool may = x1 >= mb0.x && x0 <= mb1.x && y1 >= mb0.y && y0 <= mb1.y && z1 >= mb0.z && z0 <= mb1.z;
+        if (may) {
+            bool touch = false;  // some triangle's (slightly grown) bounding box meets the voxel
+            for (int i = 0; i < k.n_tgt && !touch; ++i) {
+                const float* b = tri_box + 6 * i;
+                touch = x1 >= b[0] && x0 <= b[3] && y1 >= b[1] && y0 <= b[4] && z1 >= b[2] && z0 <= b[5];
+            }
+            TvamPcg rng;
+            rng.seed(0u, (uint64_t)v);
+            if (touch || sample_count < 3) {
+                for (uint32_t i = 0; i < sample_count; ++i) cin += sf_volume_sample(k, rng, vx, vy, vz, mb0, mb1);
+            } else {
+                int c3 = 0;
+                for (int i = 0; i < 3; ++i) c3 += sf_volume_sample(k, rng, vx, vy, vz, mb0, mb1);
+                cin = c3 >= 2 ? sample_count : 0;
+            }
+        }
+        const uint32_t cout = sample_count - cin;
+        volumes[2 * v] = (float)cin * vvol / (float)sample_count;
+        volumes[2 * v + 1] = (float)cout * vvol / (float)sample_count;
+    }
+}
+
 }  // namespace
+
+hipError_t tvam_launch_surface_paths(int mode, const TvamConsts& k, const TvamTiles& t, const float* pat,
+                                     const int32_t* idxmap, const float* gin, const float* vols, float* out,
+                                     unsigned long long* counter, hipStream_t stream) {
+    const int64_t n = (int64_t)t.n_shard * k.crop_y * k.crop_x * t.spp;
+    int64_t g = (n + 255) / 256;
+    if (g > 262144) g = 262144;
+    if (g < 1) g = 1;
+    switch (mode) {
+        case TVAM_MODE_FWD:
+            hipLaunchKernelGGL(tvam_surface_kernel<TVAM_MODE_FWD>, dim3((unsigned)g), dim3(256), 0, stream, k, t, pat,
+                               idxmap, gin, vols, out, counter);
+            break;
+        case TVAM_MODE_ADJ:
+            hipLaunchKernelGGL(tvam_surface_kernel<TVAM_MODE_ADJ>, dim3((unsigned)g), dim3(256), 0, stream, k, t, pat,
+                               idxmap, gin, vols, out, counter);
+            break;
+        default:
+            hipLaunchKernelGGL(tvam_surface_kernel<TVAM_MODE_COUNT>, dim3((unsigned)g), dim3(256), 0, stream, k, t,
+                               pat, idxmap, gin, vols, out, counter);
+    }
+    return hipGetLastError();
+}
+
+hipError_t tvam_launch_scale_volumes(int64_t n, const float* vols, float* dose, hipStream_t stream) {
+    const unsigned g = (unsigned)std::min<int64_t>(std::max<int64_t>((n + 255) / 256, 1), 16384);
+    hipLaunchKernelGGL(tvam_scale_volumes_kernel, dim3(g), dim3(256), 0, stream, n, vols, dose);
+    return hipGetLastError();
+}
+
+hipError_t tvam_launch_volumes(const TvamConsts& k, uint32_t sample_count, float* volumes, hipStream_t stream) {
+    float3 mb0 = make_float3(TVAM_INF, TVAM_INF, TVAM_INF), mb1 = make_float3(-TVAM_INF, -TVAM_INF, -TVAM_INF);
+    // the mesh bbox on the host copy is not kept: read it back from the device triangles
+    std::vector<float> h((size_t)k.n_tgt * 9);
+    hipError_t e = hipMemcpy(h.data(), k.tgt, h.size() * sizeof(float), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return e;
+    for (size_t i = 0; i < h.size(); i += 3) {
+        mb0.x = fminf(mb0.x, h[i]);
+        mb0.y = fminf(mb0.y, h[i + 1]);
+        mb0.z = fminf(mb0.z, h[i + 2]);
+        mb1.x = fmaxf(mb1.x, h[i]);
+        mb1.y = fmaxf(mb1.y, h[i + 1]);
+        mb1.z = fmaxf(mb1.z, h[i + 2]);
+    }
+    // per-triangle bounding boxes, grown by 1e-4 of the mesh extent (+ an absolute 1e-6)
+    const float ext = fmaxf(fmaxf(mb1.x - mb0.x, mb1.y - mb0.y), mb1.z - mb0.z);
+    const float grow = 1e-4f * ext + 1e-6f;
+    std::vector<float> box((size_t)k.n_tgt * 6);
+    for (int i = 0; i < k.n_tgt; ++i) {
+        const float* t = h.data() + 9 * (size_t)i;
+        for (int a = 0; a < 3; ++a) {
+            box[6 * (size_t)i + a] = fminf(fminf(t[a], t[3 + a]), t[6 + a]) - grow;
+            box[6 * (size_t)i + 3 + a] = fmaxf(fmaxf(t[a], t[3 + a]), t[6 + a]) + grow;
+        }
+    }
+    float* d_box = nullptr;
+    if ((e = hipMalloc((void**)&d_box, box.size() * sizeof(float))) != hipSuccess) return e;
+    if ((e = hipMemcpy(d_box, box.data(), box.size() * sizeof(float), hipMemcpyHostToDevice)) != hipSuccess) {
+        (void)hipFree(d_box);
+        return e;
+    }
+    const int64_t V = (int64_t)k.res[0] * k.res[1] * k.res[2];
+    const unsigned g = (unsigned)std::min<int64_t>(std::max<int64_t>((V + 255) / 256, 1), 1 << 20);
+    hipLaunchKernelGGL(tvam_volume_kernel, dim3(g), dim3(256), 0, stream, k, mb0, mb1, sample_count, d_box, volumes);
+    e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    (void)hipFree(d_box);
+    return e;
+}
 
 hipError_t tvam_launch_scatter_paths(int mode, const TvamConsts& k, const TvamTiles& t, const float* pat,
                                      const int32_t* idxmap, const float* gin, float* out,

@@ -99,6 +99,24 @@ class Projection:
                 n_active, spp, seed & 0xFFFFFFFF, out.data_ptr(), _stream_ptr(self.device)))
         return out
 
+    def compute_volume(self, sample_count: int = 2 ** 14) -> torch.Tensor:
+        """Surface-aware voxel volumes [Z, Y, X, 2] (inside, outside the target mesh) of this plan's
+        film (VolumetricSensor.compute_volume, sensor.py:47-110)."""
+        out = torch.empty(self.film_shape[:3] + (2,), dtype=torch.float32, device=self.device)
+        with torch.cuda.device(self.device):
+            _abi.check(self.lib.tvam_compute_volume(self._plan, int(sample_count), out.data_ptr(),
+                                                    _stream_ptr(self.device)))
+        return out
+
+    def set_volumes(self, volumes: torch.Tensor) -> None:
+        """Per-(voxel, channel) volumes of a surface-aware film (the forward divides by them,
+        volume.py:41-42); the projection keeps the tensor alive."""
+        self._check_tensor(volumes, torch.float32, "volumes")
+        if tuple(volumes.shape) != tuple(self.film_shape):
+            raise ValueError(f"volumes must have the film shape {self.film_shape}")
+        _abi.check(self.lib.tvam_plan_set_volumes(self._plan, volumes.data_ptr()))
+        self._volumes = volumes
+
     def radon(self, target_tris, spp: int = 4, seed: int = 0, max_depth: int = 5) -> torch.Tensor:
         """Radon filter image of this plan's DMD pixels (dense crop order of its shard):
         positive where a ray crosses the target inside the medium (radon.py:47-106)."""

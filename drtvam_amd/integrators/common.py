@@ -58,6 +58,9 @@ class TVAMIntegrator:
             d.slab_begin, d.slab_end = int(self.slab[0]), int(self.slab[1])
         d.tile = int(self.tile)
         d.flags = int(self.flags)
+        if sensor.film().surface_aware:  # the target mesh stays in the scene (optimize.py:188-191)
+            from ..utils import target_triangles
+            d.set_target(target_triangles(scene))
         return d
 
     def projection(self, scene, sensor, device=None):
@@ -68,6 +71,8 @@ class TVAMIntegrator:
         proj = self._plans.get(key)
         if proj is None:
             proj = Projection(d, dev)
+            if sensor.film().surface_aware:  # inv_vol of the two channels (volume.py:41-42)
+                proj.set_volumes(sensor.compute_volume(scene).to(dev))
             self._plans[key] = proj
         return proj
 

@@ -290,7 +290,9 @@ class TvamProblem(ShardedLoop):
         self.crop_x, self.crop_y = p.crop[0], p.crop[1]
         full_desc = VolumeIntegrator(base).desc(self.scene, self.sensor)
         self.res_z = int(full_desc.film_res[2])
-        planar = self.regular_sampling and full_desc.albedo == 0.0  # scattered paths leave their slice
+        self.surface_aware = bool(self.sensor.film().surface_aware)
+        # scattered paths leave their slice; surface-aware films run the per-path kernels
+        planar = self.regular_sampling and full_desc.albedo == 0.0 and not self.surface_aware
         if shard == 'slab' and not (planar and fusable):
             raise ValueError("z-slab sharding needs regular sampling, a non-scattering medium and the fused "
                              "thresholded loss")
@@ -314,9 +316,9 @@ class TvamProblem(ShardedLoop):
                                                            'rr_depth': config.get('rr_depth_ref', 8)})
 
         if target is None:
-            if self.sensor.film().surface_aware:
-                raise NotImplementedError("surface-aware optimisation is not supported yet")
-            if 'filename' in config['target']:
+            if self.surface_aware:  # fractional inside / outside volumes (optimize.py:131-134)
+                target = self.sensor.compute_volume(self.scene).cpu()
+            elif 'filename' in config['target']:
                 target = discretize(self.scene, sensor=self.sensor)
             else:
                 target = analytic_target(self.sensor.resolution(), self.sensor.bbox_min, self.sensor.bbox_max,
@@ -446,7 +448,11 @@ def optimize(config, patterns_fwd=None, device=None):
     os.makedirs(output, exist_ok=True)
     if prob.rank == 0:
         tgt = prob.target_full.cpu().numpy()
-        save_vol(tgt, os.path.join(output, "target.exr"))
+        if prob.surface_aware:
+            save_vol(tgt[..., 0, None], os.path.join(output, "target_in.exr"))
+            save_vol(tgt[..., 1, None], os.path.join(output, "target_out.exr"))
+        else:
+            save_vol(tgt, os.path.join(output, "target.exr"))
         np.save(os.path.join(output, "target.npy"), tgt)
     p = prob.scene.projector
     if patterns_fwd is not None:
@@ -474,6 +480,10 @@ def optimize(config, patterns_fwd=None, device=None):
     if prob.rank == 0:
         crop = pats.cpu().numpy().reshape(-1, p.crop[1], p.crop[0])
         _save_outputs(output, prob, vol_final, full_dmd(p, crop))
+        if prob.surface_aware:  # the binary target on the final sensor's grid (optimize.py:355-360)
+            tb = discretize(prob.scene, sensor=prob.final_sensor).numpy()
+            np.save(os.path.join(output, "target_binary.npy"), tb)
+            save_vol(tb, os.path.join(output, "target_binary.exr"))
     return vol_final
 
 

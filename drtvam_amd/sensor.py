@@ -53,10 +53,23 @@ class VolumetricSensor:
     def resolution(self):
         return self.m_film.resolution()
 
-    def compute_volume(self, scene=None):
+    def compute_volume(self, scene=None, sample_count=2 ** 14):
+        """Voxel volume (sensor.py:47-51), or for a surface-aware film the volumes [Z, Y, X, 2]
+        inside / outside the scene's target mesh (sensor.py:53-110, cached like the reference),
+        estimated on the GPU (tvam_compute_volume)."""
         if not self.m_film.surface_aware:
             return float(np.prod(self.voxel_size, dtype=np.float32))
-        raise NotImplementedError("surface-aware discretization is not supported yet")
+        if self.volumes is not None:
+            return self.volumes
+        if scene is None or scene.target is None:
+            raise ValueError("No target shape found in the scene")
+        from .integrators.common import TVAMIntegrator
+        from .engine import Projection
+        d = TVAMIntegrator({}).desc(scene, self)
+        proj = Projection(d, scene.projector.device)
+        self.volumes = proj.compute_volume(sample_count)
+        proj.close()
+        return self.volumes
 
     def fill_desc(self, desc: _abi.TvamDesc) -> None:
         for a in range(3):

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define TVAM_ABI_VERSION 4
+#define TVAM_ABI_VERSION 5
 
 /* error codes */
 #define TVAM_OK               0
@@ -91,7 +91,9 @@ typedef struct tvam_desc {
     int32_t sensor_type;          /* TVAM_SENSOR_* */
     float   bbox_min[3], bbox_max[3];
     int32_t film_res[3];
-    int32_t film_channels;        /* 1 (2 = surface_aware, not yet supported) */
+    int32_t film_channels;        /* 1, or 2 = 'surface_aware' (film.py:16-21): channel 0 collects
+                                     the segments inside the target mesh, 1 those outside
+                                     (sensor.py:405-409); needs target_tris */
 
     /* container (geometry.py:20-35, :75-96, :142-183) */
     int32_t vial_type;            /* TVAM_VIAL_* */
@@ -128,6 +130,12 @@ typedef struct tvam_desc {
        tvam_plan_create (not kept) */
     const float* occluder_tris;
     int32_t n_occluder_tris;
+    /* target mesh (optimize.py:64-73: null BSDF, kept in the scene when the
+       film is surface-aware, optimize.py:188-191): host array
+       [n_target_tris][3 vertices][x, y, z] in world space, read by
+       tvam_plan_create (not kept).  Used when film_channels == 2. */
+    const float* target_tris;
+    int32_t n_target_tris;
 } tvam_desc;
 
 /* tvam_desc.flags */
@@ -148,7 +156,7 @@ void tvam_plan_destroy(tvam_plan* plan);
 
 /*
  * Forward projection (primal render).  Writes the whole film
- * dose[z][y][x] (film order, C = 1) = inv_vol * sum over rays of this plan's
+ * dose[z][y][x][C] (film order) = inv_vol * sum over rays of this plan's
  * angle shard; every voxel is overwritten (no pre-zeroing needed).
  *   active_data   : f32, n_active entries (projector.active_data)
  *   active_pixels : u32 flat indices angle*H*W + row*W + col into the full DMD
@@ -185,6 +193,19 @@ int tvam_plan_stats(tvam_plan* plan, uint64_t* fallback_tiles);
    world-space triangles.  radon: device, n floats, overwritten.  Synchronous. */
 int tvam_radon(tvam_plan* plan, const float* target_tris, int32_t n_target_tris, uint32_t spp, uint32_t seed,
                int32_t max_depth, float* radon, void* stream);
+
+/* Surface-aware discretisation (film_channels == 2; VolumetricSensor.compute_volume,
+   sensor.py:47-110): volumes[z][y][x][2] (device, f32, overwritten) = the voxel volume
+   inside (channel 0) / outside (1) the target mesh, estimated from sample_count points per
+   voxel (independent sampler seeded (0, voxel)), each classified by the orientation of the
+   first target hit along a uniform random direction.  Synchronous. */
+int tvam_compute_volume(tvam_plan* plan, uint32_t sample_count, float* volumes, void* hip_stream);
+
+/* Surface-aware plans: the per-channel voxel volumes the forward divides by and the
+   adjoint multiplies the incoming gradient with (inv_vol = 1/volume, 0 where volume
+   is 0: volume.py:41-42, :130).  Device pointer [z][y][x][2], caller-owned, kept by
+   the plan until replaced; must be set before tvam_forward / tvam_adjoint. */
+int tvam_plan_set_volumes(tvam_plan* plan, const float* volumes);
 
 /* Which kernels serve this plan (bit mask; 0 = per-ray tile kernels):
    bit 0 = planar adjoint (regular sampling: one ray record per (angle,

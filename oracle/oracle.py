@@ -46,6 +46,13 @@ def lib():
         L.oracle_phase.argtypes = [D, P, ctypes.c_float, ctypes.c_float, P]
         L.oracle_radon.restype = ctypes.c_int
         L.oracle_radon.argtypes = [D, P, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, P, ctypes.c_int]
+        L.oracle_forward_surface.restype = ctypes.c_int
+        L.oracle_forward_surface.argtypes = [D, P, P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, P, P, P,
+                                             ctypes.c_int]
+        L.oracle_adjoint_surface.restype = ctypes.c_int
+        L.oracle_adjoint_surface.argtypes = L.oracle_forward_surface.argtypes
+        L.oracle_compute_volume.restype = ctypes.c_int
+        L.oracle_compute_volume.argtypes = [D, ctypes.c_uint32, P, ctypes.c_int]
         L.oracle_dda_ray.restype = ctypes.c_int
         L.oracle_dda_ray.argtypes = [D, P, P, ctypes.c_float, ctypes.c_double, P, P]
         _lib = L
@@ -124,3 +131,51 @@ def dda_ray(desc, o, d, maxt, em=1.0):
     lib().oracle_dda_ray(ctypes.byref(desc), _ptr(o), _ptr(d), maxt, em, _ptr(film),
                          ctypes.cast(ctypes.byref(visits), ctypes.c_void_p))
     return film, visits.value
+
+
+def inv_volumes(volumes):
+    """1 / volume per (voxel, channel), 0 where the volume is 0 (volume.py:41-42), fp32."""
+    v = np.asarray(volumes, dtype=np.float32)
+    out = np.zeros_like(v)
+    nz = v != 0
+    out[nz] = np.float32(1.0) / v[nz]
+    return out
+
+
+def compute_volume(desc, sample_count=2 ** 14, nthreads=1):
+    """Surface-aware voxel volumes [z, y, x, 2] (inside, outside) of the desc's target mesh."""
+    out = np.zeros(film_shape(desc) + (2,), dtype=np.float32)
+    rc = lib().oracle_compute_volume(ctypes.byref(desc), sample_count, _ptr(out), nthreads)
+    if rc:
+        raise ValueError(f"oracle_compute_volume failed ({rc})")
+    return out
+
+
+def forward_surface(desc, active_data, volumes, active_pixels=None, spp=1, seed=0, nthreads=1):
+    """Surface-aware dose [z, y, x, 2] (float64) = film / volumes per channel, and the visit count."""
+    data = np.ascontiguousarray(active_data, dtype=np.float32)
+    pix = None if active_pixels is None else np.ascontiguousarray(active_pixels, dtype=np.uint32)
+    iv = np.ascontiguousarray(inv_volumes(volumes))
+    dose = np.zeros(film_shape(desc) + (2,), dtype=np.float64)
+    visits = ctypes.c_uint64(0)
+    rc = lib().oracle_forward_surface(ctypes.byref(desc), _ptr(data), _ptr(pix), data.size, spp, seed, _ptr(iv),
+                                      _ptr(dose), ctypes.cast(ctypes.byref(visits), ctypes.c_void_p), nthreads)
+    if rc:
+        raise ValueError(f"oracle_forward_surface failed ({rc})")
+    return dose, visits.value
+
+
+def adjoint_surface(desc, grad_dose, volumes, active_pixels=None, n_active=None, spp=1, seed=0, nthreads=1):
+    """Gradient w.r.t. active_data (float64) of <grad_dose, forward_surface(.)>."""
+    g = np.ascontiguousarray(grad_dose, dtype=np.float32).reshape(film_shape(desc) + (2,))
+    pix = None if active_pixels is None else np.ascontiguousarray(active_pixels, dtype=np.uint32)
+    if n_active is None:
+        n_active = pix.size if pix is not None else desc.n_patterns * desc.crop_y * desc.crop_x
+    iv = np.ascontiguousarray(inv_volumes(volumes))
+    out = np.zeros(n_active, dtype=np.float64)
+    visits = ctypes.c_uint64(0)
+    rc = lib().oracle_adjoint_surface(ctypes.byref(desc), _ptr(g), _ptr(pix), n_active, spp, seed, _ptr(iv),
+                                      _ptr(out), ctypes.cast(ctypes.byref(visits), ctypes.c_void_p), nthreads)
+    if rc:
+        raise ValueError(f"oracle_adjoint_surface failed ({rc})")
+    return out, visits.value

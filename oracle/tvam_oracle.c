@@ -110,6 +110,8 @@ typedef struct {
     double sa_over_st;  /* sensor.py:400, :404                  */
     float st;
     int part;           /* scattering paths: -1 all segments, 0 all but the first, 1 the first only */
+    int C;              /* film channels: 1, or 2 = surface-aware (film.py:16-21) */
+    const float* inv_volumes; /* surface-aware: 1 / compute_volume() per (voxel, channel), 0 where 0 */
 } or_scene;
 
 static void or_scene_init(or_scene* s, const tvam_desc* d) {
@@ -126,6 +128,8 @@ static void or_scene_init(or_scene* s, const tvam_desc* d) {
     s->inv_vol = vol != 0.0f ? 1.0 / (double)vol : 0.0;
     s->st = d->sigma_t;
     s->part = -1;
+    s->C = d->film_channels == 2 ? 2 : 1;
+    s->inv_volumes = NULL;
     float ss = d->albedo * d->sigma_t;
     s->sa_over_st = d->sigma_t != 0.0f ? ((double)d->sigma_t - (double)ss) / (double)d->sigma_t : 0.0;
 }
@@ -541,9 +545,11 @@ static void or_coordinate_system(const float n[3], float s[3], float t[3]) {
 static void or_phase_sample(const tvam_desc* d, const float dd[3], float u1, float u2, float wo[3]) {
     float lx, ly, lz;
     if (d->phase_type == TVAM_PHASE_ISOTROPIC) {
-        float z = 1.0f - 2.0f * u1; /* warp::square_to_uniform_sphere: world space */
+        /* warp::square_to_uniform_sphere(sample) in world space: z = 1 - 2 sample.y,
+           phi = 2 pi sample.x */
+        float z = 1.0f - 2.0f * u2;
         float r = sqrtf(fmaxf(1.0f - z * z, 0.0f));
-        float sp = sinf(OR_TWO_PI * u2), cp = cosf(OR_TWO_PI * u2);
+        float sp = sinf(OR_TWO_PI * u1), cp = cosf(OR_TWO_PI * u1);
         wo[0] = r * cp;
         wo[1] = r * sp;
         wo[2] = z;
@@ -737,8 +743,10 @@ static double or_dda(const or_scene* s, const float o[3], const float dd[3], flo
         float dt = fminf(fminf(fminf(dtmax[0], dtmax[1]), dtmax[2]), remaining);
         remaining = remaining - dt;
         double w = s->sa_over_st * exp(-st * (double)t) * (1.0 - exp(-st * (double)fmaxf(dt, 0.0f)));
-        size_t idx = (size_t)cur[0] + (size_t)cur[1] * (size_t)s->res[0] +
-                     (size_t)cur[2] * (size_t)s->res[0] * (size_t)s->res[1];
+        /* film index (sensor.py:405-409): x + y res.x + z res.x res.y, times C; the
+           surface-aware channel offset is folded into the film / grad pointer */
+        size_t idx = ((size_t)cur[0] + (size_t)cur[1] * (size_t)s->res[0] +
+                      (size_t)cur[2] * (size_t)s->res[0] * (size_t)s->res[1]) * (size_t)s->C;
         if (mode == 0) film[idx] += em * w;
         else if (mode == 3) {
 #ifdef _OPENMP
@@ -793,7 +801,9 @@ static int or_check(const tvam_desc* d) {
         return TVAM_ERR_UNSUPPORTED;
     if (d->n_occluder_tris < 0 || (d->n_occluder_tris > 0 && !d->occluder_tris)) return TVAM_ERR_INVALID;
     if (d->projector_type != TVAM_PROJECTOR_COLLIMATED) return TVAM_ERR_UNSUPPORTED;
-    if (d->film_channels != 1) return TVAM_ERR_UNSUPPORTED;
+    if (d->film_channels != 1 && d->film_channels != 2) return TVAM_ERR_UNSUPPORTED;
+    if (d->film_channels == 2 && (d->n_target_tris <= 0 || !d->target_tris)) return TVAM_ERR_INVALID;
+    if (d->film_channels == 2 && d->albedo != 0.0f) return TVAM_ERR_UNSUPPORTED;
     if (d->albedo < 0.0f || d->albedo > 1.0f) return TVAM_ERR_INVALID;
     if (d->albedo != 0.0f && !(d->sigma_t > 0.0f)) return TVAM_ERR_INVALID;
     if (d->phase_type < TVAM_PHASE_ISOTROPIC || d->phase_type > TVAM_PHASE_HG) return TVAM_ERR_INVALID;
@@ -803,12 +813,89 @@ static int or_check(const tvam_desc* d) {
     return 0;
 }
 
+/* Nearest target-mesh hit along (o, dd) (Moller-Trumbore over every triangle); *tri = its index. */
+static float or_target_hit(const tvam_desc* d, const float o[3], const float dd[3], int* tri) {
+    float best = INFINITY;
+    *tri = -1;
+    for (int i = 0; i < d->n_target_tris; ++i) {
+        float t = or_tri_hit(o, dd, d->target_tris + 9 * i);
+        if (t < best) {
+            best = t;
+            *tri = i;
+        }
+    }
+    return best;
+}
+
+/* Surface-aware path (film_channels 2, non-scattering; volume.py:179-272 with the target
+   mesh in the scene, null BSDF): the medium segment is cut at every target hit.  Each
+   piece deposits from its own origin into channel 0 while inside the target, 1 outside
+   (inside_target toggles on each hit, starting outside: volume.py:175, :218); reaching a
+   surface multiplies the attenuation by e^{-st si.t} (:263, :266); a target hit spawns the
+   next piece at the hit point offset along the face normal (spawn_ray / offset_p) and does
+   not count towards max_depth (:271); the piece ending at the container (or an occluder)
+   is the last one deposited. */
+static double or_trace_surface(const or_scene* s, uint32_t pixel, uint64_t wave_index, uint32_t seed, double em,
+                               int mode, double* film, const float* grad, int only_slice, uint64_t* visits) {
+    const tvam_desc* d = s->d;
+    or_ray ray;
+    or_gen_ray(s, pixel, wave_index, seed, &ray);
+    float o[3], dd[3], maxt;
+    double attd = 1.0;
+    if (d->vial_type == TVAM_VIAL_CYLINDRICAL || d->vial_type == TVAM_VIAL_SQUARE) {
+        if (!(d->vial_type == TVAM_VIAL_SQUARE ? or_segment_square(s, &ray, o, dd, &maxt, &attd)
+                                               : or_segment_cylindrical(s, &ray, o, dd, &maxt, &attd)))
+            return 0.0;
+    } else {
+        if (d->max_depth < 2 || !or_segment_index_matched(s, &ray, o, &maxt)) return 0.0;
+        for (int k = 0; k < 3; ++k) dd[k] = ray.d[k];
+    }
+    float att = (float)attd;
+    int inside = 0;
+    double acc = 0.0;
+    float tcont = maxt;
+    for (int it = 0; it < 4096; ++it) {
+        int tri;
+        const float tt = or_target_hit(d, o, dd, &tri);
+        const int hit = tt < tcont;
+        const float tsi = hit ? tt : tcont;
+        const int ch = inside ? 0 : 1;
+        if (mode == 0 || mode == 3)
+            (void)or_dda(s, o, dd, tsi, em * (double)att, mode, film + ch, NULL, only_slice, visits);
+        else if (mode == 1)
+            acc += (double)att * or_dda(s, o, dd, tsi, em, mode, NULL, grad + ch, only_slice, visits);
+        else
+            (void)or_dda(s, o, dd, tsi, em, mode, NULL, NULL, only_slice, visits);
+        att = att * expf(-d->sigma_t * tsi);
+        if (!hit) break;
+        inside = !inside;
+        const float* v = d->target_tris + 9 * tri;
+        float e1[3] = {v[3] - v[0], v[4] - v[1], v[5] - v[2]}, e2[3] = {v[6] - v[0], v[7] - v[1], v[8] - v[2]};
+        float c[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+        float inv = 1.0f / sqrtf(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+        float n[3], p[3];
+        for (int k = 0; k < 3; ++k) {
+            n[k] = c[k] * inv;
+            p[k] = fmaf(dd[k], tt, o[k]);
+        }
+        float m = fmaxf(fmaxf(fabsf(p[0]), fabsf(p[1])), fabsf(p[2]));
+        float mag = (1.0f + m) * OR_RAY_EPS;
+        if (signbit(n[0] * dd[0] + n[1] * dd[1] + n[2] * dd[2])) mag = -mag;
+        for (int k = 0; k < 3; ++k) o[k] = fmaf(mag, n[k], p[k]);
+        int which;
+        tcont = or_container_hit(s, o, dd, &which);
+        if (!(tcont < INFINITY)) break;
+    }
+    return acc;
+}
+
 /* one ray: generate + segment + DDA.  Returns the adjoint sum (mode 1).
    mode 0: forward, 3: forward with atomic film adds (shared film). */
 static double or_trace(const or_scene* s, uint32_t pixel, uint64_t wave_index, uint32_t seed, double em,
                        int mode, double* film, const float* grad, int only_slice, uint64_t* visits) {
     if (s->d->albedo != 0.0f)  /* has_scattering (volume.py:159) */
         return or_trace_scatter(s, pixel, wave_index, seed, em, mode, film, grad, visits, s->part);
+    if (s->C == 2) return or_trace_surface(s, pixel, wave_index, seed, em, mode, film, grad, only_slice, visits);
     or_ray ray;
     or_gen_ray(s, pixel, wave_index, seed, &ray);
     float o2[3], maxt;
@@ -958,17 +1045,19 @@ int oracle_radon(const tvam_desc* d, const float* tgt, int ntgt, uint32_t spp, u
 /* ------------------------------------------------------------------------ */
 /* Public oracle entry points (called from tests/ and bench.py via ctypes)   */
 /* ------------------------------------------------------------------------ */
-int oracle_forward_part(const tvam_desc* d, const float* active_data, const uint32_t* active_pixels,
-                        uint64_t n_active, uint32_t spp, uint32_t seed, double* dose, uint64_t* visits,
-                        int nthreads, int part) {
+static int or_forward_impl(const tvam_desc* d, const float* active_data, const uint32_t* active_pixels,
+                           uint64_t n_active, uint32_t spp, uint32_t seed, double* dose, uint64_t* visits,
+                           int nthreads, int part, const float* inv_volumes) {
     int rc = or_check(d);
     if (rc) return rc;
     if (d->regular_sampling) spp = 1;
     or_scene s;
     or_scene_init(&s, d);
     s.part = part;
+    s.inv_volumes = inv_volumes;
+    if (s.C == 2 && !inv_volumes) return TVAM_ERR_INVALID;
     size_t V = (size_t)s.res[0] * s.res[1] * s.res[2];
-    memset(dose, 0, V * sizeof(double));
+    memset(dose, 0, V * (size_t)s.C * sizeof(double));
     double wr = or_ray_weight(d, n_active, spp);
     uint64_t nv_total = 0;
     if (d->albedo != 0.0f && nthreads > 1) {
@@ -1061,9 +1150,26 @@ int oracle_forward_part(const tvam_desc* d, const float* active_data, const uint
         free(row_off);
         free(row_idx);
     }
-    for (size_t v = 0; v < V; ++v) dose[v] *= s.inv_vol;
+    if (s.C == 2)  /* volume.py:41-42 with the surface-aware volumes (sensor.py:47-110) */
+        for (size_t v = 0; v < 2 * V; ++v) dose[v] *= (double)inv_volumes[v];
+    else
+        for (size_t v = 0; v < V; ++v) dose[v] *= s.inv_vol;
     if (visits) *visits = nv_total;
     return 0;
+}
+
+int oracle_forward_part(const tvam_desc* d, const float* active_data, const uint32_t* active_pixels,
+                        uint64_t n_active, uint32_t spp, uint32_t seed, double* dose, uint64_t* visits,
+                        int nthreads, int part) {
+    return or_forward_impl(d, active_data, active_pixels, n_active, spp, seed, dose, visits, nthreads, part, NULL);
+}
+
+/* Surface-aware forward: dose [V][2] = film / volume per channel (inv_volumes [V][2]). */
+int oracle_forward_surface(const tvam_desc* d, const float* active_data, const uint32_t* active_pixels,
+                           uint64_t n_active, uint32_t spp, uint32_t seed, const float* inv_volumes, double* dose,
+                           uint64_t* visits, int nthreads) {
+    return or_forward_impl(d, active_data, active_pixels, n_active, spp, seed, dose, visits, nthreads, -1,
+                           inv_volumes);
 }
 
 int oracle_forward(const tvam_desc* d, const float* active_data, const uint32_t* active_pixels,
@@ -1078,21 +1184,23 @@ int oracle_phase(const tvam_desc* d, const float* dd, float u1, float u2, float*
     return 0;
 }
 
-int oracle_adjoint(const tvam_desc* d, const float* grad_dose, const uint32_t* active_pixels,
-                   uint64_t n_active, uint32_t spp, uint32_t seed, double* grad, uint64_t* visits,
-                   int nthreads) {
+static int or_adjoint_impl(const tvam_desc* d, const float* grad_dose, const uint32_t* active_pixels,
+                           uint64_t n_active, uint32_t spp, uint32_t seed, double* grad, uint64_t* visits,
+                           int nthreads, const float* inv_volumes) {
     int rc = or_check(d);
     if (rc) return rc;
     if (d->regular_sampling) spp = 1;
     or_scene s;
     or_scene_init(&s, d);
+    s.inv_volumes = inv_volumes;
+    if (s.C == 2 && !inv_volumes) return TVAM_ERR_INVALID;
     double wr = or_ray_weight(d, n_active, spp);
     /* delta_L = grad_in * inv_vol (volume.py:130), in fp32 like the reference */
-    size_t V = (size_t)s.res[0] * s.res[1] * s.res[2];
+    size_t V = (size_t)s.res[0] * s.res[1] * s.res[2] * (size_t)s.C;
     float* dl = (float*)malloc(V * sizeof(float));
     if (!dl) return TVAM_ERR_INVALID;
     float inv_vol_f = (float)s.inv_vol;
-    for (size_t v = 0; v < V; ++v) dl[v] = grad_dose[v] * inv_vol_f;
+    for (size_t v = 0; v < V; ++v) dl[v] = grad_dose[v] * (s.C == 2 ? inv_volumes[v] : inv_vol_f);
     uint64_t nv_total = 0;
     if (nthreads < 1) nthreads = 1;
 #ifdef _OPENMP
@@ -1108,6 +1216,81 @@ int oracle_adjoint(const tvam_desc* d, const float* grad_dose, const uint32_t* a
     }
     free(dl);
     if (visits) *visits = nv_total;
+    return 0;
+}
+
+int oracle_adjoint(const tvam_desc* d, const float* grad_dose, const uint32_t* active_pixels,
+                   uint64_t n_active, uint32_t spp, uint32_t seed, double* grad, uint64_t* visits,
+                   int nthreads) {
+    return or_adjoint_impl(d, grad_dose, active_pixels, n_active, spp, seed, grad, visits, nthreads, NULL);
+}
+
+int oracle_adjoint_surface(const tvam_desc* d, const float* grad_dose, const uint32_t* active_pixels,
+                           uint64_t n_active, uint32_t spp, uint32_t seed, const float* inv_volumes, double* grad,
+                           uint64_t* visits, int nthreads) {
+    return or_adjoint_impl(d, grad_dose, active_pixels, n_active, spp, seed, grad, visits, nthreads, inv_volumes);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Surface-aware discretisation (VolumetricSensor.compute_volume,           */
+/* sensor.py:47-110): per voxel, sample_count points (independent sampler    */
+/* seeded (0, wavefront = voxels), lane = flat voxel index; draws: offset     */
+/* x, y, z, then next_2d), each shot along square_to_uniform_sphere; a point  */
+/* is inside when its origin is strictly inside the mesh bbox and the first  */
+/* target hit faces away (dot(d, n) > 0, n the geometric normal).            */
+/* volumes[2v] = inside, [2v+1] = outside, count * voxel_vol / sample_count  */
+/* in fp32.  UNPINNED like every Mitsuba internal (ray-triangle, sampler).   */
+/* ------------------------------------------------------------------------ */
+int oracle_compute_volume(const tvam_desc* d, uint32_t sample_count, float* volumes, int nthreads) {
+    if (d->n_target_tris <= 0 || !d->target_tris || sample_count == 0) return TVAM_ERR_INVALID;
+    or_scene s;
+    or_scene_init(&s, d);
+    float mb0[3] = {INFINITY, INFINITY, INFINITY}, mb1[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = 0; i < 3 * d->n_target_tris; ++i)
+        for (int k = 0; k < 3; ++k) {
+            mb0[k] = fminf(mb0[k], d->target_tris[3 * i + k]);
+            mb1[k] = fmaxf(mb1[k], d->target_tris[3 * i + k]);
+        }
+    const float vvol = s.h[0] * s.h[1] * s.h[2];
+    const int64_t V = (int64_t)s.res[0] * s.res[1] * s.res[2];
+    if (nthreads < 1) nthreads = 1;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 16) num_threads(nthreads)
+#endif
+    for (int64_t v = 0; v < V; ++v) {
+        const int vx = (int)(v % s.res[0]), vy = (int)((v / s.res[0]) % s.res[1]), vz = (int)(v / ((int64_t)s.res[0] * s.res[1]));
+        const float vox[3] = {(float)vx, (float)vy, (float)vz};
+        or_pcg32 rng;
+        or_sampler_seed(&rng, 0u, (uint64_t)v);
+        uint32_t cin = 0, cout = 0;
+        for (uint32_t i = 0; i < sample_count; ++i) {
+            float off[3];
+            for (int k = 0; k < 3; ++k) off[k] = or_pcg_float(&rng);
+            const float sx = or_pcg_float(&rng), sy = or_pcg_float(&rng);
+            float o[3], dd[3];
+            for (int k = 0; k < 3; ++k) o[k] = d->bbox_min[k] + s.h[k] * (vox[k] + off[k]);
+            const float z = 1.0f - 2.0f * sy, r = sqrtf(fmaxf(1.0f - z * z, 0.0f));
+            dd[0] = r * cosf(OR_TWO_PI * sx);
+            dd[1] = r * sinf(OR_TWO_PI * sx);
+            dd[2] = z;
+            int inside = 0;
+            if (o[0] > mb0[0] && o[1] > mb0[1] && o[2] > mb0[2] && o[0] < mb1[0] && o[1] < mb1[1] && o[2] < mb1[2]) {
+                int tri;
+                const float t = or_target_hit(d, o, dd, &tri);
+                if (t < INFINITY) {
+                    const float* p = d->target_tris + 9 * tri;
+                    float e1[3] = {p[3] - p[0], p[4] - p[1], p[5] - p[2]}, e2[3] = {p[6] - p[0], p[7] - p[1], p[8] - p[2]};
+                    float c[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2],
+                                  e1[0] * e2[1] - e1[1] * e2[0]};
+                    inside = c[0] * dd[0] + c[1] * dd[1] + c[2] * dd[2] > 0.0f;
+                }
+            }
+            if (inside) ++cin;
+            else ++cout;
+        }
+        volumes[2 * v] = (float)cin * vvol / (float)sample_count;
+        volumes[2 * v + 1] = (float)cout * vvol / (float)sample_count;
+    }
     return 0;
 }
 

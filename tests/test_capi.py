@@ -60,7 +60,8 @@ def test_desc_defaults_follow_reference():
     ("vial_r", 0.0, "radius"),
     ("crop_x", 300, "Crop resolution"),
     ("crop_offset_x", 100, "crop offset"),
-    ("film_channels", 2, "surface-aware"),
+    ("film_channels", 2, "No target shape"),  # surface-aware film without a target mesh (sensor.py:60-61)
+    ("film_channels", 3, "film_channels"),
     ("albedo", 0.5, "scattering"),
     ("abi_version", 99, "abi_version"),
 ])

@@ -1,0 +1,123 @@
+"""GPU parity of surface-aware films (film 'surface_aware') against the oracle:
+compute_volume (sensor.py:47-110), the two-channel forward / adjoint with the target mesh cutting
+the medium segments (volume.py:175-218, sensor.py:405-409), visit counts, and an end-to-end
+surface-aware optimisation of the reference's box_hole scene.
+
+Tolerances: forward / adjoint 1e-4 relative L2 (north star); compute_volume draws the same
+samples as the oracle, so all but a few voxels agree exactly (device and host sinf/cosf may
+differ in the last ulp and flip a grazing sample).
+"""
+import copy
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from drtvam_amd.configs import BOX_HOLE_INDEX_MATCHED, benchy_index_matched, cylindrical_refraction, desc_from_config
+from drtvam_amd.engine import Projection
+from drtvam_amd.optimize import optimize
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from test_oracle_surface import cube_tris  # noqa: E402
+from test_setup import box_hole_reference  # noqa: E402
+from drtvam_amd.utils import read_ply  # noqa: E402
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def rel_l2(a, b):
+    a, b = np.asarray(a, np.float64).ravel(), np.asarray(b, np.float64).ravel()
+    return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
+
+
+def box_hole_tris(size=3.0):
+    v, f = read_ply(os.path.join(GOLDEN, "box_hole.ply"))
+    t = np.asarray(v, np.float32)[np.asarray(f)]
+    lo, hi = t.reshape(-1, 3).min(0), t.reshape(-1, 3).max(0)
+    return ((t - 0.5 * (lo + hi)) * (size / np.max(hi - lo))).astype(np.float32)
+
+
+CASES = [
+    dict(vial="index_matched", regular=True, mesh="box"),
+    dict(vial="index_matched", regular=False, mesh="box_hole"),
+    dict(vial="cylindrical", regular=False, mesh="box_hole"),
+]
+
+
+def make(case, N=20, A=10):
+    spp = 1 if case["regular"] else 2
+    if case["vial"] == "index_matched":
+        cfg = benchy_index_matched(N=N, angles=A, size_mm=4.0, r=2.9, regular_sampling=case["regular"], spp=spp)
+    else:
+        cfg = cylindrical_refraction(N=N, angles=A, size_mm=4.0, r_int=3.5, r_ext=4.0, regular_sampling=case["regular"],
+                                     spp=spp)
+    d = desc_from_config(cfg)
+    d.film_channels = 2
+    d.set_target(cube_tris([-1.1, -0.7, -0.9], [0.8, 1.3, 0.6]) if case["mesh"] == "box" else box_hole_tris())
+    return d, spp
+
+
+@pytest.mark.parametrize("case", CASES, ids=lambda c: "-".join(str(v) for v in c.values()))
+def test_surface_forward_adjoint_match_oracle(oracle, case):
+    d, spp = make(case)
+    N, A = 20, 10
+    proj = Projection(d, "cuda:0")
+    vol_gpu = proj.compute_volume(256).cpu().numpy()
+    vol = oracle.compute_volume(d, sample_count=256, nthreads=8)
+    assert np.mean(vol_gpu == vol) > 0.99
+    assert np.abs(vol_gpu - vol).max() <= 3 * (4.0 / N) ** 3 / 256 + 1e-9
+    proj.set_volumes(torch.as_tensor(vol, device="cuda:0"))
+    n = A * N * N
+    rng = np.random.default_rng(0)
+    pat = rng.uniform(0, 0.1, n).astype(np.float32)
+    ref, visits = oracle.forward_surface(d, pat, vol, spp=spp, seed=4, nthreads=8)
+    got = proj.forward(torch.as_tensor(pat, device="cuda:0"), None, spp, 4).cpu().numpy()
+    assert got.shape == (N, N, N, 2)
+    assert rel_l2(got, ref) < 1e-4
+    assert abs(proj.count_visits(spp, 4) - visits) <= max(2, 1e-4 * visits)
+    G = rng.uniform(-1, 1, (N, N, N, 2)).astype(np.float32)
+    gref, _ = oracle.adjoint_surface(d, G, vol, spp=spp, seed=4, nthreads=8)
+    g = proj.adjoint(torch.as_tensor(G, device="cuda:0"), n, None, spp, 4).cpu().numpy()
+    assert rel_l2(g, gref) < 1e-4
+    proj.close()
+
+
+def test_surface_sparse_active_set(oracle):
+    d, spp = make(CASES[1])
+    N, A = 20, 10
+    n = A * N * N
+    vol = oracle.compute_volume(d, sample_count=64, nthreads=8)
+    rng = np.random.default_rng(5)
+    keep = np.sort(rng.choice(n, n // 4, replace=False))
+    a, r = keep // (N * N), keep % (N * N)
+    pix = (a * N * N + r).astype(np.uint32)  # crop == full DMD
+    pat = rng.uniform(0.01, 0.1, keep.size).astype(np.float32)
+    ref, _ = oracle.forward_surface(d, pat, vol, active_pixels=pix, spp=spp, seed=2, nthreads=8)
+    proj = Projection(d, "cuda:0")
+    proj.set_volumes(torch.as_tensor(vol, device="cuda:0"))
+    got = proj.forward(torch.as_tensor(pat, device="cuda:0"), torch.as_tensor(pix.astype(np.int32), device="cuda:0"),
+                       spp, 2).cpu().numpy()
+    assert rel_l2(got, ref) < 1e-4
+
+
+def test_surface_aware_optimization(tmp_path):
+    """box_hole_index_matched.json with a surface-aware optimisation sensor and a plain final
+    sensor (optimize.py:107-116): the final dose thresholded at (tl + tu) / 2 matches the
+    voxelised box-with-hole of test_optimization.py:130-144."""
+    cfg = copy.deepcopy(BOX_HOLE_INDEX_MATCHED)
+    cfg["target"]["filename"] = os.path.join(GOLDEN, "box_hole.ply")
+    cfg["output"] = str(tmp_path)
+    cfg["final_sensor"] = copy.deepcopy(cfg["sensor"])
+    cfg["sensor"]["film"]["surface_aware"] = True
+    vol = optimize(cfg, device="cuda:0").cpu().numpy()[..., 0]
+    th = (cfg["loss"]["tl"] + cfg["loss"]["tu"]) / 2
+    correct = np.mean(np.isclose(box_hole_reference(), vol > th)) * 100
+    print("percentage correct", correct)
+    assert correct > 99.0
+    tgt = np.load(tmp_path / "target.npy")
+    assert tgt.shape == (50, 100, 100, 2)
+    assert (tmp_path / "target_in.exr").exists() and (tmp_path / "target_binary.npy").exists()

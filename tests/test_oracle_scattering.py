@@ -48,8 +48,9 @@ def test_phase_moments(oracle, kind, g, m1, m2, dvec):
     u = (np.arange(n) + 0.5) / n  # stratified grid
     dv = np.asarray(dvec, np.float32)
     mus = []
-    for u1 in u:
-        for u2 in u[::4]:
+    for up in u:  # fine strata on the polar sample: u1 (rayleigh, hg), u2 for isotropic
+        for ua in u[::4]:  # (square_to_uniform_sphere: z = 1 - 2 u.y, phi = 2 pi u.x)
+            u1, u2 = (ua, up) if kind == "isotropic" else (up, ua)
             wo = oracle.phase(d, dv, u1, u2)
             assert abs(np.linalg.norm(wo) - 1.0) < 1e-5
             mus.append(float(np.dot(wo, dv)))

@@ -1,0 +1,147 @@
+"""Oracle for surface-aware films (film 'surface_aware'; sensor.py:47-110,
+:405-409; volume.py:175-218).
+
+Known answers, all against closed-form geometry:
+  * compute_volume: a voxel strictly inside a convex target holds its whole volume in channel 0,
+    one outside the mesh bbox in channel 1; a face through a voxel's mid-plane splits it near
+    1/2 (binomial tolerance); the channels add up to the voxel volume; the inside total matches
+    the mesh's divergence-theorem volume (box and the reference's box_hole.ply);
+  * forward: the channel films add up to the plain (one-channel) film, the target splitting
+    only re-origins segments by the spawn offset; voxels away from the target surface fill one
+    channel only, according to the side they lie on;
+  * adjoint: the exact dot test <A p, G> = <p, A^T G> with two channels.
+"""
+import os
+
+import numpy as np
+import pytest
+
+from drtvam_amd.configs import benchy_index_matched, cylindrical_refraction, desc_from_config
+from drtvam_amd.utils import read_ply
+
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
+
+
+def cube_tris(lo, hi):
+    """Closed axis-aligned box, counter-clockwise seen from outside (outward geometric normals)."""
+    lo, hi = np.asarray(lo, np.float32), np.asarray(hi, np.float32)
+    v = np.array([[lo[0] if i & 1 == 0 else hi[0], lo[1] if i & 2 == 0 else hi[1], lo[2] if i & 4 == 0 else hi[2]]
+                  for i in range(8)], np.float32)
+    quads = [(0, 2, 3, 1), (4, 5, 7, 6), (0, 1, 5, 4), (2, 6, 7, 3), (0, 4, 6, 2), (1, 3, 7, 5)]
+    tris = []
+    for a, b, c, d in quads:
+        tris += [[v[a], v[b], v[c]], [v[a], v[c], v[d]]]
+    t = np.asarray(tris, np.float32)
+    n = np.cross(t[:, 1] - t[:, 0], t[:, 2] - t[:, 0])
+    ctr = t.mean(axis=1) - 0.5 * (lo + hi)
+    assert np.all(np.sum(n * ctr, axis=1) > 0)  # outward
+    return t
+
+
+def mesh_volume(t):
+    return float(np.sum(np.einsum("ij,ij->i", t[:, 0], np.cross(t[:, 1], t[:, 2]))) / 6.0)
+
+
+def sa_desc(N=16, A=8, tris=None, size_mm=4.0, **kw):
+    d = desc_from_config(benchy_index_matched(N=N, angles=A, size_mm=size_mm, r=2.9, **kw))
+    d.film_channels = 2
+    d.set_target(tris)
+    return d
+
+
+def test_compute_volume_box(oracle):
+    # grid [-2, 2]^3 at 8^3 (h = 0.5); box [-1, 1.25] x [-1, 1] x [-0.75, 1]: the faces x = 1.25
+    # and z = -0.75 halve voxels, the others lie on voxel faces
+    N, h = 8, 0.5
+    lo, hi = np.array([-1.0, -1.0, -0.75]), np.array([1.25, 1.0, 1.0])
+    d = sa_desc(N=N, tris=cube_tris(lo, hi))
+    vv = h ** 3
+    vol = oracle.compute_volume(d, sample_count=4096, nthreads=8)
+    assert vol.shape == (N, N, N, 2)
+    np.testing.assert_allclose(vol.sum(-1), vv, rtol=1e-6)
+    e = -2.0 + h * np.arange(N)
+    # exact inside fraction per voxel = product of the per-axis overlaps (film order z, y, x)
+    ov = [np.clip(np.minimum(e + h, hi[a]) - np.maximum(e, lo[a]), 0, None) / h for a in range(3)]
+    frac = ov[2][:, None, None] * ov[1][None, :, None] * ov[0][None, None, :]
+    f = vol[..., 0] / vv
+    np.testing.assert_array_equal(f[frac == 1], 1.0)
+    np.testing.assert_array_equal(f[frac == 0], 0.0)
+    part = (frac > 0) & (frac < 1)
+    assert part.sum() > 0
+    assert np.all(np.abs(f[part] - frac[part]) < 0.04)  # 4096 samples: sd <= 0.008
+    assert vol[..., 0].sum() == pytest.approx(mesh_volume(d._targets), rel=5e-3)
+
+
+def test_compute_volume_box_hole_mesh(oracle):
+    """The reference's box_hole.ply (non-convex) scaled into the grid: inside total = mesh volume."""
+    v, f = read_ply(os.path.join(GOLDEN, "box_hole.ply"))
+    t = np.asarray(v, np.float32)[np.asarray(f)]
+    lo, hi = t.reshape(-1, 3).min(0), t.reshape(-1, 3).max(0)
+    t = ((t - 0.5 * (lo + hi)) * (3.0 / np.max(hi - lo))).astype(np.float32)
+    d = sa_desc(N=12, tris=t)
+    vol = oracle.compute_volume(d, sample_count=512, nthreads=8)
+    mv = abs(mesh_volume(t))
+    assert vol[..., 0].sum() == pytest.approx(mv, rel=0.02)
+    # sample-count independence of the fully inside / outside voxels
+    vol2 = oracle.compute_volume(d, sample_count=64, nthreads=8)
+    sure = (vol[..., 0] == 0) | (vol[..., 1] == 0)
+    assert np.mean(vol2[sure] == vol[sure]) > 0.99
+
+
+@pytest.mark.parametrize("vial", ["index_matched", "cylindrical"])
+def test_channels_add_up_to_plain_film(oracle, vial):
+    N, A = 16, 8
+    tris = cube_tris([-1.1, -0.7, -0.9], [0.8, 1.3, 0.6])
+    if vial == "index_matched":
+        cfg = benchy_index_matched(N=N, angles=A, size_mm=4.0, r=2.9, regular_sampling=False, spp=2)
+    else:
+        cfg = cylindrical_refraction(N=N, angles=A, size_mm=4.0, r_int=3.5, r_ext=4.0, regular_sampling=False, spp=2)
+    d1 = desc_from_config(cfg)
+    d2 = desc_from_config(cfg)
+    d2.film_channels = 2
+    d2.set_target(tris)
+    n = A * N * N
+    pat = np.random.default_rng(0).uniform(0, 0.1, n).astype(np.float32)
+    plain, v1 = oracle.forward(d1, pat, spp=2, seed=3, nthreads=8)
+    vol = oracle.compute_volume(d2, sample_count=64, nthreads=8)
+    sa, v2 = oracle.forward_surface(d2, pat, vol, spp=2, seed=3, nthreads=8)
+    vv = np.prod((np.asarray(d1.bbox_max) - np.asarray(d1.bbox_min)) / N)
+    film = sa[..., 0] * vol[..., 0] + sa[..., 1] * vol[..., 1]
+    # each target crossing re-origins the segment by the spawn offset (1 + max|p|) * RayEpsilon
+    # ~ 3e-4 mm, ~1e-3 of a 0.25 mm voxel chord: the films agree to ~1e-4
+    assert np.linalg.norm(film - plain * vv) / np.linalg.norm(plain * vv) < 1e-3
+    assert v2 >= v1  # segments cut at the target surface revisit the cut voxels
+    # away from the target surface a voxel's film is all in one channel
+    h = 4.0 / N
+    c = -2.0 + h * (np.arange(N) + 0.5)
+    z, y, x = np.meshgrid(c, c, c, indexing="ij")
+    deep_in = (x > -1.1 + h) & (x < 0.8 - h) & (y > -0.7 + h) & (y < 1.3 - h) & (z > -0.9 + h) & (z < 0.6 - h)
+    far_out = (x < -1.1 - h) | (x > 0.8 + h) | (y < -0.7 - h) | (y > 1.3 + h) | (z < -0.9 - h) | (z > 0.6 + h)
+    assert np.all(sa[..., 1][deep_in] == 0) and np.all(sa[..., 0][far_out] == 0)
+    assert np.all(sa[..., 0][deep_in] > 0)
+
+
+def test_adjoint_dot_product(oracle):
+    N, A = 12, 6
+    d = sa_desc(N=N, A=A, tris=cube_tris([-1.0, -0.8, -0.5], [0.9, 1.1, 0.7]), regular_sampling=False, spp=2)
+    vol = oracle.compute_volume(d, sample_count=32, nthreads=8)
+    rng = np.random.default_rng(1)
+    n = A * N * N
+    p = rng.uniform(0, 1, n).astype(np.float32)
+    G = rng.uniform(-1, 1, (N, N, N, 2)).astype(np.float32)
+    Ap, _ = oracle.forward_surface(d, p, vol, spp=2, seed=5, nthreads=8)
+    AtG, _ = oracle.adjoint_surface(d, G, vol, spp=2, seed=5, nthreads=8)
+    lhs = float(np.sum(Ap * G.astype(np.float64)))
+    rhs = float(np.dot(p.astype(np.float64), AtG))
+    assert lhs == pytest.approx(rhs, rel=1e-6)  # delta_L = grad * inv_vol rounds to fp32 (volume.py:130)
+
+
+def test_rejects_scattering_and_missing_mesh(oracle):
+    d = sa_desc(N=8, tris=cube_tris([-1, -1, -1], [1, 1, 1]))
+    d.albedo = 0.5
+    with pytest.raises(ValueError):
+        oracle.forward_surface(d, np.ones(8 * 8 * 8, np.float32), np.ones((8, 8, 8, 2), np.float32))
+    d.albedo = 0.0
+    d.n_target_tris = 0
+    with pytest.raises(ValueError):
+        oracle.forward_surface(d, np.ones(8 * 8 * 8, np.float32), np.ones((8, 8, 8, 2), np.float32))
