@@ -12,7 +12,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libtvam.so")
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 TVAM_OK = 0
 TVAM_ERR_INVALID = -1
@@ -28,6 +28,8 @@ PHASE_ISOTROPIC = 0
 PHASE_RAYLEIGH = 1
 PHASE_HG = 2
 SENSOR_DDA = 0
+SENSOR_RATIO = 1
+SENSOR_DELTA = 2
 
 FLAG_NO_ZERO_SKIP = 1
 FLAG_FWD_STATS = 2
@@ -83,6 +85,7 @@ class TvamDesc(ctypes.Structure):
         ("n_occluder_tris", ctypes.c_int32),
         ("target_tris", ctypes.c_void_p),
         ("n_target_tris", ctypes.c_int32),
+        ("majorant", ctypes.c_float),
     ]
 
     def copy(self) -> "TvamDesc":

@@ -49,6 +49,8 @@ struct TvamConsts {
     int32_t n_occ;
     const float* tgt;    // surface-aware films: target mesh triangles [n_tgt][3][3] (device), else nullptr
     int32_t n_tgt;
+    int32_t sensor_type; // TVAM_SENSOR_* (dda / ratio / delta)
+    float majorant;      // 'ratio' sensor majorant
     float eta_ext, eta_int;     // cylindrical: int/ext IOR of the outer (glass/air) and inner (medium/glass) surface
     // medium / weights
     float sig_t, sig_s;  // scattering media: sigma_t, sigma_s = albedo * sigma_t (fp32, Mitsuba homogeneous)

@@ -126,6 +126,11 @@ void tvam_bin_scratch_free(TvamBinScratch& s);
 hipError_t tvam_launch_surface_paths(int mode, const TvamConsts& k, const TvamTiles& t, const float* pat,
                                      const int32_t* idxmap, const float* gin, const float* vols, float* out,
                                      unsigned long long* counter, hipStream_t stream);
+// General per-path kernel (sample_time, 'ratio' / 'delta' sensors): the whole path
+// loop per (ray, sample), global atomics / gathers (tvam_scatter.hip).
+hipError_t tvam_launch_general_paths(int mode, const TvamConsts& k, const TvamTiles& t, const float* pat,
+                                     const int32_t* idxmap, const float* gin, float* out,
+                                     unsigned long long* counter, hipStream_t stream);
 hipError_t tvam_launch_scale_volumes(int64_t n, const float* vols, float* dose, hipStream_t stream);
 // compute_volume (sensor.py:47-110): volumes [res z][y][x][2]
 hipError_t tvam_launch_volumes(const TvamConsts& k, uint32_t sample_count, float* volumes, hipStream_t stream);

@@ -42,6 +42,7 @@ struct tvam_plan {
     bool empty;  // max_depth too small for any ray to reach the medium
     bool cyl;    // refracting (cylindrical / square) vial: per-ray directions and weights
     bool surface = false;    // surface-aware film (2 channels): per-path kernels cut at the target mesh
+    bool general = false;    // sample_time or a ratio / delta sensor: the general per-path kernel
     float* d_tgt = nullptr;  // target mesh triangles (surface-aware films)
     const float* vols = nullptr;  // caller's compute_volume() output (tvam_plan_set_volumes)
     float* d_occ = nullptr;  // occluder triangles
@@ -169,7 +170,15 @@ static int validate(const tvam_desc& d) {
     if (d.abi_version != TVAM_ABI_VERSION) return fail(TVAM_ERR_INVALID, "tvam_desc.abi_version mismatch");
     if (d.projector_type != TVAM_PROJECTOR_COLLIMATED)
         return fail(TVAM_ERR_UNSUPPORTED, "only the 'collimated' projector is implemented on the GPU path");
-    if (d.sensor_type != TVAM_SENSOR_DDA) return fail(TVAM_ERR_UNSUPPORTED, "only the 'dda' sensor is implemented");
+    if (d.sensor_type != TVAM_SENSOR_DDA && d.sensor_type != TVAM_SENSOR_RATIO && d.sensor_type != TVAM_SENSOR_DELTA)
+        return fail(TVAM_ERR_INVALID, "unknown sensor type");
+    if (d.sensor_type == TVAM_SENSOR_DELTA && d.albedo == 0.0f)  // volume.py:160-161
+        return fail(TVAM_ERR_INVALID, "Tried to render a purely absorptive volume with a delta tracking sensor. This is not supported.");
+    if (d.sensor_type == TVAM_SENSOR_RATIO && !(d.majorant > 0.0f))
+        return fail(TVAM_ERR_INVALID, "the 'ratio' sensor needs a positive majorant");
+    if ((d.sensor_type != TVAM_SENSOR_DDA || d.sample_time) &&
+        (d.film_channels != 1 || d.slab_begin != 0 || (d.slab_end >= 0 && d.slab_end != d.film_res[2])))
+        return fail(TVAM_ERR_UNSUPPORTED, "sample_time and the ratio / delta sensors need a one-channel film without slabs");
     if (d.vial_type != TVAM_VIAL_INDEX_MATCHED && d.vial_type != TVAM_VIAL_CYLINDRICAL &&
         d.vial_type != TVAM_VIAL_SQUARE)
         return fail(TVAM_ERR_UNSUPPORTED, "only the 'index_matched', 'cylindrical' and 'square' containers are implemented on the GPU path");
@@ -192,7 +201,6 @@ static int validate(const tvam_desc& d) {
         if (d.slab_begin != 0 || (d.slab_end >= 0 && d.slab_end != d.film_res[2]))
             return fail(TVAM_ERR_UNSUPPORTED, "scattered paths leave their slice: film slabs need a non-scattering medium");
     }
-    if (d.sample_time) return fail(TVAM_ERR_UNSUPPORTED, "sample_time is not implemented on the GPU path");
     // the medium segment is path vertex 1 (index matched) or 2 (behind two glass
     // surfaces); Russian roulette starts at depth > rr_depth (volume.py:182-185)
     if (d.rr_depth < (d.vial_type == TVAM_VIAL_INDEX_MATCHED ? 1 : 2))
@@ -266,6 +274,8 @@ static TvamConsts make_consts(const tvam_desc& d, int a0, int a1) {
     k.rr_depth = d.rr_depth;
     k.phase_type = d.phase_type;
     k.phase_g = d.phase_g;
+    k.sensor_type = d.sensor_type;
+    k.majorant = d.majorant;
     k.wscale = 0.0f;  // per call
     {
         double hxy = std::max((double)k.h[0], (double)k.h[1]);
@@ -688,6 +698,7 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
     // surfaces + medium segment (volume.py:179, :271-272)
     p->empty = d.max_depth < (p->cyl ? 3 : 2);
     p->surface = d.film_channels == 2;
+    p->general = !p->surface && (d.sample_time || d.sensor_type != TVAM_SENSOR_DDA);
     if (p->surface) {  // target mesh to the device (TvamConsts::tgt)
         std::vector<float> tri(d.target_tris, d.target_tris + 9 * (size_t)d.n_target_tris);
         if ((rc = upload(&p->d_tgt, tri))) {
@@ -867,7 +878,7 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
     p->tiles.tsx = tsx;
     p->tiles.tsy = tsy;
     p->tiles.n_shard = ns;
-    if (!p->surface && (rc = planar_setup(p, cs))) {
+    if (!p->surface && !p->general && (rc = planar_setup(p, cs))) {
         plan_free(p);
         return rc;
     }
@@ -960,7 +971,7 @@ extern "C" int tvam_forward(tvam_plan* p, const float* active_data, const uint32
     size_t V = (size_t)kc.res[0] * kc.res[1] * kc.nz * (p->surface ? 2 : 1);
     hipError_t e;
     if (p->surface && !p->vols) return fail(TVAM_ERR_INVALID, "surface-aware film: call tvam_plan_set_volumes first");
-    if (p->empty || n_active == 0 || p->surface) {
+    if (p->empty || n_active == 0 || p->surface || p->general) {
         e = hipMemsetAsync(dose, 0, V * sizeof(float), stream);
         if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
         if (p->empty || n_active == 0) return 0;
@@ -977,6 +988,13 @@ extern "C" int tvam_forward(tvam_plan* p, const float* active_data, const uint32
             return hip_fail(e, "scatter launch");
         pat = p->d_dense;
         idxmap = p->d_idxmap;
+    }
+    if (p->general) {
+        TvamTiles t = p->tiles;
+        t.spp = spp;
+        t.seed = seed;
+        e = tvam_launch_general_paths(TVAM_MODE_FWD, kc, t, pat, idxmap, nullptr, dose, nullptr, stream);
+        return e == hipSuccess ? 0 : hip_fail(e, "path forward launch");
     }
     if (p->surface) {
         TvamTiles t = p->tiles;
@@ -1048,6 +1066,14 @@ extern "C" int tvam_adjoint(tvam_plan* p, const float* grad_dose, const uint32_t
     }
     if ((e = hipMemsetAsync(grad_active, 0, n_active * sizeof(float), stream)) != hipSuccess)
         return hip_fail(e, "hipMemsetAsync");
+    if (p->general) {
+        if (p->empty) return 0;
+        TvamTiles t = p->tiles;
+        t.spp = spp;
+        t.seed = seed;
+        e = tvam_launch_general_paths(TVAM_MODE_ADJ, k, t, nullptr, idxmap, grad_dose, grad_active, nullptr, stream);
+        return e == hipSuccess ? 0 : hip_fail(e, "path adjoint launch");
+    }
     if (p->surface) {
         if (!p->vols) return fail(TVAM_ERR_INVALID, "surface-aware film: call tvam_plan_set_volumes first");
         if (p->empty) return 0;
@@ -1098,7 +1124,9 @@ extern "C" int tvam_count_visits(tvam_plan* p, uint32_t spp, uint32_t seed, uint
     TvamTiles t = p->tiles;
     t.spp = spp;
     t.seed = seed;
-    if (p->surface) {
+    if (p->general) {
+        e = tvam_launch_general_paths(TVAM_MODE_COUNT, k, t, nullptr, nullptr, nullptr, nullptr, p->d_counter, nullptr);
+    } else if (p->surface) {
         e = tvam_launch_surface_paths(TVAM_MODE_COUNT, k, t, nullptr, nullptr, nullptr, nullptr, nullptr, p->d_counter,
                                       nullptr);
     } else {
@@ -1107,7 +1135,7 @@ extern "C" int tvam_count_visits(tvam_plan* p, uint32_t spp, uint32_t seed, uint
                               nullptr);
     }
     if (e != hipSuccess) return hip_fail(e, "count launch");
-    if (p->desc.albedo != 0.0f) {
+    if (p->desc.albedo != 0.0f && !p->general) {
         e = tvam_launch_scatter_paths(TVAM_MODE_COUNT, k, t, nullptr, nullptr, nullptr, nullptr, p->d_counter, nullptr);
         if (e != hipSuccess) return hip_fail(e, "scatter count launch");
     }

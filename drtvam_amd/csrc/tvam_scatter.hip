@@ -531,6 +531,160 @@ __global__ __launch_bounds__(256) void tvam_surface_kernel(TvamConsts k, TvamTil
     }
 }
 
+// ---------------------------------------------------------------------------
+// General per-path kernel: the whole path loop of volume.py:179-272 per (ray,
+// sample), every medium segment included, for the configurations the planar /
+// tile kernels do not serve:
+//   * sample_time (common.py:101-104): each ray's own rotation angle
+//     2 pi (angle + u) / A, so the rays of one pattern are not parallel;
+//   * the 'ratio' sensor (sensor.py:193-295): deposits at ray(t), t stepping
+//     by -log(1 - u) / majorant (draws inside accumulate), weight
+//     (1 - st / mu)^k st / mu;
+//   * the 'delta' sensor (sensor.py:112-191): a deposit at each medium
+//     interaction (collision estimator, weight 1 with sa / st in wscale).
+// Forward: global float atomics; adjoint: gathers, one atomic per path.
+// Restated op for op in oracle or_trace_estimator / or_trace_scatter.
+// ---------------------------------------------------------------------------
+template <int MODE>
+__device__ __forceinline__ float gp_point(const TvamConsts& k, float px, float py, float pz, float w,
+                                          float* __restrict__ out, const float* __restrict__ gin, uint64_t& nvis) {
+    const int vx = (int)floorf((px - k.bmin[0]) / k.h[0]);
+    const int vy = (int)floorf((py - k.bmin[1]) / k.h[1]);
+    const int vz = (int)floorf((pz - k.bmin[2]) / k.h[2]);
+    if (vx < 0 || vy < 0 || vz < 0 || vx >= k.res[0] || vy >= k.res[1] || vz >= k.res[2]) return 0.0f;
+    const int64_t idx = vx + (int64_t)vy * k.res[0] + (int64_t)vz * k.res[0] * k.res[1];
+    ++nvis;
+    if (MODE == TVAM_MODE_FWD) atomicAdd(&out[idx], w);
+    else if (MODE == TVAM_MODE_ADJ) return w * (gin[idx] * k.inv_vol);
+    return 0.0f;
+}
+
+template <int MODE>
+__global__ __launch_bounds__(256) void tvam_path_kernel(TvamConsts k, TvamTiles tp, const float* __restrict__ pat,
+                                                        const int32_t* __restrict__ idxmap,
+                                                        const float* __restrict__ gin, float* __restrict__ out,
+                                                        unsigned long long* __restrict__ counter) {
+    const int spp = (int)tp.spp;
+    const int64_t per_angle = (int64_t)k.crop_y * k.crop_x;
+    const int64_t n = (int64_t)tp.n_shard * per_angle * spp;
+    const float st = k.sig_t, ss = k.sig_s, mj = k.majorant;
+    const bool has_sc = ss != 0.0f;
+    const int nsurf = k.vial_type == 0 ? 1 : 2;
+    uint64_t nvis = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t local = i / spp;
+        const int smp = (int)(i - local * spp);
+        float em = 1.0f;
+        int64_t act = local;
+        if (MODE == TVAM_MODE_FWD) {
+            const float p = pat[local];
+            if (p == 0.0f && k.skip_zero) continue;
+            em = p * k.wscale * k.inv_vol;
+        } else if (idxmap) {
+            act = idxmap[local];
+            if (act < 0) continue;
+        }
+        const int al = (int)(local / per_angle);
+        const int64_t pix = local - (int64_t)al * per_angle;
+        const int rowc = (int)(pix / k.crop_x), colc = (int)(pix - (int64_t)rowc * k.crop_x);
+        const int64_t dense = local + k.shard_base;
+        TvamPcg rng;
+        rng.seed(tp.seed, (uint64_t)dense * (uint64_t)spp + (uint64_t)smp);
+        float jx = 0.5f, jy = 0.5f;
+        if (!k.regular) {
+            jx = rng.next_float();
+            jy = rng.next_float();
+        }
+        float c, sn;
+        if (k.sample_time) {  // common.py:101-104: time = (angle + u) / n_patterns
+            float time = (float)(k.a0 + al);
+            time = time + rng.next_float();
+            time = time / (float)k.n_patterns;
+            float alpha = TVAM_TWO_PI * time;
+            if (k.clockwise) alpha = -alpha;
+            c = cosf(alpha);
+            sn = sinf(alpha);
+        } else {
+            const float2 csv = tp.cs[al];
+            c = csv.x;
+            sn = csv.y;
+        }
+        (void)rng.next_float();  // aperture sample (projector.py:160)
+        (void)rng.next_float();
+        float xc, yc, ox, oy, oz, dx, dy;
+        tvam_ray_camera(k, k.crop_off_x + colc, k.crop_off_y + rowc, jx, jy, xc, yc);
+        tvam_ray_world(k, c, sn, xc, yc, ox, oy, oz, dx, dy);
+        float o2x, o2y, d2x, d2y, maxt, wgt;
+        if (!tvam_segment(k, ox, oy, oz, dx, dy, o2x, o2y, d2x, d2y, maxt, wgt)) continue;
+        for (int q = 0; q < (has_sc ? 5 : 4) * nsurf; ++q) (void)rng.next_float();  // RR, (medium), BSDF
+        float px = o2x, py = o2y, pz = oz, vx = d2x, vy = d2y, vz = 0.0f;
+        float att = wgt;
+        int depth = nsurf;
+        float acc = 0.0f;
+        for (int seg = 0;; ++seg) {
+            const float q = fminf(0.99f, att);
+            const float u_rr = rng.next_float();
+            if (depth > k.rr_depth) {  // Russian roulette (volume.py:182-185)
+                if (!(u_rr < q)) break;
+                att = att * (1.0f / q);
+            }
+            if (!(att != 0.0f)) break;
+            float tsi = maxt;
+            if (seg > 0) {
+                tsi = sc_container_hit(k, px, py, pz, vx, vy, vz);
+                if (!(tsi < TVAM_INF)) break;
+            }
+            float tmi = TVAM_INF;
+            if (has_sc) tmi = -logf(1.0f - rng.next_float()) / st;
+            const bool reached = !(tmi <= tsi);
+            if (k.sensor_type == TVAM_SENSOR_DDA) {
+                const float r = sc_dda<MODE>(k, px, py, pz, vx, vy, vz, tsi, em * att, out, gin, nvis);
+                if (MODE == TVAM_MODE_ADJ) acc = fmaf(att, r, acc);
+            } else if (k.sensor_type == TVAM_SENSOR_RATIO) {
+                const float ratio = st / mj, keep = 1.0f - ratio;
+                float t = 0.0f, pk = 1.0f;
+                for (int it = 0; it < (1 << 20); ++it) {
+                    t = t + (-logf(1.0f - rng.next_float()) / mj);
+                    if (!(t < tsi)) break;
+                    const float w = att * pk * ratio;
+                    const float r = gp_point<MODE>(k, fmaf(vx, t, px), fmaf(vy, t, py), fmaf(vz, t, pz), em * w, out,
+                                                   gin, nvis);
+                    if (MODE == TVAM_MODE_ADJ) acc += r;  // w * grad * inv_vol (em = 1 in the adjoint)
+                    pk = pk * keep;
+                }
+            } else if (!reached) {  // delta: the medium interaction ray(mei.t)
+                const float r = gp_point<MODE>(k, fmaf(vx, tmi, px), fmaf(vy, tmi, py), fmaf(vz, tmi, pz), em * att,
+                                               out, gin, nvis);
+                if (MODE == TVAM_MODE_ADJ) acc += r;
+            }
+            if (reached) break;  // leaves the medium (transmission only, convex containers)
+            const float tr = expf(-tmi * st);
+            const float pdf = tr * st;
+            const float inv = pdf > 0.0f ? 1.0f / pdf : 0.0f;
+            float w = tr * inv;
+            w = w * ss;
+            (void)rng.next_float();  // phase next_1d
+            const float u1 = rng.next_float(), u2 = rng.next_float();
+            float wx, wy, wz;
+            sc_phase(k, vx, vy, vz, u1, u2, wx, wy, wz);
+            px = fmaf(vx, tmi, px);
+            py = fmaf(vy, tmi, py);
+            pz = fmaf(vz, tmi, pz);
+            vx = wx;
+            vy = wy;
+            vz = wz;
+            att = att * w;
+            ++depth;
+            if (depth >= k.max_depth) break;
+        }
+        if (MODE == TVAM_MODE_ADJ && acc != 0.0f) atomicAdd(&out[act], acc * k.wscale);
+    }
+    if (MODE == TVAM_MODE_COUNT) {
+        for (int off = 32; off > 0; off >>= 1) nvis += __shfl_down(nvis, off, 64);
+        if ((threadIdx.x & 63) == 0 && nvis) atomicAdd(counter, (unsigned long long)nvis);
+    }
+}
+
 __global__ __launch_bounds__(256) void tvam_scale_volumes_kernel(int64_t n, const float* __restrict__ vols,
                                                                  float* __restrict__ dose) {
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
@@ -622,6 +776,29 @@ hipError_t tvam_launch_surface_paths(int mode, const TvamConsts& k, const TvamTi
         default:
             hipLaunchKernelGGL(tvam_surface_kernel<TVAM_MODE_COUNT>, dim3((unsigned)g), dim3(256), 0, stream, k, t,
                                pat, idxmap, gin, vols, out, counter);
+    }
+    return hipGetLastError();
+}
+
+hipError_t tvam_launch_general_paths(int mode, const TvamConsts& k, const TvamTiles& t, const float* pat,
+                                     const int32_t* idxmap, const float* gin, float* out,
+                                     unsigned long long* counter, hipStream_t stream) {
+    const int64_t n = (int64_t)t.n_shard * k.crop_y * k.crop_x * t.spp;
+    int64_t g = (n + 255) / 256;
+    if (g > 262144) g = 262144;
+    if (g < 1) g = 1;
+    switch (mode) {
+        case TVAM_MODE_FWD:
+            hipLaunchKernelGGL(tvam_path_kernel<TVAM_MODE_FWD>, dim3((unsigned)g), dim3(256), 0, stream, k, t, pat,
+                               idxmap, gin, out, counter);
+            break;
+        case TVAM_MODE_ADJ:
+            hipLaunchKernelGGL(tvam_path_kernel<TVAM_MODE_ADJ>, dim3((unsigned)g), dim3(256), 0, stream, k, t, pat,
+                               idxmap, gin, out, counter);
+            break;
+        default:
+            hipLaunchKernelGGL(tvam_path_kernel<TVAM_MODE_COUNT>, dim3((unsigned)g), dim3(256), 0, stream, k, t, pat,
+                               idxmap, gin, out, counter);
     }
     return hipGetLastError();
 }

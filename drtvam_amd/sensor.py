@@ -88,21 +88,32 @@ class DDAVolumetricSensor(VolumetricSensor):
 
 
 class RatioVolumetricSensor(VolumetricSensor):
-    """Ratio-tracking estimator (sensor.py:193-295); not on the GPU path yet."""
+    """Ratio-tracking estimator (sensor.py:193-295): deposits at points stepped by a majorant
+    along every medium segment (the general per-path kernel)."""
 
     def __init__(self, props):
         super().__init__(props)
         self.majorant = props['majorant']
 
+    def to_string(self):
+        return f'RatioVolumetricSensor[\n    majorant = {self.majorant},\n]'
+
     def fill_desc(self, desc):
-        raise NotImplementedError("the 'ratio' sensor is not supported by the GPU engine yet")
+        super().fill_desc(desc)
+        desc.sensor_type = _abi.SENSOR_RATIO
+        desc.majorant = float(self.majorant)
 
 
 class DeltaVolumetricSensor(VolumetricSensor):
-    """Collision estimator (sensor.py:112-191); not on the GPU path yet."""
+    """Collision estimator (sensor.py:112-191): deposits at the medium interactions of
+    scattering media (the general per-path kernel)."""
+
+    def to_string(self):
+        return 'DeltaVolumetricSensor[]'
 
     def fill_desc(self, desc):
-        raise NotImplementedError("the 'delta' sensor is not supported by the GPU engine yet")
+        super().fill_desc(desc)
+        desc.sensor_type = _abi.SENSOR_DELTA
 
 
 sensors = {

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define TVAM_ABI_VERSION 5
+#define TVAM_ABI_VERSION 6
 
 /* error codes */
 #define TVAM_OK               0
@@ -64,7 +64,9 @@ extern "C" {
 #define TVAM_PHASE_RAYLEIGH       1
 #define TVAM_PHASE_HG             2
 /* sensor kinds (sensor.py:442-444) */
-#define TVAM_SENSOR_DDA           0
+#define TVAM_SENSOR_DDA           0  /* analytic absorption per voxel visit (sensor.py:297-440) */
+#define TVAM_SENSOR_RATIO         1  /* ratio tracking at a majorant (sensor.py:193-295) */
+#define TVAM_SENSOR_DELTA         2  /* collision estimator at the medium interactions (sensor.py:112-191) */
 
 /*
  * Scene + integrator description.  Plain old data; every field mirrors a
@@ -136,6 +138,8 @@ typedef struct tvam_desc {
        tvam_plan_create (not kept).  Used when film_channels == 2. */
     const float* target_tris;
     int32_t n_target_tris;
+    /* 'ratio' sensor: its 'majorant' (sensor.py:195) */
+    float   majorant;
 } tvam_desc;
 
 /* tvam_desc.flags */

@@ -27,6 +27,8 @@
  *   path loop         integrators/volume.py:136-282 for the non-scattering,
  *                     transmission-only case: one medium segment per ray
  *   DDA accumulate    sensor.py:306-440 (op for op, fp32 geometry)
+ *   ratio / delta     sensor.py:193-295 (ratio tracking at a majorant) and
+ *     sensors         :112-191 (collision estimator), or_trace_estimator
  *   film              film.py:9-21, :40-41 (layout, scatter-add)
  *   render scale      integrators/volume.py:41-54 (inv_vol), :130 (adjoint)
  *   sampler           Mitsuba 'independent' sampler (TEA-scrambled PCG32),
@@ -804,6 +806,11 @@ static int or_check(const tvam_desc* d) {
     if (d->film_channels != 1 && d->film_channels != 2) return TVAM_ERR_UNSUPPORTED;
     if (d->film_channels == 2 && (d->n_target_tris <= 0 || !d->target_tris)) return TVAM_ERR_INVALID;
     if (d->film_channels == 2 && d->albedo != 0.0f) return TVAM_ERR_UNSUPPORTED;
+    if (d->sensor_type != TVAM_SENSOR_DDA && d->sensor_type != TVAM_SENSOR_RATIO && d->sensor_type != TVAM_SENSOR_DELTA)
+        return TVAM_ERR_INVALID;
+    if (d->sensor_type != TVAM_SENSOR_DDA && d->film_channels == 2) return TVAM_ERR_UNSUPPORTED;
+    if (d->sensor_type == TVAM_SENSOR_DELTA && d->albedo == 0.0f) return TVAM_ERR_INVALID; /* volume.py:160-161 */
+    if (d->sensor_type == TVAM_SENSOR_RATIO && !(d->majorant > 0.0f)) return TVAM_ERR_INVALID;
     if (d->albedo < 0.0f || d->albedo > 1.0f) return TVAM_ERR_INVALID;
     if (d->albedo != 0.0f && !(d->sigma_t > 0.0f)) return TVAM_ERR_INVALID;
     if (d->phase_type < TVAM_PHASE_ISOTROPIC || d->phase_type > TVAM_PHASE_HG) return TVAM_ERR_INVALID;
@@ -811,6 +818,129 @@ static int or_check(const tvam_desc* d) {
        segment (path vertex 1 index matched, 2 behind the glass) is not restated */
     if (d->rr_depth < (d->vial_type == TVAM_VIAL_INDEX_MATCHED ? 1 : 2)) return TVAM_ERR_UNSUPPORTED;
     return 0;
+}
+
+/* Deposit / gather at point p of a medium segment (ratio / delta sensors: the voxel is
+   floor((p - bbox.min) / voxel_size), skipped outside the grid; sensor.py:143-146, :248-252). */
+static double or_point(const or_scene* s, const float p[3], double w, int mode, double* film, const float* grad,
+                       uint64_t* visits) {
+    const tvam_desc* d = s->d;
+    int v[3];
+    for (int k = 0; k < 3; ++k) {
+        v[k] = (int)floorf((p[k] - d->bbox_min[k]) / s->h[k]);
+        if (v[k] < 0 || v[k] >= s->res[k]) return 0.0;
+    }
+    size_t idx = ((size_t)v[0] + (size_t)v[1] * (size_t)s->res[0] + (size_t)v[2] * (size_t)s->res[0] * (size_t)s->res[1]) *
+                 (size_t)s->C;
+    if (visits) ++*visits;
+    if (mode == 0) film[idx] += w;
+    else if (mode == 3) {
+#ifdef _OPENMP
+#pragma omp atomic
+#endif
+        film[idx] += w;
+    } else if (mode == 1) return w * (double)grad[idx];
+    return 0.0;
+}
+
+/* The path loop (volume.py:179-272) with the 'ratio' or 'delta' sensor (sensor.py:112-295):
+   every medium segment [0, si.t) of the path either
+     ratio:  steps t += -log(1 - u) / majorant (one sampler draw per step, inside accumulate,
+             i.e. after the free-flight draw and before the BSDF / phase draws) and deposits
+             att * (sa / st) * em * (1 - st / majorant)^k * st / majorant at ray(t), k = the
+             step's index, while t < si.t;
+     delta:  deposits att * (sa / st) * em at the medium interaction ray(mei.t) when the free
+             flight ends before the surface (mei valid; tr * inv_pdf = 1 / st).
+   Scattering continues the path as in or_trace_scatter; non-scattering media (ratio only:
+   delta needs scattering, volume.py:160-161) have one segment and no free-flight draw. */
+static double or_trace_estimator(const or_scene* s, uint32_t pixel, uint64_t wave_index, uint32_t seed, double em,
+                                 int mode, double* film, const float* grad, uint64_t* visits) {
+    const tvam_desc* d = s->d;
+    or_ray ray;
+    or_pcg32 rng;
+    or_gen_ray_rng(s, pixel, wave_index, seed, &ray, &rng);
+    const int has_sc = d->albedo != 0.0f;
+    float o[3], dd[3], maxt;
+    double attd = 1.0;
+    int nsurf;
+    if (d->vial_type == TVAM_VIAL_CYLINDRICAL || d->vial_type == TVAM_VIAL_SQUARE) {
+        if (!(d->vial_type == TVAM_VIAL_SQUARE ? or_segment_square(s, &ray, o, dd, &maxt, &attd)
+                                               : or_segment_cylindrical(s, &ray, o, dd, &maxt, &attd)))
+            return 0.0;
+        nsurf = 2;
+    } else {
+        if (d->max_depth < 2 || !or_segment_index_matched(s, &ray, o, &maxt)) return 0.0;
+        for (int k = 0; k < 3; ++k) dd[k] = ray.d[k];
+        nsurf = 1;
+    }
+    /* the surface iterations before the medium: RR, (medium), BSDF 1d + 2d */
+    for (int i = 0; i < (has_sc ? 5 : 4) * nsurf; ++i) (void)or_pcg_float(&rng);
+    float att = (float)attd;
+    int depth = nsurf;
+    const float st = d->sigma_t, ss = d->albedo * d->sigma_t;
+    const float mj = d->majorant;
+    double acc = 0.0;
+    for (int seg = 0;; ++seg) {
+        const float q = fminf(0.99f, att);
+        const float u_rr = or_pcg_float(&rng);
+        if (depth > d->rr_depth) {
+            if (!(u_rr < q)) break;
+            att = att * (1.0f / q);
+        }
+        if (!(att != 0.0f)) break;
+        float tsi = maxt;
+        if (seg > 0) {
+            int which;
+            tsi = or_container_hit(s, o, dd, &which);
+            if (!(tsi < INFINITY)) break;
+        }
+        float tmi = INFINITY;
+        if (has_sc) {
+            const float u_m = or_pcg_float(&rng);
+            tmi = -logf(1.0f - u_m) / st;
+        }
+        const int reached = !(tmi <= tsi);
+        const double wseg = (double)att * s->sa_over_st;
+        if (d->sensor_type == TVAM_SENSOR_RATIO) {
+            float t = 0.0f;
+            double pk = 1.0;
+            const double ratio = (double)st / (double)mj;
+            for (int it = 0; it < (1 << 20); ++it) {
+                const float u = or_pcg_float(&rng);
+                t = t + (-logf(1.0f - u) / mj);
+                if (!(t < tsi)) break;
+                float p[3];
+                for (int k = 0; k < 3; ++k) p[k] = fmaf(dd[k], t, o[k]);
+                const double w = wseg * pk * ratio;
+                if (mode == 1) acc += or_point(s, p, w, 1, NULL, grad, visits);
+                else or_point(s, p, w * em, mode, film, NULL, visits);
+                pk *= 1.0 - ratio;
+            }
+        } else if (!reached) { /* delta: the medium interaction */
+            float p[3];
+            for (int k = 0; k < 3; ++k) p[k] = fmaf(dd[k], tmi, o[k]);
+            if (mode == 1) acc += or_point(s, p, wseg, 1, NULL, grad, visits);
+            else or_point(s, p, wseg * em, mode, film, NULL, visits);
+        }
+        if (reached) break;
+        const float tr = expf(-tmi * st);
+        const float pdf = tr * st;
+        const float inv = pdf > 0.0f ? 1.0f / pdf : 0.0f;
+        float w = tr * inv;
+        w = w * ss;
+        (void)or_pcg_float(&rng); /* phase next_1d (unused) */
+        const float u1 = or_pcg_float(&rng), u2 = or_pcg_float(&rng);
+        float wo[3];
+        or_phase_sample(d, dd, u1, u2, wo);
+        for (int k = 0; k < 3; ++k) {
+            o[k] = fmaf(dd[k], tmi, o[k]);
+            dd[k] = wo[k];
+        }
+        att = att * w;
+        ++depth;
+        if (depth >= d->max_depth) break;
+    }
+    return acc;
 }
 
 /* Nearest target-mesh hit along (o, dd) (Moller-Trumbore over every triangle); *tri = its index. */
@@ -893,6 +1023,8 @@ static double or_trace_surface(const or_scene* s, uint32_t pixel, uint64_t wave_
    mode 0: forward, 3: forward with atomic film adds (shared film). */
 static double or_trace(const or_scene* s, uint32_t pixel, uint64_t wave_index, uint32_t seed, double em,
                        int mode, double* film, const float* grad, int only_slice, uint64_t* visits) {
+    if (s->d->sensor_type != TVAM_SENSOR_DDA)
+        return or_trace_estimator(s, pixel, wave_index, seed, em, mode, film, grad, visits);
     if (s->d->albedo != 0.0f)  /* has_scattering (volume.py:159) */
         return or_trace_scatter(s, pixel, wave_index, seed, em, mode, film, grad, visits, s->part);
     if (s->C == 2) return or_trace_surface(s, pixel, wave_index, seed, em, mode, film, grad, only_slice, visits);
@@ -1060,7 +1192,7 @@ static int or_forward_impl(const tvam_desc* d, const float* active_data, const u
     memset(dose, 0, V * (size_t)s.C * sizeof(double));
     double wr = or_ray_weight(d, n_active, spp);
     uint64_t nv_total = 0;
-    if (d->albedo != 0.0f && nthreads > 1) {
+    if ((d->albedo != 0.0f || d->sensor_type != TVAM_SENSOR_DDA) && nthreads > 1) {
         /* scattered paths leave their slice: per-thread films (static
            schedule, fixed-order reduction), or atomics when those would not fit */
         const int priv = (double)V * (double)nthreads * 8.0 <= 2.0e9;
