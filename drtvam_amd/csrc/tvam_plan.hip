@@ -361,6 +361,7 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
         const int es = env_int("TVAM_ADJ_SPLIT", 0);
         if (es >= 1 && es <= 64) split = es;
         p->pl.adj_split = split;
+        p->pl.adj_prefetch = env_int("TVAM_ADJ_PREFETCH", 1);
     }
     if (tvam_planar_rayfwd_lds(p->pl, p->tiles, p->planar_rz) > 160 * 1024) p->planar_rz = 4;
     if (tvam_planar_rayfwd_lds(p->pl, p->tiles, p->planar_rz) > 160 * 1024) return 0;

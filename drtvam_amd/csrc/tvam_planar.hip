@@ -395,7 +395,7 @@ static hipError_t tvam_launch_fwd_planar_z(dim3 grid, size_t lds, hipStream_t st
 // tvam_kernels.hip), marches it once, and accumulates Z dot products; each
 // row of each slice then receives its slice's value (volume.py:274-276).
 // ---------------------------------------------------------------------------
-template <int Z>
+template <int Z, bool PF>
 __global__ __launch_bounds__(TVAM_PB) void tvam_adj_planar_kernel(TvamConsts k, TvamPlanar pl, TvamTiles tp,
                                                                   const int32_t* __restrict__ idxmap,
                                                                   const float* __restrict__ gin,
@@ -440,14 +440,18 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_adj_planar_kernel(TvamConsts k, 
     const int nall = (int)(tp.slot_off[tile_id + 1] - tp.slot_off[tile_id]);
     const int gb = (int)(((int64_t)nall * blockIdx.z) / gridDim.z);
     const int nrt = (int)(((int64_t)nall * (blockIdx.z + 1)) / gridDim.z);
-    for (int g = gb + (int)threadIdx.x; g < nrt; g += TVAM_PB) {
-        const uint32_t e = slots[g];
+    // PF: a two-stage software pipeline over this lane's rays -- the slot of ray
+    // k + 2 and the records of ray k + 1 are loaded while ray k marches
+    int g = gb + (int)threadIdx.x;
+    uint32_t e_n = 0, e_nn = 0;
+    int ri_n = -1;
+    float4 ff_n = make_float4(0.0f, 0.0f, 0.0f, 0.0f), an_n = ff_n;
+    float w_n = 1.0f;
+    auto records = [&](uint32_t e, int& ri, float4& ff, float4& an, float& wray) {
         const int al = (int)(e >> 16), colc = (int)(e & 0xffffu);
-        const int ri = pl.rec_i[(size_t)al * k.crop_x + colc];
-        if (ri < 0) continue;  // misses the vial / grid
-        const float4 ff = pl.rec_f[(size_t)al * k.crop_x + colc];
-        float4 an;
-        float wray = 1.0f;
+        ri = pl.rec_i[(size_t)al * k.crop_x + colc];
+        ff = pl.rec_f[(size_t)al * k.crop_x + colc];
+        wray = 1.0f;
         if (pl.rec_g) {  // refracted ray: its own direction (signed step times) and weight
             const float4 gg = pl.rec_g[(size_t)al * k.crop_x + colc];
             an = make_float4(fabsf(gg.x), fabsf(gg.y), gg.x < 0.0f ? -1.0f : 1.0f, gg.y < 0.0f ? -1.0f : 1.0f);
@@ -455,6 +459,36 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_adj_planar_kernel(TvamConsts k, 
         } else {
             an = tp.ang[al];
         }
+    };
+    if (PF) {
+        if (g < nrt) {
+            e_n = slots[g];
+            records(e_n, ri_n, ff_n, an_n, w_n);
+        }
+        if (g + TVAM_PB < nrt) e_nn = slots[g + TVAM_PB];
+    }
+    for (; g < nrt; g += TVAM_PB) {
+        uint32_t e;
+        int ri;
+        float4 ff, an;
+        float wray;
+        if (PF) {
+            e = e_n;
+            ri = ri_n;
+            ff = ff_n;
+            an = an_n;
+            wray = w_n;
+            if (g + TVAM_PB < nrt) {
+                e_n = e_nn;
+                records(e_n, ri_n, ff_n, an_n, w_n);
+            }
+            if (g + 2 * TVAM_PB < nrt) e_nn = slots[g + 2 * TVAM_PB];
+        } else {
+            e = slots[g];
+            records(e, ri, ff, an, wray);
+        }
+        const int al = (int)(e >> 16), colc = (int)(e & 0xffffu);
+        if (ri < 0) continue;  // misses the vial / grid
         const int svx = ri & 0xffff, svy = ri >> 16;
         const int stx = (int)an.z, sty = (int)an.w;
         float tin0, tout0, tin1, tout1;
@@ -526,12 +560,23 @@ hipError_t tvam_launch_adj_planar(const TvamConsts& k, const TvamPlanar& pl, con
                                   const int32_t* idxmap, const float* gin, float* out, hipStream_t stream) {
     dim3 grid((unsigned)(t.ntx * t.nty), (unsigned)((k.nz + Z - 1) / Z), (unsigned)std::max(pl.adj_split, 1));
     const size_t lds = tvam_planar_adj_lds(pl, t, Z);
+    const bool pf = pl.adj_prefetch != 0;
     switch (Z) {
         case 4:
-            hipLaunchKernelGGL(tvam_adj_planar_kernel<4>, grid, dim3(TVAM_PB), lds, stream, k, pl, t, idxmap, gin, out);
+            if (pf)
+                hipLaunchKernelGGL((tvam_adj_planar_kernel<4, true>), grid, dim3(TVAM_PB), lds, stream, k, pl, t, idxmap,
+                                   gin, out);
+            else
+                hipLaunchKernelGGL((tvam_adj_planar_kernel<4, false>), grid, dim3(TVAM_PB), lds, stream, k, pl, t,
+                                   idxmap, gin, out);
             break;
         case 8:
-            hipLaunchKernelGGL(tvam_adj_planar_kernel<8>, grid, dim3(TVAM_PB), lds, stream, k, pl, t, idxmap, gin, out);
+            if (pf)
+                hipLaunchKernelGGL((tvam_adj_planar_kernel<8, true>), grid, dim3(TVAM_PB), lds, stream, k, pl, t, idxmap,
+                                   gin, out);
+            else
+                hipLaunchKernelGGL((tvam_adj_planar_kernel<8, false>), grid, dim3(TVAM_PB), lds, stream, k, pl, t,
+                                   idxmap, gin, out);
             break;
         default:
             return hipErrorInvalidValue;
