@@ -196,7 +196,11 @@ class FusedLinearLBFGS(LinearLBFGS):
         return st
 
     @torch.no_grad()
-    def step(self, vol, loss):
+    def step(self, vol, loss, loss_dev=None, loss_summed=False):
+        """One L-BFGS step.  loss: the host value, or None with loss_dev (f64 device scalar)
+        read together with the dot vector -- one all-reduce (loss_summed: the ranks' values
+        add up, else every rank holds the same value) and one host sync; returns the loss
+        value (and skips the update when it is exactly 0, the converged case)."""
         import numpy as np
         from . import _abi
         lib = self._lib()
@@ -228,9 +232,20 @@ class FusedLinearLBFGS(LinearLBFGS):
                 st['work'].data_ptr(), st['dots'].data_ptr(), stream))
             nd = 5 * (h + 1) + 1 if new else 2 * h + 1
             dots = st['dots'][:nd]
+            if loss_dev is not None and loss is None:
+                dots = torch.cat([dots, loss_dev.reshape(1).to(torch.float64)])
             if self.allreduce is not None:
                 dots = self.allreduce(dots.clone())
             dv = dots.cpu().numpy().astype(np.float64)
+            if loss_dev is not None and loss is None:
+                lv = float(dv[-1])
+                if self.allreduce is not None and not loss_summed:
+                    import torch.distributed as _d
+                    lv = lv / _d.get_world_size()
+                loss = lv
+                dv = dv[:-1]
+                if loss == 0.0:  # converged (optimize.py:305-307): no update
+                    return loss
             if new:
                 st['free'].pop(0)
                 st['slots'].append(slot)
@@ -300,3 +315,4 @@ class FusedLinearLBFGS(LinearLBFGS):
             _abi.check(lib.tvam_axpy_clamp(pf.numel(), pf.data_ptr(), float(alpha), search[k].data_ptr(), lo,
                                            out.data_ptr(), self._stream(pf.device)))
             self.variables[k] = out.reshape(p.shape).requires_grad_(True)
+        return float(loss)

@@ -152,15 +152,18 @@ class ShardedLoop:
         return self.adjoint_local(grad_vol, seed)
 
     # ---- loss -------------------------------------------------------------------
-    def loss_value_grad(self, vol, x):
+    def loss_value_grad(self, vol, x, reduce=True):
         """(loss f64 device scalar, dL/dvol) — fused kernel or torch autograd.  The film
-        term is summed over the slabs when the dose is sharded; the sparsity term
-        (loss.py:54-59) is added once, summed over the pattern shards."""
+        term is summed over the slabs when the dose is sharded (reduce=False leaves this
+        rank's slab term, for a caller that folds the sum into a later all-reduce); the
+        sparsity term (loss.py:54-59) is added once, summed over the pattern shards."""
         s = self.sparsity(x)
         if self.fused:
             v = self.loss_fn.fused_value_grad(vol, self.target, None, self.grad_vol, count=self.n_vox)
-            if self.dose_sharded:
+            if self.dose_sharded and reduce:
                 v = self.allreduce_(v)
+            if s is not None and not reduce and self.dose_sharded and self.dist is not None:
+                s = s / self.dist.get_world_size()  # summed again with the slab terms
             return (v if s is None else v + s), self.grad_vol
         vv = vol.detach().requires_grad_(True)
         with torch.enable_grad():
@@ -209,6 +212,19 @@ class ShardedLoop:
         self._seed = i
         x = self.opt[key]
         vol = self.forward(x, i)
+        if isinstance(self.opt, FusedLinearLBFGS) and self.fused:
+            # The loss value is read with the L-BFGS dot vector: the adjoint and the history
+            # pass run first, and one collective + one host sync carry both (the reference
+            # reads the loss right away, optimize.py:303; the value and the update agree).
+            loss, gvol = self.loss_value_grad(vol, x, reduce=False)
+            g = self.adjoint(gvol, i)
+            sg = self.sparsity_grad(x)
+            if sg is not None:
+                g = g + sg
+            x.grad = g
+            loss_v = self.opt.step(vol, None, loss_dev=loss, loss_summed=self.dose_sharded)
+            self.loss_hist.append(loss_v)
+            return loss_v
         loss, gvol = self.loss_value_grad(vol, x)
         loss_v = float(loss)  # host sync, optimize.py:303
         self.loss_hist.append(loss_v)
