@@ -473,6 +473,10 @@ static bool planar_fwd_setup(tvam_plan* p, const std::vector<float2>& cs, const 
         for (int z = 0; z < k.nz; ++z) multi |= off[z + 1] - off[z] > 1;
         p->pl.fwd_multi = multi ? 1 : 0;
     }
+    {
+        const int ab = env_int("TVAM_FWD_AB", 2);
+        p->pl.fwd_ab = ab == 4 ? 4 : (ab == 1 ? 1 : 2);
+    }
     if (p->planar_fz == 0) {
         // slices per workgroup: the fewest padded slice-passes ceil(nz / Z) * (Z + 4)
         // (the +4 prices the per-angle candidate geometry shared by the Z slices)

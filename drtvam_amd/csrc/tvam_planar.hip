@@ -106,22 +106,22 @@ __host__ __device__ constexpr int tvam_fwd_zs(int Z) { return ((Z + 4) / 4) % 2 
 // Z: slices per thread; NC: candidate DMD columns per (voxel, angle), a
 // bound the plan derives from the voxel's lateral width in columns; MULTI:
 // some slice collects several DMD rows; PF: staged values per thread.
-template <int Z, int NC, bool MULTI, int PF>
+template <int Z, int NC, bool MULTI, int PF, int AB>
 __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, TvamPlanar pl,
                                                                   const float* __restrict__ pat,
                                                                   float* __restrict__ dose) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int ncm = pl.ncmax;
-    // [2][ncm][ZS] (double buffer), ZS = tvam_fwd_zs(Z)
+    // [2][AB][ncm][ZS] (double buffer of AB angles per barrier), ZS = tvam_fwd_zs(Z)
     constexpr int ZS = tvam_fwd_zs(Z);
     float* s_p = reinterpret_cast<float*>(smem);
-    float4* s_r = reinterpret_cast<float4*>(s_p + 2 * ncm * ZS);  // [2][ncm]
+    float4* s_r = reinterpret_cast<float4*>(s_p + 2 * AB * ncm * ZS);  // [2][AB][ncm]
     // per-angle constants of TVAM_ACH (+2 look-ahead) angles, copied to LDS so the
     // angle loop issues no scalar loads (an s_load's lgkmcnt wait would also
     // drain every outstanding LDS read)
-    float4* s_ang = reinterpret_cast<float4*>(s_r + 2 * ncm);     // [TVAM_ACH + 2][2]
-    int* s_cb = reinterpret_cast<int*>(s_ang + 2 * (TVAM_ACH + 2)); // [TVAM_ACH + 2]
-    int* s_row = s_cb + (TVAM_ACH + 2);                            // [Z]: the slice's row, -1 none, -2 several
+    float4* s_ang = reinterpret_cast<float4*>(s_r + 2 * AB * ncm);  // [TVAM_ACH + 4][2]
+    int* s_cb = reinterpret_cast<int*>(s_ang + 2 * (TVAM_ACH + 4)); // [TVAM_ACH + 4]
+    int* s_row = s_cb + (TVAM_ACH + 4);                            // [Z]: the slice's row, -1 none, -2 several
 
     const int ntx = (k.res[0] + 15) >> 4, nty = (k.res[1] + 15) >> 4;
     const int ntiles = ntx * nty, nwg1 = ntiles * ((k.nz + Z - 1) / Z);
@@ -164,7 +164,7 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
     const int ns = pl.ns;
     int tbase = ab;
     auto load_table = [&](int base) {
-        for (int i = threadIdx.x; i < TVAM_ACH + 2; i += TVAM_PB) {
+        for (int i = threadIdx.x; i < TVAM_ACH + 4; i += TVAM_PB) {
             const int a = base + i;
             if (a < ns) {
                 s_ang[2 * i] = pl.fwd_ang[2 * a];
@@ -223,6 +223,7 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
         S.rv = make_float4(0.0f, 0.0f, -1.0f, 0.0f);
         if ((int)threadIdx.x < ncm && (unsigned)col < (unsigned)k.crop_x) S.rv = pl.vox[(size_t)al * k.crop_x + col];
     };
+    // buffer b = (double-buffer half) * AB + (angle within the barrier group)
     auto store = [&](int buf, const Stage& S) {
         float* sp = s_p + buf * ncm * ZS;
 #pragma unroll
@@ -285,19 +286,33 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
     // Software pipeline over angles: angle a is computed from LDS buffer a & 1
     // while the loads of angle a + 1 are in flight in registers.
     if (ab < ae) {
-        Stage S;
-        fetch(ab, S);
-        store(0, S);
+        // AB angles per barrier: the next group's global loads are in flight in
+        // registers while this group is computed from LDS
+        Stage S[AB];
+#pragma unroll
+        for (int j = 0; j < AB; ++j)
+            if (ab + j < ae) fetch(ab + j, S[j]);
+#pragma unroll
+        for (int j = 0; j < AB; ++j)
+            if (ab + j < ae) store(j, S[j]);
         __syncthreads();
-        for (int al = ab; al < ae; ++al) {
-            if (al - tbase == TVAM_ACH) {  // next chunk of per-angle constants
+        int half = 0;
+        for (int al = ab; al < ae; al += AB) {
+            if (al - tbase > TVAM_ACH + 4 - 2 * AB) {  // next chunk of per-angle constants
                 tbase = al;
                 load_table(al);
                 __syncthreads();
             }
-            if (al + 1 < ae) fetch(al + 1, S);
-            compute(al, (al - ab) & 1);
-            if (al + 1 < ae) store((al + 1 - ab) & 1, S);
+#pragma unroll
+            for (int j = 0; j < AB; ++j)
+                if (al + AB + j < ae) fetch(al + AB + j, S[j]);
+#pragma unroll
+            for (int j = 0; j < AB; ++j)
+                if (al + j < ae) compute(al + j, half * AB + j);
+            half ^= 1;
+#pragma unroll
+            for (int j = 0; j < AB; ++j)
+                if (al + AB + j < ae) store(half * AB + j, S[j]);
             __syncthreads();
         }
     }
@@ -323,8 +338,9 @@ __global__ __launch_bounds__(256) void tvam_fwd_parts_kernel(int64_t n, int part
 }
 
 size_t tvam_planar_fwd_lds(const TvamPlanar& pl, int Z) {
-    return 2 * ((size_t)pl.ncmax * tvam_fwd_zs(Z) * sizeof(float) + (size_t)pl.ncmax * sizeof(float4)) +
-           (size_t)(TVAM_ACH + 2) * (2 * sizeof(float4) + sizeof(int)) + (size_t)Z * sizeof(int);
+    const int ab = pl.fwd_ab > 1 ? pl.fwd_ab : 1;
+    return 2 * ab * ((size_t)pl.ncmax * tvam_fwd_zs(Z) * sizeof(float) + (size_t)pl.ncmax * sizeof(float4)) +
+           (size_t)(TVAM_ACH + 4) * (2 * sizeof(float4) + sizeof(int)) + (size_t)Z * sizeof(int);
 }
 
 bool tvam_planar_fwd_fits(const TvamPlanar& pl, int Z) {
@@ -336,11 +352,15 @@ template <int Z, int NC>
 static void launch_fwd(dim3 grid, size_t lds, hipStream_t stream, const TvamConsts& k, const TvamPlanar& pl,
                        const float* pat, float* dose) {
     if (pl.fwd_multi)
-        hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, true, 4>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
+        hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, true, 4, 1>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
     else if (pl.fwd_pf == 2)
-        hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 2>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
+        hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 2, 1>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
+    else if (NC == 2 && pl.fwd_ab == 4)
+        hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 4, 4>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
+    else if (NC == 2 && pl.fwd_ab == 2)
+        hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 4, 2>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
     else
-        hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 4>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
+        hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 4, 1>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
 }
 
 template <int Z>

@@ -3,7 +3,7 @@
 
   * a 2-angle shard of the full-size scene (the exact per-angle plan the 8-way angle
     sharding uses) against the CPU oracle: forward dose and adjoint gradient within 1e-4
-    relative L2, visit counts equal;
+    relative L2, visit counts equal up to the end-voxel rounding deviation of DESIGN.md section 2;
   * the adjoint identity <A p, G> = <p, A^T G> over all 400 angles (fp64 sums);
   * linearity A(a p + b q) = a A p + b A q;
   * the sum of shard forwards = the full forward (angle sharding is exact up to fp32 sums).
@@ -49,7 +49,8 @@ def test_angle_shard_matches_oracle(oracle):
     # the oracle's ray weight uses its own active-set size (n); the shard plan its shard
     # size (n as well): same weight
     assert rel_l2(got, ref) < 1e-4
-    assert proj.count_visits(1, 0) == visits
+    # visit counts agree up to the documented end-voxel rounding deviation
+    assert abs(proj.count_visits(1, 0) - visits) <= max(2, 1e-4 * visits)
     G = rng.uniform(-1, 1, (N, N, N)).astype(np.float32)
     g = proj.adjoint(torch.as_tensor(G, device=DEV), n, None, 1, 0).cpu().numpy()
     gref, _ = oracle.adjoint(dfull, G, active_pixels=pix, nthreads=16)
