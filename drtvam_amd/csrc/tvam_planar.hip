@@ -415,8 +415,8 @@ static hipError_t tvam_launch_fwd_planar_z(dim3 grid, size_t lds, hipStream_t st
 // tvam_kernels.hip), marches it once, and accumulates Z dot products; each
 // row of each slice then receives its slice's value (volume.py:274-276).
 // ---------------------------------------------------------------------------
-template <int Z, bool PF>
-__global__ __launch_bounds__(TVAM_PB) void tvam_adj_planar_kernel(TvamConsts k, TvamPlanar pl, TvamTiles tp,
+template <int Z, bool PF, int NT>
+__global__ __launch_bounds__(NT) void tvam_adj_planar_kernel(TvamConsts k, TvamPlanar pl, TvamTiles tp,
                                                                   const int32_t* __restrict__ idxmap,
                                                                   const float* __restrict__ gin,
                                                                   float* __restrict__ out) {
@@ -434,7 +434,7 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_adj_planar_kernel(TvamConsts k, 
     const size_t plane = (size_t)k.res[0] * k.res[1];
 
     // gradient tile, [voxel][z], scaled by 1/voxel volume (volume.py:130)
-    for (int i = threadIdx.x; i < tw * th * Z; i += TVAM_PB) {
+    for (int i = threadIdx.x; i < tw * th * Z; i += NT) {
         const int z = i / (tw * th), li = i - z * (tw * th);
         const int ly = li / tw - 1, lx = li - (ly + 1) * tw - 1;
         float v = 0.0f;
@@ -485,9 +485,9 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_adj_planar_kernel(TvamConsts k, 
             e_n = slots[g];
             records(e_n, ri_n, ff_n, an_n, w_n);
         }
-        if (g + TVAM_PB < nrt) e_nn = slots[g + TVAM_PB];
+        if (g + NT < nrt) e_nn = slots[g + NT];
     }
-    for (; g < nrt; g += TVAM_PB) {
+    for (; g < nrt; g += NT) {
         uint32_t e;
         int ri;
         float4 ff, an;
@@ -498,11 +498,11 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_adj_planar_kernel(TvamConsts k, 
             ff = ff_n;
             an = an_n;
             wray = w_n;
-            if (g + TVAM_PB < nrt) {
+            if (g + NT < nrt) {
                 e_n = e_nn;
                 records(e_n, ri_n, ff_n, an_n, w_n);
             }
-            if (g + 2 * TVAM_PB < nrt) e_nn = slots[g + 2 * TVAM_PB];
+            if (g + 2 * NT < nrt) e_nn = slots[g + 2 * NT];
         } else {
             e = slots[g];
             records(e, ri, ff, an, wray);
@@ -581,26 +581,24 @@ hipError_t tvam_launch_adj_planar(const TvamConsts& k, const TvamPlanar& pl, con
     dim3 grid((unsigned)(t.ntx * t.nty), (unsigned)((k.nz + Z - 1) / Z), (unsigned)std::max(pl.adj_split, 1));
     const size_t lds = tvam_planar_adj_lds(pl, t, Z);
     const bool pf = pl.adj_prefetch != 0;
+    // 512-thread workgroups (adj_nt): the LDS tile (28 KB at 40 x 40 x 4) admits 5
+    // workgroups per CU, i.e. 5 waves per SIMD at 256 threads, 8 at 512
+#define TVAM_ADJ_LAUNCH(ZZ)                                                                                        \
+    if (pl.adj_nt == 512)                                                                                          \
+        hipLaunchKernelGGL((tvam_adj_planar_kernel<ZZ, true, 512>), grid, dim3(512), lds, stream, k, pl, t, idxmap,  \
+                           gin, out);                                                                              \
+    else if (pf)                                                                                                   \
+        hipLaunchKernelGGL((tvam_adj_planar_kernel<ZZ, true, 256>), grid, dim3(256), lds, stream, k, pl, t, idxmap,  \
+                           gin, out);                                                                              \
+    else                                                                                                           \
+        hipLaunchKernelGGL((tvam_adj_planar_kernel<ZZ, false, 256>), grid, dim3(256), lds, stream, k, pl, t, idxmap, \
+                           gin, out);
     switch (Z) {
-        case 4:
-            if (pf)
-                hipLaunchKernelGGL((tvam_adj_planar_kernel<4, true>), grid, dim3(TVAM_PB), lds, stream, k, pl, t, idxmap,
-                                   gin, out);
-            else
-                hipLaunchKernelGGL((tvam_adj_planar_kernel<4, false>), grid, dim3(TVAM_PB), lds, stream, k, pl, t,
-                                   idxmap, gin, out);
-            break;
-        case 8:
-            if (pf)
-                hipLaunchKernelGGL((tvam_adj_planar_kernel<8, true>), grid, dim3(TVAM_PB), lds, stream, k, pl, t, idxmap,
-                                   gin, out);
-            else
-                hipLaunchKernelGGL((tvam_adj_planar_kernel<8, false>), grid, dim3(TVAM_PB), lds, stream, k, pl, t,
-                                   idxmap, gin, out);
-            break;
-        default:
-            return hipErrorInvalidValue;
+        case 4: TVAM_ADJ_LAUNCH(4) break;
+        case 8: TVAM_ADJ_LAUNCH(8) break;
+        default: return hipErrorInvalidValue;
     }
+#undef TVAM_ADJ_LAUNCH
     return hipGetLastError();
 }
 
