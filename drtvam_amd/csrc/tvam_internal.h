@@ -48,6 +48,7 @@ struct TvamPlanar {
     int32_t adj_split;         // adjoint: workgroups sharing one (tile, slice chunk)'s ray list (thin slabs)
     int32_t adj_prefetch;      // adjoint: software-pipelined record loads (slot k + 2, records k + 1)
     int32_t adj_nt;            // adjoint: threads per workgroup (256 or 512)
+    int32_t rayfwd_nt;         // ray-driven forward: threads per workgroup (256 or 512)
     int32_t fwd_parts;         // forward: angle parts per (tile, slice chunk) (thin slabs; 1 = none)
     int32_t fwd_ab;            // forward: angles per barrier (1 or 2)
     float* fwd_part;           // forward: [fwd_parts][nz][res_y][res_x] partial doses when fwd_parts > 1

@@ -365,6 +365,7 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
         p->pl.adj_split = split;
         p->pl.adj_prefetch = env_int("TVAM_ADJ_PREFETCH", 1);
         p->pl.adj_nt = env_int("TVAM_ADJ_NT", 512) == 256 ? 256 : 512;
+        p->pl.rayfwd_nt = env_int("TVAM_RAYFWD_NT", 512) == 256 ? 256 : 512;
     }
     if (tvam_planar_rayfwd_lds(p->pl, p->tiles, p->planar_rz) > 160 * 1024) p->planar_rz = 4;
     if (tvam_planar_rayfwd_lds(p->pl, p->tiles, p->planar_rz) > 160 * 1024) return 0;

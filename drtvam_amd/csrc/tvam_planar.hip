@@ -696,7 +696,7 @@ __device__ __forceinline__ void fwd_rays_body(const TvamConsts& k, const TvamPla
     const uint32_t* slots = tp.slots + tp.slot_off[tile_id];
     const int nrt = (int)(tp.slot_off[tile_id + 1] - tp.slot_off[tile_id]);
     const int64_t per_angle = (int64_t)k.crop_y * k.crop_x;
-    for (int g = threadIdx.x; g < nrt; g += TVAM_PB) {
+    for (int g = threadIdx.x; g < nrt; g += (int)blockDim.x) {
         const uint32_t e = slots[g];
         const int al = (int)(e >> 16), colc = (int)(e & 0xffffu);
         const int ri = pl.rec_i[(size_t)al * k.crop_x + colc];
@@ -769,7 +769,7 @@ __device__ __forceinline__ void fwd_rays_body(const TvamConsts& k, const TvamPla
 }
 
 template <int Z>
-__global__ __launch_bounds__(TVAM_PB) void tvam_fwd_rays_planar_kernel(TvamConsts k, TvamPlanar pl, TvamTiles tp,
+__global__ __launch_bounds__(512) void tvam_fwd_rays_planar_kernel(TvamConsts k, TvamPlanar pl, TvamTiles tp,
                                                                        const float* __restrict__ pat,
                                                                        const float* __restrict__ scale,
                                                                        float* __restrict__ dose) {
@@ -789,7 +789,7 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_rays_planar_kernel(TvamConst
     const float fscale = scale[0];
     const bool fixed = scale[1] != 0.0f;
 
-    for (int i = threadIdx.x; i < pw * Z; i += TVAM_PB) itile[i] = 0;  // 0 == 0.0f
+    for (int i = threadIdx.x; i < pw * Z; i += (int)blockDim.x) itile[i] = 0;  // 0 == 0.0f
     if (threadIdx.x == 0) {
         int n = 0;
         for (int z = 0; z < Z; ++z) {
@@ -811,7 +811,7 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_rays_planar_kernel(TvamConst
     const float outscale = k.inv_vol / fscale;
     const float* ftile = reinterpret_cast<const float*>(smem);
     for (int z = 0; z < Z && z0 + z < k.nz; ++z)
-        for (int i = threadIdx.x; i < wx * wy; i += TVAM_PB) {
+        for (int i = threadIdx.x; i < wx * wy; i += (int)blockDim.x) {
             const int ly = i / wx, lx = i - ly * wx;
             const size_t li = (size_t)z * pw + (size_t)(ly + 1) * tw + (lx + 1);
             const float v = fixed ? (float)itile[li] * outscale : ftile[li] * k.inv_vol;
@@ -831,14 +831,13 @@ hipError_t tvam_launch_fwd_rays_planar(const TvamConsts& k, const TvamPlanar& pl
     hipLaunchKernelGGL(tvam_fwd_scale_kernel, dim3(1), dim3(256), 0, stream, k, pl.ns, pl.max_rows_slice, amax, scale);
     dim3 grid((unsigned)(t.ntx * t.nty), (unsigned)((k.nz + Z - 1) / Z));
     const size_t lds = tvam_planar_rayfwd_lds(pl, t, Z);
+    const dim3 block(pl.rayfwd_nt == 512 ? 512 : 256);
     switch (Z) {
         case 4:
-            hipLaunchKernelGGL(tvam_fwd_rays_planar_kernel<4>, grid, dim3(TVAM_PB), lds, stream, k, pl, t, pat, scale,
-                               dose);
+            hipLaunchKernelGGL(tvam_fwd_rays_planar_kernel<4>, grid, block, lds, stream, k, pl, t, pat, scale, dose);
             break;
         case 8:
-            hipLaunchKernelGGL(tvam_fwd_rays_planar_kernel<8>, grid, dim3(TVAM_PB), lds, stream, k, pl, t, pat, scale,
-                               dose);
+            hipLaunchKernelGGL(tvam_fwd_rays_planar_kernel<8>, grid, block, lds, stream, k, pl, t, pat, scale, dose);
             break;
         default:
             return hipErrorInvalidValue;
