@@ -36,7 +36,7 @@ FLAG_FWD_STATS = 2
 FLAG_NO_PLANAR = 4
 FLAG_RAY_FWD = 8
 FLAG_SCATTER_ATOMIC = 16
-LBFGS_WORK_DOUBLES = 512 * 64
+LBFGS_WORK_DOUBLES = 2048 * 64
 
 
 class TvamDesc(ctypes.Structure):

@@ -17,8 +17,25 @@
 #include "tvam_internal.h"
 
 #define TVAM_VB 256       // threads per block
-#define TVAM_VGRID 512    // blocks of the reduction kernels (work[] holds TVAM_VGRID * ndots doubles)
+#define TVAM_VGRID_MAX 2048  // most blocks of the reduction kernels (work[] holds grid * ndots doubles)
 #define TVAM_HMAX 8
+
+#include <cstdlib>
+
+// launch geometry knobs (read once): blocks of the history pass and of the direction pass
+static int vec_knob(const char* name, int def) {
+    const char* v = std::getenv(name);
+    const int x = v && *v ? std::atoi(v) : def;
+    return x > 0 ? x : def;
+}
+static int hist_grid() {
+    static const int g = std::min(vec_knob("TVAM_VEC_HGRID", 768), TVAM_VGRID_MAX);
+    return g;
+}
+static int dir_grid() {
+    static const int g = vec_knob("TVAM_VEC_DGRID", 1024);
+    return g;
+}
 
 struct VecPtrs {
     const float* s[TVAM_HMAX];
@@ -143,12 +160,12 @@ __global__ __launch_bounds__(TVAM_VB) void tvam_lbfgs_hist_kernel(uint64_t n, co
 }
 
 // Sum the per-block partials of dot d over the blocks, in block order.
-__global__ __launch_bounds__(TVAM_VB) void tvam_partials_kernel(int nd, const double* __restrict__ work,
+__global__ __launch_bounds__(TVAM_VB) void tvam_partials_kernel(int nd, int nblocks, const double* __restrict__ work,
                                                                 double* __restrict__ dots) {
     __shared__ double red[TVAM_VB / 64];
     const int d = blockIdx.x;
     double s = 0.0;
-    for (int b = threadIdx.x; b < TVAM_VGRID; b += TVAM_VB) s += work[(size_t)b * nd + d];
+    for (int b = threadIdx.x; b < nblocks; b += TVAM_VB) s += work[(size_t)b * nd + d];
     s = warp_sum(s);
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = s;
     __syncthreads();
@@ -163,10 +180,11 @@ template <int H, bool NEW>
 static hipError_t launch_hist(uint64_t n, const float* p, const float* p_old, const float* g, const float* g_old,
                               const VecPtrs& hv, float* s_new, float* y_new, double* work, double* dots,
                               hipStream_t stream) {
-    hipLaunchKernelGGL((tvam_lbfgs_hist_kernel<H, NEW>), dim3(TVAM_VGRID), dim3(TVAM_VB), 0, stream, n, p, p_old, g,
+    const int nb = hist_grid();
+    hipLaunchKernelGGL((tvam_lbfgs_hist_kernel<H, NEW>), dim3(nb), dim3(TVAM_VB), 0, stream, n, p, p_old, g,
                        g_old, hv, s_new, y_new, work);
     hipLaunchKernelGGL(tvam_partials_kernel, dim3(HistLayout<H, NEW>::ND), dim3(TVAM_VB), 0, stream,
-                       HistLayout<H, NEW>::ND, work, dots);
+                       HistLayout<H, NEW>::ND, nb, work, dots);
     return hipGetLastError();
 }
 
@@ -240,7 +258,7 @@ hipError_t tvam_launch_lbfgs_direction(uint64_t n, const float* g, int h, const 
         c.cs[j] = cs[j];
         c.cy[j] = cy[j];
     }
-    const dim3 grid(2048), block(TVAM_VB);
+    const dim3 grid(dir_grid()), block(TVAM_VB);
     switch (h) {
 #define TVAM_H(H) \
     case H: hipLaunchKernelGGL(tvam_lbfgs_dir_kernel<H>, grid, block, 0, stream, n, g, hv, c, d); break;

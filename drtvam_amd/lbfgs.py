@@ -20,6 +20,11 @@ def _dot(a, b):
     return torch.dot(a, b)
 
 
+
+def _abi_work_doubles():
+    from ._abi import LBFGS_WORK_DOUBLES
+    return LBFGS_WORK_DOUBLES
+
 class LinearLBFGS:
     def __init__(self, lr=1.0, m=5, params=None, render_fn=None, loss_fn=None, search_it=20, dot=None,
                  loss_step=None):
@@ -189,7 +194,7 @@ class FusedLinearLBFGS(LinearLBFGS):
             st = {'n': n, 't': 0, 'slots': [], 'free': list(range(self.m)), 'p_old': None, 'g_old': None,
                   'S': torch.empty((self.m, npad), dtype=torch.float32, device=dev)[:, :n],
                   'Y': torch.empty((self.m, npad), dtype=torch.float32, device=dev)[:, :n],
-                  'work': torch.empty(512 * 64, dtype=torch.float64, device=dev),
+                  'work': torch.empty(_abi_work_doubles(), dtype=torch.float64, device=dev),
                   'dots': torch.empty(5 * (self.m + 1) + 1, dtype=torch.float64, device=dev),
                   'SY': {}, 'YY': {}}
             self.state[k] = st

@@ -230,7 +230,7 @@ int tvam_plan_path(const tvam_plan* plan);
  * tvam_lbfgs_direction: d = cg g + sum_j (cs[j] S[j] + cy[j] Y[j]), h <= 8.
  * tvam_axpy_clamp: out = max(p + alpha d, lo) (out may alias p).
  */
-#define TVAM_LBFGS_WORK_DOUBLES (512 * 64)
+#define TVAM_LBFGS_WORK_DOUBLES (2048 * 64)
 int tvam_lbfgs_history(uint64_t n, const float* p, const float* p_old, const float* g, const float* g_old,
                        int32_t h, const float* const* S, const float* const* Y, float* s_new, float* y_new,
                        double* work, double* dots, void* hip_stream);
