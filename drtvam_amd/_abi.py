@@ -10,7 +10,7 @@ import os
 import threading
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libtvam.so")
+LIB_PATH = os.environ.get("TVAM_LIB") or os.path.join(_HERE, "libtvam.so")  # TVAM_LIB: a variant build
 
 ABI_VERSION = 6
 

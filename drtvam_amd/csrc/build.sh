@@ -9,6 +9,6 @@ HIPCC="${HIPCC:-/opt/rocm/bin/hipcc}"
 "$HIPCC" --offload-arch=gfx950 -O3 -std=c++17 -fPIC -shared \
   -ffp-contract=off -fhip-fp32-correctly-rounded-divide-sqrt -munsafe-fp-atomics \
   -Wall -Wno-unused-function \
-  -I"$here/../../include" \
+  -I"$here/../../include" ${TVAM_CXXFLAGS:-} \
   "$here/tvam_plan.hip" "$here/tvam_kernels.hip" "$here/tvam_planar.hip" "$here/tvam_vec.hip" "$here/tvam_scatter.hip" "$here/tvam_radon.hip" \
   -o "$out"

@@ -329,10 +329,12 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     }
     off[k.nz] = (int32_t)rows.size();
     p->planar_fz = env_int("TVAM_PLANAR_FWD_Z", 0);  // 0: chosen from the slab depth (planar_fwd_setup)
-    p->planar_az = env_int("TVAM_PLANAR_ADJ_Z", 4);
+    // adjoint slices per workgroup: 8 (one march gathers 8 slices: measured 5.2 -> 3.9 ms on
+    // config 2 with 1024-thread workgroups and 45 x 45 tiles), 4 for films under 8 slices
+    p->planar_az = env_int("TVAM_PLANAR_ADJ_Z", k.nz >= 8 ? 8 : 4);
     if (p->planar_fz != 8 && p->planar_fz != 16 && p->planar_fz != 24 && p->planar_fz != 28 && p->planar_fz != 32)
         p->planar_fz = 0;
-    if (p->planar_az != 4 && p->planar_az != 8) p->planar_az = 4;
+    if (p->planar_az != 4 && p->planar_az != 8 && p->planar_az != 16) p->planar_az = 4;
     const int ns = (int)cs.size();
     int32_t mrc = 0;
     for (int z0 = 0; z0 < k.nz; z0 += p->planar_az)
@@ -364,7 +366,9 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
         if (es >= 1 && es <= 64) split = es;
         p->pl.adj_split = split;
         p->pl.adj_prefetch = env_int("TVAM_ADJ_PREFETCH", 1);
-        p->pl.adj_nt = env_int("TVAM_ADJ_NT", 512) == 256 ? 256 : 512;
+        // 1024 threads at Z = 8: the 71 KB tile admits 2 workgroups per CU = 8 waves per SIMD
+        const int ant = env_int("TVAM_ADJ_NT", p->planar_az >= 8 ? 1024 : 512);
+        p->pl.adj_nt = ant == 256 || ant == 1024 ? ant : 512;
         p->pl.rayfwd_nt = env_int("TVAM_RAYFWD_NT", 512) == 256 ? 256 : 512;
     }
     if (tvam_planar_rayfwd_lds(p->pl, p->tiles, p->planar_rz) > 160 * 1024) p->planar_rz = 4;
@@ -479,7 +483,7 @@ static bool planar_fwd_setup(tvam_plan* p, const std::vector<float2>& cs, const 
     }
     {
         const int ab = env_int("TVAM_FWD_AB", 2);
-        p->pl.fwd_ab = ab == 4 ? 4 : (ab == 1 ? 1 : 2);
+        p->pl.fwd_ab = (ab >= 1 && ab <= 4) ? ab : 2;
     }
     if (p->planar_fz == 0) {
         // slices per workgroup: the fewest padded slice-passes ceil(nz / Z) * (Z + 4)
@@ -731,9 +735,10 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
 
     // tile geometry: LDS-resident xy tile of one z-slice
     auto pick = [&](int res) {
-        // measured optimum (400^3 / 400 angles): the planar adjoint (regular sampling, 4
-        // interleaved slices in LDS) at 40, the per-ray tile kernels at 64
-        int ts = d.tile > 0 ? d.tile : (d.regular_sampling && !(d.flags & TVAM_FLAG_NO_PLANAR) ? 40 : 64);
+        // measured optimum (400^3 / 400 angles): the planar adjoint (regular sampling, 8
+        // interleaved slices in LDS) at <= 48 (45 at 400: two 71 KB tiles per CU), the
+        // per-ray tile kernels at 64
+        int ts = d.tile > 0 ? d.tile : (d.regular_sampling && !(d.flags & TVAM_FLAG_NO_PLANAR) ? 48 : 64);
         int nt = (res + ts - 1) / ts;
         return (res + nt - 1) / nt;
     };

@@ -106,8 +106,12 @@ __host__ __device__ constexpr int tvam_fwd_zs(int Z) { return ((Z + 4) / 4) % 2 
 // Z: slices per thread; NC: candidate DMD columns per (voxel, angle), a
 // bound the plan derives from the voxel's lateral width in columns; MULTI:
 // some slice collects several DMD rows; PF: staged values per thread.
+#ifndef TVAM_FWD_WPE
+#define TVAM_FWD_WPE 1
+#endif
 template <int Z, int NC, bool MULTI, int PF, int AB>
-__global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, TvamPlanar pl,
+__global__ __launch_bounds__(TVAM_PB) __attribute__((amdgpu_waves_per_eu(AB == 2 ? TVAM_FWD_WPE : 1)))
+void tvam_fwd_planar_kernel(TvamConsts k, TvamPlanar pl,
                                                                   const float* __restrict__ pat,
                                                                   float* __restrict__ dose) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -357,6 +361,8 @@ static void launch_fwd(dim3 grid, size_t lds, hipStream_t stream, const TvamCons
         hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 2, 1>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
     else if (NC == 2 && pl.fwd_ab == 4)
         hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 4, 4>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
+    else if (NC == 2 && pl.fwd_ab == 3)
+        hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 4, 3>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
     else if (NC == 2 && pl.fwd_ab == 2)
         hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 4, 2>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
     else
@@ -584,7 +590,10 @@ hipError_t tvam_launch_adj_planar(const TvamConsts& k, const TvamPlanar& pl, con
     // 512-thread workgroups (adj_nt): the LDS tile (28 KB at 40 x 40 x 4) admits 5
     // workgroups per CU, i.e. 5 waves per SIMD at 256 threads, 8 at 512
 #define TVAM_ADJ_LAUNCH(ZZ)                                                                                        \
-    if (pl.adj_nt == 512)                                                                                          \
+    if (pl.adj_nt == 1024)                                                                                         \
+        hipLaunchKernelGGL((tvam_adj_planar_kernel<ZZ, true, 1024>), grid, dim3(1024), lds, stream, k, pl, t, idxmap, \
+                           gin, out);                                                                              \
+    else if (pl.adj_nt == 512)                                                                                     \
         hipLaunchKernelGGL((tvam_adj_planar_kernel<ZZ, true, 512>), grid, dim3(512), lds, stream, k, pl, t, idxmap,  \
                            gin, out);                                                                              \
     else if (pf)                                                                                                   \
@@ -596,6 +605,7 @@ hipError_t tvam_launch_adj_planar(const TvamConsts& k, const TvamPlanar& pl, con
     switch (Z) {
         case 4: TVAM_ADJ_LAUNCH(4) break;
         case 8: TVAM_ADJ_LAUNCH(8) break;
+        case 16: TVAM_ADJ_LAUNCH(16) break;
         default: return hipErrorInvalidValue;
     }
 #undef TVAM_ADJ_LAUNCH

@@ -106,14 +106,18 @@ def test_adjoint_matches_oracle(oracle, case):
     assert rel_l2(g, ref) < RTOL_L2
 
 
-@pytest.mark.parametrize("parts,split,fz", [(1, 1, 32), (3, 5, 28), (7, 2, 24), (2, 3, 8)])
-def test_work_splits_match_oracle(oracle, monkeypatch, parts, split, fz):
+@pytest.mark.parametrize("parts,split,fz,az,nt", [(1, 1, 32, 8, 1024), (3, 5, 28, 4, 512), (7, 2, 24, 16, 1024),
+                                                   (2, 3, 8, 8, 256), (1, 2, 16, 4, 256)])
+def test_work_splits_match_oracle(oracle, monkeypatch, parts, split, fz, az, nt):
     """Angle parts of the voxel-driven forward (partial doses summed in part order),
-    ray-list splits of the planar adjoint and every slab depth Z give the oracle's
-    results (the plan picks them from the slab depth; forced here)."""
+    ray-list splits of the planar adjoint, every forward slab depth Z, the adjoint's
+    slices per workgroup and its workgroup size give the oracle's results (the plan
+    picks them from the slab depth; forced here)."""
     monkeypatch.setenv("TVAM_FWD_PARTS", str(parts))
     monkeypatch.setenv("TVAM_ADJ_SPLIT", str(split))
     monkeypatch.setenv("TVAM_PLANAR_FWD_Z", str(fz))
+    monkeypatch.setenv("TVAM_PLANAR_ADJ_Z", str(az))
+    monkeypatch.setenv("TVAM_ADJ_NT", str(nt))
     d = make(N=40, A=30)
     n = d.n_patterns * d.crop_y * d.crop_x
     rng = np.random.default_rng(4)
