@@ -52,6 +52,10 @@ struct TvamPlanar {
     int32_t fwd_parts;         // forward: angle parts per (tile, slice chunk) (thin slabs; 1 = none)
     int32_t fwd_ab;            // forward: angles per barrier (1 or 2)
     float* fwd_part;           // forward: [fwd_parts][nz][res_y][res_x] partial doses when fwd_parts > 1
+    float* fwd_bin;            // forward: [ns][crop_x + 2 bin_pad][bin_nz] slice-binned patterns (nullptr: staged
+                               // from the [row][col] patterns directly)
+    int32_t bin_pad;           // forward: zero columns on either side of the binned patterns (= ncmax)
+    int32_t bin_nz;            // forward: slices per binned column (nz rounded up to the slab depth Z)
 };
 
 hipError_t tvam_launch_planar_rays(const TvamConsts& k, const TvamPlanar& pl, hipStream_t stream);

@@ -77,6 +77,7 @@ struct tvam_plan {
     int32_t* d_pl_rec_i = nullptr;
     float4* d_pl_rec_g = nullptr;
     float* d_pl_part = nullptr;  // voxel-driven forward: partial doses of the angle parts
+    float* d_pl_bin = nullptr;   // voxel-driven forward: slice-binned patterns
     unsigned* d_amax = nullptr;  // ray-driven forward: per-angle max |pattern|, fixed-point scale
     float* d_fscale = nullptr;
     int32_t planar_rz = 4;
@@ -149,6 +150,7 @@ static void plan_free(tvam_plan* p) {
     (void)hipFree(p->d_pl_rec_i);
     (void)hipFree(p->d_pl_rec_g);
     (void)hipFree(p->d_pl_part);
+    (void)hipFree(p->d_pl_bin);
     (void)hipFree(p->d_amax);
     (void)hipFree(p->d_occ);
     (void)hipFree(p->d_tgt);
@@ -369,7 +371,7 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
         // 1024 threads at Z = 8: the 71 KB tile admits 2 workgroups per CU = 8 waves per SIMD
         const int ant = env_int("TVAM_ADJ_NT", p->planar_az >= 8 ? 1024 : 512);
         p->pl.adj_nt = ant == 256 || ant == 1024 ? ant : 512;
-        p->pl.rayfwd_nt = env_int("TVAM_RAYFWD_NT", 512) == 256 ? 256 : 512;
+        p->pl.rayfwd_nt = env_int("TVAM_RAYFWD_NT", 512) == 1024 ? 1024 : 512;
     }
     if (tvam_planar_rayfwd_lds(p->pl, p->tiles, p->planar_rz) > 160 * 1024) p->planar_rz = 4;
     if (tvam_planar_rayfwd_lds(p->pl, p->tiles, p->planar_rz) > 160 * 1024) return 0;
@@ -402,6 +404,20 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
             p->pl.fwd_part = p->d_pl_part;
         }
         p->pl.fwd_parts = parts;
+        // Slice-binned patterns ([angle][pad + column][slice], tvam_slice_bin_kernel): the
+        // forward stages each window column's Z slices with 16-byte loads and stores
+        const int Z = p->planar_fz;
+        const int nq = (p->pl.ncmax * (Z / 4) + 255) / 256;
+        if (env_int("TVAM_FWD_BIN", 1) && nq <= 2 && ns > 0) {
+            if (p->pl.fwd_ab > 2 || (nq == 2 && p->pl.fwd_ab != 2)) p->pl.fwd_ab = 2;  // the instantiated variants
+            p->pl.bin_pad = p->pl.ncmax;
+            p->pl.bin_nz = (k.nz + Z - 1) / Z * Z;
+            const size_t bytes = (size_t)ns * (d.crop_x + 2 * p->pl.bin_pad) * p->pl.bin_nz * sizeof(float);
+            if ((e = hipMalloc((void**)&p->d_pl_bin, bytes)) != hipSuccess) return hip_fail(e, "hipMalloc (binned patterns)");
+            if ((e = hipMemset(p->d_pl_bin, 0, bytes)) != hipSuccess) return hip_fail(e, "hipMemset (binned patterns)");
+            p->pl.fwd_bin = p->d_pl_bin;
+            p->pl.fwd_pf = nq;
+        }
     }
     if ((e = hipMalloc((void**)&p->d_pl_vox, nrec * sizeof(float4))) != hipSuccess ||
         (e = hipMalloc((void**)&p->d_pl_rec_f, nrec * sizeof(float4))) != hipSuccess ||
@@ -472,6 +488,9 @@ static bool planar_fwd_setup(tvam_plan* p, const std::vector<float2>& cs, const 
             need = std::max(need, (int)std::ceil(umax - w) + 1 + nc - cb);
         }
     }
+    // a window wholly outside the crop stages only zero columns: clamp it into the
+    // slice-binned patterns' zero pads (ncmax columns either side)
+    for (auto& cb : fcb) cb = std::min(std::max(cb, -need), (int)d.crop_x);
     p->pl.marg_u = (float)marg_u;
     p->pl.u0 = u0;
     p->pl.fwd_nc = nc;

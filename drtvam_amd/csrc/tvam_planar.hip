@@ -105,21 +105,21 @@ __host__ __device__ constexpr int tvam_fwd_zs(int Z) { return ((Z + 4) / 4) % 2 
 
 // Z: slices per thread; NC: candidate DMD columns per (voxel, angle), a
 // bound the plan derives from the voxel's lateral width in columns; MULTI:
-// some slice collects several DMD rows; PF: staged values per thread.
-#ifndef TVAM_FWD_WPE
-#define TVAM_FWD_WPE 1
-#endif
-template <int Z, int NC, bool MULTI, int PF, int AB>
-__global__ __launch_bounds__(TVAM_PB) __attribute__((amdgpu_waves_per_eu(AB == 2 ? TVAM_FWD_WPE : 1)))
-void tvam_fwd_planar_kernel(TvamConsts k, TvamPlanar pl,
+// some slice collects several DMD rows; PF: staged values per thread (BIN:
+// staged float4s); BIN: the window is staged from the slice-binned patterns
+// (pl.fwd_bin, [angle][column][slice]) with one 16-byte load and store per slot.
+template <int Z, int NC, bool MULTI, int PF, int AB, bool BIN = false>
+__global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, TvamPlanar pl,
                                                                   const float* __restrict__ pat,
                                                                   float* __restrict__ dose) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int ncm = pl.ncmax;
-    // [2][AB][ncm][ZS] (double buffer of AB angles per barrier), ZS = tvam_fwd_zs(Z)
+    // [2][AB][ncm * ZS + 4] (double buffer of AB angles per barrier), ZS = tvam_fwd_zs(Z);
+    // the 4 words past a buffer's slab take the BIN staging's idle slots
     constexpr int ZS = tvam_fwd_zs(Z);
+    const int bstride = ncm * ZS + 4;
     float* s_p = reinterpret_cast<float*>(smem);
-    float4* s_r = reinterpret_cast<float4*>(s_p + 2 * AB * ncm * ZS);  // [2][AB][ncm]
+    float4* s_r = reinterpret_cast<float4*>(s_p + 2 * AB * bstride);  // [2][AB][ncm]
     // per-angle constants of TVAM_ACH (+2 look-ahead) angles, copied to LDS so the
     // angle loop issues no scalar loads (an s_load's lgkmcnt wait would also
     // drain every outstanding LDS read)
@@ -182,7 +182,9 @@ void tvam_fwd_planar_kernel(TvamConsts k, TvamPlanar pl,
 
     // This thread's staging slots i = tid + q * 256 of the [Z][ncm] slab are
     // angle-independent: window column jj, the slice's row offset (or -2 - z
-    // when several rows share the slice) and the LDS offset.
+    // when several rows share the slice) and the LDS offset.  BIN: slots of the
+    // [ncm][Z / 4] float4 slab, source and LDS offsets in float4s (an idle slot
+    // re-reads slot 0's source and writes past the slab).
     int st_jj[PF], st_row[PF], st_off[PF];
 #pragma unroll
     for (int q = 0; q < PF; ++q) {
@@ -190,7 +192,13 @@ void tvam_fwd_planar_kernel(TvamConsts k, TvamPlanar pl,
         st_jj[q] = -1;
         st_row[q] = -1;
         st_off[q] = 0;
-        if (i < ncm * Z) {
+        if (BIN) {
+            constexpr int G = Z / 4;
+            const bool use = i < ncm * G;
+            const int jj = use ? i / G : 0, gq = use ? i - (i / G) * G : 0;
+            st_jj[q] = jj * (pl.bin_nz / 4) + gq;
+            st_off[q] = use ? jj * (ZS / 4) + gq : ncm * ZS / 4;
+        } else if (i < ncm * Z) {
             const int z = i / ncm, jj = i - z * ncm;
             const int r = s_row[z];
             st_jj[q] = jj;
@@ -199,29 +207,41 @@ void tvam_fwd_planar_kernel(TvamConsts k, TvamPlanar pl,
         }
     }
     // global loads of angle al's slab (slice-binned pattern + ray table) into registers
-    struct Stage {
+    struct StageDirect {
         float pv[PF];
         float4 rv;
     };
+    struct StageBinned {
+        float4 p4[PF];
+        float4 rv;
+    };
+    using Stage = typename std::conditional<BIN, StageBinned, StageDirect>::type;
     auto fetch = [&](int al, Stage& S) {
         const int cb = s_cb[al - tbase];
-        const float* pa = pat + (size_t)al * k.crop_y * k.crop_x;
+        if constexpr (BIN) {
+            const float4* src = reinterpret_cast<const float4*>(pl.fwd_bin) +
+                                ((size_t)al * (k.crop_x + 2 * pl.bin_pad) + (cb + pl.bin_pad)) * (pl.bin_nz / 4) + z0 / 4;
 #pragma unroll
-        for (int q = 0; q < PF; ++q) {
-            const int col = cb + st_jj[q], r = st_row[q];
-            float v = 0.0f;
-            const bool in = st_jj[q] >= 0 && (unsigned)col < (unsigned)k.crop_x;
-            if (!MULTI) {
-                if (in && r >= 0) v = pa[(unsigned)(r + col)];
-            } else if (in && r != -1) {
-                if (r >= 0) v = pa[(unsigned)(r + col)];
-                else {
-                    const int z = -2 - r;
-                    for (int t = pl.slice_off[z0 + z]; t < pl.slice_off[z0 + z + 1]; ++t)
-                        v += pa[(size_t)pl.slice_rows[t] * k.crop_x + col];
+            for (int q = 0; q < PF; ++q) S.p4[q] = src[st_jj[q]];
+        } else {
+            const float* pa = pat + (size_t)al * k.crop_y * k.crop_x;
+#pragma unroll
+            for (int q = 0; q < PF; ++q) {
+                const int col = cb + st_jj[q], r = st_row[q];
+                float v = 0.0f;
+                const bool in = st_jj[q] >= 0 && (unsigned)col < (unsigned)k.crop_x;
+                if (!MULTI) {
+                    if (in && r >= 0) v = pa[(unsigned)(r + col)];
+                } else if (in && r != -1) {
+                    if (r >= 0) v = pa[(unsigned)(r + col)];
+                    else {
+                        const int z = -2 - r;
+                        for (int t = pl.slice_off[z0 + z]; t < pl.slice_off[z0 + z + 1]; ++t)
+                            v += pa[(size_t)pl.slice_rows[t] * k.crop_x + col];
+                    }
                 }
+                S.pv[q] = v;
             }
-            S.pv[q] = v;
         }
         const int col = cb + (int)threadIdx.x;
         S.rv = make_float4(0.0f, 0.0f, -1.0f, 0.0f);
@@ -229,10 +249,15 @@ void tvam_fwd_planar_kernel(TvamConsts k, TvamPlanar pl,
     };
     // buffer b = (double-buffer half) * AB + (angle within the barrier group)
     auto store = [&](int buf, const Stage& S) {
-        float* sp = s_p + buf * ncm * ZS;
+        float* sp = s_p + buf * bstride;
+        if constexpr (BIN) {
 #pragma unroll
-        for (int q = 0; q < PF; ++q)
-            if (st_jj[q] >= 0) sp[st_off[q]] = S.pv[q];
+            for (int q = 0; q < PF; ++q) reinterpret_cast<float4*>(sp)[st_off[q]] = S.p4[q];
+        } else {
+#pragma unroll
+            for (int q = 0; q < PF; ++q)
+                if (st_jj[q] >= 0) sp[st_off[q]] = S.pv[q];
+        }
         if ((int)threadIdx.x < ncm) s_r[buf * ncm + threadIdx.x] = S.rv;
     };
 
@@ -242,7 +267,7 @@ void tvam_fwd_planar_kernel(TvamConsts k, TvamPlanar pl,
 
     auto compute = [&](int al, int buf) {
         const int cb = s_cb[al - tbase];
-        const float* sp = s_p + buf * ncm * ZS;
+        const float* sp = s_p + buf * bstride;
         const float4* sr = s_r + buf * ncm;
         // per-angle constants {s*du, -c*du, 1/d.x, 1/d.y}, {half width in columns, axis flags}
         const float4 g0 = s_ang[2 * (al - tbase)], g1 = s_ang[2 * (al - tbase) + 1];
@@ -341,9 +366,53 @@ __global__ __launch_bounds__(256) void tvam_fwd_parts_kernel(int64_t n, int part
     }
 }
 
+// Slice binning of the patterns for the voxel-driven forward: bin[a][pad + col][z] =
+// the sum of slice z's DMD rows of column col at angle a (in slice_rows order, as the
+// direct staging sums them; 0 for a slice without rows).  A 64-column x 64-slice
+// block goes through LDS, read along columns and written along slices.  Pads and
+// slices past nz stay 0 from the plan's memset.
+__global__ __launch_bounds__(256) void tvam_slice_bin_kernel(TvamConsts k, TvamPlanar pl,
+                                                            const float* __restrict__ pat) {
+    __shared__ float s_t[64][65];
+    __shared__ int s_row[64];  // the slice's row x crop_x; -1: no row; -2: several rows
+    const int c0 = blockIdx.x * 64, z0 = blockIdx.y * 64, al = blockIdx.z;
+    if (threadIdx.x < 64) {
+        const int z = z0 + (int)threadIdx.x;
+        int r = -1;
+        if (z < k.nz) {
+            const int b = pl.slice_off[z], e = pl.slice_off[z + 1];
+            r = e - b == 1 ? pl.slice_rows[b] * k.crop_x : (e == b ? -1 : -2);
+        }
+        s_row[threadIdx.x] = r;
+    }
+    __syncthreads();
+    const float* pa = pat + (size_t)al * k.crop_y * k.crop_x;
+    const int lc = threadIdx.x & 63, lz = threadIdx.x >> 6;
+    const int c = c0 + lc;
+    const bool cin = c < k.crop_x;
+#pragma unroll 4
+    for (int zz = lz; zz < 64; zz += 4) {
+        const int r = s_row[zz];
+        float v = 0.0f;
+        if (cin && r >= 0) {
+            v = pa[(size_t)r + c];
+        } else if (cin && r == -2) {
+            for (int t = pl.slice_off[z0 + zz]; t < pl.slice_off[z0 + zz + 1]; ++t)
+                v += pa[(size_t)pl.slice_rows[t] * k.crop_x + c];
+        }
+        s_t[lc][zz] = v;
+    }
+    __syncthreads();
+    float* out = pl.fwd_bin + ((size_t)al * (k.crop_x + 2 * pl.bin_pad) + pl.bin_pad) * pl.bin_nz;
+    const int z = z0 + lc;
+    if (z >= k.nz) return;
+    for (int cc = lz; cc < 64; cc += 4)
+        if (c0 + cc < k.crop_x) out[(size_t)(c0 + cc) * pl.bin_nz + z] = s_t[cc][lc];
+}
+
 size_t tvam_planar_fwd_lds(const TvamPlanar& pl, int Z) {
     const int ab = pl.fwd_ab > 1 ? pl.fwd_ab : 1;
-    return 2 * ab * ((size_t)pl.ncmax * tvam_fwd_zs(Z) * sizeof(float) + (size_t)pl.ncmax * sizeof(float4)) +
+    return 2 * ab * (((size_t)pl.ncmax * tvam_fwd_zs(Z) + 4) * sizeof(float) + (size_t)pl.ncmax * sizeof(float4)) +
            (size_t)(TVAM_ACH + 4) * (2 * sizeof(float4) + sizeof(int)) + (size_t)Z * sizeof(int);
 }
 
@@ -355,7 +424,13 @@ bool tvam_planar_fwd_fits(const TvamPlanar& pl, int Z) {
 template <int Z, int NC>
 static void launch_fwd(dim3 grid, size_t lds, hipStream_t stream, const TvamConsts& k, const TvamPlanar& pl,
                        const float* pat, float* dose) {
-    if (pl.fwd_multi)
+    if (pl.fwd_bin && pl.fwd_pf == 1 && pl.fwd_ab == 1)
+        hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 1, 1, true>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
+    else if (pl.fwd_bin && pl.fwd_pf == 1)
+        hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 1, 2, true>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
+    else if (pl.fwd_bin)
+        hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 2, 2, true>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
+    else if (pl.fwd_multi)
         hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, true, 4, 1>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
     else if (pl.fwd_pf == 2)
         hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 2, 1>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
@@ -393,6 +468,11 @@ hipError_t tvam_launch_fwd_planar(const TvamConsts& k, const TvamPlanar& pl, int
     const unsigned nwg = (unsigned)(ntx * nty) * (unsigned)((k.nz + Z - 1) / Z) * (unsigned)parts;
     dim3 grid(pl.xcd_remap ? (nwg + 7) / 8 * 8 : nwg);
     const size_t lds = tvam_planar_fwd_lds(pl, Z);
+    if (pl.fwd_bin) {
+        if (pl.bin_nz % Z != 0 || pl.bin_nz < k.nz) return hipErrorInvalidValue;
+        const dim3 bg((unsigned)((k.crop_x + 63) / 64), (unsigned)((k.nz + 63) / 64), (unsigned)pl.ns);
+        hipLaunchKernelGGL(tvam_slice_bin_kernel, bg, dim3(256), 0, stream, k, pl, pat);
+    }
     hipError_t e = tvam_launch_fwd_planar_z(grid, lds, stream, k, pl, Z, pat, dose);
     if (e != hipSuccess || parts == 1) return e;
     const int64_t n = (int64_t)k.nz * k.res[0] * k.res[1];
@@ -778,8 +858,8 @@ __device__ __forceinline__ void fwd_rays_body(const TvamConsts& k, const TvamPla
     }
 }
 
-template <int Z>
-__global__ __launch_bounds__(512) void tvam_fwd_rays_planar_kernel(TvamConsts k, TvamPlanar pl, TvamTiles tp,
+template <int Z, int NT>
+__global__ __launch_bounds__(NT) void tvam_fwd_rays_planar_kernel(TvamConsts k, TvamPlanar pl, TvamTiles tp,
                                                                        const float* __restrict__ pat,
                                                                        const float* __restrict__ scale,
                                                                        float* __restrict__ dose) {
@@ -841,16 +921,18 @@ hipError_t tvam_launch_fwd_rays_planar(const TvamConsts& k, const TvamPlanar& pl
     hipLaunchKernelGGL(tvam_fwd_scale_kernel, dim3(1), dim3(256), 0, stream, k, pl.ns, pl.max_rows_slice, amax, scale);
     dim3 grid((unsigned)(t.ntx * t.nty), (unsigned)((k.nz + Z - 1) / Z));
     const size_t lds = tvam_planar_rayfwd_lds(pl, t, Z);
-    const dim3 block(pl.rayfwd_nt == 512 ? 512 : 256);
+#define TVAM_RAYFWD_LAUNCH(ZZ)                                                                                  \
+    if (pl.rayfwd_nt == 1024)                                                                                   \
+        hipLaunchKernelGGL((tvam_fwd_rays_planar_kernel<ZZ, 1024>), grid, dim3(1024), lds, stream, k, pl, t, pat, \
+                           scale, dose);                                                                        \
+    else                                                                                                        \
+        hipLaunchKernelGGL((tvam_fwd_rays_planar_kernel<ZZ, 512>), grid, dim3(512), lds, stream, k, pl, t, pat,   \
+                           scale, dose);
     switch (Z) {
-        case 4:
-            hipLaunchKernelGGL(tvam_fwd_rays_planar_kernel<4>, grid, block, lds, stream, k, pl, t, pat, scale, dose);
-            break;
-        case 8:
-            hipLaunchKernelGGL(tvam_fwd_rays_planar_kernel<8>, grid, block, lds, stream, k, pl, t, pat, scale, dose);
-            break;
-        default:
-            return hipErrorInvalidValue;
+        case 4: TVAM_RAYFWD_LAUNCH(4) break;
+        case 8: TVAM_RAYFWD_LAUNCH(8) break;
+        default: return hipErrorInvalidValue;
     }
+#undef TVAM_RAYFWD_LAUNCH
     return hipGetLastError();
 }

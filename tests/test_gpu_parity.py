@@ -132,6 +132,21 @@ def test_work_splits_match_oracle(oracle, monkeypatch, parts, split, fz, az, nt)
     assert rel_l2(g, gref) < RTOL_L2
 
 
+@pytest.mark.parametrize("case", [dict(N=40, A=30), dict(N=24, A=12, zres=12), dict(N=24, A=12, zres=48)],
+                         ids=lambda c: "-".join(f"{k}{v}" for k, v in c.items()))
+def test_forward_direct_staging_matches_oracle(oracle, monkeypatch, case):
+    """The voxel-driven forward staging its windows from the [row][col] patterns directly
+    (TVAM_FWD_BIN=0) instead of the slice-binned copy: same results."""
+    monkeypatch.setenv("TVAM_FWD_BIN", "0")
+    d = make(**case)
+    n = d.n_patterns * d.crop_y * d.crop_x
+    pat = np.random.default_rng(6).uniform(0.0, 0.1, n).astype(np.float32)
+    ref, _ = oracle.forward(d, pat, nthreads=8)
+    got, proj = gpu_forward(d, pat)
+    assert proj.planar_forward
+    assert rel_l2(got, ref) < RTOL_L2
+
+
 @pytest.mark.parametrize("regular", [False, True])
 def test_dot_product_gpu(regular):
     d = make(N=48, A=40, regular=regular, spp=2)
