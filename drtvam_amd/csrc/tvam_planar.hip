@@ -32,6 +32,9 @@
 #define TVAM_PB 256
 
 __device__ __forceinline__ float pl_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
+// native 4-vector for staged registers (HIP's float4 is a union wrapper that can keep a
+// staged copy out of registers)
+typedef float pl_f4 __attribute__((ext_vector_type(4)));
 
 // ---------------------------------------------------------------------------
 // (angle, column) table: ray generation (common.py:81-108, jitter 0.5), vial
@@ -207,22 +210,21 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
         }
     }
     // global loads of angle al's slab (slice-binned pattern + ray table) into registers
+    // (the ray-table entry travels in its own array: a 48-byte stage struct is left in scratch)
     struct StageDirect {
         float pv[PF];
-        float4 rv;
     };
-    struct StageBinned {
-        float4 p4[PF];
-        float4 rv;
+    struct StageBinned {  // PF <= 2
+        pl_f4 p0, p1;
     };
     using Stage = typename std::conditional<BIN, StageBinned, StageDirect>::type;
-    auto fetch = [&](int al, Stage& S) {
+    auto fetch = [&](int al, Stage& S, pl_f4& rv) {
         const int cb = s_cb[al - tbase];
         if constexpr (BIN) {
-            const float4* src = reinterpret_cast<const float4*>(pl.fwd_bin) +
+            const pl_f4* src = reinterpret_cast<const pl_f4*>(pl.fwd_bin) +
                                 ((size_t)al * (k.crop_x + 2 * pl.bin_pad) + (cb + pl.bin_pad)) * (pl.bin_nz / 4) + z0 / 4;
-#pragma unroll
-            for (int q = 0; q < PF; ++q) S.p4[q] = src[st_jj[q]];
+            S.p0 = src[st_jj[0]];
+            if constexpr (PF > 1) S.p1 = src[st_jj[1]];
         } else {
             const float* pa = pat + (size_t)al * k.crop_y * k.crop_x;
 #pragma unroll
@@ -244,21 +246,22 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
             }
         }
         const int col = cb + (int)threadIdx.x;
-        S.rv = make_float4(0.0f, 0.0f, -1.0f, 0.0f);
-        if ((int)threadIdx.x < ncm && (unsigned)col < (unsigned)k.crop_x) S.rv = pl.vox[(size_t)al * k.crop_x + col];
+        rv = pl_f4{0.0f, 0.0f, -1.0f, 0.0f};
+        if ((int)threadIdx.x < ncm && (unsigned)col < (unsigned)k.crop_x)
+            rv = reinterpret_cast<const pl_f4*>(pl.vox)[(size_t)al * k.crop_x + col];
     };
     // buffer b = (double-buffer half) * AB + (angle within the barrier group)
-    auto store = [&](int buf, const Stage& S) {
+    auto store = [&](int buf, const Stage& S, const pl_f4& rv) {
         float* sp = s_p + buf * bstride;
         if constexpr (BIN) {
-#pragma unroll
-            for (int q = 0; q < PF; ++q) reinterpret_cast<float4*>(sp)[st_off[q]] = S.p4[q];
+            reinterpret_cast<pl_f4*>(sp)[st_off[0]] = S.p0;
+            if constexpr (PF > 1) reinterpret_cast<pl_f4*>(sp)[st_off[1]] = S.p1;
         } else {
 #pragma unroll
             for (int q = 0; q < PF; ++q)
                 if (st_jj[q] >= 0) sp[st_off[q]] = S.pv[q];
         }
-        if ((int)threadIdx.x < ncm) s_r[buf * ncm + threadIdx.x] = S.rv;
+        if ((int)threadIdx.x < ncm) reinterpret_cast<pl_f4*>(s_r)[buf * ncm + threadIdx.x] = rv;
     };
 
     float acc[Z];
@@ -314,16 +317,16 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
 
     // Software pipeline over angles: angle a is computed from LDS buffer a & 1
     // while the loads of angle a + 1 are in flight in registers.
-    if (ab < ae) {
+    if (ab < ae && AB <= 2) {
         // AB angles per barrier: the next group's global loads are in flight in
-        // registers while this group is computed from LDS
-        Stage S[AB];
-#pragma unroll
-        for (int j = 0; j < AB; ++j)
-            if (ab + j < ae) fetch(ab + j, S[j]);
-#pragma unroll
-        for (int j = 0; j < AB; ++j)
-            if (ab + j < ae) store(j, S[j]);
+        // registers while this group is computed from LDS (named stages: an
+        // array of them indexed by the angle in the group can end up in scratch)
+        Stage S0, S1;
+        pl_f4 R0, R1;
+        fetch(ab, S0, R0);
+        if (AB > 1 && ab + 1 < ae) fetch(ab + 1, S1, R1);
+        store(0, S0, R0);
+        if (AB > 1 && ab + 1 < ae) store(1, S1, R1);
         __syncthreads();
         int half = 0;
         for (int al = ab; al < ae; al += AB) {
@@ -332,16 +335,42 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
                 load_table(al);
                 __syncthreads();
             }
+            if (al + AB < ae) fetch(al + AB, S0, R0);
+            if (AB > 1 && al + AB + 1 < ae) fetch(al + AB + 1, S1, R1);
+            compute(al, half * AB);
+            if (AB > 1 && al + 1 < ae) compute(al + 1, half * AB + 1);
+            half ^= 1;
+            if (al + AB < ae) store(half * AB, S0, R0);
+            if (AB > 1 && al + AB + 1 < ae) store(half * AB + 1, S1, R1);
+            __syncthreads();
+        }
+    } else if (ab < ae) {
+        Stage S[AB];
+        pl_f4 R[AB];
+#pragma unroll
+        for (int j = 0; j < AB; ++j)
+            if (ab + j < ae) fetch(ab + j, S[j], R[j]);
+#pragma unroll
+        for (int j = 0; j < AB; ++j)
+            if (ab + j < ae) store(j, S[j], R[j]);
+        __syncthreads();
+        int half = 0;
+        for (int al = ab; al < ae; al += AB) {
+            if (al - tbase > TVAM_ACH + 4 - 2 * AB) {
+                tbase = al;
+                load_table(al);
+                __syncthreads();
+            }
 #pragma unroll
             for (int j = 0; j < AB; ++j)
-                if (al + AB + j < ae) fetch(al + AB + j, S[j]);
+                if (al + AB + j < ae) fetch(al + AB + j, S[j], R[j]);
 #pragma unroll
             for (int j = 0; j < AB; ++j)
                 if (al + j < ae) compute(al + j, half * AB + j);
             half ^= 1;
 #pragma unroll
             for (int j = 0; j < AB; ++j)
-                if (al + AB + j < ae) store(half * AB + j, S[j]);
+                if (al + AB + j < ae) store(half * AB + j, S[j], R[j]);
             __syncthreads();
         }
     }
