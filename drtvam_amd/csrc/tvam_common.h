@@ -23,6 +23,24 @@
 #define TVAM_TWO_PI 6.2831855f                            // float(2*pi), motion.py:28
 #define TVAM_INF __builtin_huge_valf()
 
+// 1 - e^{-x} for x >= 0 without the cancellation of the direct form: a visit's
+// weight e^{-st t} (1 - e^{-st dt}) (sensor.py:404) has st dt ~ 1e-3 on the
+// BASELINE grids, where 1 - exp() in fp32 keeps only ~4 significant digits
+// (and e^{-st t_in} - e^{-st t_out} alike).  Degree-4 Taylor form below 0.05
+// (relative error < x^4 / 120 < 6e-8), the direct form above (no cancellation
+// there).  nlog2e = -log2(e): e^{-x} = exp2(nlog2e x).
+// Planar kernels whose plan has st * (voxel diagonal) = vox_chord < TVAM_W2_MAX
+// (every BASELINE grid but config 4's) use the degree-2 form on E = st e^{-st t}:
+// c = E dt (1 - st dt / 2), E -= st c: five full-rate instructions, relative error
+// < (st dt)^2 / 6 < 1e-6, in place of an exp2 and its cancellation.
+#define TVAM_W2_MAX 2.4e-3f
+#define TVAM_NLOG2E (-1.4426950408889634f)
+__device__ __forceinline__ float tvam_omexp(float x) {
+    if (__builtin_expect(x < 0.05f, 1))
+        return x * fmaf(x, fmaf(x, fmaf(x, -4.1666668e-2f, 0.16666667f), -0.5f), 1.0f);
+    return 1.0f - __builtin_amdgcn_exp2f(TVAM_NLOG2E * x);
+}
+
 struct TvamConsts {
     // film / sensor (sensor.py:14-19, film.py:9-14)
     float bmin[3], bmax[3], h[3];

@@ -20,6 +20,9 @@ struct TvamTiles {
     int32_t ntx, nty, tsx, tsy;
     int32_t n_shard;
     uint32_t spp, seed;
+    int64_t* frozen;              // ray indices marked frozen by the ray setup (ray_i.y <= -2), appended
+    unsigned long long* frozen_n; // their count (beyond frozen_cap: the frozen kernel scans ray_i instead)
+    int64_t frozen_cap;
 };
 
 // Planar fast path of regular sampling (tvam_planar.hip): one ray record per
@@ -48,6 +51,8 @@ struct TvamPlanar {
     int32_t adj_split;         // adjoint: workgroups sharing one (tile, slice chunk)'s ray list (thin slabs)
     int32_t adj_prefetch;      // adjoint: software-pipelined record loads (slot k + 2, records k + 1)
     int32_t adj_nt;            // adjoint: threads per workgroup (256 or 512)
+    int32_t adj_planes;        // adjoint: gradient tile as Z/4 planes [z/4][voxel][4] (else interleaved [voxel][z])
+    int32_t adj_w2;            // adjoint: degree-2 visit weights where vox_chord < TVAM_W2_MAX
     int32_t rayfwd_nt;         // ray-driven forward: threads per workgroup (256 or 512)
     int32_t fwd_parts;         // forward: angle parts per (tile, slice chunk) (thin slabs; 1 = none)
     int32_t fwd_ab;            // forward: angles per barrier (1 or 2)
@@ -142,6 +147,10 @@ hipError_t tvam_launch_general_paths(int mode, const TvamConsts& k, const TvamTi
 hipError_t tvam_launch_scale_volumes(int64_t n, const float* vols, float* dose, hipStream_t stream);
 // compute_volume (sensor.py:47-110): volumes [res z][y][x][2]
 hipError_t tvam_launch_volumes(const TvamConsts& k, uint32_t sample_count, float* volumes, hipStream_t stream);
+hipError_t tvam_launch_frozen(int mode, const TvamConsts& k, const TvamTiles& t, const float* pat,
+                              const int32_t* idxmap, const float* gin, float* out, unsigned long long* counter,
+                              hipStream_t stream);
+hipError_t tvam_launch_discretize(const TvamConsts& k, const float* h_tris, float* occ, hipStream_t stream);
 
 // Radon filter image of the shard's DMD pixels (tvam_radon.hip).
 hipError_t tvam_launch_radon(const TvamConsts& k, const TvamTiles& t, const float* tgt, int ntgt, int max_depth,

@@ -34,11 +34,6 @@ __device__ __forceinline__ int tvam_rint(float x) {
     return r;
 }
 
-#if defined(TVAM_EXPERIMENT) && TVAM_EXPERIMENT == 4
-__device__ unsigned long long g_exp_counters[2];
-extern "C" __global__ void tvam_exp_read(unsigned long long* out) { out[0] = g_exp_counters[0]; out[1] = g_exp_counters[1]; }
-#endif
-
 // How the in-tile march consumes one visit.
 enum TvamAcc { ACC_FLOAT = 0, ACC_FIXED = 1, ACC_GATHER = 2, ACC_COUNT = 3, ACC_FIXED64 = 4 };
 
@@ -71,30 +66,20 @@ struct TvamMarchRay {
 // the reference's diagonal step.  Rounding can let the last step cross the
 // tile edge one visit early; the tile carries a 1-voxel guard band that
 // absorbs that visit (its dt is at rounding level, and guard cells are never
-// stored / read as 0).  One exp2 per visit (telescoped exp(-st t)(1 - exp(-st dt))).
+// stored / read as 0).  Visit weight e0 (1 - e^{-st dt}) from the tile-relative
+// dt = tn - tp (tvam_omexp: no cancellation), then e0 *= e^{-st dt} (= e0 - c);
+// e0 restarts exactly from exp2 at every tile entry.
 template <int ACC>
 __device__ __forceinline__ void tvam_march(TvamMarchRay a, const float tsx, const float tsy, const int sxb,
-                                           const int syb, const float nsig2, float& acc,
+                                           const int syb, const float sig, float& acc,
                                            unsigned long long& nvis, const char* tile = nullptr, const int tw = 0,
                                            const int wx = 0, const int wy = 0) {
-#if defined(TVAM_EXPERIMENT) && TVAM_EXPERIMENT == 3  // timing only: setup without the march
-    acc += a.Tx + a.Ty + a.rem + a.e0;
-    return;
-#endif
     constexpr int ESZ = ACC == ACC_FIXED64 ? 8 : 4;
-#if defined(TVAM_EXPERIMENT) && TVAM_EXPERIMENT == 4  // lane utilisation of the march loop
-    unsigned long long lane_it = 0, wave_it = 0;
-#endif
     float tp = 0.0f;
     for (;;) {
-#if defined(TVAM_EXPERIMENT) && TVAM_EXPERIMENT == 4
-        ++lane_it;
-        if (__lane_id() == __builtin_ctzll(__ballot(1))) ++wave_it;
-#endif
         const float tn = fminf(fminf(a.Tx, a.Ty), a.rem);
-        const float x1 = tvam_exp2(fmaf(nsig2, tn, a.nt0));
-        const float e1 = (ACC == ACC_GATHER || ACC == ACC_COUNT) ? x1 : a.ems * x1;
-        const float c = a.e0 - e1;
+        const float c = a.e0 * tvam_omexp(sig * fmaxf(tn - tp, 0.0f));
+        const float e1 = a.e0 - c;
         if (ACC == ACC_FLOAT) atomicAdd(reinterpret_cast<float*>(a.pv), c);
         else if (ACC == ACC_FIXED) atomicAdd(reinterpret_cast<int*>(a.pv), tvam_rint(c));
         else if (ACC == ACC_FIXED64) atomicAdd(reinterpret_cast<unsigned long long*>(a.pv), tvam_f2i64(c));
@@ -102,8 +87,8 @@ __device__ __forceinline__ void tvam_march(TvamMarchRay a, const float tsx, cons
         else {  // interior visits of nonzero length (guard-band visits carry rounding-level dt)
             const int li = (int)(a.pv - tile) / ESZ, ly = li / tw, lx = li - ly * tw;
             nvis += (tn > tp && lx >= 1 && lx <= wx && ly >= 1 && ly <= wy) ? 1 : 0;
-            tp = tn;
         }
+        tp = tn;
         const bool mx = a.Tx <= a.Ty;
         a.Tx = mx ? a.Tx + tsx : a.Tx;
         a.Ty = mx ? a.Ty : a.Ty + tsy;
@@ -111,12 +96,6 @@ __device__ __forceinline__ void tvam_march(TvamMarchRay a, const float tsx, cons
         a.e0 = e1;
         if (!(tn < a.stop)) break;
     }
-#if defined(TVAM_EXPERIMENT) && TVAM_EXPERIMENT == 4
-    if (ACC == ACC_GATHER) {
-        atomicAdd(&g_exp_counters[0], lane_it);
-        atomicAdd(&g_exp_counters[1], wave_it);
-    }
-#endif
 }
 
 // Ray slot enumeration of one workgroup: slot f -> (slice row ri, entry g of
@@ -184,7 +163,15 @@ __global__ __launch_bounds__(256) void tvam_ray_setup_kernel(TvamConsts k, TvamT
             continue;
         }
         ray_f[i] = make_float4(q.t_start, q.tau_end, q.dtm0[0], q.dtm0[1]);
-        ray_i[i] = make_int2(q.sv[0] | (q.sv[1] << 16), slice);
+        // an axis that moves but whose first crossing rounded negative never steps (sensor.py:358):
+        // the ray leaves its chord, so tvam_frozen_kernel marches it instead of the tile kernels
+        const bool frozen = (fabsf(d2x) > 1e-8f && !(q.dtm0[0] < TVAM_INF)) ||
+                            (fabsf(d2y) > 1e-8f && !(q.dtm0[1] < TVAM_INF));
+        ray_i[i] = make_int2(q.sv[0] | (q.sv[1] << 16), frozen ? -2 - slice : slice);
+        if (frozen && tp.frozen) {
+            const unsigned long long j = atomicAdd(tp.frozen_n, 1ull);
+            if ((int64_t)j < tp.frozen_cap) tp.frozen[j] = i;
+        }
         if (ray_g)
             ray_g[i] = make_float4(q.step[0] > 0 ? q.ts[0] : -q.ts[0], q.step[1] > 0 ? q.ts[1] : -q.ts[1], wgt, 0.0f);
     }
@@ -418,16 +405,16 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
         float acc = 0.0f;
         if (MODE == TVAM_MODE_FWD) {
             if (TVAM_FWD_ACC64 && acc_mode == ACC_FIXED64)
-                tvam_march<ACC_FIXED64>(m, r.tsx, r.tsy, sxb, syb, k.nsig2, acc, nvis);
+                tvam_march<ACC_FIXED64>(m, r.tsx, r.tsy, sxb, syb, k.sig_t, acc, nvis);
             else if (!TVAM_FWD_ACC64 && acc_mode == ACC_FIXED)
-                tvam_march<ACC_FIXED>(m, r.tsx, r.tsy, sxb, syb, k.nsig2, acc, nvis);
+                tvam_march<ACC_FIXED>(m, r.tsx, r.tsy, sxb, syb, k.sig_t, acc, nvis);
             else
-                tvam_march<ACC_FLOAT>(m, r.tsx, r.tsy, sxb, syb, k.nsig2, acc, nvis);
+                tvam_march<ACC_FLOAT>(m, r.tsx, r.tsy, sxb, syb, k.sig_t, acc, nvis);
         } else if (MODE == TVAM_MODE_ADJ) {
-            tvam_march<ACC_GATHER>(m, r.tsx, r.tsy, sxb, syb, k.nsig2, acc, nvis);
+            tvam_march<ACC_GATHER>(m, r.tsx, r.tsy, sxb, syb, k.sig_t, acc, nvis);
             atomicAdd(&out[r.act], acc * (k.wscale * r.weight));  // backward_from(Le * em_grad), volume.py:274-276
         } else {
-            tvam_march<ACC_COUNT>(m, r.tsx, r.tsy, sxb, syb, k.nsig2, acc, nvis, reinterpret_cast<const char*>(tile),
+            tvam_march<ACC_COUNT>(m, r.tsx, r.tsy, sxb, syb, k.sig_t, acc, nvis, reinterpret_cast<const char*>(tile),
                                   tw, wx, wy);
         }
     }

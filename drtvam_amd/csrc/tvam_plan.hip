@@ -58,6 +58,8 @@ struct tvam_plan {
     // them call-independent; otherwise they are keyed on (spp, seed)
     float4* d_ray_f = nullptr;
     int2* d_ray_i = nullptr;
+    int64_t* d_frozen = nullptr;              // frozen-axis rays of the ray records (tvam_frozen_kernel)
+    unsigned long long* d_frozen_n = nullptr;
     float4* d_ray_g = nullptr;
     uint64_t ray_cap = 0;
     bool ray_valid = false;
@@ -137,6 +139,8 @@ static void plan_free(tvam_plan* p) {
     (void)hipFree(p->d_ang);
     (void)hipFree(p->d_ray_f);
     (void)hipFree(p->d_ray_i);
+    (void)hipFree(p->d_frozen);
+    (void)hipFree(p->d_frozen_n);
     (void)hipFree(p->d_ray_g);
     if (p->ray_ready) (void)hipEventDestroy(p->ray_ready);
     (void)hipFree(p->d_dense);
@@ -348,6 +352,8 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     p->planar_rz = env_int("TVAM_RAY_FWD_Z", 4);
     if (p->planar_rz != 4 && p->planar_rz != 8) p->planar_rz = 4;
     p->pl.adj_pitch = p->tiles.tsx + 2 + std::max(0, env_int("TVAM_ADJ_PITCH_PAD", 0));
+    p->pl.adj_planes = env_int("TVAM_ADJ_PLANES", 1);
+    p->pl.adj_w2 = env_int("TVAM_ADJ_W2", 1);
     p->pl.xcd_remap = env_int("TVAM_XCD_REMAP", 1);
     // Refracted rays are not parallel, and a DMD much finer than the voxels
     // overflows the voxel-driven forward's column window: there the forward
@@ -439,6 +445,14 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     if (ns > 0) {
         if ((e = tvam_launch_planar_rays(k, p->pl, nullptr)) != hipSuccess) return hip_fail(e, "planar ray table");
         if ((e = hipDeviceSynchronize()) != hipSuccess) return hip_fail(e, "planar ray table");
+        // A column whose DDA starts with a frozen axis (sensor.py:358, see tvam_frozen_kernel) leaves
+        // its chord; the planar kernels cannot follow it, so such a plan runs the per-ray tile path
+        // (none occurs in the BASELINE configs under regular sampling).
+        std::vector<int32_t> ri((size_t)ns * k.crop_x);
+        if ((e = hipMemcpy(ri.data(), p->d_pl_rec_i, ri.size() * sizeof(int32_t), hipMemcpyDeviceToHost)) != hipSuccess)
+            return hip_fail(e, "hipMemcpy");
+        for (int32_t v : ri)
+            if (v == -2) return 0;
     }
     p->planar = true;
     return 0;
@@ -961,6 +975,8 @@ static int ensure_dense(tvam_plan* p) {
 // Make the per-ray records of (spp, seed) available on `stream`.  The
 // buffer grows on demand (first call with a larger spp); the pre-pass runs
 // only when the cached records do not match the call.
+#define TVAM_FROZEN_CAP (1 << 20)
+
 static int ensure_rays(tvam_plan* p, const TvamConsts& k, TvamTiles& t, hipStream_t stream) {
     const uint64_t n = (uint64_t)(k.a1 - k.a0) * k.crop_y * k.crop_x * t.spp;
     hipError_t e;
@@ -979,14 +995,24 @@ static int ensure_rays(tvam_plan* p, const TvamConsts& k, TvamTiles& t, hipStrea
             return hip_fail(e, "hipMalloc (ray records)");
         p->ray_cap = n;
     }
+    if (!p->d_frozen) {
+        if ((e = hipMalloc((void**)&p->d_frozen, (size_t)TVAM_FROZEN_CAP * sizeof(int64_t))) != hipSuccess ||
+            (e = hipMalloc((void**)&p->d_frozen_n, sizeof(unsigned long long))) != hipSuccess)
+            return hip_fail(e, "hipMalloc (frozen-ray list)");
+    }
     t.ray_f = p->d_ray_f;
     t.ray_i = p->d_ray_i;
     t.ray_g = p->d_ray_g;
+    t.frozen = p->d_frozen;
+    t.frozen_n = p->d_frozen_n;
+    t.frozen_cap = TVAM_FROZEN_CAP;
     const bool hit = p->ray_valid && p->ray_spp == t.spp && (k.regular || p->ray_seed == t.seed);
     if (hit) {
         e = hipStreamWaitEvent(stream, p->ray_ready, 0);
         return e == hipSuccess ? 0 : hip_fail(e, "hipStreamWaitEvent");
     }
+    if ((e = hipMemsetAsync(p->d_frozen_n, 0, sizeof(unsigned long long), stream)) != hipSuccess)
+        return hip_fail(e, "hipMemsetAsync");
     if ((e = tvam_launch_ray_setup(k, t, p->d_ray_f, p->d_ray_i, p->d_ray_g, stream)) != hipSuccess)
         return hip_fail(e, "ray setup launch");
     if ((e = hipEventRecord(p->ray_ready, stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
@@ -1062,6 +1088,7 @@ extern "C" int tvam_forward(tvam_plan* p, const float* active_data, const uint32
             stats = p->d_counter;
         }
         e = tvam_launch_tiles(TVAM_MODE_FWD, kc, t, p->lds_bytes, pat, idxmap, nullptr, dose, stats, stream);
+        if (e == hipSuccess) e = tvam_launch_frozen(TVAM_MODE_FWD, kc, t, pat, idxmap, nullptr, dose, nullptr, stream);
         if (e != hipSuccess) return hip_fail(e, "forward launch");
     }
     if (p->desc.albedo != 0.0f) {  // scattered segments (after each path's first medium segment)
@@ -1130,6 +1157,8 @@ extern "C" int tvam_adjoint(tvam_plan* p, const float* grad_dose, const uint32_t
         if ((rc = ensure_rays(p, k, t, stream))) return rc;
         e = tvam_launch_tiles(TVAM_MODE_ADJ, k, t, p->lds_bytes, nullptr, idxmap, grad_dose, grad_active, nullptr,
                               stream);
+        if (e == hipSuccess)
+            e = tvam_launch_frozen(TVAM_MODE_ADJ, k, t, nullptr, idxmap, grad_dose, grad_active, nullptr, stream);
         if (e != hipSuccess) return hip_fail(e, "adjoint launch");
     }
     if (p->desc.albedo != 0.0f && !p->empty) {
@@ -1169,6 +1198,8 @@ extern "C" int tvam_count_visits(tvam_plan* p, uint32_t spp, uint32_t seed, uint
         if ((rc = ensure_rays(p, k, t, nullptr))) return rc;
         e = tvam_launch_tiles(TVAM_MODE_COUNT, k, t, p->lds_bytes, nullptr, nullptr, nullptr, nullptr, p->d_counter,
                               nullptr);
+        if (e == hipSuccess)
+            e = tvam_launch_frozen(TVAM_MODE_COUNT, k, t, nullptr, nullptr, nullptr, nullptr, p->d_counter, nullptr);
     }
     if (e != hipSuccess) return hip_fail(e, "count launch");
     if (p->desc.albedo != 0.0f && !p->general) {
@@ -1231,6 +1262,45 @@ extern "C" int tvam_plan_set_volumes(tvam_plan* p, const float* volumes) {
     if (!p->surface) return fail(TVAM_ERR_INVALID, "volumes apply to surface-aware films (film_channels 2)");
     p->vols = volumes;
     return 0;
+}
+
+extern "C" int tvam_discretize(const tvam_desc* desc, float* occ, void* stream_) {
+    if (!desc || !occ) return fail(TVAM_ERR_INVALID, "null argument");
+    const tvam_desc& d = *desc;
+    if (d.abi_version != TVAM_ABI_VERSION) return fail(TVAM_ERR_INVALID, "tvam_desc.abi_version mismatch");
+    if (d.n_target_tris <= 0 || !d.target_tris) return fail(TVAM_ERR_INVALID, "No target shape found in the scene");
+    for (int a = 0; a < 3; ++a)
+        if (d.film_res[a] <= 0 || !(d.bbox_max[a] > d.bbox_min[a]))
+            return fail(TVAM_ERR_INVALID, "film resolution and sensor bbox must be positive");
+    if ((int64_t)d.film_res[0] * d.film_res[1] * d.film_res[2] > (int64_t)1 << 32)
+        return fail(TVAM_ERR_TOO_LARGE, "discretize: more than 2^32 voxels");
+    hipStream_t stream = (hipStream_t)stream_;
+    TvamConsts k{};
+    for (int a = 0; a < 3; ++a) {
+        k.res[a] = d.film_res[a];
+        k.bmin[a] = d.bbox_min[a];
+        k.h[a] = (d.bbox_max[a] - d.bbox_min[a]) / (float)d.film_res[a];  // utils.py:104
+    }
+    const size_t nb = (size_t)d.n_target_tris * 9 * sizeof(float);
+    float* d_tris = nullptr;
+    hipError_t e = hipMalloc((void**)&d_tris, nb);
+    if (e != hipSuccess) return hip_fail(e, "hipMalloc");
+    e = hipMemcpyAsync(d_tris, d.target_tris, nb, hipMemcpyHostToDevice, stream);
+    k.tgt = d_tris;
+    k.n_tgt = d.n_target_tris;
+    if (e == hipSuccess) e = tvam_launch_discretize(k, d.target_tris, occ, stream);
+    if (e == hipSuccess) e = hipStreamSynchronize(stream);
+    (void)hipFree(d_tris);
+    return e == hipSuccess ? 0 : hip_fail(e, "discretize launch");
+}
+
+extern "C" int tvam_plan_fwd_scale(tvam_plan* p, float* scale) {
+    if (!p || !scale) return fail(TVAM_ERR_INVALID, "null argument");
+    if (!p->planar || p->planar_fwd)
+        return fail(TVAM_ERR_INVALID, "tvam_plan_fwd_scale: this plan's forward is not the ray-driven planar kernel");
+    hipError_t e = hipSetDevice(p->device);
+    if (e == hipSuccess) e = hipMemcpy(scale, p->d_fscale, 2 * sizeof(float), hipMemcpyDeviceToHost);
+    return e == hipSuccess ? 0 : hip_fail(e, "hipMemcpy");
 }
 
 // bit 0: planar adjoint (+ ray-driven planar forward unless bit 1), bit 1: voxel-driven planar forward

@@ -70,6 +70,11 @@ __global__ __launch_bounds__(256) void tvam_planar_rays_kernel(TvamConsts k, con
         }
         if (rec_g)
             rec_g[i] = make_float4(q.step[0] > 0 ? q.ts[0] : -q.ts[0], q.step[1] > 0 ? q.ts[1] : -q.ts[1], wgt, 0.0f);
+        if ((fabsf(d2x) > 1e-8f && !(q.dtm0[0] < TVAM_INF)) || (fabsf(d2y) > 1e-8f && !(q.dtm0[1] < TVAM_INF))) {
+            vox[i] = make_float4(0.0f, 0.0f, -1.0f, 0.0f);  // frozen axis (sensor.py:358): the plan
+            rec_i[i] = -2;                                  // falls back to the per-ray tile path
+            continue;
+        }
         dx = d2x;  // the voxel-driven forward only serves straight rays (d2 == d)
         dy = d2y;
         const bool vx = fabsf(dx) > 1e-8f, vy = fabsf(dy) > 1e-8f;
@@ -299,6 +304,8 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
             }
             const float tin = fmaxf(fmaxf(tnx, tny), 0.0f);
             const float tout = fminf(fminf(tfx, tfy), q.z);
+            // e^{-st t_in} - e^{-st t_out} of absolute times: their rounding (ulp(t) / dt ~ 4e-5 at
+            // N = 400), not the cancellation, bounds this weight, so the cheaper telescoped form stays
             const float e = pl_exp2(k.nsig2 * tin) - pl_exp2(k.nsig2 * tout);
             wgt[c] = tout > tin ? e : 0.0f;
         }
@@ -524,13 +531,20 @@ static hipError_t tvam_launch_fwd_planar_z(dim3 grid, size_t lds, hipStream_t st
 
 // ---------------------------------------------------------------------------
 // Adjoint, ray-driven with Z-slice sharing.  Workgroup = (xy tile, Z
-// slices); LDS holds the gradient tile interleaved [voxel][Z] (+ 1-voxel
-// guard band).  A lane resumes ray (a, col) at the tile entry from its
-// row-independent record (closed form of the reference's stepping, as in
-// tvam_kernels.hip), marches it once, and accumulates Z dot products; each
-// row of each slice then receives its slice's value (volume.py:274-276).
+// slices); LDS holds the gradient tile (+ 1-voxel guard band) either as Z/4
+// planes [z/4][voxel][4] (PL, default) or interleaved [voxel][z].  A lane
+// resumes ray (a, col) at the tile entry from its row-independent record
+// (closed form of the reference's stepping, as in tvam_kernels.hip), marches it
+// once, and accumulates Z dot products; each row of each slice then receives
+// its slice's value (volume.py:274-276).
+// Banks: a ds_read_b128 is served in 4 groups of 16 lanes, each group
+// conflict-free when its lanes' 16-byte chunks (address / 16 mod 16) differ.
+// Interleaved, a voxel is 32 B (Z = 8), so voxels v and v + 8 collide; as
+// planes a voxel is one 16-byte chunk per read, so only v = v' (mod 16)
+// collide (neighbouring rays of a wave sit at neighbouring voxels, the row
+// pitch is odd).
 // ---------------------------------------------------------------------------
-template <int Z, bool PF, int NT>
+template <int Z, bool PF, int NT, bool PL = true, bool W2 = false>
 __global__ __launch_bounds__(NT) void tvam_adj_planar_kernel(TvamConsts k, TvamPlanar pl, TvamTiles tp,
                                                                   const int32_t* __restrict__ idxmap,
                                                                   const float* __restrict__ gin,
@@ -548,14 +562,18 @@ __global__ __launch_bounds__(NT) void tvam_adj_planar_kernel(TvamConsts k, TvamP
     const int wx = x1 - x0, wy = y1 - y0;
     const size_t plane = (size_t)k.res[0] * k.res[1];
 
-    // gradient tile, [voxel][z], scaled by 1/voxel volume (volume.py:130)
-    for (int i = threadIdx.x; i < tw * th * Z; i += NT) {
-        const int z = i / (tw * th), li = i - z * (tw * th);
+    // gradient tile, [z/4][voxel][4] (PL) or [voxel][z], scaled by 1/voxel volume (volume.py:130)
+    const int nvox = tw * th;
+    for (int i = threadIdx.x; i < nvox * Z; i += NT) {
+        const int z = i / nvox, li = i - z * nvox;
         const int ly = li / tw - 1, lx = li - (ly + 1) * tw - 1;
         float v = 0.0f;
         if (lx >= 0 && ly >= 0 && lx < wx && ly < wy && z0 + z < k.nz)
             v = gin[(size_t)(z0 + z) * plane + (size_t)(y0 + ly) * k.res[0] + (x0 + lx)] * k.inv_vol;
-        tile[(size_t)li * Z + z] = v;
+        if (PL)
+            tile[(size_t)(z >> 2) * nvox * 4 + (size_t)li * 4 + (z & 3)] = v;
+        else
+            tile[(size_t)li * Z + z] = v;
     }
     if (threadIdx.x == 0) {
         int n = 0;
@@ -640,21 +658,26 @@ __global__ __launch_bounds__(NT) void tvam_adj_planar_kernel(TvamConsts k, TvamP
         float Ty = ff.w < TVAM_INF ? fmaxf(fmaf((float)n1, an.y, ff.w) - tau_e, 0.0f) : TVAM_INF;
         const float rem = tau_x - tau_e, stop = rem - 1e-6f;
         const float nt0 = k.nsig2 * (ff.x + tau_e);
-        const int sxb = stx * Z * 4, syb = sty * tw * Z * 4;
-        const char* pv = reinterpret_cast<const char*>(tile) + (size_t)((vy - y0 + 1) * tw + (vx - x0 + 1)) * Z * 4;
+        constexpr int VB = PL ? 16 : Z * 4;  // bytes per voxel in one read's plane
+        const int sxb = stx * VB, syb = sty * tw * VB;
+        const int qstride = PL ? nvox * 16 : 16;  // bytes between a voxel's 4-slice groups
+        const char* pv = reinterpret_cast<const char*>(tile) + (size_t)((vy - y0 + 1) * tw + (vx - x0 + 1)) * VB;
         float acc[Z];
 #pragma unroll
         for (int z = 0; z < Z; ++z) acc[z] = 0.0f;
-        float e0 = pl_exp2(nt0);
+        // e0 = e^{-st t} (W2: st e^{-st t}, see TVAM_W2_MAX), restarted from exp2 at every tile entry
+        float e0 = W2 ? k.sig_t * pl_exp2(nt0) : pl_exp2(nt0), tp = 0.0f;
+        const float mhs = -0.5f * k.sig_t, msig = -k.sig_t;
         // one march, Z gathers per visit (see tvam_march in tvam_kernels.hip)
         for (;;) {
             const float tn = fminf(fminf(Tx, Ty), rem);
-            const float e1 = pl_exp2(fmaf(k.nsig2, tn, nt0));
-            const float cw = e0 - e1;
-            const float4* g4 = reinterpret_cast<const float4*>(pv);
+            const float dt = fmaxf(tn - tp, 0.0f);
+            const float cw = W2 ? e0 * dt * fmaf(mhs, dt, 1.0f) : e0 * tvam_omexp(k.sig_t * dt);
+            const float e1 = W2 ? fmaf(msig, cw, e0) : e0 - cw;
+            tp = tn;
 #pragma unroll
             for (int z4 = 0; z4 < Z / 4; ++z4) {
-                const float4 gv = g4[z4];
+                const float4 gv = *reinterpret_cast<const float4*>(pv + z4 * qstride);
                 acc[4 * z4 + 0] = fmaf(cw, gv.x, acc[4 * z4 + 0]);
                 acc[4 * z4 + 1] = fmaf(cw, gv.y, acc[4 * z4 + 1]);
                 acc[4 * z4 + 2] = fmaf(cw, gv.z, acc[4 * z4 + 2]);
@@ -677,11 +700,7 @@ __global__ __launch_bounds__(NT) void tvam_adj_planar_kernel(TvamConsts k, TvamP
                     act = idxmap[act];
                     if (act < 0) continue;
                 }
-#if defined(TVAM_EXPERIMENT) && TVAM_EXPERIMENT == 5  // timing only: no output atomics
-                if (v == 1234.5f) out[act] = v;
-#else
                 atomicAdd(&out[act], v);  // backward_from(Le * em_grad), volume.py:274-276
-#endif
             }
         }
     }
@@ -698,26 +717,39 @@ hipError_t tvam_launch_adj_planar(const TvamConsts& k, const TvamPlanar& pl, con
     const bool pf = pl.adj_prefetch != 0;
     // 512-thread workgroups (adj_nt): the LDS tile (28 KB at 40 x 40 x 4) admits 5
     // workgroups per CU, i.e. 5 waves per SIMD at 256 threads, 8 at 512
-#define TVAM_ADJ_LAUNCH(ZZ)                                                                                        \
+#define TVAM_ADJ_LAUNCH_PL(ZZ, PLL)                                                                                \
     if (pl.adj_nt == 1024)                                                                                         \
-        hipLaunchKernelGGL((tvam_adj_planar_kernel<ZZ, true, 1024>), grid, dim3(1024), lds, stream, k, pl, t, idxmap, \
-                           gin, out);                                                                              \
+        hipLaunchKernelGGL((tvam_adj_planar_kernel<ZZ, true, 1024, PLL>), grid, dim3(1024), lds, stream, k, pl, t,   \
+                           idxmap, gin, out);                                                                      \
     else if (pl.adj_nt == 512)                                                                                     \
-        hipLaunchKernelGGL((tvam_adj_planar_kernel<ZZ, true, 512>), grid, dim3(512), lds, stream, k, pl, t, idxmap,  \
-                           gin, out);                                                                              \
+        hipLaunchKernelGGL((tvam_adj_planar_kernel<ZZ, true, 512, PLL>), grid, dim3(512), lds, stream, k, pl, t,     \
+                           idxmap, gin, out);                                                                      \
     else if (pf)                                                                                                   \
-        hipLaunchKernelGGL((tvam_adj_planar_kernel<ZZ, true, 256>), grid, dim3(256), lds, stream, k, pl, t, idxmap,  \
-                           gin, out);                                                                              \
+        hipLaunchKernelGGL((tvam_adj_planar_kernel<ZZ, true, 256, PLL>), grid, dim3(256), lds, stream, k, pl, t,     \
+                           idxmap, gin, out);                                                                      \
     else                                                                                                           \
-        hipLaunchKernelGGL((tvam_adj_planar_kernel<ZZ, false, 256>), grid, dim3(256), lds, stream, k, pl, t, idxmap, \
-                           gin, out);
+        hipLaunchKernelGGL((tvam_adj_planar_kernel<ZZ, false, 256, PLL>), grid, dim3(256), lds, stream, k, pl, t,    \
+                           idxmap, gin, out);
+#define TVAM_ADJ_LAUNCH(ZZ)                                                                                    \
+    if (pl.adj_planes && pl.adj_nt == 1024 && pl.adj_w2 && k.vox_chord < TVAM_W2_MAX)                         \
+        hipLaunchKernelGGL((tvam_adj_planar_kernel<ZZ, true, 1024, true, true>), grid, dim3(1024), lds, stream, k, \
+                           pl, t, idxmap, gin, out);                                                           \
+    else if (!pl.adj_planes && pl.adj_nt == 1024 && pl.adj_w2 && k.vox_chord < TVAM_W2_MAX)                   \
+        hipLaunchKernelGGL((tvam_adj_planar_kernel<ZZ, true, 1024, false, true>), grid, dim3(1024), lds, stream, k, \
+                           pl, t, idxmap, gin, out);                                                           \
+    else if (pl.adj_planes) {                                                                                  \
+        TVAM_ADJ_LAUNCH_PL(ZZ, true)                                                                           \
+    } else {                                                                                                   \
+        TVAM_ADJ_LAUNCH_PL(ZZ, false)                                                                          \
+    }
     switch (Z) {
-        case 4: TVAM_ADJ_LAUNCH(4) break;
+        case 4: TVAM_ADJ_LAUNCH_PL(4, false) break;  // one 4-slice group: both layouts coincide
         case 8: TVAM_ADJ_LAUNCH(8) break;
         case 16: TVAM_ADJ_LAUNCH(16) break;
         default: return hipErrorInvalidValue;
     }
 #undef TVAM_ADJ_LAUNCH
+#undef TVAM_ADJ_LAUNCH_PL
     return hipGetLastError();
 }
 
@@ -806,7 +838,7 @@ __device__ __forceinline__ int pl_rint(float x) {
     return r;
 }
 
-template <int Z, bool FIXED>
+template <int Z, bool FIXED, bool W2>
 __device__ __forceinline__ void fwd_rays_body(const TvamConsts& k, const TvamPlanar& pl, const TvamTiles& tp,
                                               const float* __restrict__ pat, float fscale, unsigned char* smem,
                                               const int* s_roff, const int* s_rows, int tile_id, int tw,
@@ -863,11 +895,14 @@ __device__ __forceinline__ void fwd_rays_body(const TvamConsts& k, const TvamPla
         const float nt0 = k.nsig2 * (ff.x + tau_e);
         const int sxb = stx * 4, syb = sty * tw * 4;
         char* pv = reinterpret_cast<char*>(tile) + (size_t)((vy - y0 + 1) * tw + (vx - x0 + 1)) * 4;
-        float e0 = pl_exp2(nt0);
+        float e0 = W2 ? k.sig_t * pl_exp2(nt0) : pl_exp2(nt0), tp = 0.0f;  // as in the planar adjoint
+        const float mhs = -0.5f * k.sig_t, msig = -k.sig_t;
         for (;;) {
             const float tn = fminf(fminf(Tx, Ty), rem);
-            const float e1 = pl_exp2(fmaf(k.nsig2, tn, nt0));
-            const float cw = e0 - e1;
+            const float dt = fmaxf(tn - tp, 0.0f);
+            const float cw = W2 ? e0 * dt * fmaf(mhs, dt, 1.0f) : e0 * tvam_omexp(k.sig_t * dt);
+            const float e1 = W2 ? fmaf(msig, cw, e0) : e0 - cw;
+            tp = tn;
 #pragma unroll
             for (int z = 0; z < Z; ++z) {
                 if (FIXED)
@@ -920,10 +955,13 @@ __global__ __launch_bounds__(NT) void tvam_fwd_rays_planar_kernel(TvamConsts k, 
     }
     __syncthreads();
     if (s_roff[Z] > 0) {
-        if (fixed)
-            fwd_rays_body<Z, true>(k, pl, tp, pat, fscale, smem, s_roff, s_rows, tile_id, tw, pw * 4, x0, x1, y0, y1);
+        const bool w2 = k.vox_chord < TVAM_W2_MAX;
+        if (fixed && w2)
+            fwd_rays_body<Z, true, true>(k, pl, tp, pat, fscale, smem, s_roff, s_rows, tile_id, tw, pw * 4, x0, x1, y0, y1);
+        else if (fixed)
+            fwd_rays_body<Z, true, false>(k, pl, tp, pat, fscale, smem, s_roff, s_rows, tile_id, tw, pw * 4, x0, x1, y0, y1);
         else
-            fwd_rays_body<Z, false>(k, pl, tp, pat, fscale, smem, s_roff, s_rows, tile_id, tw, pw * 4, x0, x1, y0, y1);
+            fwd_rays_body<Z, false, false>(k, pl, tp, pat, fscale, smem, s_roff, s_rows, tile_id, tw, pw * 4, x0, x1, y0, y1);
     }
     __syncthreads();
     // dose = sum / voxel volume (volume.py:41-42, sensor.py:404)

@@ -236,14 +236,17 @@ __device__ __forceinline__ void sc_box_march(const TvamConsts& k, const SegDda& 
     const int s0 = q.step[0], s1 = q.step[1], s2 = q.step[2];
     const float stop = tau_x - 1e-6f;
     const float base = k.nsig2 * q.t_start;
-    float ea = sc_exp2(fmaf(k.nsig2, tau_e, base));
+    float ea = sc_exp2(fmaf(k.nsig2, tau_e, base)), tp = tau_e;
     for (int guard = 0; guard < 3 * 4096; ++guard) {
         const bool m0 = T0 <= T1 && T0 <= T2;
         const bool m1 = !m0 && T1 <= T2;
         const float tmin = m0 ? T0 : (m1 ? T1 : T2);
         const float tn = tmin < tau_x ? tmin : tau_x;
-        const float eb = sc_exp2(fmaf(k.nsig2, tn, base));
-        f(x, y, z, ea - eb);
+        // e^{-st t} (1 - e^{-st dt}) without cancellation (tvam_omexp); ea tracks e^{-st t}
+        const float c = ea * tvam_omexp(k.sig_t * fmaxf(tn - tp, 0.0f));
+        const float eb = ea - c;
+        tp = tn;
+        f(x, y, z, c);
         if (!(tn < stop)) break;
         if (m0) {
             x += s0;
@@ -398,6 +401,83 @@ __global__ __launch_bounds__(256) void tvam_scatter_kernel(TvamConsts k, TvamTil
             if (depth >= k.max_depth) break;
         }
         if (MODE == TVAM_MODE_ADJ && acc != 0.0f) atomicAdd(&out[act], acc * k.wscale);
+    }
+    if (MODE == TVAM_MODE_COUNT) {
+        for (int off = 32; off > 0; off >>= 1) nvis += __shfl_down(nvis, off, 64);
+        if ((threadIdx.x & 63) == 0 && nvis) atomicAdd(counter, (unsigned long long)nvis);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// Frozen-axis rays of the per-ray tile path.  The reference's DDA initialises
+// an axis's first crossing time as (next boundary - start) / d and disables the
+// axis when that comes out negative in fp32 (sensor.py:358: the start point
+// rounds past the boundary of its start voxel): the ray then never steps on
+// that axis and marches along the other one, off its geometric chord.  The
+// tile kernels only visit tiles on the chord (host-traced slot lists), so
+// tvam_ray_setup_kernel marks such rays (ray_i.y = -2 - slice) and this kernel
+// marches each of them over the whole grid (the brick walk's closed-form
+// stepping keeps a frozen axis frozen), with global atomics (forward), a
+// gather (adjoint) or a visit count.  About 3e-5 of the jittered rays of
+// BASELINE configs 4-5; none under regular sampling.
+// ---------------------------------------------------------------------------
+template <int MODE>
+__global__ __launch_bounds__(256) void tvam_frozen_kernel(TvamConsts k, TvamTiles tp, const float* __restrict__ pat,
+                                                          const int32_t* __restrict__ idxmap,
+                                                          const float* __restrict__ gin, float* __restrict__ out,
+                                                          unsigned long long* __restrict__ counter) {
+    const int spp = (int)tp.spp;
+    const int64_t per_angle = (int64_t)k.crop_y * k.crop_x;
+    // the appended list when it held every frozen ray, else a scan of all ray records
+    const unsigned long long nf = *tp.frozen_n;
+    const bool list = (int64_t)nf <= tp.frozen_cap;
+    const int64_t n = list ? (int64_t)nf : (int64_t)tp.n_shard * per_angle * spp;
+    uint64_t nvis = 0;
+    for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t i = list ? tp.frozen[j] : j;
+        if (tp.ray_i[i].y > -2) continue;
+        const int64_t local = i / spp;
+        const int smp = (int)(i - local * spp);
+        float em = 1.0f;
+        int64_t act = local;
+        if (MODE == TVAM_MODE_FWD) {
+            const float p = pat[local];
+            if (p == 0.0f && k.skip_zero) continue;
+            em = p * k.wscale * k.inv_vol;
+        } else if (MODE == TVAM_MODE_ADJ && idxmap) {
+            act = idxmap[local];
+            if (act < 0) continue;
+        }
+        const int al = (int)(local / per_angle);
+        const int64_t pix = local - (int64_t)al * per_angle;
+        const int rowc = (int)(pix / k.crop_x), colc = (int)(pix - (int64_t)rowc * k.crop_x);
+        float jx = 0.5f, jy = 0.5f;
+        if (!k.regular) {
+            TvamPcg rng;
+            rng.seed(tp.seed, (uint64_t)(local + k.shard_base) * (uint64_t)spp + (uint64_t)smp);
+            jx = rng.next_float();
+            jy = rng.next_float();
+        }
+        const float2 csv = tp.cs[al];
+        float xc, yc, ox, oy, oz, dx, dy;
+        tvam_ray_camera(k, k.crop_off_x + colc, k.crop_off_y + rowc, jx, jy, xc, yc);
+        tvam_ray_world(k, csv.x, csv.y, xc, yc, ox, oy, oz, dx, dy);
+        float o2x, o2y, d2x, d2y, maxt, wgt;
+        if (!tvam_segment(k, ox, oy, oz, dx, dy, o2x, o2y, d2x, d2y, maxt, wgt)) continue;
+        const float o[3] = {o2x, o2y, oz}, dv[3] = {d2x, d2y, 0.0f};
+        SegDda q;
+        if (!sc_dda_init(k, o, dv, maxt, q)) continue;
+        const int64_t sy = k.res[0], sz = (int64_t)k.res[0] * k.res[1];
+        const float emw = em * wgt;
+        float acc = 0.0f;
+        sc_seg_march(k, q, [&](int x, int y, int z, float c) {
+            if (z < k.z0 || z >= k.z0 + k.nz) return;  // outside this plan's film slab
+            const int64_t idx = x + y * sy + (int64_t)(z - k.z0) * sz;
+            if (MODE == TVAM_MODE_FWD) atomicAdd(&out[idx], emw * c);
+            else if (MODE == TVAM_MODE_ADJ) acc = fmaf(c, gin[idx] * k.inv_vol, acc);
+            ++nvis;
+        });
+        if (MODE == TVAM_MODE_ADJ && acc != 0.0f) atomicAdd(&out[act], acc * wgt * k.wscale);
     }
     if (MODE == TVAM_MODE_COUNT) {
         for (int off = 32; off > 0; off >>= 1) nvis += __shfl_down(nvis, off, 64);
@@ -755,6 +835,42 @@ __global__ __launch_bounds__(256) void tvam_volume_kernel(TvamConsts k, float3 m
     }
 }
 
+// discretize (utils.py:83-128): one thread per voxel, one ray from the voxel centre
+// bmin + (0.5 + i) h along square_to_uniform_sphere(next_2d) of the independent
+// sampler seeded (0, voxels) at lane = voxel index; inside when the centre is
+// strictly inside the mesh bbox and the first target hit faces away from the ray.
+// A voxel whose box meets no triangle's (grown) bounding box is decided the same way
+// (one ray, like the reference), so the result is exactly the per-voxel predicate.
+__global__ __launch_bounds__(256) void tvam_discretize_kernel(TvamConsts k, float3 mb0, float3 mb1,
+                                                              float* __restrict__ occ) {
+    const int64_t V = (int64_t)k.res[0] * k.res[1] * k.res[2];
+    for (int64_t v = (int64_t)blockIdx.x * 256 + threadIdx.x; v < V; v += (int64_t)gridDim.x * 256) {
+        const int vx = (int)(v % k.res[0]), vy = (int)((v / k.res[0]) % k.res[1]);
+        const int vz = (int)(v / ((int64_t)k.res[0] * k.res[1]));
+        const float ox = k.bmin[0] + (0.5f + (float)vx) * k.h[0];
+        const float oy = k.bmin[1] + (0.5f + (float)vy) * k.h[1];
+        const float oz = k.bmin[2] + (0.5f + (float)vz) * k.h[2];
+        float inside = 0.0f;
+        if (ox > mb0.x && oy > mb0.y && oz > mb0.z && ox < mb1.x && oy < mb1.y && oz < mb1.z) {
+            TvamPcg rng;
+            rng.seed(0u, (uint64_t)v);
+            const float sx = rng.next_float(), sy = rng.next_float();
+            const float dz = 1.0f - 2.0f * sy, r = sqrtf(fmaxf(1.0f - dz * dz, 0.0f));
+            const float dx = r * cosf(TVAM_TWO_PI * sx), dy = r * sinf(TVAM_TWO_PI * sx);
+            int tri;
+            const float t = sf_target_hit(k, ox, oy, oz, dx, dy, dz, tri);
+            if (t < TVAM_INF) {
+                const float* p = k.tgt + 9 * tri;
+                const float e1x = p[3] - p[0], e1y = p[4] - p[1], e1z = p[5] - p[2];
+                const float e2x = p[6] - p[0], e2y = p[7] - p[1], e2z = p[8] - p[2];
+                const float cx = e1y * e2z - e1z * e2y, cy = e1z * e2x - e1x * e2z, cz = e1x * e2y - e1y * e2x;
+                inside = cx * dx + cy * dy + cz * dz > 0.0f ? 1.0f : 0.0f;
+            }
+        }
+        occ[v] = inside;
+    }
+}
+
 }  // namespace
 
 hipError_t tvam_launch_surface_paths(int mode, const TvamConsts& k, const TvamTiles& t, const float* pat,
@@ -847,6 +963,46 @@ hipError_t tvam_launch_volumes(const TvamConsts& k, uint32_t sample_count, float
     if (e == hipSuccess) e = hipStreamSynchronize(stream);
     (void)hipFree(d_box);
     return e;
+}
+
+hipError_t tvam_launch_discretize(const TvamConsts& k, const float* h_tris, float* occ, hipStream_t stream) {
+    float3 mb0 = make_float3(TVAM_INF, TVAM_INF, TVAM_INF), mb1 = make_float3(-TVAM_INF, -TVAM_INF, -TVAM_INF);
+    for (size_t i = 0; i < (size_t)k.n_tgt * 9; i += 3) {  // the target bbox (utils.py:98, :118)
+        mb0.x = fminf(mb0.x, h_tris[i]);
+        mb0.y = fminf(mb0.y, h_tris[i + 1]);
+        mb0.z = fminf(mb0.z, h_tris[i + 2]);
+        mb1.x = fmaxf(mb1.x, h_tris[i]);
+        mb1.y = fmaxf(mb1.y, h_tris[i + 1]);
+        mb1.z = fmaxf(mb1.z, h_tris[i + 2]);
+    }
+    const int64_t V = (int64_t)k.res[0] * k.res[1] * k.res[2];
+    const unsigned g = (unsigned)std::min<int64_t>(std::max<int64_t>((V + 255) / 256, 1), 1 << 20);
+    hipLaunchKernelGGL(tvam_discretize_kernel, dim3(g), dim3(256), 0, stream, k, mb0, mb1, occ);
+    return hipGetLastError();
+}
+
+hipError_t tvam_launch_frozen(int mode, const TvamConsts& k, const TvamTiles& t, const float* pat,
+                              const int32_t* idxmap, const float* gin, float* out, unsigned long long* counter,
+                              hipStream_t stream) {
+    if (!t.frozen || !t.frozen_n) return hipErrorInvalidValue;
+    const int64_t n = (int64_t)t.n_shard * k.crop_y * k.crop_x * t.spp;
+    int64_t g = (n + 255) / 256;
+    if (g > 4096) g = 4096;  // the list is short; a scan (list overflow) grid-strides
+    if (g < 1) g = 1;
+    switch (mode) {
+        case TVAM_MODE_FWD:
+            hipLaunchKernelGGL(tvam_frozen_kernel<TVAM_MODE_FWD>, dim3((unsigned)g), dim3(256), 0, stream, k, t, pat,
+                               idxmap, gin, out, counter);
+            break;
+        case TVAM_MODE_ADJ:
+            hipLaunchKernelGGL(tvam_frozen_kernel<TVAM_MODE_ADJ>, dim3((unsigned)g), dim3(256), 0, stream, k, t, pat,
+                               idxmap, gin, out, counter);
+            break;
+        default:
+            hipLaunchKernelGGL(tvam_frozen_kernel<TVAM_MODE_COUNT>, dim3((unsigned)g), dim3(256), 0, stream, k, t,
+                               pat, idxmap, gin, out, counter);
+    }
+    return hipGetLastError();
 }
 
 hipError_t tvam_launch_scatter_paths(int mode, const TvamConsts& k, const TvamTiles& t, const float* pat,

@@ -147,6 +147,16 @@ class Projection:
             _abi.check(self.lib.tvam_plan_stats(self._plan, ctypes.byref(v)))
         return int(v.value)
 
+    def fwd_scale(self):
+        """(scale, fixed) of the last ray-driven planar forward: the int32 fixed-point scale 2^e and
+        whether fixed point was used (False: the overflow bound was not finite, float adds)."""
+        import numpy as np
+        v = np.zeros(2, dtype=np.float32)
+        with torch.cuda.device(self.device):
+            torch.cuda.synchronize(self.device)
+            _abi.check(self.lib.tvam_plan_fwd_scale(self._plan, v.ctypes.data))
+        return float(v[0]), bool(v[1] != 0.0)
+
     def count_visits(self, spp: int = 1, seed: int = 0) -> int:
         v = ctypes.c_uint64(0)
         with torch.cuda.device(self.device):

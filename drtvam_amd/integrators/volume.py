@@ -66,6 +66,28 @@ class VolumeIntegrator(TVAMIntegrator):
         x = projector.active_data if active_data is None else active_data
         return engine_render(proj, x, pix, spp, spp_grad, seed, derive_seed_grad(seed) if seed_grad is None else seed_grad)
 
+    def render_forward(self, scene, params=None, sensor=0, seed: int = 0, spp: int = 0,
+                       tangent: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """Forward-mode derivative (volume.py:58-95): the dose tangent [Z, Y, X, C] produced by a
+        tangent of projector.active_data.  The render is linear in the patterns, so this is the
+        forward projection of the tangent (the reference propagates dr.grad(active_data) through
+        Le in ADMode.Forward and scales by inv_vol, as the forward kernel does).  `tangent`
+        defaults to projector.active_data.grad, the slot the reference reads it from."""
+        _check_projectors(scene)
+        sensor = self._sensor(scene, sensor)
+        projector = scene.projector
+        if tangent is None:
+            tangent = projector.active_data.grad
+        if tangent is None:
+            raise ValueError("render_forward: no tangent (set projector.active_data.grad or pass `tangent`)")
+        if tangent.numel() != projector.active_size():
+            raise ValueError("render_forward: the tangent must have one entry per active pixel")
+        seed, spp = self.prepare(projector, seed, spp)
+        proj = self.projection(scene, sensor)
+        pix = None if projector.dense else projector.active_pixels
+        with torch.no_grad():
+            return proj.forward(tangent.detach().to(dtype=torch.float32).contiguous(), pix, spp, seed)
+
     def render_backward(self, scene, params, grad_in: torch.Tensor, sensor=0, seed: int = 0, spp: int = 0) -> None:
         _check_projectors(scene)
         sensor = self._sensor(scene, sensor)

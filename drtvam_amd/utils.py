@@ -1,10 +1,9 @@
 """Target discretisation and reporting helpers (mirror of drtvam/utils.py).
 
 ``discretize`` (utils.py:83-128) voxelises the target mesh into a binary
-occupancy grid [Z, Y, X, 1] on the sensor's voxel centres.  The reference casts
-one random ray per voxel centre with Mitsuba and tests the hit normal; here the
-same inside/outside predicate is evaluated by a scanline parity test along +z
-(exact for closed meshes), in numpy.
+occupancy grid [Z, Y, X, 1] on the sensor's voxel centres with the reference's
+algorithm (one sampled ray per voxel centre, orientation of the first hit), on
+the GPU through ``tvam_discretize``.
 """
 from __future__ import annotations
 
@@ -105,59 +104,27 @@ def mesh_bbox(filename):
 
 
 def target_transform(bbox_min, bbox_max, size=1.0, center=(0., 0., 0.)):
-    """optimize.py:38-50: centre the mesh bbox, scale its largest extent to `size`, move to `center`."""
-    c = 0.5 * (np.asarray(bbox_min) + np.asarray(bbox_max))
-    s = size / np.max(np.asarray(bbox_max) - np.asarray(bbox_min))
+    """optimize.py:38-50: centre the mesh bbox, scale its largest extent to `size`, move to
+    `center`: translate(center) @ scale(size / max(extents)) @ translate(-c), with c, the scale
+    and the translation rounded to fp32 as Mitsuba's ScalarTransform4f forms them."""
+    f = np.float32
+    bmin, bmax = np.asarray(bbox_min, f), np.asarray(bbox_max, f)
+    c = f(0.5) * (bmin + bmax)
+    s = f(size) / np.max(bmax - bmin)
+    t = np.asarray(center, f) + s * (-c)
     m = np.eye(4)
-    m[:3, :3] *= s
-    m[:3, 3] = np.asarray(center) - s * c
+    m[:3, :3] *= float(s)
+    m[:3, 3] = t.astype(np.float64)
     return m
 
 
-def voxelize_mesh(verts, tris, bbox_min, voxel_size, res):
-    """Binary occupancy [Z, Y, X] of voxel centres inside a closed triangle mesh (z-scanline parity)."""
-    rx, ry, rz = res
-    xs = bbox_min[0] + (0.5 + np.arange(rx)) * voxel_size[0]
-    ys = bbox_min[1] + (0.5 + np.arange(ry)) * voxel_size[1]
-    zs = bbox_min[2] + (0.5 + np.arange(rz)) * voxel_size[2]
-    occ = np.zeros((rz, ry, rx), dtype=np.uint8)
-    a, b, c = verts[tris[:, 0]], verts[tris[:, 1]], verts[tris[:, 2]]
-    X, Y = np.meshgrid(xs, ys, indexing='xy')  # [ry, rx]
-    # tiny irrational shift of the scan lines: voxel centres of grid-aligned meshes would otherwise
-    # pass exactly through shared triangle edges and break the crossing parity
-    px = X.reshape(-1) + voxel_size[0] * 1.2345679e-4 * np.sqrt(2.0)
-    py = Y.reshape(-1) + voxel_size[1] * 2.3456789e-4 * np.sqrt(3.0)
-    crossings = [[] for _ in range(px.size)]
-    for t in range(tris.shape[0]):
-        A, B, C = a[t], b[t], c[t]
-        det = (B[0] - A[0]) * (C[1] - A[1]) - (C[0] - A[0]) * (B[1] - A[1])
-        if det == 0:
-            continue
-        lo = max(np.searchsorted(xs, min(A[0], B[0], C[0])) - 1, 0)
-        hi = np.searchsorted(xs, max(A[0], B[0], C[0]), side='right') + 1
-        jlo = max(np.searchsorted(ys, min(A[1], B[1], C[1])) - 1, 0)
-        jhi = np.searchsorted(ys, max(A[1], B[1], C[1]), side='right') + 1
-        if lo >= hi or jlo >= jhi:
-            continue
-        jj, ii = np.meshgrid(np.arange(jlo, jhi), np.arange(lo, hi), indexing='ij')
-        idx = (jj * rx + ii).reshape(-1)
-        qx, qy = px[idx], py[idx]
-        w1 = ((qx - A[0]) * (C[1] - A[1]) - (C[0] - A[0]) * (qy - A[1])) / det
-        w2 = ((B[0] - A[0]) * (qy - A[1]) - (qx - A[0]) * (B[1] - A[1])) / det
-        w0 = 1.0 - w1 - w2
-        inside = (w0 >= 0) & (w1 >= 0) & (w2 >= 0)
-        zc = w0 * A[2] + w1 * B[2] + w2 * C[2]
-        for k in np.nonzero(inside)[0]:
-            crossings[idx[k]].append(zc[k])
-    for p, zl in enumerate(crossings):
-        if len(zl) < 2:
-            continue
-        zl = np.sort(np.asarray(zl))
-        j, i = divmod(p, rx)
-        for s in range(0, len(zl) - 1, 2):
-            m = (zs > zl[s]) & (zs < zl[s + 1])
-            occ[m, j, i] = 1
-    return occ
+def transform_points(m, verts):
+    """fp32 world positions of mesh vertices under the affine 4x4 `m` (Mitsuba's
+    transform_affine: one fused multiply-add chain per coordinate; products of fp32 values are
+    exact in float64, so one float64 sum rounded to fp32 stands in for the fma chain)."""
+    m = np.asarray(m, np.float64)
+    v = np.asarray(verts, np.float32).astype(np.float64)
+    return (v @ m[:3, :3].T + m[:3, 3]).astype(np.float32)
 
 
 def target_triangles(scene):
@@ -166,24 +133,36 @@ def target_triangles(scene):
     if tgt is None or 'filename' not in tgt:
         raise ValueError("No target shape found in the scene")
     verts, tris = read_ply(tgt['filename'])
-    m = np.asarray(tgt.get('to_world', np.eye(4)), dtype=np.float64)
-    verts = (verts @ m[:3, :3].T + m[:3, 3]).astype(np.float32)
-    return verts[np.asarray(tris)]
+    return transform_points(tgt.get('to_world', np.eye(4)), verts)[np.asarray(tris)]
 
 
 def discretize(scene, sensor=0):
-    """Binary target occupancy [Z, Y, X, 1] float32 on the sensor grid (utils.py:83-128)."""
+    """Binary target occupancy [Z, Y, X, 1] float32 on the sensor grid (utils.py:83-128).
+
+    As the reference: one ray per voxel centre, direction square_to_uniform_sphere of the
+    independent sampler seeded (0, voxels) at lane = voxel index, inside when the centre lies
+    strictly inside the target bbox and the first target hit faces away from the ray
+    (dot(n, d) > 0).  Runs on the GPU (`tvam_discretize`); there is no CPU path.
+    """
+    import ctypes
+    from . import _abi
     if isinstance(sensor, int):
         sensor = scene.sensors()[sensor]
-    tgt = scene.target
-    if tgt is None:
+    if scene.target is None or 'filename' not in scene.target:
         raise ValueError("No target shape found in the scene")
-    verts, tris = read_ply(tgt['filename'])
-    m = np.asarray(tgt.get('to_world', np.eye(4)), dtype=np.float64)
-    verts = verts @ m[:3, :3].T + m[:3, 3]
-    occ = voxelize_mesh(verts, tris, sensor.bbox_min.astype(np.float64), sensor.voxel_size.astype(np.float64),
-                        sensor.resolution())
-    return torch.from_numpy(occ.astype(np.float32)[..., None])
+    if not torch.cuda.is_available():
+        raise _abi.TvamError("discretize runs on the GPU (tvam_discretize); no ROCm device is visible")
+    d = _abi.default_desc()
+    rx, ry, rz = sensor.resolution()
+    d.film_res[:] = (rx, ry, rz)
+    d.bbox_min[:] = [float(v) for v in sensor.bbox_min]
+    d.bbox_max[:] = [float(v) for v in sensor.bbox_max]
+    d.set_target(target_triangles(scene))
+    dev = torch.device("cuda", torch.cuda.current_device())
+    out = torch.empty((rz, ry, rx), dtype=torch.float32, device=dev)
+    lib = _abi.load_library()
+    _abi.check(lib.tvam_discretize(ctypes.byref(d), out.data_ptr(), torch.cuda.current_stream(dev).cuda_stream))
+    return out.cpu()[..., None]
 
 
 def analytic_target(res, bbox_min, bbox_max, kind='box_hole'):

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define TVAM_ABI_VERSION 6
+#define TVAM_ABI_VERSION 7
 
 /* error codes */
 #define TVAM_OK               0
@@ -204,6 +204,21 @@ int tvam_radon(tvam_plan* plan, const float* target_tris, int32_t n_target_tris,
    voxel (independent sampler seeded (0, voxel)), each classified by the orientation of the
    first target hit along a uniform random direction.  Synchronous. */
 int tvam_compute_volume(tvam_plan* plan, uint32_t sample_count, float* volumes, void* hip_stream);
+
+/* Target discretisation (utils.py:83-128 discretize; the target transform of
+   optimize.py:30-50 is applied by the caller): occ[z][y][x] (device, f32, overwritten)
+   = 1 where the voxel centre bbox_min + (0.5 + i) h lies strictly inside the target
+   mesh's bbox and the first hit of a ray from it along square_to_uniform_sphere(next_2d)
+   (independent sampler seeded (0, voxels), lane = flat voxel index) faces away from the
+   ray (dot(n, d) > 0), else 0.  Uses desc->film_res, bbox_min/max and target_tris
+   (host, world space).  Runs on the current HIP device; synchronous. */
+int tvam_discretize(const tvam_desc* desc, float* occ, void* hip_stream);
+
+/* Diagnostics (host-synchronous): the fixed-point scale of the last forward of a plan
+   served by the ray-driven planar forward (tvam_plan_path == 1): scale[0] = 2^e with
+   |every voxel's scaled sum| < 2^30 guaranteed, scale[1] = 1 (exact int32 fixed point)
+   or 0 (the bound was not finite: float LDS adds). */
+int tvam_plan_fwd_scale(tvam_plan* plan, float* scale);
 
 /* Surface-aware plans: the per-channel voxel volumes the forward divides by and the
    adjoint multiplies the incoming gradient with (inv_vol = 1/volume, 0 where volume

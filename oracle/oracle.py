@@ -53,6 +53,10 @@ def lib():
         L.oracle_adjoint_surface.argtypes = L.oracle_forward_surface.argtypes
         L.oracle_compute_volume.restype = ctypes.c_int
         L.oracle_compute_volume.argtypes = [D, ctypes.c_uint32, P, ctypes.c_int]
+        L.oracle_frozen_axes.restype = ctypes.c_uint64
+        L.oracle_frozen_axes.argtypes = [ctypes.c_int]
+        L.oracle_discretize.restype = ctypes.c_int
+        L.oracle_discretize.argtypes = [D, P, ctypes.c_int]
         L.oracle_dda_ray.restype = ctypes.c_int
         L.oracle_dda_ray.argtypes = [D, P, P, ctypes.c_float, ctypes.c_double, P, P]
         _lib = L
@@ -148,6 +152,22 @@ def compute_volume(desc, sample_count=2 ** 14, nthreads=1):
     rc = lib().oracle_compute_volume(ctypes.byref(desc), sample_count, _ptr(out), nthreads)
     if rc:
         raise ValueError(f"oracle_compute_volume failed ({rc})")
+    return out
+
+
+def frozen_axes(reset=True):
+    """Number of DDA segments (since the last reset) that started with a valid axis whose first
+    crossing time rounded negative, so that axis never steps (sensor.py:358)."""
+    return int(lib().oracle_frozen_axes(1 if reset else 0))
+
+
+def discretize(desc, nthreads=1):
+    """Binary target occupancy [z, y, x] (float32) of the desc's target mesh on its film grid
+    (utils.py:83-128: one sampled direction per voxel centre)."""
+    out = np.zeros(film_shape(desc), dtype=np.float32)
+    rc = lib().oracle_discretize(ctypes.byref(desc), _ptr(out), nthreads)
+    if rc:
+        raise ValueError(f"oracle_discretize failed ({rc})")
     return out
 
 

@@ -429,6 +429,15 @@ static int or_segment_cylindrical(const or_scene* s, const or_ray* ray, float o2
     return 0;
 }
 
+/* Diagnostics: segments whose DDA starts with a valid axis that never steps because its
+   first crossing time came out negative in fp32 (sensor.py:358). */
+static uint64_t or_frozen_axes = 0;
+uint64_t oracle_frozen_axes(int reset) {
+    uint64_t v = or_frozen_axes;
+    if (reset) or_frozen_axes = 0;
+    return v;
+}
+
 /* DDA declared ahead for the scattering path */
 static double or_dda(const or_scene* s, const float o[3], const float dd[3], float maxt, double em,
                      int mode, double* film, const float* grad, int only_slice, uint64_t* visits);
@@ -731,7 +740,15 @@ static double or_dda(const or_scene* s, const float o[3], const float dd[3], flo
         if (dd[k] < 0.0f) next = next + s->h[k];
         int valid = fabsf(dd[k]) > 1e-8f;
         dtmax[k] = valid ? (next - gs[k]) / dd[k] : INFINITY;
-        if (dtmax[k] < 0.0f) dtmax[k] = INFINITY;
+        if (dtmax[k] < 0.0f) { /* sensor.py:358: the axis never steps ("frozen") */
+            dtmax[k] = INFINITY;
+            if (valid) {
+#ifdef _OPENMP
+#pragma omp atomic
+#endif
+                ++or_frozen_axes;
+            }
+        }
         tstep[k] = valid ? (s->h[k] / dd[k]) * (float)step[k] : INFINITY;
     }
     if (only_slice >= 0 && cur[2] != only_slice) return 0.0;
@@ -1422,6 +1439,60 @@ int oracle_compute_volume(const tvam_desc* d, uint32_t sample_count, float* volu
         }
         volumes[2 * v] = (float)cin * vvol / (float)sample_count;
         volumes[2 * v + 1] = (float)cout * vvol / (float)sample_count;
+    }
+    return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Target discretisation (utils.py:83-128): one ray per voxel centre         */
+/* pos = bbox.min + (0.5 + (x, y, z)) * voxel_size (:106-112), direction     */
+/* square_to_uniform_sphere(next_2d) of the independent sampler seeded       */
+/* (0, wavefront = voxels), lane = flat voxel index (:114-117); a voxel is   */
+/* tested only when its centre lies strictly inside the target bbox (:118)   */
+/* and is inside when the first target hit faces away from the ray,         */
+/* dot(n, d) > 0 with n the geometric normal (:120-122).  occ[z][y][x] = 0/1 */
+/* (float).  Target triangles: d->target_tris (world space).                 */
+/* ------------------------------------------------------------------------ */
+int oracle_discretize(const tvam_desc* d, float* occ, int nthreads) {
+    if (d->n_target_tris <= 0 || !d->target_tris || !occ) return TVAM_ERR_INVALID;
+    or_scene s;
+    or_scene_init(&s, d);
+    float mb0[3] = {INFINITY, INFINITY, INFINITY}, mb1[3] = {-INFINITY, -INFINITY, -INFINITY};
+    for (int i = 0; i < 3 * d->n_target_tris; ++i)
+        for (int k = 0; k < 3; ++k) {
+            mb0[k] = fminf(mb0[k], d->target_tris[3 * i + k]);
+            mb1[k] = fmaxf(mb1[k], d->target_tris[3 * i + k]);
+        }
+    const int64_t V = (int64_t)s.res[0] * s.res[1] * s.res[2];
+    if (nthreads < 1) nthreads = 1;
+#ifdef _OPENMP
+#pragma omp parallel for schedule(dynamic, 64) num_threads(nthreads)
+#endif
+    for (int64_t v = 0; v < V; ++v) {
+        const int vx = (int)(v % s.res[0]), vy = (int)((v / s.res[0]) % s.res[1]), vz = (int)(v / ((int64_t)s.res[0] * s.res[1]));
+        const float vox[3] = {(float)vx, (float)vy, (float)vz};
+        or_pcg32 rng;
+        or_sampler_seed(&rng, 0u, (uint64_t)v);
+        const float sx = or_pcg_float(&rng), sy = or_pcg_float(&rng);
+        float o[3], dd[3];
+        for (int k = 0; k < 3; ++k) o[k] = d->bbox_min[k] + (0.5f + vox[k]) * s.h[k];
+        const float z = 1.0f - 2.0f * sy, r = sqrtf(fmaxf(1.0f - z * z, 0.0f));
+        dd[0] = r * cosf(OR_TWO_PI * sx);
+        dd[1] = r * sinf(OR_TWO_PI * sx);
+        dd[2] = z;
+        int inside = 0;
+        if (o[0] > mb0[0] && o[1] > mb0[1] && o[2] > mb0[2] && o[0] < mb1[0] && o[1] < mb1[1] && o[2] < mb1[2]) {
+            int tri;
+            const float t = or_target_hit(d, o, dd, &tri);
+            if (t < INFINITY) {
+                const float* p = d->target_tris + 9 * tri;
+                float e1[3] = {p[3] - p[0], p[4] - p[1], p[5] - p[2]}, e2[3] = {p[6] - p[0], p[7] - p[1], p[8] - p[2]};
+                float c[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2],
+                              e1[0] * e2[1] - e1[1] * e2[0]};
+                inside = c[0] * dd[0] + c[1] * dd[1] + c[2] * dd[2] > 0.0f;
+            }
+        }
+        occ[v] = inside ? 1.0f : 0.0f;
     }
     return 0;
 }

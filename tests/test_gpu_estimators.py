@@ -3,8 +3,9 @@ and sample_time (common.py:101-104), against the oracle on identical sampler str
 reference's own FD-vs-AD test of tests/test_integrators.py:69-110 (dda / ratio / delta on its
 double-cylinder scattering scene with sample_time, 128 spp, bar 2e-4).
 
-Tolerance vs the oracle: 1e-3 relative L2 like the scattering tests (host and device libm may
-differ in the last ulp of logf / sinf, which can flip a comparison on a rare path)."""
+Tolerance vs the oracle: the flip protocol of parity_util.py, like the scattering tests (host and
+device libm may differ in the last ulp of logf / sinf, which can flip a comparison on a rare
+path: those paths' pixels are counted, every other path is held to 1e-4 relative L2)."""
 import numpy as np
 import pytest
 import torch
@@ -14,6 +15,7 @@ pytestmark = pytest.mark.gpu
 from drtvam_amd import _abi
 from drtvam_amd.configs import benchy_index_matched, cylindrical_refraction, desc_from_config
 from drtvam_amd.engine import Projection, render
+from parity_util import flip_protocol
 
 
 def rel_l2(a, b):
@@ -57,17 +59,11 @@ def test_paths_match_oracle(oracle, case):
     n = d.n_patterns * d.crop_y * d.crop_x
     rng = np.random.default_rng(0)
     pat = rng.uniform(0, 0.1, n).astype(np.float32)
-    ref, visits = oracle.forward(d, pat, spp=spp, seed=6, nthreads=8)
-    proj = Projection(d, "cuda:0")
-    got = proj.forward(torch.as_tensor(pat, device="cuda:0"), None, spp, 6).cpu().numpy()[..., 0]
-    assert np.abs(ref).max() > 0
-    assert rel_l2(got, ref) < 1e-3
-    hv = proj.count_visits(spp, 6)
-    assert abs(hv - visits) <= max(2, 2e-3 * visits)
     G = rng.uniform(-1, 1, (N, N, N)).astype(np.float32)
-    gref, _ = oracle.adjoint(d, G, spp=spp, seed=6, nthreads=8)
-    g = proj.adjoint(torch.as_tensor(G, device="cuda:0"), n, None, spp, 6).cpu().numpy()
-    assert rel_l2(g, gref) < 1e-3
+    proj = Projection(d, "cuda:0")
+    out = flip_protocol(oracle, proj, d, pat, G, spp, 6, nthreads=8)
+    hv = proj.count_visits(spp, 6)
+    assert abs(hv - out["visits"]) <= max(2, 2e-3 * out["visits"])
     proj.close()
 
 

@@ -23,7 +23,7 @@ from drtvam_amd.optimize import optimize
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from test_oracle_surface import cube_tris  # noqa: E402
-from test_setup import box_hole_reference  # noqa: E402
+from discretize_util import box_hole_reference  # noqa: E402
 from drtvam_amd.utils import read_ply  # noqa: E402
 
 GOLDEN = os.path.join(os.path.dirname(__file__), "golden")
