@@ -39,8 +39,29 @@ def scene_config(config, N, A):
             5: square_occluded}[config](N=N, angles=A)
 
 
+def host_info():
+    """CPU model, logical CPUs of the machine and of this process's affinity / OpenMP share."""
+    model = "unknown"
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    nproc = os.cpu_count() or 1
+    try:
+        affinity = len(os.sched_getaffinity(0))
+    except AttributeError:
+        affinity = nproc
+    omp = os.environ.get("OMP_NUM_THREADS")
+    threads = min(affinity, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else affinity
+    return {"cpu_model": model, "nproc": nproc, "affinity": affinity, "omp_num_threads": omp, "threads": threads}
+
+
 def cpu_baseline(config, N, seconds, threads):
-    """Oracle (C/OpenMP port of the reference march) on a bounded angle subset of the same workload."""
+    """Oracle (C/OpenMP port of the reference march) on a bounded angle subset of the same workload,
+    plus the loss / L-BFGS vector work of an iteration (numpy, timed on one pass and scaled)."""
     import numpy as np
     from oracle import oracle
     from drtvam_amd.configs import desc_from_config
@@ -66,12 +87,69 @@ def cpu_baseline(config, N, seconds, threads):
     per_angle = (2 * tf + ta) / 2
     na = int(max(2, min(N, seconds / max(per_angle, 1e-6))))
     tf, ta, v = run(na)
-    t_iter = (2 * tf + ta) * (N / na)
+    t_march = (2 * tf + ta) * (N / na)
+    # vector work of one iteration: ~3 loss passes (value + dL/dD, Armijo probes) over the film and
+    # ~20 L-BFGS passes (history dots, direction, update) over the patterns (lbfgs.py:198-275), each
+    # timed as one fused numpy pass a * x + y over N^3 floats
+    x = np.random.default_rng(2).uniform(0, 1, N ** 3).astype(np.float32)
+    y = np.empty_like(x)
+    t0 = time.perf_counter()
+    np.multiply(x, np.float32(0.5), out=y)
+    np.add(y, x, out=y)
+    t_pass = time.perf_counter() - t0
+    t_vec = 23 * t_pass
+    t_iter = t_march + t_vec
     return {"value": 1.0 / t_iter, "unit": "it/s", "cores": threads, "kind": "port",
-            "sample": f"oracle/tvam_oracle.c (C/OpenMP, {threads} threads, slice-private accumulation) on {na} of {N} "
-                      f"angles of the {N}^3 config-{config} workload: fwd {tf:.2f}s + adj {ta:.2f}s, "
-                      f"{v / tf / 1e6:.0f} M visits/s; iteration = 2 fwd + 1 adj scaled to {N} angles "
-                      f"(loss/L-BFGS vector work not included)"}
+            "impl": "oracle/tvam_oracle.c: scalar C restatement (gcc -O3 -fopenmp, no SIMD intrinsics), "
+                    "slice-private accumulation -- not Dr.Jit's LLVM backend (mitsuba/drjit are not installed)",
+            "host": host_info(),
+            "sample": f"{na} of {N} angles of the {N}^3 config-{config} workload: fwd {tf:.2f}s + adj {ta:.2f}s "
+                      f"({v / tf / 1e6:.0f} M visits/s); iteration = (2 fwd + 1 adj) x {N}/{na} = {t_march:.1f}s "
+                      f"+ 23 vector passes over {N}^3 floats (numpy, {t_pass * 1e3:.0f} ms each) = {t_vec:.2f}s"}
+
+
+# Peaks (MI355X_MICROARCH.md): HBM3E 8 TB/s; LDS 256 B/clk/CU for ds_read_b128 (64 banks x 4 B) on
+# 256 CUs; VALU: a wave64 instruction occupies a SIMD-32 for 2 cycles (F32 157.3 TF = 1024 SIMDs x
+# 32 lanes x 2 flop x 2.4 GHz); clock 2.4 GHz (spec peak engine clock).
+CLOCK_GHZ = 2.4
+LDS_PEAK_GBS = 256 * 256 * CLOCK_GHZ  # 157,286 GB/s
+VALU_PEAK_WAVE_INSTR = 1024 * CLOCK_GHZ * 1e9 / 2  # wave64 VALU instructions / s
+PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02", "pmc_config2.json")
+
+
+def make_roofline(args, N, A, world, prob, visits, rays, fwd_s):
+    """Roofline of the dominant kernel, the forward projection (two per iteration): the voxel-driven
+    tvam_fwd_planar_kernel (+ its slice-binning pass) on config 2.  Its binding resource is the LDS
+    array (staged pattern slabs, 16-B reads), not HBM: per launch the LDS-array cycles and VALU
+    instructions come from the committed rocprofv3 counters of the same kernels
+    (profiles/r02/pmc_config2.json, tools/pmc_round.sh + tools/summarize_pmc.py), the duration is this
+    run's HIP-event time of the forward call (binning pass included, so the fractions are slightly
+    conservative)."""
+    alg_bytes = 8.0 * visits + 4.0 * rays  # SURVEY.md 8(d): forward = 8 B per visit + 4 B per ray
+    info = {"kernel": "tvam_fwd_planar_kernel" if prob.proj.planar_forward else "forward projection",
+            "fwd_call_s": fwd_s,
+            "survey_8d_model": {"alg_bytes_per_launch": alg_bytes, "rate_gbs": alg_bytes / fwd_s / 1e9,
+                                "note": "per-visit dose read-modify-write model of SURVEY 8(d); the kernel keeps "
+                                        "the dose in registers, so this rate exceeds HBM and is not a roofline"}}
+    if not (args.config == 2 and N == 400 and A == 400 and world == 1 and os.path.exists(PMC_SUMMARY)
+            and prob.proj.planar_forward):
+        return {"bound": "lds", "achieved": None, "peak": LDS_PEAK_GBS, "unit": "GB/s", "frac": None,
+                "traffic": None, "note": "counters committed for config 2 at 400^3 only", **info}
+    pmc = json.load(open(PMC_SUMMARY))["kernels"]["forward"]
+    c = pmc["sum"]
+    lds_bytes = c["SQ_LDS_IDX_ACTIVE"] * 256.0  # LDS-array cycles (summed over CUs) x 256 B per cycle
+    achieved = lds_bytes / fwd_s / 1e9
+    traffic = 2.0 * c["FETCH_SIZE"] * 1024 + c["WRITE_SIZE"] * 1024  # KiB; FETCH x2: gfx950 wide reads
+    valu = c["SQ_INSTS_VALU"] / fwd_s / VALU_PEAK_WAVE_INSTR
+    main = pmc["launches"][pmc["main"]]
+    return {"bound": "lds", "achieved": achieved, "peak": LDS_PEAK_GBS, "unit": "GB/s",
+            "frac": achieved / LDS_PEAK_GBS, "traffic": traffic,
+            "secondary": {"valu_issue_frac": valu, "hbm_gbs": traffic / fwd_s / 1e9,
+                          "hbm_frac": traffic / fwd_s / 1e9 / HBM_PEAK_GBS,
+                          "lds_bank_conflict_cycles": c["SQ_LDS_BANK_CONFLICT"],
+                          "clock_ghz_measured": main.get("clock_ghz"),
+                          "rocprof_avg_ns": c["avg_ns"]},
+            "counters": os.path.relpath(PMC_SUMMARY, ROOT), **info}
 
 
 def main():
@@ -84,7 +162,9 @@ def main():
                          "(3: cylindrical vial, refraction) or configs[3] (4: cylindrical vial, scattering "
                          "resin, 16 jittered rays per pixel) or configs[4] (5: square vial + occluder mesh, 4 jittered rays per "
                          "pixel; use --n 800)")
-    ap.add_argument("--n", type=int, default=400, help="voxels per axis = DMD pixels per axis = angles")
+    ap.add_argument("--res", "--n", dest="n", type=int, default=400,
+                    help="voxels per axis = DMD pixels per axis = angles (--res under torch.distributed.run, "
+                         "whose parser takes --n for its own --nnodes)")
     ap.add_argument("--angles", type=int, default=None)
     ap.add_argument("--tile", type=int, default=0)
     ap.add_argument("--zero-skip", action="store_true", help="skip rays whose pattern value is 0 (exact)")
@@ -97,6 +177,10 @@ def main():
     ap.add_argument("--emulate", type=str, default=None, metavar="RANK/WORLD",
                     help="time one rank's shard of a WORLD-rank run on this single GPU (no collectives; "
                          "scaling study only, never the bench line)")
+    ap.add_argument("--ar-gbs", type=float, default=300.0,
+                    help="--emulate with --shard angle: RCCL all-reduce bus bandwidth (GB/s) of the cost model")
+    ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
+                    help="torch.distributed backend for WORLD_SIZE > 1 (nccl = RCCL over xGMI; gloo: tests)")
     args = ap.parse_args()
 
     import torch
@@ -106,12 +190,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    torch.cuda.set_device(local)
+    ndev = torch.cuda.device_count()
+    gpu = local % max(ndev, 1)  # one GPU per rank; ranks share a GPU only when there are fewer (tests)
+    torch.cuda.set_device(gpu)
     dist = None
     if world > 1:
         import torch.distributed as dist
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    dev = torch.device("cuda", local)
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", gpu))
+        else:
+            dist.init_process_group("gloo")
+    dev = torch.device("cuda", gpu)
 
     N = args.n
     A = args.angles or N
@@ -187,10 +276,21 @@ def main():
         f"last loss {prob.loss_hist[-1]:.6e}")
 
     if args.emulate:
-        print(json.dumps({"emulate": args.emulate, "shard": prob.shard, "ms_per_step": elapsed / args.steps * 1e3,
-                          "fwd_ms": fwd_avg * 1e3, "adj_ms": adj_avg * 1e3, "visits_per_pass": visits,
-                          "slices": [prob.z0, prob.z1], "rows": [prob.r0, prob.r1],
-                          "angles": [prob.a0, prob.a1]}), flush=True)
+        ew = int(args.emulate.split("/")[1])
+        ms = elapsed / args.steps * 1e3
+        rec = {"emulate": args.emulate, "shard": prob.shard, "ms_per_step": ms,
+               "fwd_ms": fwd_avg * 1e3, "adj_ms": adj_avg * 1e3, "visits_per_pass": visits,
+               "slices": [prob.z0, prob.z1], "rows": [prob.r0, prob.r1], "angles": [prob.a0, prob.a1]}
+        if prob.shard == "angle" and ew > 1:
+            # two ring all-reduces of the full dose per iteration (main forward + line-search forward):
+            # each moves 2 (W - 1) / W of the film per rank at the RCCL bus bandwidth --ar-gbs
+            fr = prob.proj.desc.film_res
+            film = 4.0 * fr[0] * fr[1] * fr[2]
+            ar_ms = 2 * (2.0 * (ew - 1) / ew) * film / (args.ar_gbs * 1e9) * 1e3
+            rec.update({"allreduce_model": {"bytes_per_allreduce": film, "per_iteration": 2, "bus_gbs": args.ar_gbs,
+                                            "ms_per_iteration": ar_ms},
+                        "ms_per_step_with_allreduce": ms + ar_ms})
+        print(json.dumps(rec), flush=True)
         return
     if rank != 0:
         if dist:
@@ -198,21 +298,14 @@ def main():
             dist.destroy_process_group()
         return
 
-    alg_bytes = 8.0 * visits + 4.0 * rays  # forward = 8 B per visit + 4 B per ray
-    achieved = alg_bytes / fwd_avg / 1e9
-    # HBM bytes per forward launch from the committed rocprofv3 PMC passes
-    # (profiles/pmc_traffic.json, made by tools/profile_round.sh + tools/summarize_profile.py)
-    traffic = None
-    tpath = os.path.join(ROOT, "profiles", "pmc_traffic.json")
-    if N == 400 and A == 400 and world == 1 and args.config == 2 and os.path.exists(tpath):
-        traffic = json.load(open(tpath))["per_launch"]["forward"]["hbm_bytes"]
+    roofline = make_roofline(args, N, A, world, prob, visits, rays, fwd_avg)
     cpu = None
     if args.cpu_baseline == "auto" and world == 1:
-        threads = min(16, os.cpu_count() or 1)
+        threads = host_info()["threads"]
         log(f"cpu baseline ({threads} threads, ~{args.cpu_seconds:.0f}s) ...")
         cpu = cpu_baseline(args.config, N, args.cpu_seconds, threads)
     result = {
-        "metric": "optimizer iterations/sec (fwd+adjoint), 400³ voxels × 400 angles",
+        "metric": f"optimizer iterations/sec (fwd+adjoint), {N}³ voxels × {A} angles",
         "value": args.steps / elapsed,
         "unit": "it/s",
         "n_gpus": world,
@@ -236,18 +329,13 @@ def main():
             "voxels": N ** 3, "angles": A, "dmd": [N, N], "spp": prob.spp, "sigma_t": cfg["vial"]["medium"]["extinction"],
             "parallelism": ("single GPU" if world == 1 else
                             f"z-slab x{world} (film slabs + DMD row bands, scalar all-reduces only)"
-                            if prob.shard == "slab" else f"angle-shard x{world} + RCCL dose all-reduce"),
+                            if prob.shard == "slab" else
+                            f"angle-shard x{world} + {'RCCL' if args.backend == 'nccl' else 'gloo'} dose all-reduce"),
             "zero_skip": bool(args.zero_skip), "tile": prob.proj.desc.tile,
             "fwd_ms": fwd_avg * 1e3, "adj_ms": adj_avg * 1e3, "visits_per_pass": visits, "rays_per_pass": rays,
             "final_loss": prob.loss_hist[-1],
         },
-        "roofline": {"bound": "hbm", "achieved": achieved, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                     "kernel": "tvam_fwd_planar_kernel" if prob.proj.planar_forward else "tvam_tile_kernel<FWD>",
-                     "alg_bytes_per_launch": alg_bytes,
-                     "note": "SURVEY 8(d) algorithmic bytes (per-visit dose RMW); the LDS / register-resident "
-                             "kernels move far fewer real bytes, so frac > 1 means past the naive HBM roofline "
-                             "(the real limit is VALU / LDS issue, DESIGN.md)"},
+        "roofline": roofline,
         "cpu_baseline": cpu,
     }
     print(json.dumps(result), flush=True)
