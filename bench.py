@@ -179,6 +179,8 @@ def main():
                          "scaling study only, never the bench line)")
     ap.add_argument("--ar-gbs", type=float, default=300.0,
                     help="--emulate with --shard angle: RCCL all-reduce bus bandwidth (GB/s) of the cost model")
+    ap.add_argument("--filter-radon", action="store_true",
+                    help="compact the active set to the pixels whose rays cross the target (optimize.py:143-163)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="torch.distributed backend for WORLD_SIZE > 1 (nccl = RCCL over xGMI; gloo: tests)")
     args = ap.parse_args()
@@ -208,6 +210,8 @@ def main():
     cfg["tile"] = args.tile
     cfg["shard"] = args.shard
     cfg["flags"] = (0 if args.zero_skip else _abi.FLAG_NO_ZERO_SKIP) | (_abi.FLAG_FWD_STATS if args.stats else 0)
+    if args.filter_radon:
+        cfg["filter_radon"] = True
     t_setup = time.perf_counter()
     if args.emulate:
         er, ew = (int(v) for v in args.emulate.split("/"))
@@ -218,6 +222,8 @@ def main():
     g = torch.Generator().manual_seed(0)
     full = torch.rand(prob.n_global, generator=g) * 0.1
     prob.x0 = prob.local_from_global(full)
+    if prob.active_dense is not None:  # filter_radon: the compacted active set's entries
+        prob.x0 = prob.x0[prob.active_dense].contiguous()
     del full
     visits = prob.proj.count_visits(prob.spp, 0)
     rays = prob.n_local * prob.spp
@@ -332,6 +338,8 @@ def main():
                             if prob.shard == "slab" else
                             f"angle-shard x{world} + {'RCCL' if args.backend == 'nccl' else 'gloo'} dose all-reduce"),
             "zero_skip": bool(args.zero_skip), "tile": prob.proj.desc.tile,
+            "filter_radon": ({"active": prob.n_filtered, "of": prob.n_global} if prob.active_pixels is not None
+                             else None),
             "fwd_ms": fwd_avg * 1e3, "adj_ms": adj_avg * 1e3, "visits_per_pass": visits, "rays_per_pass": rays,
             "final_loss": prob.loss_hist[-1],
         },

@@ -12,7 +12,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TVAM_LIB") or os.path.join(_HERE, "libtvam.so")  # TVAM_LIB: a variant build
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 TVAM_OK = 0
 TVAM_ERR_INVALID = -1
@@ -86,6 +86,9 @@ class TvamDesc(ctypes.Structure):
         ("target_tris", ctypes.c_void_p),
         ("n_target_tris", ctypes.c_int32),
         ("majorant", ctypes.c_float),
+        ("reserved0", ctypes.c_int32),
+        ("active_base", ctypes.c_int64),
+        ("active_total", ctypes.c_int64),
     ]
 
     def copy(self) -> "TvamDesc":
@@ -135,6 +138,7 @@ EXPORTS = {
     "tvam_axpy_clamp": (ctypes.c_int, [ctypes.c_uint64, _P, ctypes.c_float, _P, ctypes.c_float, _P, _P]),
     "tvam_row_slices": (ctypes.c_int, [ctypes.POINTER(TvamDesc), _P]),
     "tvam_plan_path": (ctypes.c_int, [_P]),
+    "tvam_plan_set_active": (ctypes.c_int, [_P, ctypes.c_int64, ctypes.c_int64]),
     "tvam_compute_volume": (ctypes.c_int, [_P, ctypes.c_uint32, _P, _P]),
     "tvam_plan_set_volumes": (ctypes.c_int, [_P, _P]),
     "tvam_radon": (ctypes.c_int, [_P, _P, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int32, _P, _P]),

@@ -52,6 +52,7 @@ struct TvamConsts {
     int32_t n_patterns;  // A
     int32_t a0, a1;      // angle shard
     int64_t shard_base;  // a0 * crop_y * crop_x: first dense index of the shard
+    int64_t stream_base; // sparse active sets: position of this plan's first active entry (desc.active_base)
     float ex, ey;        // emitter size W*a_x, H*a_y
     float inv_w, inv_h;  // rcp(ScalarVector2f(w, h)) (common.py:98)
     float dist_m_zc;     // distance - 0.005 (camera-space z of ray origins)
@@ -112,6 +113,20 @@ struct TvamPcg {
         (void)next();
     }
 };
+
+// Sampler stream of the ray of dense shard entry `local`, sample `smp`: the
+// reference seeds stream i * spp + smp for entry i of projector.active_pixels
+// (common.py:57-67 sampler.seed(seed, active_size * spp), :81 dr.repeat).  A
+// sparse active set (idxmap = dense -> active position) uses that position; the
+// dense crop order's position is the global dense index itself.
+TVAM_HD uint64_t tvam_stream(const TvamConsts& k, const int32_t* idxmap, int64_t local, uint32_t spp, int smp) {
+    int64_t pos = local + k.shard_base;
+    if (idxmap) {
+        const int32_t a = idxmap[local];
+        pos = k.stream_base + (a < 0 ? 0 : a);  // inactive entries never reach the film
+    }
+    return (uint64_t)pos * (uint64_t)spp + (uint64_t)smp;
+}
 
 // --------------------------------------------------------------------------
 // Ray generation

@@ -159,7 +159,7 @@ hipError_t tvam_launch_radon(const TvamConsts& k, const TvamTiles& t, const floa
 // Per-ray pre-pass: ray generation, vial segment and DDA initialisation of
 // every ray of the shard, stored as the records the tile kernels resume from.
 hipError_t tvam_launch_ray_setup(const TvamConsts& k, const TvamTiles& t, float4* ray_f, int2* ray_i,
-                                 float4* ray_g, hipStream_t stream);
+                                 float4* ray_g, const int32_t* idxmap, hipStream_t stream);
 
 hipError_t tvam_launch_scatter(const TvamConsts& k, const float* data, const uint32_t* pixels,
                                uint64_t n, float* dense, int32_t* idxmap, hipStream_t stream);

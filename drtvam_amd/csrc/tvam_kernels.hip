@@ -130,7 +130,8 @@ struct TvamTileRay {
 // (common.py:81-108), index-matched vial segment (volume.py:179-216) and DDA
 // initialisation (sensor.py:327-365).  Record index = local * spp + sample.
 __global__ __launch_bounds__(256) void tvam_ray_setup_kernel(TvamConsts k, TvamTiles tp, float4* __restrict__ ray_f,
-                                                             int2* __restrict__ ray_i, float4* __restrict__ ray_g) {
+                                                             int2* __restrict__ ray_i, float4* __restrict__ ray_g,
+                                                             const int32_t* __restrict__ idxmap) {
     const int spp = (int)tp.spp;
     const int64_t per_angle = (int64_t)k.crop_y * k.crop_x;
     const int64_t n = (int64_t)tp.n_shard * per_angle * spp;
@@ -140,11 +141,10 @@ __global__ __launch_bounds__(256) void tvam_ray_setup_kernel(TvamConsts k, TvamT
         const int al = (int)(local / per_angle);
         const int64_t pix = local - (int64_t)al * per_angle;
         const int rowc = (int)(pix / k.crop_x), colc = (int)(pix - (int64_t)rowc * k.crop_x);
-        const int64_t dense = local + k.shard_base;  // sampler stream (global dense crop index)
         float jx = 0.5f, jy = 0.5f;
         if (!k.regular) {
             TvamPcg rng;
-            rng.seed(tp.seed, (uint64_t)dense * (uint64_t)spp + (uint64_t)smp);
+            rng.seed(tp.seed, tvam_stream(k, idxmap, local, (uint32_t)spp, smp));
             jx = rng.next_float();
             jy = rng.next_float();
         }
@@ -178,12 +178,12 @@ __global__ __launch_bounds__(256) void tvam_ray_setup_kernel(TvamConsts k, TvamT
 }
 
 hipError_t tvam_launch_ray_setup(const TvamConsts& k, const TvamTiles& t, float4* ray_f, int2* ray_i,
-                                 float4* ray_g, hipStream_t stream) {
+                                 float4* ray_g, const int32_t* idxmap, hipStream_t stream) {
     const int64_t n = (int64_t)t.n_shard * k.crop_y * k.crop_x * t.spp;
     int64_t g = (n + 255) / 256;
     if (g > 65536) g = 65536;
     if (g < 1) g = 1;
-    hipLaunchKernelGGL(tvam_ray_setup_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, t, ray_f, ray_i, ray_g);
+    hipLaunchKernelGGL(tvam_ray_setup_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, t, ray_f, ray_i, ray_g, idxmap);
     return hipGetLastError();
 }
 

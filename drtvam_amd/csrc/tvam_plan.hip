@@ -64,6 +64,7 @@ struct tvam_plan {
     uint64_t ray_cap = 0;
     bool ray_valid = false;
     uint32_t ray_spp = 0, ray_seed = 0;
+    bool ray_sparse = false;  // records built for a sparse active set (streams by active position)
     hipEvent_t ray_ready = nullptr;
     // planar fast path (regular sampling; tvam_planar.hip)
     bool planar = false;      // planar adjoint
@@ -231,6 +232,7 @@ static int validate(const tvam_desc& d) {
             return fail(TVAM_ERR_INVALID, "invalid film slab [slab_begin, slab_end)");
     }
     if (!(d.pixel_size_x > 0.0f && d.pixel_size_y > 0.0f)) return fail(TVAM_ERR_INVALID, "pixel_size must be positive");
+    if (d.active_base < 0 || d.active_total < 0) return fail(TVAM_ERR_INVALID, "active_base / active_total must be >= 0");
     return 0;
 }
 
@@ -257,6 +259,7 @@ static TvamConsts make_consts(const tvam_desc& d, int a0, int a1) {
     k.a0 = a0;
     k.a1 = a1;
     k.shard_base = (int64_t)a0 * d.crop_y * d.crop_x;
+    k.stream_base = d.active_base;
     k.ex = (float)d.res_x * d.pixel_size_x;
     k.ey = (float)d.res_y * d.pixel_size_y;
     k.inv_w = 1.0f / (float)d.res_x;
@@ -945,13 +948,16 @@ static int call_setup(tvam_plan* p, uint64_t n_active, const uint32_t* active_pi
         return fail(TVAM_ERR_INVALID, "active_data and active_pixels must have the same length.");  // projector.py:137-138
     if (d.regular_sampling) spp = 1;
     if (spp == 0) spp = 4;  // optimize.py:96
-    if (n_active * (uint64_t)spp > (1ull << 32))
+    if ((d.active_total > 0 ? (uint64_t)d.active_total : n_active) * (uint64_t)spp > (1ull << 32))
         return fail(TVAM_ERR_TOO_LARGE,
                     "The total number of Monte Carlo samples required by this rendering task exceeds 2^32 = "
                     "4294967296. Please use fewer samples per pixel or render using multiple passes.");  // common.py:60-65
     k = p->k;
-    float area = d.pixel_size_x * d.pixel_size_y * (float)n_active;
-    float w = area / (float)(n_active * (uint64_t)spp);
+    // inv_pdf / n_samples over the whole active set (projector.py:164-165, :187): a shard's
+    // call carries its own n_active, the reference's len(active_data) is desc.active_total
+    const uint64_t n_all = d.active_total > 0 ? (uint64_t)d.active_total : n_active;
+    float area = d.pixel_size_x * d.pixel_size_y * (float)n_all;
+    float w = area / (float)(n_all * (uint64_t)spp);
     w = w * d.print_time;
     float ss = d.albedo * d.sigma_t;
     float sa_st = d.sigma_t != 0.0f ? (float)(((double)d.sigma_t - (double)ss) / (double)d.sigma_t) : 0.0f;
@@ -977,7 +983,7 @@ static int ensure_dense(tvam_plan* p) {
 // only when the cached records do not match the call.
 #define TVAM_FROZEN_CAP (1 << 20)
 
-static int ensure_rays(tvam_plan* p, const TvamConsts& k, TvamTiles& t, hipStream_t stream) {
+static int ensure_rays(tvam_plan* p, const TvamConsts& k, TvamTiles& t, const int32_t* idxmap, hipStream_t stream) {
     const uint64_t n = (uint64_t)(k.a1 - k.a0) * k.crop_y * k.crop_x * t.spp;
     hipError_t e;
     if (n > p->ray_cap) {
@@ -1006,19 +1012,32 @@ static int ensure_rays(tvam_plan* p, const TvamConsts& k, TvamTiles& t, hipStrea
     t.frozen = p->d_frozen;
     t.frozen_n = p->d_frozen_n;
     t.frozen_cap = TVAM_FROZEN_CAP;
-    const bool hit = p->ray_valid && p->ray_spp == t.spp && (k.regular || p->ray_seed == t.seed);
+    // jittered records of a sparse active set depend on the set (sampler streams by active
+    // position): recomputed every call, like every call with a new seed
+    const bool hit = p->ray_valid && p->ray_spp == t.spp && (k.regular || (p->ray_seed == t.seed && !p->ray_sparse && !idxmap));
     if (hit) {
         e = hipStreamWaitEvent(stream, p->ray_ready, 0);
         return e == hipSuccess ? 0 : hip_fail(e, "hipStreamWaitEvent");
     }
     if ((e = hipMemsetAsync(p->d_frozen_n, 0, sizeof(unsigned long long), stream)) != hipSuccess)
         return hip_fail(e, "hipMemsetAsync");
-    if ((e = tvam_launch_ray_setup(k, t, p->d_ray_f, p->d_ray_i, p->d_ray_g, stream)) != hipSuccess)
+    if ((e = tvam_launch_ray_setup(k, t, p->d_ray_f, p->d_ray_i, p->d_ray_g, idxmap, stream)) != hipSuccess)
         return hip_fail(e, "ray setup launch");
     if ((e = hipEventRecord(p->ray_ready, stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     p->ray_valid = true;
     p->ray_spp = t.spp;
     p->ray_seed = t.seed;
+    p->ray_sparse = idxmap != nullptr;
+    return 0;
+}
+
+extern "C" int tvam_plan_set_active(tvam_plan* p, int64_t active_base, int64_t active_total) {
+    if (!p) return fail(TVAM_ERR_INVALID, "null argument");
+    if (active_base < 0 || active_total < 0) return fail(TVAM_ERR_INVALID, "active_base / active_total must be >= 0");
+    p->desc.active_base = active_base;
+    p->desc.active_total = active_total;
+    p->k.stream_base = active_base;
+    p->ray_valid = false;
     return 0;
 }
 
@@ -1080,7 +1099,7 @@ extern "C" int tvam_forward(tvam_plan* p, const float* active_data, const uint32
         TvamTiles t = p->tiles;
         t.spp = spp;
         t.seed = seed;
-        if ((rc = ensure_rays(p, kc, t, stream))) return rc;
+        if ((rc = ensure_rays(p, kc, t, idxmap, stream))) return rc;
         unsigned long long* stats = nullptr;
         if (p->desc.flags & TVAM_FLAG_FWD_STATS) {
             if ((e = hipMemsetAsync(p->d_counter, 0, sizeof(unsigned long long), stream)) != hipSuccess)
@@ -1154,7 +1173,7 @@ extern "C" int tvam_adjoint(tvam_plan* p, const float* grad_dose, const uint32_t
         TvamTiles t = p->tiles;
         t.spp = spp;
         t.seed = seed;
-        if ((rc = ensure_rays(p, k, t, stream))) return rc;
+        if ((rc = ensure_rays(p, k, t, idxmap, stream))) return rc;
         e = tvam_launch_tiles(TVAM_MODE_ADJ, k, t, p->lds_bytes, nullptr, idxmap, grad_dose, grad_active, nullptr,
                               stream);
         if (e == hipSuccess)
@@ -1195,7 +1214,7 @@ extern "C" int tvam_count_visits(tvam_plan* p, uint32_t spp, uint32_t seed, uint
         e = tvam_launch_surface_paths(TVAM_MODE_COUNT, k, t, nullptr, nullptr, nullptr, nullptr, nullptr, p->d_counter,
                                       nullptr);
     } else {
-        if ((rc = ensure_rays(p, k, t, nullptr))) return rc;
+        if ((rc = ensure_rays(p, k, t, nullptr, nullptr))) return rc;
         e = tvam_launch_tiles(TVAM_MODE_COUNT, k, t, p->lds_bytes, nullptr, nullptr, nullptr, nullptr, p->d_counter,
                               nullptr);
         if (e == hipSuccess)

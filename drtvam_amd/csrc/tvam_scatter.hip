@@ -16,8 +16,8 @@
 //   adjoint:  gathers of grad * inv_vol, one atomic per path into its pattern
 //             gradient;
 //   count:    visits of the later segments.
-// One thread per (ray, sample); the stream is `dense crop index * spp +
-// sample`, as for the ray records.  Draw order per loop iteration (restated
+// One thread per (ray, sample); the stream is `active position * spp +
+// sample` (tvam_stream), as for the ray records.  Draw order per loop iteration (restated
 // in oracle/tvam_oracle.c, or_trace_scatter): RR next_1d, medium next_1d,
 // BSDF next_1d + next_2d on surfaces, phase next_1d + next_2d on scattering.
 #include "tvam_internal.h"
@@ -329,9 +329,8 @@ __global__ __launch_bounds__(256) void tvam_scatter_kernel(TvamConsts k, TvamTil
         const int al = (int)(local / per_angle);
         const int64_t pix = local - (int64_t)al * per_angle;
         const int rowc = (int)(pix / k.crop_x), colc = (int)(pix - (int64_t)rowc * k.crop_x);
-        const int64_t dense = local + k.shard_base;
         TvamPcg rng;
-        rng.seed(tp.seed, (uint64_t)dense * (uint64_t)spp + (uint64_t)smp);
+        rng.seed(tp.seed, tvam_stream(k, idxmap, local, (uint32_t)spp, smp));
         float jx = 0.5f, jy = 0.5f;
         if (!k.regular) {
             jx = rng.next_float();
@@ -454,7 +453,7 @@ __global__ __launch_bounds__(256) void tvam_frozen_kernel(TvamConsts k, TvamTile
         float jx = 0.5f, jy = 0.5f;
         if (!k.regular) {
             TvamPcg rng;
-            rng.seed(tp.seed, (uint64_t)(local + k.shard_base) * (uint64_t)spp + (uint64_t)smp);
+            rng.seed(tp.seed, tvam_stream(k, idxmap, local, (uint32_t)spp, smp));
             jx = rng.next_float();
             jy = rng.next_float();
         }
@@ -558,11 +557,10 @@ __global__ __launch_bounds__(256) void tvam_surface_kernel(TvamConsts k, TvamTil
         const int al = (int)(local / per_angle);
         const int64_t pix = local - (int64_t)al * per_angle;
         const int rowc = (int)(pix / k.crop_x), colc = (int)(pix - (int64_t)rowc * k.crop_x);
-        const int64_t dense = local + k.shard_base;
         float jx = 0.5f, jy = 0.5f;
         if (!k.regular) {
             TvamPcg rng;
-            rng.seed(tp.seed, (uint64_t)dense * (uint64_t)spp + (uint64_t)smp);
+            rng.seed(tp.seed, tvam_stream(k, idxmap, local, (uint32_t)spp, smp));
             jx = rng.next_float();
             jy = rng.next_float();
         }
@@ -667,9 +665,8 @@ __global__ __launch_bounds__(256) void tvam_path_kernel(TvamConsts k, TvamTiles 
         const int al = (int)(local / per_angle);
         const int64_t pix = local - (int64_t)al * per_angle;
         const int rowc = (int)(pix / k.crop_x), colc = (int)(pix - (int64_t)rowc * k.crop_x);
-        const int64_t dense = local + k.shard_base;
         TvamPcg rng;
-        rng.seed(tp.seed, (uint64_t)dense * (uint64_t)spp + (uint64_t)smp);
+        rng.seed(tp.seed, tvam_stream(k, idxmap, local, (uint32_t)spp, smp));
         float jx = 0.5f, jy = 0.5f;
         if (!k.regular) {
             jx = rng.next_float();

@@ -99,6 +99,14 @@ class Projection:
                 n_active, spp, seed & 0xFFFFFFFF, out.data_ptr(), _stream_ptr(self.device)))
         return out
 
+    def set_active(self, active_base: int, active_total: int) -> None:
+        """Position of this plan's first active entry in the whole active set and that set's
+        size (desc.active_base / active_total): sampler streams and the ray weight of later
+        calls follow the reference's whole projector.active_pixels (common.py:57-67)."""
+        _abi.check(self.lib.tvam_plan_set_active(self._plan, int(active_base), int(active_total)))
+        self.desc.active_base = int(active_base)
+        self.desc.active_total = int(active_total)
+
     def compute_volume(self, sample_count: int = 2 ** 14) -> torch.Tensor:
         """Surface-aware voxel volumes [Z, Y, X, 2] (inside, outside the target mesh) of this plan's
         film (VolumetricSensor.compute_volume, sensor.py:47-110)."""

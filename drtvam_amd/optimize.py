@@ -347,8 +347,12 @@ class TvamProblem(ShardedLoop):
         self.n_global = A * per_angle
         self.n_local = (self.a1 - self.a0) * (self.r1 - self.r0) * self.crop_x
         self.x0 = self.local_from_global(p.active_data)
-        self.proj = self.integrator.projection(self.scene, self.sensor)
-        self.mask = None
+        # the dense crop order unless filter_radon compacts the set; the ray weight divides by
+        # the whole (all ranks') active set size, as the unsharded reference does
+        self.active_pixels = None
+        self.active_dense = None
+        self.active_set = (0, self.n_global)
+        self.proj = self._active_projection(self.integrator, self.sensor)
         if config.get('filter_radon', False) and filter_pixels:
             self._filter_radon(config)
         self.fused = fusable and self.target.shape[-1] == 1
@@ -360,8 +364,11 @@ class TvamProblem(ShardedLoop):
     def _filter_radon(self, config):
         """Deactivate the pixels whose rays never cross the target inside the medium
         (optimize.py:143-163): the Radon integrator (max_depth 5, jittered, spp_filter_radon
-        samples) on this rank's pixels; patterns and gradients of the others stay 0, which is
-        the reference's compressed active set in the dense layout."""
+        samples) on this rank's pixels, then the active set is compacted like the reference's
+        dr.compress: projector.active_pixels holds only the surviving pixels (full-DMD indices
+        in dense order), active_data is a zero vector of that length, and the forward, the
+        adjoint and every L-BFGS vector run over the compacted set.  Sampler streams follow
+        the position in the whole (all ranks') active set, as common.py:57-67 seeds them."""
         from .engine import Projection
         from .utils import target_triangles
         d = self.proj.desc.copy()
@@ -370,16 +377,35 @@ class TvamProblem(ShardedLoop):
         d.flags |= 4  # TVAM_FLAG_NO_PLANAR: no planar tables needed for a setup pass
         radon = Projection(d, self.device).radon(target_triangles(self.scene), spp=config.get('spp_filter_radon', 4),
                                                  seed=0, max_depth=5)
-        self.mask = (radon > 0).to(torch.float32)
-        n = self.mask.sum().to(torch.float64)
-        self.n_filtered = int(self.allreduce_(n).item())
+        local = torch.nonzero(radon > 0).reshape(-1)  # dense indices of this rank's shard, ascending
+        counts = [int(local.numel())]
+        if self.dist is not None:
+            counts = [None] * self.world
+            self.dist.all_gather_object(counts, int(local.numel()))
+        self.n_filtered = int(sum(counts))
         if self.n_filtered == 0:
             raise ValueError("No active pixels found in the Radon transform.")
-        self.x0 = self.x0 * self.mask
-
-    def adjoint(self, grad_vol, seed):
-        g = self.adjoint_local(grad_vol, seed)
-        return g if self.mask is None else g.mul_(self.mask)
+        # full-DMD pixel index of each surviving dense entry [angle][crop row][crop col] of the plan
+        pd = self.proj.desc
+        cx, cy = int(pd.crop_x), int(pd.crop_y)
+        al = local // (cx * cy)
+        rem = local - al * (cx * cy)
+        row = rem // cx
+        col = rem - row * cx
+        W, H = int(pd.res_x), int(pd.res_y)
+        pix = (al + int(pd.angle_begin)) * (W * H) + (row + int(pd.crop_offset_y)) * W + col + int(pd.crop_offset_x)
+        if pix.numel() and int(pix.max()) >= 2 ** 31:
+            raise ValueError("filter_radon: DMD pixel index exceeds the int32 active_pixels range")
+        self.active_pixels = pix.to(torch.int32).contiguous()
+        self.active_dense = local  # scatter positions of the compacted vector in this rank's dense layout
+        self.n_dense_local = self.n_local
+        self.n_local = int(local.numel())
+        # angle shards are contiguous blocks of the global dense order: this rank's first
+        # active entry sits after every lower rank's (slab shards interleave, but run only
+        # under regular sampling, where no sampler stream is drawn)
+        self.active_set = (sum(counts[:self.rank]) if self.shard == 'angle' else 0, self.n_filtered)
+        self.proj.set_active(*self.active_set)
+        self.x0 = torch.zeros(self.n_local, dtype=torch.float32, device=self.device)
 
     def _row_band(self, desc):
         """Crop rows [r0, r1) whose rays lie in this rank's slab (rows outside the grid go to the
@@ -410,8 +436,18 @@ class TvamProblem(ShardedLoop):
         full = torch.as_tensor(full).reshape(-1, self.crop_y, self.crop_x)
         return full[self.a0:self.a1, self.r0:self.r1, :].reshape(-1).to(self.device).contiguous()
 
+    def dense_local(self, local):
+        """This rank's patterns in its dense layout (zeros at the pixels filter_radon disabled:
+        projector.patterns(), projector.py:125-129)."""
+        if self.active_dense is None:
+            return local
+        full = torch.zeros(self.n_dense_local, dtype=local.dtype, device=local.device)
+        full[self.active_dense] = local
+        return full
+
     def gather_patterns(self, local):
         """The global dense pattern vector (every rank), from the ranks' parts."""
+        local = self.dense_local(local)
         if self.dist is None:
             return local
         A = self.scene.projector.n_patterns
@@ -442,18 +478,23 @@ class TvamProblem(ShardedLoop):
         return torch.cat([part[:z1 - z0] for (z0, z1), part in zip(slabs, parts)])
 
     def forward_local(self, x, seed):
-        return self.proj.forward(x.detach().contiguous(), None, self.spp, seed)
+        return self.proj.forward(x.detach().contiguous(), self.active_pixels, self.spp, seed)
 
     def adjoint_local(self, grad_vol, seed):
-        return self.proj.adjoint(grad_vol, self.n_local, None, self.spp_grad, derive_seed_grad(seed))
+        return self.proj.adjoint(grad_vol, self.n_local, self.active_pixels, self.spp_grad, derive_seed_grad(seed))
+
+    def _active_projection(self, integrator, sensor):
+        proj = integrator.projection(self.scene, sensor)
+        proj.set_active(*self.active_set)
+        return proj
 
     def on_progressive(self):
         self.integrator.max_depth = self.max_depth
-        self.proj = self.integrator.projection(self.scene, self.sensor)
+        self.proj = self._active_projection(self.integrator, self.sensor)
 
     def final_render(self, spp=None):
-        proj = self.final_integrator.projection(self.scene, self.final_sensor)
-        vol = proj.forward(self.patterns_local().contiguous(), None, spp or self.spp_ref, 0)
+        proj = self._active_projection(self.final_integrator, self.final_sensor)
+        vol = proj.forward(self.patterns_local().contiguous(), self.active_pixels, spp or self.spp_ref, 0)
         return self.gather_dose(vol) if self.dose_sharded else self.allreduce_(vol)
 
 

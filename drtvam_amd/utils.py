@@ -127,9 +127,31 @@ def transform_points(m, verts):
     return (v @ m[:3, :3].T + m[:3, 3]).astype(np.float32)
 
 
+def cuboid_triangles(lo, hi):
+    """The 12 outward-facing triangles [12, 3, 3] (float32) of the box [lo, hi]."""
+    lo, hi = np.asarray(lo, np.float32), np.asarray(hi, np.float32)
+    c = np.array([[(hi if (i >> a) & 1 else lo)[a] for a in range(3)] for i in range(8)], np.float32)
+    quads = [(0, 2, 6, 4), (1, 5, 7, 3), (0, 4, 5, 1), (2, 3, 7, 6), (0, 1, 3, 2), (4, 6, 7, 5)]  # -x +x -y +y -z +z
+    tris = []
+    for q in quads:
+        tris += [(q[0], q[1], q[2]), (q[0], q[2], q[3])]
+    t = c[np.asarray(tris)]
+    inward = np.einsum('ij,ij->i', np.cross(t[:, 1] - t[:, 0], t[:, 2] - t[:, 0]),
+                       t.mean(axis=1) - 0.5 * (lo + hi)) < 0
+    t[inward] = t[inward][:, ::-1]
+    return t
+
+
 def target_triangles(scene):
-    """World-space triangles [n, 3, 3] (float32) of the scene's target mesh (optimize.py:30-65)."""
+    """World-space triangles [n, 3, 3] (float32) of the scene's target mesh (optimize.py:30-65).
+    An analytic target (no mesh file, analytic_target) is represented by the cuboid that bounds
+    its occupied voxels, u, v, w in [0.1, 0.9] of the sensor box: the Radon filter keeps a
+    superset of the pixels whose rays cross the shape."""
     tgt = scene.target
+    if tgt is not None and tgt.get('type') == 'analytic':
+        sensor = scene.sensor_by_id('sensor')
+        bmin, bmax = np.asarray(sensor.bbox_min, np.float64), np.asarray(sensor.bbox_max, np.float64)
+        return cuboid_triangles(bmin + 0.1 * (bmax - bmin), bmin + 0.9 * (bmax - bmin))
     if tgt is None or 'filename' not in tgt:
         raise ValueError("No target shape found in the scene")
     verts, tris = read_ply(tgt['filename'])

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define TVAM_ABI_VERSION 7
+#define TVAM_ABI_VERSION 8
 
 /* error codes */
 #define TVAM_OK               0
@@ -140,6 +140,18 @@ typedef struct tvam_desc {
     int32_t n_target_tris;
     /* 'ratio' sensor: its 'majorant' (sensor.py:195) */
     float   majorant;
+    int32_t reserved0;
+    /* Position of a sparse active_pixels[0] in the whole projector.active_pixels
+       when the active set is split over plans (angle shards): the sampler stream of
+       entry i is (active_base + i) * spp + sample, as TVAMIntegrator.prepare /
+       sample_rays seed it (common.py:57-67, :81).  Dense calls (active_pixels ==
+       NULL) use the global dense crop index, which is that position already. */
+    int64_t active_base;
+    /* len(projector.active_data) of the whole (unsharded) active set: the ray weight
+       inv_pdf / n_samples = pixel area * active_total / (active_total * spp)
+       (projector.py:164-165, :187) in the reference's fp32 rounding; 0 = the call's
+       n_active. */
+    int64_t active_total;
 } tvam_desc;
 
 /* tvam_desc.flags */
@@ -182,6 +194,11 @@ int tvam_adjoint(tvam_plan* plan, const float* grad_dose,
                  const uint32_t* active_pixels, uint64_t n_active,
                  uint32_t spp, uint32_t seed, float* grad_active,
                  void* hip_stream);
+
+/* Update desc.active_base / desc.active_total of a plan (after the active set was
+   compacted, e.g. by 'filter_radon', optimize.py:143-163); later calls seed and
+   weight their rays with them. */
+int tvam_plan_set_active(tvam_plan* plan, int64_t active_base, int64_t active_total);
 
 /* Diagnostics (host-synchronous): number of (slice, tile) workgroups of the
    last forward that accumulated with float atomics instead of fixed point

@@ -802,16 +802,18 @@ static uint32_t or_pixel(const tvam_desc* d, const uint32_t* active_pixels, uint
                       (uint64_t)d->crop_offset_x);
 }
 
-/* Sampler stream of a pixel: its dense crop index (angle, crop row, crop col).
-   The reference seeds stream i*spp+k for active entry i (common.py:57-67);
-   for the dense active set i IS this index.  Sparse sets use the same
-   definition so that angle-sharded runs draw identical samples. */
-static uint64_t or_stream(const tvam_desc* d, uint32_t pixel) {
-    uint64_t hw = (uint64_t)d->res_x * (uint64_t)d->res_y;
-    uint64_t a = pixel / hw, r = pixel % hw;
-    uint64_t row = r / (uint64_t)d->res_x, col = r % (uint64_t)d->res_x;
-    return (a * (uint64_t)d->crop_y + (row - (uint64_t)d->crop_offset_y)) * (uint64_t)d->crop_x +
-           (col - (uint64_t)d->crop_offset_x);
+/* Sampler stream of active entry i (before the * spp + sample): the reference seeds
+   sampler.seed(seed, active_size * spp) and repeats active_pixels spp times
+   (common.py:57-67, :81), so entry i of projector.active_pixels draws streams
+   i*spp .. i*spp+spp-1.  For the dense crop order i is the dense crop index; a
+   sparse set that is one shard of a larger one starts at desc.active_base. */
+static uint64_t or_stream(const tvam_desc* d, const uint32_t* active_pixels, uint64_t i) {
+    return active_pixels ? (uint64_t)d->active_base + i : i;
+}
+
+/* len(projector.active_data) the ray weight divides by (projector.py:164-165, :187) */
+static uint64_t or_n_total(const tvam_desc* d, uint64_t n_active) {
+    return d->active_total > 0 ? (uint64_t)d->active_total : n_active;
 }
 
 static int or_check(const tvam_desc* d) {
@@ -1179,7 +1181,7 @@ int oracle_radon(const tvam_desc* d, const float* tgt, int ntgt, uint32_t spp, u
 #endif
     for (int64_t i = 0; i < (int64_t)n; ++i) {
         uint32_t pixel = or_pixel(d, NULL, (uint64_t)i);
-        uint64_t st = or_stream(d, pixel);
+        uint64_t st = or_stream(d, NULL, (uint64_t)i);
         double acc = 0.0;
         for (uint32_t k = 0; k < spp; ++k) {
             or_ray ray;
@@ -1207,7 +1209,7 @@ static int or_forward_impl(const tvam_desc* d, const float* active_data, const u
     if (s.C == 2 && !inv_volumes) return TVAM_ERR_INVALID;
     size_t V = (size_t)s.res[0] * s.res[1] * s.res[2];
     memset(dose, 0, V * (size_t)s.C * sizeof(double));
-    double wr = or_ray_weight(d, n_active, spp);
+    double wr = or_ray_weight(d, or_n_total(d, n_active), spp);
     uint64_t nv_total = 0;
     if ((d->albedo != 0.0f || d->sensor_type != TVAM_SENSOR_DDA) && nthreads > 1) {
         /* scattered paths leave their slice: per-thread films (static
@@ -1231,7 +1233,7 @@ static int or_forward_impl(const tvam_desc* d, const float* active_data, const u
             for (int64_t i = 0; i < (int64_t)n_active; ++i) {
                 uint32_t pixel = or_pixel(d, active_pixels, (uint64_t)i);
                 double em = (double)active_data[i] * wr;
-                uint64_t st = or_stream(d, pixel);
+                uint64_t st = or_stream(d, active_pixels, (uint64_t)i);
                 for (uint32_t k = 0; k < spp; ++k)
                     or_trace(&s, pixel, st * spp + k, seed, em, priv ? 0 : 3, mine, NULL, -1, &nv_total);
             }
@@ -1245,7 +1247,7 @@ static int or_forward_impl(const tvam_desc* d, const float* active_data, const u
         for (uint64_t i = 0; i < n_active; ++i) {
             uint32_t pixel = or_pixel(d, active_pixels, i);
             double em = (double)active_data[i] * wr;
-            uint64_t st = or_stream(d, pixel);
+            uint64_t st = or_stream(d, active_pixels, (uint64_t)i);
             for (uint32_t k = 0; k < spp; ++k)
                 or_trace(&s, pixel, st * spp + k, seed, em, 0, dose, NULL, -1, &nv_total);
         }
@@ -1290,7 +1292,7 @@ static int or_forward_impl(const tvam_desc* d, const float* active_data, const u
                     uint64_t i = row_idx[j];
                     uint32_t pixel = or_pixel(d, active_pixels, i);
                     double em = (double)active_data[i] * wr;
-                    uint64_t st = or_stream(d, pixel);
+                    uint64_t st = or_stream(d, active_pixels, (uint64_t)i);
                     for (uint32_t q = 0; q < spp; ++q)
                         or_trace(&s, pixel, st * spp + q, seed, em, 0, dose, NULL, k, &nv_total);
                 }
@@ -1343,7 +1345,7 @@ static int or_adjoint_impl(const tvam_desc* d, const float* grad_dose, const uin
     or_scene_init(&s, d);
     s.inv_volumes = inv_volumes;
     if (s.C == 2 && !inv_volumes) return TVAM_ERR_INVALID;
-    double wr = or_ray_weight(d, n_active, spp);
+    double wr = or_ray_weight(d, or_n_total(d, n_active), spp);
     /* delta_L = grad_in * inv_vol (volume.py:130), in fp32 like the reference */
     size_t V = (size_t)s.res[0] * s.res[1] * s.res[2] * (size_t)s.C;
     float* dl = (float*)malloc(V * sizeof(float));
@@ -1358,7 +1360,7 @@ static int or_adjoint_impl(const tvam_desc* d, const float* grad_dose, const uin
     for (int64_t i = 0; i < (int64_t)n_active; ++i) {
         uint32_t pixel = or_pixel(d, active_pixels, (uint64_t)i);
         double g = 0.0;
-        uint64_t st = or_stream(d, pixel);
+        uint64_t st = or_stream(d, active_pixels, (uint64_t)i);
         for (uint32_t k = 0; k < spp; ++k)
             g += or_trace(&s, pixel, st * spp + k, seed, 1.0, 1, NULL, dl, -1, &nv_total);
         grad[i] = wr * g;

@@ -102,6 +102,10 @@ def _one_angle(oracle, cfg, N, a0, spp, seed):
     d = desc_from_config(cfg, angle_range=(a0, a0 + 1))
     dfull = desc_from_config(cfg)
     n = N * N
+    # the shard is entries [a0 n, a0 n + n) of the whole dense set: the oracle's sparse call
+    # draws the streams of those positions, and both weight rays by the whole set's size
+    dfull.active_base = a0 * n
+    d.active_total = dfull.active_total = N * n
     rng = np.random.default_rng(seed)
     pat = rng.uniform(0.0, 0.1, n).astype(np.float32)
     G = rng.uniform(-1, 1, (N, N, N)).astype(np.float32)

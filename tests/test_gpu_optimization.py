@@ -81,10 +81,15 @@ def test_box_hole_scattering_optimization(tmp_path):
     assert correct > 99.0
 
 
-def test_box_hole_occlusion_optimization(tmp_path):
-    """tests/files/box_hole_occlusion.json: the occluder box is carved out of the reference;
-    bar 97 % (test_optimization.py:43-99)."""
+@pytest.mark.parametrize("filter_radon", [False, True])
+def test_box_hole_occlusion_optimization(tmp_path, filter_radon):
+    """tests/files/box_hole_occlusion.json and box_hole_occlusion_filter_radon.json: the occluder
+    box is carved out of the reference; bar 97 % (test_optimization.py:43-99).  The reference's
+    *_filter_radon.json holds the same keys as box_hole_occlusion.json (no 'filter_radon'); the
+    second case sets it, so the compacted active set (optimize.py:143-163) runs this scene."""
     cfg = copy.deepcopy(BOX_HOLE_OCCLUSION)
+    if filter_radon:
+        cfg["filter_radon"] = True
     cfg["vial"]["occlusions"] = [{"filename": os.path.join(GOLDEN, "occlusion.ply")}]
     cfg, vol = _run(cfg, tmp_path)
     reference = np.zeros((50, 100, 100))

@@ -24,3 +24,16 @@ def test_film_resolution_swap():
     f = VolumetricFilm({'resx': 10, 'resy': 20, 'resz': 30})
     assert f.resolution() == (20, 10, 30)
     assert f.shape == (30, 10, 20, 1)
+
+
+def test_cuboid_triangles_outward():
+    """The analytic target's Radon-filter mesh: 12 triangles, outward normals, covering the box."""
+    from drtvam_amd.utils import cuboid_triangles
+    lo, hi = np.array([-1.0, 0.0, 2.0]), np.array([1.0, 3.0, 2.5])
+    t = cuboid_triangles(lo, hi).astype(np.float64)
+    assert t.shape == (12, 3, 3)
+    n = np.cross(t[:, 1] - t[:, 0], t[:, 2] - t[:, 0])
+    assert np.all(np.einsum('ij,ij->i', n, t.mean(axis=1) - 0.5 * (lo + hi)) > 0)
+    area = 0.5 * np.linalg.norm(n, axis=1).sum()
+    e = hi - lo
+    assert np.isclose(area, 2 * (e[0] * e[1] + e[1] * e[2] + e[0] * e[2]))
