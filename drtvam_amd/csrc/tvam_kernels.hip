@@ -128,16 +128,19 @@ struct TvamTileRay {
 
 // Ray record pre-pass (one thread per ray of the shard): ray generation
 // (common.py:81-108), index-matched vial segment (volume.py:179-216) and DDA
-// initialisation (sensor.py:327-365).  Record index = local * spp + sample.
+// initialisation (sensor.py:327-365).  Record index = sample * n_local + local.
 __global__ __launch_bounds__(256) void tvam_ray_setup_kernel(TvamConsts k, TvamTiles tp, float4* __restrict__ ray_f,
                                                              int2* __restrict__ ray_i, float4* __restrict__ ray_g,
                                                              const int32_t* __restrict__ idxmap) {
     const int spp = (int)tp.spp;
     const int64_t per_angle = (int64_t)k.crop_y * k.crop_x;
-    const int64_t n = (int64_t)tp.n_shard * per_angle * spp;
+    const int64_t n_local = (int64_t)tp.n_shard * per_angle;
+    const int64_t n = n_local * spp;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t local = i / spp;
-        const int smp = (int)(i - local * spp);
+        // record i = smp * n_local + local (sample-major: the tile kernels' lanes, which enumerate
+        // the sample slowest, read consecutive records of neighbouring pixels)
+        const int smp = (int)(i / n_local);
+        const int64_t local = i - (int64_t)smp * n_local;
         const int al = (int)(local / per_angle);
         const int64_t pix = local - (int64_t)al * per_angle;
         const int rowc = (int)(pix / k.crop_x), colc = (int)(pix - (int64_t)rowc * k.crop_x);
@@ -198,7 +201,7 @@ __device__ __forceinline__ bool tvam_tile_ray(const TvamConsts& k, const TvamTil
         r.act = idxmap[r.local];
         if (r.act < 0) return false;  // inactive pixel
     }
-    const int64_t ri = r.local * (int64_t)tp.spp + smp;
+    const int64_t ri = (int64_t)smp * ((int64_t)tp.n_shard * k.crop_y * k.crop_x) + r.local;  // sample-major records
     const int2 ii = tp.ray_i[ri];
     if (ii.y != kz + k.z0) return false;  // misses the grid / vial, or lies in another z-slice
     const float4 ff = tp.ray_f[ri];
@@ -294,8 +297,13 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
     const int rbeg = tp.slice_off[kz], rend = tp.slice_off[kz + 1];
     const int nrows = rend - rbeg;
     const int spp = (int)tp.spp;
-    const int per_row = nrt * spp;
-    const int total = nrows * per_row;
+    // slot f -> (sample, slice row, list entry) with the sample slowest: the lanes of a wave march
+    // different pixels.  With the sample fastest, spp neighbouring lanes marched one pixel's
+    // jittered rays through the same voxels, and their LDS atomics / the adjoint's per-pixel
+    // global atomics hit the same addresses (90 % of the forward's LDS cycles were bank conflicts).
+    const int per_row = nrt;
+    const int first = nrows * per_row;  // the slots of sample 0
+    const int total = first * spp;
 
     // Forward: pick the accumulator.  Fixed point (int32 ds_add: ~4x the
     // throughput of ds_add_f32 on gfx950) with a per-workgroup scale 2^e
@@ -313,9 +321,8 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
         float nz = 0.0f;
         TvamSlot sl;
         tvam_slot_init(sl, threadIdx.x, max(per_row, 1));
-        for (int f = threadIdx.x; f < total; f += TVAM_BLOCK, tvam_slot_next(sl, per_row)) {
-            if (spp > 1 && sl.rrem % spp) continue;  // one look per (angle, column)
-            const uint32_t e = slots[spp == 1 ? sl.rrem : sl.rrem / spp];
+        for (int f = threadIdx.x; f < first; f += TVAM_BLOCK, tvam_slot_next(sl, per_row)) {  // one look per (angle, column)
+            const uint32_t e = slots[sl.rrem];
             const int al = (int)(e >> 16), colc = (int)(e & 0xffffu);
             const int rowc = tp.slice_rows[rbeg + sl.ri];
             const int64_t local = ((int64_t)(k.a0 + al) * k.crop_y + rowc) * k.crop_x + colc - k.shard_base;
@@ -341,9 +348,8 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
         if (!TVAM_FWD_ACC64 && pmax > 0.0f && isfinite(pmax)) {
             const float thr = pmax * (1.0f / 1024.0f);
             tvam_slot_init(sl, threadIdx.x, max(per_row, 1));
-            for (int f = threadIdx.x; f < total; f += TVAM_BLOCK, tvam_slot_next(sl, per_row)) {
-                if (spp > 1 && sl.rrem % spp) continue;
-                const uint32_t e = slots[spp == 1 ? sl.rrem : sl.rrem / spp];
+            for (int f = threadIdx.x; f < first; f += TVAM_BLOCK, tvam_slot_next(sl, per_row)) {
+                const uint32_t e = slots[sl.rrem];
                 const int al = (int)(e >> 16), colc = (int)(e & 0xffffu);
                 const int rowc = tp.slice_rows[rbeg + sl.ri];
                 const int64_t local = ((int64_t)(k.a0 + al) * k.crop_y + rowc) * k.crop_x + colc - k.shard_base;
@@ -376,11 +382,10 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
     TvamSlot sl;
     tvam_slot_init(sl, threadIdx.x, max(per_row, 1));
     for (int f = threadIdx.x; f < total; f += TVAM_BLOCK, tvam_slot_next(sl, per_row)) {
-        const int g = spp == 1 ? sl.rrem : sl.rrem / spp;
-        const int smp = sl.rrem - g * spp;
-        const uint32_t e = slots[g];
+        const int smp = spp == 1 ? 0 : sl.ri / nrows;
+        const uint32_t e = slots[sl.rrem];
         const int al = (int)(e >> 16), colc = (int)(e & 0xffffu);
-        const int rowc = tp.slice_rows[rbeg + sl.ri];
+        const int rowc = tp.slice_rows[rbeg + sl.ri - smp * nrows];
         float em = 1.0f;
         if (MODE == TVAM_MODE_FWD) {
             const int64_t local = ((int64_t)(k.a0 + al) * k.crop_y + rowc) * k.crop_x + colc - k.shard_base;

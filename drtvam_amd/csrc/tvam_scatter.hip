@@ -435,8 +435,9 @@ __global__ __launch_bounds__(256) void tvam_frozen_kernel(TvamConsts k, TvamTile
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
         const int64_t i = list ? tp.frozen[j] : j;
         if (tp.ray_i[i].y > -2) continue;
-        const int64_t local = i / spp;
-        const int smp = (int)(i - local * spp);
+        const int64_t n_local = (int64_t)tp.n_shard * per_angle;  // sample-major ray records
+        const int smp = (int)(i / n_local);
+        const int64_t local = i - (int64_t)smp * n_local;
         float em = 1.0f;
         int64_t act = local;
         if (MODE == TVAM_MODE_FWD) {
