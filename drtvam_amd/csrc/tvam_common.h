@@ -29,11 +29,12 @@
 // (and e^{-st t_in} - e^{-st t_out} alike).  Degree-4 Taylor form below 0.05
 // (relative error < x^4 / 120 < 6e-8), the direct form above (no cancellation
 // there).  nlog2e = -log2(e): e^{-x} = exp2(nlog2e x).
-// Planar kernels whose plan has st * (voxel diagonal) = vox_chord < TVAM_W2_MAX
-// (every BASELINE grid but config 4's) use the degree-2 form on E = st e^{-st t}:
-// c = E dt (1 - st dt / 2), E -= st c: five full-rate instructions, relative error
-// < (st dt)^2 / 6 < 1e-6, in place of an exp2 and its cancellation.
-#define TVAM_W2_MAX 2.4e-3f
+// Kernels whose plan has st * (voxel xy diagonal) = vox_chord < TVAM_W2_MAX (every BASELINE
+// grid) use the degree-2 form on E = st e^{-st t}: c = E dt (1 - st dt / 2), E -= st c: five
+// full-rate instructions in place of an exp2 and its cancellation; the visit weight is low by a
+// relative (st dt)^2 / 6 < 2.7e-6, E drifts by (st dt)^3 / 6 per visit (< 1e-8) and restarts
+// from exp2 at every tile entry.
+#define TVAM_W2_MAX 4.0e-3f
 #define TVAM_NLOG2E (-1.4426950408889634f)
 __device__ __forceinline__ float tvam_omexp(float x) {
     if (__builtin_expect(x < 0.05f, 1))

@@ -1,6 +1,13 @@
 // tvam_internal.h — plan layout and kernel launchers shared by tvam_plan.hip
 // and tvam_kernels.hip (not part of the public ABI).
 #pragma once
+
+// Row pitch (voxels) of the per-ray tile kernels' LDS tile (tile + 1-voxel guard band): odd, so
+// that lanes stepping through one tile column (stride = pitch) never share an LDS bank.  An even
+// pitch of 64 (800^3 tiles of 62) put a whole column on one bank: 86 % of the forward's LDS cycles
+// were bank-conflict stalls.
+#define TVAM_TILE_PITCH(tsx) (((tsx) + 2) | 1)
+
 #include "tvam_common.h"
 #include "../../include/tvam.h"
 
@@ -84,6 +91,10 @@ enum TvamMode { TVAM_MODE_FWD = 0, TVAM_MODE_ADJ = 1, TVAM_MODE_COUNT = 2, TVAM_
 #define TVAM_BX 32
 #define TVAM_BY 32
 #define TVAM_BZ 16
+// brick-bin sort keys: brick id << TVAM_BIN_CLASS_BITS | class of the entry's predicted in-brick
+// visit count (entries of one brick run in class order: similar march lengths per wave)
+#define TVAM_BIN_CLASS_BITS 4
+#define TVAM_BIN_CLASSES (1 << TVAM_BIN_CLASS_BITS)
 
 // Scattered segments of paths [p0, p1): `slots` records per path
 // (a = {t_start, tau_end, dtm0_x, dtm0_y}, b = {dtm0_z, +-ts_x, +-ts_y, +-ts_z},
@@ -113,6 +124,9 @@ struct TvamBinScratch {
     int acc_float = 0;            // 1: float LDS adds instead of int64 fixed point (TVAM_BIN_FLOAT)
     uint32_t* slot_of = nullptr;  // [cap_entries] segment slot of each (segment, brick) entry
     float* part = nullptr;        // [cap_entries] adjoint partial of each entry
+    float4* ra = nullptr;         // [cap_entries] segment records in sorted (brick) order
+    float4* rb = nullptr;
+    int2* rc = nullptr;
 };
 
 hipError_t tvam_launch_tiles(int mode, const TvamConsts& k, const TvamTiles& t, size_t lds_bytes,

@@ -69,17 +69,23 @@ struct TvamMarchRay {
 // stored / read as 0).  Visit weight e0 (1 - e^{-st dt}) from the tile-relative
 // dt = tn - tp (tvam_omexp: no cancellation), then e0 *= e^{-st dt} (= e0 - c);
 // e0 restarts exactly from exp2 at every tile entry.
-template <int ACC>
+// W2 (plans with st * voxel diagonal < TVAM_W2_MAX): e0 carries st e^{-st t} and a visit costs
+// c = e0 dt (1 - st dt / 2), e0 -= st c (the planar kernels' form; five full-rate instructions
+// in place of the degree-4 polynomial, its range test and the cancellation-free product).
+template <int ACC, bool W2 = false>
 __device__ __forceinline__ void tvam_march(TvamMarchRay a, const float tsx, const float tsy, const int sxb,
                                            const int syb, const float sig, float& acc,
                                            unsigned long long& nvis, const char* tile = nullptr, const int tw = 0,
                                            const int wx = 0, const int wy = 0) {
     constexpr int ESZ = ACC == ACC_FIXED64 ? 8 : 4;
+    const float mhs = -0.5f * sig, msig = -sig;
     float tp = 0.0f;
     for (;;) {
         const float tn = fminf(fminf(a.Tx, a.Ty), a.rem);
-        const float c = a.e0 * tvam_omexp(sig * fmaxf(tn - tp, 0.0f));
-        const float e1 = a.e0 - c;
+        // tn never decreases (the crossings only grow, tp starts at the clamped tile entry 0)
+        const float dt = tn - tp;
+        const float c = W2 ? a.e0 * dt * fmaf(mhs, dt, 1.0f) : a.e0 * tvam_omexp(sig * fmaxf(dt, 0.0f));
+        const float e1 = W2 ? fmaf(msig, c, a.e0) : a.e0 - c;
         if (ACC == ACC_FLOAT) atomicAdd(reinterpret_cast<float*>(a.pv), c);
         else if (ACC == ACC_FIXED) atomicAdd(reinterpret_cast<int*>(a.pv), tvam_rint(c));
         else if (ACC == ACC_FIXED64) atomicAdd(reinterpret_cast<unsigned long long*>(a.pv), tvam_f2i64(c));
@@ -231,7 +237,7 @@ __device__ __forceinline__ bool tvam_tile_ray(const TvamConsts& k, const TvamTil
     r.dty = ff.w < TVAM_INF ? fmaxf(fmaf((float)n1, an.y, ff.w) - tau_e, 0.0f) : TVAM_INF;
     r.tsx = an.x;
     r.tsy = an.y;
-    const int tw = tp.tsx + 2;  // guard band of one voxel on every side
+    const int tw = TVAM_TILE_PITCH(tp.tsx);  // guard band of one voxel on every side, odd pitch
     r.sx = stx;
     r.sy = sty * tw;
     r.lidx = (vy - y0 + 1) * tw + (vx - x0 + 1);
@@ -260,14 +266,14 @@ __device__ __forceinline__ float tvam_block_sum(float v, float* red) {
     return m;
 }
 
-template <int MODE>
+template <int MODE, bool W2>
 __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
     TvamConsts k, TvamTiles tp, const float* __restrict__ pat, const int32_t* __restrict__ idxmap,
     const float* __restrict__ gin, float* __restrict__ out, unsigned long long* __restrict__ counter) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float* tile = reinterpret_cast<float*>(smem);
     const int tsx = tp.tsx, tsy = tp.tsy, ns = tp.n_shard;
-    const int tw = tsx + 2, th = tsy + 2;  // tile + 1-voxel guard band
+    const int tw = TVAM_TILE_PITCH(tsx), th = tsy + 2;  // tile + 1-voxel guard band, odd row pitch
     const int tile_words = (MODE == TVAM_MODE_FWD && TVAM_FWD_ACC64) ? 2 * tw * th : tw * th;
     float* s_red = tile + tile_words;
     unsigned* s_amax = reinterpret_cast<unsigned*>(s_red + 16);  // forward: per-angle max |p|
@@ -405,21 +411,21 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
         m.stop = r.rem - 1e-6f;
         m.nt0 = k.nsig2 * r.t;
         m.ems = em;
-        m.e0 = em * tvam_exp2(m.nt0);
+        m.e0 = (W2 ? em * k.sig_t : em) * tvam_exp2(m.nt0);
         const int sxb = r.sx * ESZ, syb = r.sy * ESZ;
         float acc = 0.0f;
         if (MODE == TVAM_MODE_FWD) {
             if (TVAM_FWD_ACC64 && acc_mode == ACC_FIXED64)
-                tvam_march<ACC_FIXED64>(m, r.tsx, r.tsy, sxb, syb, k.sig_t, acc, nvis);
+                tvam_march<ACC_FIXED64, W2>(m, r.tsx, r.tsy, sxb, syb, k.sig_t, acc, nvis);
             else if (!TVAM_FWD_ACC64 && acc_mode == ACC_FIXED)
-                tvam_march<ACC_FIXED>(m, r.tsx, r.tsy, sxb, syb, k.sig_t, acc, nvis);
+                tvam_march<ACC_FIXED, W2>(m, r.tsx, r.tsy, sxb, syb, k.sig_t, acc, nvis);
             else
-                tvam_march<ACC_FLOAT>(m, r.tsx, r.tsy, sxb, syb, k.sig_t, acc, nvis);
+                tvam_march<ACC_FLOAT, W2>(m, r.tsx, r.tsy, sxb, syb, k.sig_t, acc, nvis);
         } else if (MODE == TVAM_MODE_ADJ) {
-            tvam_march<ACC_GATHER>(m, r.tsx, r.tsy, sxb, syb, k.sig_t, acc, nvis);
+            tvam_march<ACC_GATHER, W2>(m, r.tsx, r.tsy, sxb, syb, k.sig_t, acc, nvis);
             atomicAdd(&out[r.act], acc * (k.wscale * r.weight));  // backward_from(Le * em_grad), volume.py:274-276
         } else {
-            tvam_march<ACC_COUNT>(m, r.tsx, r.tsy, sxb, syb, k.sig_t, acc, nvis, reinterpret_cast<const char*>(tile),
+            tvam_march<ACC_COUNT, W2>(m, r.tsx, r.tsy, sxb, syb, k.sig_t, acc, nvis, reinterpret_cast<const char*>(tile),
                                   tw, wx, wy);
         }
     }
@@ -448,20 +454,26 @@ hipError_t tvam_launch_tiles(int mode, const TvamConsts& k, const TvamTiles& t, 
                              unsigned long long* counter, hipStream_t stream) {
     dim3 grid((unsigned)(t.ntx * t.nty), (unsigned)k.nz);
     dim3 block(TVAM_BLOCK);
+    const bool w2 = k.vox_chord < TVAM_W2_MAX;
+#define TVAM_TILE_LAUNCH(M)                                                                                      \
+    if (w2)                                                                                                      \
+        hipLaunchKernelGGL((tvam_tile_kernel<M, true>), grid, block, lds_bytes, stream, k, t, pat, idxmap, gin, out, \
+                           counter);                                                                             \
+    else                                                                                                         \
+        hipLaunchKernelGGL((tvam_tile_kernel<M, false>), grid, block, lds_bytes, stream, k, t, pat, idxmap, gin, out, \
+                           counter);
     switch (mode) {
         case TVAM_MODE_FWD:
-            hipLaunchKernelGGL(tvam_tile_kernel<TVAM_MODE_FWD>, grid, block, lds_bytes, stream, k, t, pat,
-                               idxmap, gin, out, counter);
+            TVAM_TILE_LAUNCH(TVAM_MODE_FWD)
             break;
         case TVAM_MODE_ADJ:
-            hipLaunchKernelGGL(tvam_tile_kernel<TVAM_MODE_ADJ>, grid, block, lds_bytes, stream, k, t, pat,
-                               idxmap, gin, out, counter);
+            TVAM_TILE_LAUNCH(TVAM_MODE_ADJ)
             break;
         default:
-            hipLaunchKernelGGL(tvam_tile_kernel<TVAM_MODE_COUNT>, grid, block, lds_bytes, stream, k, t, pat,
-                               idxmap, gin, out, counter);
+            TVAM_TILE_LAUNCH(TVAM_MODE_COUNT)
             break;
     }
+#undef TVAM_TILE_LAUNCH
     return hipGetLastError();
 }
 

@@ -788,7 +788,7 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
 #ifndef TVAM_FWD_ACC64
 #define TVAM_FWD_ACC64 0
 #endif
-    p->lds_bytes = (size_t)(tsx + 2) * (tsy + 2) * sizeof(float) * (TVAM_FWD_ACC64 ? 2 : 1) +
+    p->lds_bytes = (size_t)TVAM_TILE_PITCH(tsx) * (tsy + 2) * sizeof(float) * (TVAM_FWD_ACC64 ? 2 : 1) +
                    16 * sizeof(float) + (size_t)ns * sizeof(float);
     if (p->lds_bytes > 160 * 1024) {
         plan_free(p);

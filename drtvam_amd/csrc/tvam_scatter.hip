@@ -169,14 +169,16 @@ __device__ __forceinline__ int sc_nbr(const TvamConsts& k, int a) {
 // Bricks a segment's DDA visits, in time order: each axis' brick windows
 // partition time exactly (tvam_axis_window on brick bounds), so stepping the
 // axis whose window closes first walks the same sequence the brick kernel
-// resumes from.  F(brick id) per brick; returns the count.
+// resumes from.  F(brick id, relative time the segment enters / leaves the
+// brick) per brick; returns the count.
 template <typename F>
 __device__ __forceinline__ int sc_walk_bricks(const TvamConsts& k, const SegDda& q, F&& f) {
     const int nb0 = sc_nbr(k, 0), nb1 = sc_nbr(k, 1), nb2 = sc_nbr(k, 2);
     int b0 = q.sv[0] / TVAM_BX, b1 = q.sv[1] / TVAM_BY, b2 = q.sv[2] / TVAM_BZ;
     int cnt = 0;
+    float tprev = 0.0f;
     for (int guard = 0; guard < 4096; ++guard) {
-        f((b2 * nb1 + b1) * nb0 + b0);
+        const int bid = (b2 * nb1 + b1) * nb0 + b0;
         ++cnt;
         float tin, t0, t1, t2;
         int nin, nout;
@@ -189,6 +191,8 @@ __device__ __forceinline__ int sc_walk_bricks(const TvamConsts& k, const SegDda&
         const bool m0 = t0 <= t1 && t0 <= t2;
         const bool m1 = !m0 && t1 <= t2;
         const float tm = m0 ? t0 : (m1 ? t1 : t2);
+        f(bid, tprev, fminf(tm, q.tau_end));
+        tprev = tm;
         if (!(tm < q.tau_end)) break;
         if (m0) {
             b0 += q.step[0];
@@ -270,7 +274,7 @@ template <typename F>
 __device__ __forceinline__ void sc_seg_march(const TvamConsts& k, const SegDda& q, F&& f) {
     const int B[3] = {TVAM_BX, TVAM_BY, TVAM_BZ};
     const int nb[3] = {sc_nbr(k, 0), sc_nbr(k, 1), sc_nbr(k, 2)};
-    sc_walk_bricks(k, q, [&](int bid) {
+    sc_walk_bricks(k, q, [&](int bid, float, float) {
         const int bx = bid % nb[0], by = (bid / nb[0]) % nb[1], bz = bid / (nb[0] * nb[1]);
         const int lo[3] = {bx * B[0], by * B[1], bz * B[2]};
         const int hi[3] = {min(lo[0] + B[0], k.res[0]), min(lo[1] + B[1], k.res[1]), min(lo[2] + B[2], k.res[2])};
@@ -373,7 +377,7 @@ __global__ __launch_bounds__(256) void tvam_scatter_kernel(TvamConsts k, TvamTil
                     sb.b[slot] = make_float4(q.dtm0[2], q.ts[0] * (float)q.step[0], q.ts[1] * (float)q.step[1],
                                              q.ts[2] * (float)q.step[2]);
                     sb.c[slot] = make_int2(q.sv[0] | (q.sv[1] << 11) | (q.sv[2] << 22), __float_as_int(em * att));
-                    sb.m[slot] = (uint32_t)sc_walk_bricks(k, q, [](int) {});
+                    sb.m[slot] = (uint32_t)sc_walk_bricks(k, q, [](int, float, float) {});
                 }
             } else if (seg > 0) {
                 const float r = sc_dda<MODE>(k, px, py, pz, vx, vy, vz, tsi, em * att, out, gin, nvis);
@@ -1064,8 +1068,15 @@ __global__ __launch_bounds__(256) void tvam_bin_fill_kernel(TvamConsts k, TvamSe
         float w;
         sc_unpack(sb.a[s], sb.b[s], sb.c[s], q, w);
         uint32_t o = off[s];
-        sc_walk_bricks(k, q, [&](int bid) {
-            keys[o] = (uint32_t)bid;
+        // visits per unit length: one per voxel-face crossing of each moving axis
+        float rate = 0.0f;
+#pragma unroll
+        for (int a = 0; a < 3; ++a) rate += q.ts[a] < TVAM_INF ? 1.0f / q.ts[a] : 0.0f;
+        sc_walk_bricks(k, q, [&](int bid, float t0, float t1) {
+            // low key bits: a class of the predicted in-brick visit count, so that the lanes of a
+            // wave of the brick kernel march entries of similar length
+            const int cls = (int)fminf((float)(TVAM_BIN_CLASSES - 1), fmaxf(t1 - t0, 0.0f) * rate * 0.25f);
+            keys[o] = ((uint32_t)bid << TVAM_BIN_CLASS_BITS) | (uint32_t)cls;
             vals[o] = o;
             slot_of[o] = (uint32_t)s;
             ++o;
@@ -1076,9 +1087,23 @@ __global__ __launch_bounds__(256) void tvam_bin_fill_kernel(TvamConsts k, TvamSe
 __global__ void tvam_bin_start_kernel(const uint32_t* __restrict__ keys, int64_t n, int nbricks,
                                       uint32_t* __restrict__ bstart) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += (int64_t)gridDim.x * blockDim.x) {
-        const int kc = i < n ? (int)keys[i] : nbricks;
-        const int kp = i > 0 ? (int)keys[i - 1] : -1;
+        const int kc = i < n ? (int)(keys[i] >> TVAM_BIN_CLASS_BITS) : nbricks;
+        const int kp = i > 0 ? (int)(keys[i - 1] >> TVAM_BIN_CLASS_BITS) : -1;
         for (int b = kp + 1; b <= kc; ++b) bstart[b] = (uint32_t)i;  // bricks (kp, kc] start here
+    }
+}
+
+// Records of the sorted entries in brick order (entry e <- slot_of[vals[e]]): the brick kernel
+// then reads its entries' records with coalesced loads instead of two dependent random gathers.
+__global__ __launch_bounds__(256) void tvam_bin_gather_kernel(TvamSegBuf sb, const uint32_t* __restrict__ vals,
+                                                              const uint32_t* __restrict__ slot_of, int64_t n,
+                                                              float4* __restrict__ ra, float4* __restrict__ rb,
+                                                              int2* __restrict__ rc) {
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
+        const uint32_t s = slot_of[vals[e]];
+        ra[e] = sb.a[s];
+        rb[e] = sb.b[s];
+        rc[e] = sb.c[s];
     }
 }
 
@@ -1090,9 +1115,10 @@ __global__ void tvam_bin_start_kernel(const uint32_t* __restrict__ keys, int64_t
 // Adjoint (ACC 2): the brick's grad * inv_vol staged in LDS, each entry's
 // weighted gather written to part[entry] (no atomics; summed per path later).
 template <int ACC>
-__global__ __launch_bounds__(512) void tvam_bin_march_kernel(TvamConsts k, TvamSegBuf sb,
+__global__ __launch_bounds__(512) void tvam_bin_march_kernel(TvamConsts k, const float4* __restrict__ ra,
+                                                             const float4* __restrict__ rb,
+                                                             const int2* __restrict__ rc,
                                                              const uint32_t* __restrict__ vals,
-                                                             const uint32_t* __restrict__ slot_of,
                                                              const uint32_t* __restrict__ bstart,
                                                              float* __restrict__ dose, const float* __restrict__ gin,
                                                              float* __restrict__ part) {
@@ -1114,7 +1140,7 @@ __global__ __launch_bounds__(512) void tvam_bin_march_kernel(TvamConsts k, TvamS
     if (ACC == 0) {
         // per-add bound: each add rounds to int32 (one v_cvt), the int64 sums cannot overflow
         float sw = 0.0f;
-        for (uint32_t e = e0 + threadIdx.x; e < e1; e += 512) sw = fmaxf(sw, fabsf(__int_as_float(sb.c[slot_of[vals[e]]].y)));
+        for (uint32_t e = e0 + threadIdx.x; e < e1; e += 512) sw = fmaxf(sw, fabsf(__int_as_float(rc[e].y)));
         for (int o = 32; o > 0; o >>= 1) sw = fmaxf(sw, __shfl_xor(sw, o, 64));
         if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sw;
         for (int i = threadIdx.x; i < NV; i += 512) ltile[i] = 0;
@@ -1141,12 +1167,25 @@ __global__ __launch_bounds__(512) void tvam_bin_march_kernel(TvamConsts k, TvamS
         }
         __syncthreads();
     }
+    // the next entry's record is loaded while this one marches
+    float4 na = make_float4(0.0f, 0.0f, 0.0f, 0.0f), nb = na;
+    int2 nc = make_int2(0, 0);
+    if (e0 + threadIdx.x < e1) {
+        na = ra[e0 + threadIdx.x];
+        nb = rb[e0 + threadIdx.x];
+        nc = rc[e0 + threadIdx.x];
+    }
     for (uint32_t e = e0 + threadIdx.x; e < e1; e += 512) {
-        const uint32_t ent = vals[e];
-        const uint32_t s = slot_of[ent];
+        const float4 ca = na, cb = nb;
+        const int2 cc = nc;
+        if (e + 512 < e1) {
+            na = ra[e + 512];
+            nb = rb[e + 512];
+            nc = rc[e + 512];
+        }
         SegDda q;
         float w;
-        sc_unpack(sb.a[s], sb.b[s], sb.c[s], q, w);
+        sc_unpack(ca, cb, cc, q, w);
         const float ws = w * scale;
         float acc = 0.0f;
         sc_box_march(k, q, lo, hi, [&](int x, int y, int z, float c) {
@@ -1159,7 +1198,7 @@ __global__ __launch_bounds__(512) void tvam_bin_march_kernel(TvamConsts k, TvamS
             else
                 acc = fmaf(c, ftile[li], acc);
         });
-        if (ACC == 2) part[ent] = w * acc;
+        if (ACC == 2) part[vals[e]] = w * acc;
     }
     if (ACC == 2) return;
     __syncthreads();
@@ -1227,6 +1266,9 @@ void tvam_bin_scratch_free(TvamBinScratch& s) {
     (void)hipFree(s.temp);
     (void)hipFree(s.slot_of);
     (void)hipFree(s.part);
+    (void)hipFree(s.ra);
+    (void)hipFree(s.rb);
+    (void)hipFree(s.rc);
     s = TvamBinScratch{};
 }
 
@@ -1243,6 +1285,7 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
     const int nbricks = nbx * nby * nbz;
     int bits = 1;
     while ((1 << bits) < nbricks) ++bits;
+    bits += TVAM_BIN_CLASS_BITS;
     const int spp = (int)t.spp;
     const int64_t npaths = (int64_t)t.n_shard * k.crop_y * k.crop_x * spp;
     // chunk of paths: a whole number of pixels (the adjoint reduces a pixel's samples together)
@@ -1304,8 +1347,13 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
             }
             (void)hipFree(s.slot_of);
             (void)hipFree(s.part);
+            (void)hipFree(s.ra);
+            (void)hipFree(s.rb);
+            (void)hipFree(s.rc);
             s.slot_of = nullptr;
             s.part = nullptr;
+            s.ra = s.rb = nullptr;
+            s.rc = nullptr;
             s.cap_entries = 0;
             const int64_t cap = (int64_t)total + total / 4;
             for (int i = 0; i < 2; ++i)
@@ -1313,7 +1361,10 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
                     (e = hipMalloc((void**)&s.vals[i], cap * sizeof(uint32_t))) != hipSuccess)
                     return e;
             if ((e = hipMalloc((void**)&s.slot_of, cap * sizeof(uint32_t))) != hipSuccess ||
-                (e = hipMalloc((void**)&s.part, cap * sizeof(float))) != hipSuccess)
+                (e = hipMalloc((void**)&s.part, cap * sizeof(float))) != hipSuccess ||
+                (e = hipMalloc((void**)&s.ra, cap * sizeof(float4))) != hipSuccess ||
+                (e = hipMalloc((void**)&s.rb, cap * sizeof(float4))) != hipSuccess ||
+                (e = hipMalloc((void**)&s.rc, cap * sizeof(int2))) != hipSuccess)
                 return e;
             s.cap_entries = cap;
         }
@@ -1337,19 +1388,22 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
         g = std::min<int64_t>(((int64_t)total + 256) / 256, 65536);
         hipLaunchKernelGGL(tvam_bin_start_kernel, dim3((unsigned)g), dim3(256), 0, stream, s.keys[1], (int64_t)total,
                            nbricks, s.bstart);
+        g = std::min<int64_t>(((int64_t)total + 255) / 256, 262144);
+        hipLaunchKernelGGL(tvam_bin_gather_kernel, dim3((unsigned)g), dim3(256), 0, stream, sb, s.vals[1], s.slot_of,
+                           (int64_t)total, s.ra, s.rb, s.rc);
         if (adj) {
-            hipLaunchKernelGGL(tvam_bin_march_kernel<2>, dim3((unsigned)nbricks), dim3(512), 0, stream, k, sb,
-                               s.vals[1], s.slot_of, s.bstart, nullptr, gin, s.part);
+            hipLaunchKernelGGL(tvam_bin_march_kernel<2>, dim3((unsigned)nbricks), dim3(512), 0, stream, k, s.ra, s.rb,
+                               s.rc, s.vals[1], s.bstart, nullptr, gin, s.part);
             const int64_t npix = (p1 - p0) / spp;
             g = std::min<int64_t>((npix + 255) / 256, 65536);
             hipLaunchKernelGGL(tvam_bin_reduce_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, sb, spp, s.off,
                                s.part, idxmap, out);
         } else if (s.acc_float) {
-            hipLaunchKernelGGL(tvam_bin_march_kernel<1>, dim3((unsigned)nbricks), dim3(512), 0, stream, k, sb,
-                               s.vals[1], s.slot_of, s.bstart, out, nullptr, nullptr);
+            hipLaunchKernelGGL(tvam_bin_march_kernel<1>, dim3((unsigned)nbricks), dim3(512), 0, stream, k, s.ra, s.rb,
+                               s.rc, s.vals[1], s.bstart, out, nullptr, nullptr);
         } else {
-            hipLaunchKernelGGL(tvam_bin_march_kernel<0>, dim3((unsigned)nbricks), dim3(512), 0, stream, k, sb,
-                               s.vals[1], s.slot_of, s.bstart, out, nullptr, nullptr);
+            hipLaunchKernelGGL(tvam_bin_march_kernel<0>, dim3((unsigned)nbricks), dim3(512), 0, stream, k, s.ra, s.rb,
+                               s.rc, s.vals[1], s.bstart, out, nullptr, nullptr);
         }
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }

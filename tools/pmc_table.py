@@ -6,6 +6,12 @@ import sys
 from collections import defaultdict
 
 
+def short(name):
+    """Kernel name without its argument list ('(anonymous namespace)::' kept out of the split)."""
+    name = name.replace("(anonymous namespace)::", "")
+    return name.split("(")[0][:60]
+
+
 def main():
     src = sys.argv[1]
     min_ms = float(sys.argv[2]) if len(sys.argv) > 2 else 1.0
@@ -14,10 +20,10 @@ def main():
         f = os.path.join(src, p, "p_counter_collection.csv")
         if os.path.exists(f):
             for r in csv.DictReader(open(f)):
-                cnt[r["Kernel_Name"].split("(")[0][:60]][r["Counter_Name"]].append(float(r["Counter_Value"]))
+                cnt[short(r["Kernel_Name"])][r["Counter_Name"]].append(float(r["Counter_Value"]))
     dur = {}
     for r in csv.DictReader(open(os.path.join(src, "trace", "k_kernel_stats.csv"))):
-        dur[r["Name"].split("(")[0][:60]] = (int(r["Calls"]), float(r["AverageNs"]) / 1e6, float(r["TotalDurationNs"]) / 1e6)
+        dur[short(r["Name"])] = (int(r["Calls"]), float(r["AverageNs"]) / 1e6, float(r["TotalDurationNs"]) / 1e6)
     print(f"{'kernel':60s} {'calls':>5s} {'avg ms':>8s} {'VALU%':>6s} {'lane':>5s} {'LDS%':>5s} {'bank%':>5s} "
           f"{'act/wait_any/inst':>17s} {'HBM GB/s':>8s} {'waves':>8s}")
     for k, (calls, avg, tot) in sorted(dur.items(), key=lambda kv: -kv[1][2]):
