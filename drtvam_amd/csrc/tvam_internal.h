@@ -103,9 +103,7 @@ struct TvamSegBuf {
     int64_t p0, p1;
     int32_t slots;
     int32_t adj;                  // records for the adjoint (weight att * wscale)
-    float4* a;
-    float4* b;
-    int2* c;
+    float4* r;                    // [slots][3] segment records (48 B, one cache-line span per gather)
     uint32_t* m;
 };
 
@@ -124,9 +122,6 @@ struct TvamBinScratch {
     int acc_float = 0;            // 1: float LDS adds instead of int64 fixed point (TVAM_BIN_FLOAT)
     uint32_t* slot_of = nullptr;  // [cap_entries] segment slot of each (segment, brick) entry
     float* part = nullptr;        // [cap_entries] adjoint partial of each entry
-    float4* ra = nullptr;         // [cap_entries] segment records in sorted (brick) order
-    float4* rb = nullptr;
-    int2* rc = nullptr;
 };
 
 hipError_t tvam_launch_tiles(int mode, const TvamConsts& k, const TvamTiles& t, size_t lds_bytes,

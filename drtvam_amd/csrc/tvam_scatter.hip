@@ -373,10 +373,10 @@ __global__ __launch_bounds__(256) void tvam_scatter_kernel(TvamConsts k, TvamTil
                 SegDda q;
                 if (seg <= sb.slots && sc_dda_init(k, o, dv, tsi, q)) {
                     const int64_t slot = (i - sb.p0) * sb.slots + (seg - 1);
-                    sb.a[slot] = make_float4(q.t_start, q.tau_end, q.dtm0[0], q.dtm0[1]);
-                    sb.b[slot] = make_float4(q.dtm0[2], q.ts[0] * (float)q.step[0], q.ts[1] * (float)q.step[1],
+                    sb.r[3 * slot] = make_float4(q.t_start, q.tau_end, q.dtm0[0], q.dtm0[1]);
+                    sb.r[3 * slot + 1] = make_float4(q.dtm0[2], q.ts[0] * (float)q.step[0], q.ts[1] * (float)q.step[1],
                                              q.ts[2] * (float)q.step[2]);
-                    sb.c[slot] = make_int2(q.sv[0] | (q.sv[1] << 11) | (q.sv[2] << 22), __float_as_int(em * att));
+                    sb.r[3 * slot + 2] = make_float4(__int_as_float(q.sv[0] | (q.sv[1] << 11) | (q.sv[2] << 22)), em * att, 0.0f, 0.0f);
                     sb.m[slot] = (uint32_t)sc_walk_bricks(k, q, [](int, float, float) {});
                 }
             } else if (seg > 0) {
@@ -1038,7 +1038,8 @@ hipError_t tvam_launch_scatter_paths(int mode, const TvamConsts& k, const TvamTi
 
 namespace {
 
-__device__ __forceinline__ void sc_unpack(const float4 a, const float4 b, const int2 c, SegDda& q, float& w) {
+__device__ __forceinline__ void sc_unpack(const float4 a, const float4 b, const float4 cf, SegDda& q, float& w) {
+    const int2 c = make_int2(__float_as_int(cf.x), __float_as_int(cf.y));
     q.t_start = a.x;
     q.tau_end = a.y;
     q.dtm0[0] = a.z;
@@ -1066,7 +1067,7 @@ __global__ __launch_bounds__(256) void tvam_bin_fill_kernel(TvamConsts k, TvamSe
         if (sb.m[s] == 0) continue;
         SegDda q;
         float w;
-        sc_unpack(sb.a[s], sb.b[s], sb.c[s], q, w);
+        sc_unpack(sb.r[3 * s], sb.r[3 * s + 1], sb.r[3 * s + 2], q, w);
         uint32_t o = off[s];
         // visits per unit length: one per voxel-face crossing of each moving axis
         float rate = 0.0f;
@@ -1077,8 +1078,14 @@ __global__ __launch_bounds__(256) void tvam_bin_fill_kernel(TvamConsts k, TvamSe
             // wave of the brick kernel march entries of similar length
             const int cls = (int)fminf((float)(TVAM_BIN_CLASSES - 1), fmaxf(t1 - t0, 0.0f) * rate * 0.25f);
             keys[o] = ((uint32_t)bid << TVAM_BIN_CLASS_BITS) | (uint32_t)cls;
-            vals[o] = o;
-            slot_of[o] = (uint32_t)s;
+            // forward: the value is the segment slot itself (the brick kernel reads the record
+            // without a slot_of gather); adjoint: the entry, whose partial the pixel reduce sums
+            if (slot_of) {
+                vals[o] = o;
+                slot_of[o] = (uint32_t)s;
+            } else {
+                vals[o] = (uint32_t)s;
+            }
             ++o;
         });
     }
@@ -1093,20 +1100,6 @@ __global__ void tvam_bin_start_kernel(const uint32_t* __restrict__ keys, int64_t
     }
 }
 
-// Records of the sorted entries in brick order (entry e <- slot_of[vals[e]]): the brick kernel
-// then reads its entries' records with coalesced loads instead of two dependent random gathers.
-__global__ __launch_bounds__(256) void tvam_bin_gather_kernel(TvamSegBuf sb, const uint32_t* __restrict__ vals,
-                                                              const uint32_t* __restrict__ slot_of, int64_t n,
-                                                              float4* __restrict__ ra, float4* __restrict__ rb,
-                                                              int2* __restrict__ rc) {
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < n; e += (int64_t)gridDim.x * blockDim.x) {
-        const uint32_t s = slot_of[vals[e]];
-        ra[e] = sb.a[s];
-        rb[e] = sb.b[s];
-        rc[e] = sb.c[s];
-    }
-}
-
 // One workgroup per brick.  Forward (ACC 0: exact int64 fixed point; every add
 // rounds to int32 with a per-brick scale 2^e from max |w| * the largest
 // per-visit weight min(1, st sqrt3 h), so the step is 2^-30 of the largest
@@ -1115,10 +1108,9 @@ __global__ __launch_bounds__(256) void tvam_bin_gather_kernel(TvamSegBuf sb, con
 // Adjoint (ACC 2): the brick's grad * inv_vol staged in LDS, each entry's
 // weighted gather written to part[entry] (no atomics; summed per path later).
 template <int ACC>
-__global__ __launch_bounds__(512) void tvam_bin_march_kernel(TvamConsts k, const float4* __restrict__ ra,
-                                                             const float4* __restrict__ rb,
-                                                             const int2* __restrict__ rc,
+__global__ __launch_bounds__(512) void tvam_bin_march_kernel(TvamConsts k, TvamSegBuf sb,
                                                              const uint32_t* __restrict__ vals,
+                                                             const uint32_t* __restrict__ slot_of,
                                                              const uint32_t* __restrict__ bstart,
                                                              float* __restrict__ dose, const float* __restrict__ gin,
                                                              float* __restrict__ part) {
@@ -1140,7 +1132,7 @@ __global__ __launch_bounds__(512) void tvam_bin_march_kernel(TvamConsts k, const
     if (ACC == 0) {
         // per-add bound: each add rounds to int32 (one v_cvt), the int64 sums cannot overflow
         float sw = 0.0f;
-        for (uint32_t e = e0 + threadIdx.x; e < e1; e += 512) sw = fmaxf(sw, fabsf(__int_as_float(rc[e].y)));
+        for (uint32_t e = e0 + threadIdx.x; e < e1; e += 512) sw = fmaxf(sw, fabsf(sb.r[3 * vals[e] + 2].y));
         for (int o = 32; o > 0; o >>= 1) sw = fmaxf(sw, __shfl_xor(sw, o, 64));
         if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sw;
         for (int i = threadIdx.x; i < NV; i += 512) ltile[i] = 0;
@@ -1167,22 +1159,32 @@ __global__ __launch_bounds__(512) void tvam_bin_march_kernel(TvamConsts k, const
         }
         __syncthreads();
     }
-    // the next entry's record is loaded while this one marches
+    // Three-stage load pipeline over this thread's entries e, e + S, e + 2S, ... (S = 512): while
+    // entry e marches, the record of e + S, the slot of e + 2S and the entry id of e + 3S are in
+    // flight (the chain vals -> slot_of -> record is three dependent gathers).
+    constexpr uint32_t S = 512;
+    const uint32_t et = e0 + threadIdx.x;
+    // forward (ACC 0 / 1): vals hold the slots themselves
+    auto slot_at = [&](uint32_t v) { return ACC == 2 ? slot_of[v] : v; };
+    uint32_t v2 = et + 2 * S < e1 ? vals[et + 2 * S] : 0u;
+    uint32_t s1 = et + S < e1 ? slot_at(vals[et + S]) : 0u;
+    uint32_t s0 = et < e1 ? slot_at(vals[et]) : 0u;
     float4 na = make_float4(0.0f, 0.0f, 0.0f, 0.0f), nb = na;
-    int2 nc = make_int2(0, 0);
-    if (e0 + threadIdx.x < e1) {
-        na = ra[e0 + threadIdx.x];
-        nb = rb[e0 + threadIdx.x];
-        nc = rc[e0 + threadIdx.x];
+    float4 nc = na;
+    if (et < e1) {
+        na = sb.r[3 * s0];
+        nb = sb.r[3 * s0 + 1];
+        nc = sb.r[3 * s0 + 2];
     }
-    for (uint32_t e = e0 + threadIdx.x; e < e1; e += 512) {
-        const float4 ca = na, cb = nb;
-        const int2 cc = nc;
-        if (e + 512 < e1) {
-            na = ra[e + 512];
-            nb = rb[e + 512];
-            nc = rc[e + 512];
+    for (uint32_t e = et; e < e1; e += S) {
+        const float4 ca = na, cb = nb, cc = nc;
+        if (e + S < e1) {
+            na = sb.r[3 * s1];
+            nb = sb.r[3 * s1 + 1];
+            nc = sb.r[3 * s1 + 2];
         }
+        s1 = e + 2 * S < e1 ? slot_at(v2) : 0u;
+        v2 = e + 3 * S < e1 ? vals[e + 3 * S] : 0u;
         SegDda q;
         float w;
         sc_unpack(ca, cb, cc, q, w);
@@ -1253,9 +1255,7 @@ hipError_t grow(T** p, int64_t& cap, int64_t need) {
 }  // namespace
 
 void tvam_bin_scratch_free(TvamBinScratch& s) {
-    (void)hipFree(s.sb.a);
-    (void)hipFree(s.sb.b);
-    (void)hipFree(s.sb.c);
+    (void)hipFree(s.sb.r);
     (void)hipFree(s.sb.m);
     (void)hipFree(s.off);
     for (int i = 0; i < 2; ++i) {
@@ -1266,9 +1266,6 @@ void tvam_bin_scratch_free(TvamBinScratch& s) {
     (void)hipFree(s.temp);
     (void)hipFree(s.slot_of);
     (void)hipFree(s.part);
-    (void)hipFree(s.ra);
-    (void)hipFree(s.rb);
-    (void)hipFree(s.rc);
     s = TvamBinScratch{};
 }
 
@@ -1298,9 +1295,7 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
         const int keep_float = s.acc_float;
         tvam_bin_scratch_free(s);
         s.acc_float = keep_float;
-        if ((e = hipMalloc((void**)&s.sb.a, nsl * sizeof(float4))) != hipSuccess ||
-            (e = hipMalloc((void**)&s.sb.b, nsl * sizeof(float4))) != hipSuccess ||
-            (e = hipMalloc((void**)&s.sb.c, nsl * sizeof(int2))) != hipSuccess ||
+        if ((e = hipMalloc((void**)&s.sb.r, 3 * nsl * sizeof(float4))) != hipSuccess ||
             (e = hipMalloc((void**)&s.sb.m, (nsl + 1) * sizeof(uint32_t))) != hipSuccess ||
             (e = hipMalloc((void**)&s.off, (nsl + 1) * sizeof(uint32_t))) != hipSuccess)
             return e;
@@ -1347,13 +1342,8 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
             }
             (void)hipFree(s.slot_of);
             (void)hipFree(s.part);
-            (void)hipFree(s.ra);
-            (void)hipFree(s.rb);
-            (void)hipFree(s.rc);
             s.slot_of = nullptr;
             s.part = nullptr;
-            s.ra = s.rb = nullptr;
-            s.rc = nullptr;
             s.cap_entries = 0;
             const int64_t cap = (int64_t)total + total / 4;
             for (int i = 0; i < 2; ++i)
@@ -1361,10 +1351,7 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
                     (e = hipMalloc((void**)&s.vals[i], cap * sizeof(uint32_t))) != hipSuccess)
                     return e;
             if ((e = hipMalloc((void**)&s.slot_of, cap * sizeof(uint32_t))) != hipSuccess ||
-                (e = hipMalloc((void**)&s.part, cap * sizeof(float))) != hipSuccess ||
-                (e = hipMalloc((void**)&s.ra, cap * sizeof(float4))) != hipSuccess ||
-                (e = hipMalloc((void**)&s.rb, cap * sizeof(float4))) != hipSuccess ||
-                (e = hipMalloc((void**)&s.rc, cap * sizeof(int2))) != hipSuccess)
+                (e = hipMalloc((void**)&s.part, cap * sizeof(float))) != hipSuccess)
                 return e;
             s.cap_entries = cap;
         }
@@ -1381,29 +1368,26 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
         }
         g = std::min<int64_t>((ns + 255) / 256, 262144);
         hipLaunchKernelGGL(tvam_bin_fill_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, sb, s.off, ns, s.keys[0],
-                           s.vals[0], s.slot_of);
+                           s.vals[0], adj ? s.slot_of : nullptr);
         if ((e = hipcub::DeviceRadixSort::SortPairs(s.temp, tb2, s.keys[0], s.keys[1], s.vals[0], s.vals[1],
                                                     (int)total, 0, bits, stream)) != hipSuccess)
             return e;
         g = std::min<int64_t>(((int64_t)total + 256) / 256, 65536);
         hipLaunchKernelGGL(tvam_bin_start_kernel, dim3((unsigned)g), dim3(256), 0, stream, s.keys[1], (int64_t)total,
                            nbricks, s.bstart);
-        g = std::min<int64_t>(((int64_t)total + 255) / 256, 262144);
-        hipLaunchKernelGGL(tvam_bin_gather_kernel, dim3((unsigned)g), dim3(256), 0, stream, sb, s.vals[1], s.slot_of,
-                           (int64_t)total, s.ra, s.rb, s.rc);
         if (adj) {
-            hipLaunchKernelGGL(tvam_bin_march_kernel<2>, dim3((unsigned)nbricks), dim3(512), 0, stream, k, s.ra, s.rb,
-                               s.rc, s.vals[1], s.bstart, nullptr, gin, s.part);
+            hipLaunchKernelGGL(tvam_bin_march_kernel<2>, dim3((unsigned)nbricks), dim3(512), 0, stream, k, sb,
+                               s.vals[1], s.slot_of, s.bstart, nullptr, gin, s.part);
             const int64_t npix = (p1 - p0) / spp;
             g = std::min<int64_t>((npix + 255) / 256, 65536);
             hipLaunchKernelGGL(tvam_bin_reduce_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, sb, spp, s.off,
                                s.part, idxmap, out);
         } else if (s.acc_float) {
-            hipLaunchKernelGGL(tvam_bin_march_kernel<1>, dim3((unsigned)nbricks), dim3(512), 0, stream, k, s.ra, s.rb,
-                               s.rc, s.vals[1], s.bstart, out, nullptr, nullptr);
+            hipLaunchKernelGGL(tvam_bin_march_kernel<1>, dim3((unsigned)nbricks), dim3(512), 0, stream, k, sb,
+                               s.vals[1], s.slot_of, s.bstart, out, nullptr, nullptr);
         } else {
-            hipLaunchKernelGGL(tvam_bin_march_kernel<0>, dim3((unsigned)nbricks), dim3(512), 0, stream, k, s.ra, s.rb,
-                               s.rc, s.vals[1], s.bstart, out, nullptr, nullptr);
+            hipLaunchKernelGGL(tvam_bin_march_kernel<0>, dim3((unsigned)nbricks), dim3(512), 0, stream, k, sb,
+                               s.vals[1], s.slot_of, s.bstart, out, nullptr, nullptr);
         }
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }
