@@ -829,11 +829,18 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
             int s = tvam_slice_of(k, yc) - k.z0;
             if (s >= 0 && s < k.nz) rows_of[s].push_back(rc);
         } else {
+            // jittered rows: a ray's height yc(jy) is monotone in jy in fp32 (tvam_ray_camera), and so is
+            // its slice (int)((yc - bmin) / h) (tvam_slice_of), so the slices of jy in [0, 1) lie between
+            // those of jy = 1 and jy = 0, computed with the kernels' own fp32 expressions (a slice list
+            // with a +-1 margin made two of every three row slots of the tile kernels idle at 1:1 rows)
             float xc, ytop, ybot;
             tvam_ray_camera(k, 0, row, 0.5f, 0.0f, xc, ytop);
             tvam_ray_camera(k, 0, row, 0.5f, 1.0f, xc, ybot);
-            double lo = ((double)ybot - k.bmin[2]) / k.h[2] - 1.0, hi = ((double)ytop - k.bmin[2]) / k.h[2] + 1.0;
-            int s0 = std::max(k.z0, (int)std::floor(lo)), s1 = std::min(k.z0 + k.nz - 1, (int)std::floor(hi));
+            if (!(ytop > k.bmin[2] && ybot < k.bmax[2])) continue;  // every jittered ray misses the grid
+            const float zlo = ybot > k.bmin[2] ? ybot : k.bmin[2], zhi = ytop < k.bmax[2] ? ytop : k.bmax[2];
+            int s0 = (int)((zlo - k.bmin[2]) / k.h[2]), s1 = (int)((zhi - k.bmin[2]) / k.h[2]);
+            s0 = std::max(k.z0, std::max(s0, 0));
+            s1 = std::min(k.z0 + k.nz - 1, std::min(s1, k.res[2] - 1));
             for (int s = s0; s <= s1; ++s) rows_of[s - k.z0].push_back(rc);
         }
     }
