@@ -19,5 +19,7 @@ for src in tvam_plan tvam_kernels tvam_planar tvam_vec tvam_scatter tvam_radon; 
   pids+=($!)
   objs+=("$objdir/$src.o")
 done
-for pid in "${pids[@]}"; do wait "$pid"; done
+fail=0
+for pid in "${pids[@]}"; do wait "$pid" || fail=1; done
+[ "$fail" = 0 ] || { echo "build.sh: compilation failed" >&2; exit 1; }
 "$HIPCC" --offload-arch=gfx950 -shared -fPIC "${objs[@]}" -o "$out"

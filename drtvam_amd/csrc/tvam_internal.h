@@ -68,9 +68,22 @@ struct TvamPlanar {
                                // from the [row][col] patterns directly)
     int32_t bin_pad;           // forward: zero columns on either side of the binned patterns (= ncmax)
     int32_t bin_nz;            // forward: slices per binned column (nz rounded up to the slab depth Z)
+    // voxel-driven forward behind a refracting vial (fwd_refr = 1): every column's chord has its
+    // own direction, and the candidate columns of a voxel come from a per-(16x16 tile, angle)
+    // bilinear model of the chord index u(x, y) (tvam_refr_model_kernel)
+    int32_t fwd_refr;
+    float4* vox2;              // [ns][crop_x] {1/d.x, 1/d.y, axis flags (int bits), interface weight}
+    float4* chord;             // plan creation only: [ns][crop_x] {o2.x, o2.y, d2.x, d2.y} of the medium chord
+    const float4* fwd_model;   // [16x16 tiles][ns][2] {u00, du/dlx, du/dly, d2u/dlx dly},
+                               //   {half width + model error, candidates (int bits), first window column (int bits), 0}
 };
 
 hipError_t tvam_launch_planar_rays(const TvamConsts& k, const TvamPlanar& pl, hipStream_t stream);
+// Refracted voxel-driven forward: per (16x16 tile, angle) model of the chord index (needs pl.chord);
+// model: [tiles][ns][2] float4, need: [tiles][ns] window width in columns.  range: [ns] first / last
+// column whose chord reaches the medium.
+hipError_t tvam_launch_refr_model(const TvamConsts& k, const TvamPlanar& pl, const int2* range, float4* model,
+                                  int32_t* need, hipStream_t stream);
 size_t tvam_planar_fwd_lds(const TvamPlanar& pl, int Z);
 bool tvam_planar_fwd_fits(const TvamPlanar& pl, int Z);
 hipError_t tvam_launch_fwd_planar(const TvamConsts& k, const TvamPlanar& pl, int Z, const float* pat, float* dose,

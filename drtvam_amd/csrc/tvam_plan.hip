@@ -81,6 +81,8 @@ struct tvam_plan {
     float4* d_pl_rec_g = nullptr;
     float* d_pl_part = nullptr;  // voxel-driven forward: partial doses of the angle parts
     float* d_pl_bin = nullptr;   // voxel-driven forward: slice-binned patterns
+    float4* d_pl_vox2 = nullptr;      // refracted voxel-driven forward: per-column 1/d, flags, weight
+    float4* d_pl_fwd_model = nullptr; // refracted voxel-driven forward: per-(tile, angle) chord-index models
     unsigned* d_amax = nullptr;  // ray-driven forward: per-angle max |pattern|, fixed-point scale
     float* d_fscale = nullptr;
     int32_t planar_rz = 4;
@@ -156,6 +158,8 @@ static void plan_free(tvam_plan* p) {
     (void)hipFree(p->d_pl_rec_g);
     (void)hipFree(p->d_pl_part);
     (void)hipFree(p->d_pl_bin);
+    (void)hipFree(p->d_pl_vox2);
+    (void)hipFree(p->d_pl_fwd_model);
     (void)hipFree(p->d_amax);
     (void)hipFree(p->d_occ);
     (void)hipFree(p->d_tgt);
@@ -316,6 +320,9 @@ static int env_int(const char* name, int def) {
 // vial wall).  Builds the row -> slice CSR of valid rows and the per-(angle,
 // column) ray table (computed once, here).
 static bool planar_fwd_setup(tvam_plan* p, const std::vector<float2>& cs, const std::vector<int32_t>& off);
+static int fwd_buffers(tvam_plan* p);
+static int choose_fwd_z(tvam_plan* p);
+static int refr_fwd_setup(tvam_plan* p, const std::vector<int32_t>& off);
 
 static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     const tvam_desc& d = p->desc;
@@ -399,38 +406,7 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     p->fwd_ang_h.clear();
     p->fwd_cb_h.clear();
     p->pl.fwd_parts = 1;
-    if (p->planar_fwd) {
-        // A thin slab leaves few (16x16 tile, slice chunk) workgroups, each running
-        // every angle: at 3 resident workgroups per CU, 1250 of them (400^2 film,
-        // 50 slices) fill 1.6 rounds of the 768 slots.  Split the angles into parts
-        // until >= 4 rounds; the partial doses are summed in fixed order.
-        const int64_t nwg = (int64_t)((k.res[0] + 15) / 16) * ((k.res[1] + 15) / 16) *
-                            ((k.nz + p->planar_fz - 1) / p->planar_fz);
-        int parts = (int)std::min<int64_t>(4, std::max<int64_t>(1, (4 * 768 + nwg - 1) / std::max<int64_t>(nwg, 1)));
-        const int ep = env_int("TVAM_FWD_PARTS", 0);
-        if (ep >= 1 && ep <= 16) parts = ep;
-        parts = std::max(1, std::min(parts, ns));
-        if (parts > 1) {
-            const size_t bytes = (size_t)parts * k.nz * k.res[0] * k.res[1] * sizeof(float);
-            if ((e = hipMalloc((void**)&p->d_pl_part, bytes)) != hipSuccess) return hip_fail(e, "hipMalloc (forward parts)");
-            p->pl.fwd_part = p->d_pl_part;
-        }
-        p->pl.fwd_parts = parts;
-        // Slice-binned patterns ([angle][pad + column][slice], tvam_slice_bin_kernel): the
-        // forward stages each window column's Z slices with 16-byte loads and stores
-        const int Z = p->planar_fz;
-        const int nq = (p->pl.ncmax * (Z / 4) + 255) / 256;
-        if (env_int("TVAM_FWD_BIN", 1) && nq <= 2 && ns > 0) {
-            if (p->pl.fwd_ab > 2 || (nq == 2 && p->pl.fwd_ab != 2)) p->pl.fwd_ab = 2;  // the instantiated variants
-            p->pl.bin_pad = p->pl.ncmax;
-            p->pl.bin_nz = (k.nz + Z - 1) / Z * Z;
-            const size_t bytes = (size_t)ns * (d.crop_x + 2 * p->pl.bin_pad) * p->pl.bin_nz * sizeof(float);
-            if ((e = hipMalloc((void**)&p->d_pl_bin, bytes)) != hipSuccess) return hip_fail(e, "hipMalloc (binned patterns)");
-            if ((e = hipMemset(p->d_pl_bin, 0, bytes)) != hipSuccess) return hip_fail(e, "hipMemset (binned patterns)");
-            p->pl.fwd_bin = p->d_pl_bin;
-            p->pl.fwd_pf = nq;
-        }
-    }
+    if (p->planar_fwd && (rc = fwd_buffers(p))) return rc;
     if ((e = hipMalloc((void**)&p->d_pl_vox, nrec * sizeof(float4))) != hipSuccess ||
         (e = hipMalloc((void**)&p->d_pl_rec_f, nrec * sizeof(float4))) != hipSuccess ||
         (e = hipMalloc((void**)&p->d_pl_rec_i, nrec * sizeof(int32_t))) != hipSuccess ||
@@ -438,6 +414,16 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
         (e = hipMalloc((void**)&p->d_amax, (size_t)std::max(ns, 1) * sizeof(unsigned))) != hipSuccess ||
         (e = hipMalloc((void**)&p->d_fscale, 2 * sizeof(float))) != hipSuccess)
         return hip_fail(e, "hipMalloc (planar tables)");
+    // refracting vial: the voxel-driven forward over per-column chords (tvam_refr_model_kernel)
+    const bool try_refr = p->cyl && !(d.flags & TVAM_FLAG_RAY_FWD) && env_int("TVAM_REFR_FWD", 1) && ns > 0;
+    float4* d_chord = nullptr;
+    if (try_refr && ((e = hipMalloc((void**)&p->d_pl_vox2, nrec * sizeof(float4))) != hipSuccess ||
+                     (e = hipMalloc((void**)&d_chord, nrec * sizeof(float4))) != hipSuccess)) {
+        (void)hipFree(d_chord);
+        return hip_fail(e, "hipMalloc (refracted forward tables)");
+    }
+    p->pl.vox2 = p->d_pl_vox2;
+    p->pl.chord = d_chord;
     p->pl.cs = p->d_cs;
     p->pl.vox = p->d_pl_vox;
     p->pl.rec_f = p->d_pl_rec_f;
@@ -455,9 +441,174 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
         if ((e = hipMemcpy(ri.data(), p->d_pl_rec_i, ri.size() * sizeof(int32_t), hipMemcpyDeviceToHost)) != hipSuccess)
             return hip_fail(e, "hipMemcpy");
         for (int32_t v : ri)
-            if (v == -2) return 0;
+            if (v == -2) {
+                (void)hipFree(d_chord);
+                p->pl.chord = nullptr;
+                return 0;
+            }
+    }
+    if (try_refr) {
+        rc = refr_fwd_setup(p, off);
+        (void)hipFree(d_chord);
+        p->pl.chord = nullptr;
+        if (rc) return rc;
     }
     p->planar = true;
+    return 0;
+}
+
+
+// Buffers of the voxel-driven forward (straight or refracted): angle parts of thin slabs and
+// the slice-binned patterns.
+static int fwd_buffers(tvam_plan* p) {
+    const tvam_desc& d = p->desc;
+    const TvamConsts& k = p->k;
+    const int ns = p->pl.ns;
+    hipError_t e;
+    // A thin slab leaves few (16x16 tile, slice chunk) workgroups, each running
+    // every angle: at 3 resident workgroups per CU, 1250 of them (400^2 film,
+    // 50 slices) fill 1.6 rounds of the 768 slots.  Split the angles into parts
+    // until >= 4 rounds; the partial doses are summed in fixed order.
+    const int64_t nwg = (int64_t)((k.res[0] + 15) / 16) * ((k.res[1] + 15) / 16) *
+                        ((k.nz + p->planar_fz - 1) / p->planar_fz);
+    int parts = (int)std::min<int64_t>(4, std::max<int64_t>(1, (4 * 768 + nwg - 1) / std::max<int64_t>(nwg, 1)));
+    const int ep = env_int("TVAM_FWD_PARTS", 0);
+    if (ep >= 1 && ep <= 16) parts = ep;
+    parts = std::max(1, std::min(parts, ns));
+    if (parts > 1) {
+        const size_t bytes = (size_t)parts * k.nz * k.res[0] * k.res[1] * sizeof(float);
+        if ((e = hipMalloc((void**)&p->d_pl_part, bytes)) != hipSuccess) return hip_fail(e, "hipMalloc (forward parts)");
+        p->pl.fwd_part = p->d_pl_part;
+    }
+    p->pl.fwd_parts = parts;
+    // Slice-binned patterns ([angle][pad + column][slice], tvam_slice_bin_kernel): the
+    // forward stages each window column's Z slices with 16-byte loads and stores
+    const int Z = p->planar_fz;
+    const int nq = (p->pl.ncmax * (Z / 4) + 255) / 256;
+    if (env_int("TVAM_FWD_BIN", 1) && nq <= 2 && ns > 0) {
+        if (p->pl.fwd_ab > 2 || (nq == 2 && p->pl.fwd_ab != 2)) p->pl.fwd_ab = 2;  // the instantiated variants
+        p->pl.bin_pad = p->pl.ncmax;
+        p->pl.bin_nz = (k.nz + Z - 1) / Z * Z;
+        const size_t bytes = (size_t)ns * (d.crop_x + 2 * p->pl.bin_pad) * p->pl.bin_nz * sizeof(float);
+        if ((e = hipMalloc((void**)&p->d_pl_bin, bytes)) != hipSuccess) return hip_fail(e, "hipMalloc (binned patterns)");
+        if ((e = hipMemset(p->d_pl_bin, 0, bytes)) != hipSuccess) return hip_fail(e, "hipMemset (binned patterns)");
+        p->pl.fwd_bin = p->d_pl_bin;
+        p->pl.fwd_pf = nq;
+    }
+    return 0;
+}
+
+
+// Slices per workgroup of the voxel-driven forward: the fewest padded slice-passes
+// ceil(nz / Z) * (Z + 4) (the +4 prices the per-angle candidate geometry shared by the Z
+// slices) among the depths whose staging fits.  Returns false when none fits.
+static int choose_fwd_z(tvam_plan* p) {
+    const TvamConsts& k = p->k;
+    if (p->planar_fz == 0) {
+        int best = 8;
+        int64_t bcost = INT64_MAX;
+        for (int Z : {32, 28, 24, 16, 8}) {
+            if (!tvam_planar_fwd_fits(p->pl, Z)) continue;
+            const int64_t cost = (int64_t)((k.nz + Z - 1) / Z) * (Z + 4);
+            if (cost < bcost) bcost = cost, best = Z;
+        }
+        p->planar_fz = best;
+    }
+    while (p->planar_fz > 8 && !tvam_planar_fwd_fits(p->pl, p->planar_fz)) p->planar_fz /= 2;
+    return tvam_planar_fwd_fits(p->pl, p->planar_fz) ? 1 : 0;
+}
+
+// Refracted voxel-driven forward (after the planar ray table, with pl.chord filled): the
+// per-angle run of columns whose chords reach the medium (contiguous, else no voxel-driven
+// forward), the per-(tile, angle) chord-index models and the staged window width.  Leaves
+// planar_fwd false (the ray-driven forward serves) when the tables do not fit.
+static int refr_fwd_setup(tvam_plan* p, const std::vector<int32_t>& off) {
+    const tvam_desc& d = p->desc;
+    const TvamConsts& k = p->k;
+    const int ns = p->pl.ns;
+    hipError_t e;
+    std::vector<float4> vox((size_t)ns * d.crop_x);
+    if ((e = hipMemcpy(vox.data(), p->d_pl_vox, vox.size() * sizeof(float4), hipMemcpyDeviceToHost)) != hipSuccess)
+        return hip_fail(e, "hipMemcpy");
+    std::vector<int2> range(ns);
+    for (int a = 0; a < ns; ++a) {
+        int c0 = -1, c1 = -2;
+        for (int c = 0; c < d.crop_x; ++c)
+            if (vox[(size_t)a * d.crop_x + c].z >= 0.0f) {
+                if (c0 < 0) c0 = c;
+                if (c1 >= 0 && c1 != c - 1) return 0;  // a gap in the run: the bisection needs one
+                c1 = c;
+            }
+        range[a] = make_int2(c0, c1);
+    }
+    const int ntiles = ((k.res[0] + 15) / 16) * ((k.res[1] + 15) / 16);
+    const size_t nm = (size_t)ntiles * ns;
+    int2* d_range = nullptr;
+    int32_t* d_need = nullptr;
+    int rc = upload(&d_range, range);
+    if (rc) return rc;
+    if ((e = hipMalloc((void**)&p->d_pl_fwd_model, 2 * nm * sizeof(float4))) != hipSuccess ||
+        (e = hipMalloc((void**)&d_need, nm * sizeof(int32_t))) != hipSuccess) {
+        (void)hipFree(d_range);
+        (void)hipFree(d_need);
+        return hip_fail(e, "hipMalloc (refracted forward models)");
+    }
+    e = tvam_launch_refr_model(k, p->pl, d_range, p->d_pl_fwd_model, d_need, nullptr);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    std::vector<int32_t> need(nm);
+    std::vector<float4> mdl(2 * nm);
+    if (e == hipSuccess) e = hipMemcpy(need.data(), d_need, nm * sizeof(int32_t), hipMemcpyDeviceToHost);
+    if (e == hipSuccess) e = hipMemcpy(mdl.data(), p->d_pl_fwd_model, 2 * nm * sizeof(float4), hipMemcpyDeviceToHost);
+    (void)hipFree(d_range);
+    (void)hipFree(d_need);
+    if (e != hipSuccess) return hip_fail(e, "refracted forward models");
+    int ncm = 1, ncmax_c = 1;
+    for (size_t i = 0; i < nm; ++i) {
+        int nc;
+        std::memcpy(&nc, &mdl[2 * i + 1].y, sizeof(int));
+        ncm = std::max(ncm, need[i]);
+        ncmax_c = std::max(ncmax_c, nc);
+        // windows wholly outside the crop stage only the binned patterns' zero pads
+        int cb;
+        std::memcpy(&cb, &mdl[2 * i + 1].z, sizeof(int));
+        (void)cb;
+    }
+    TvamPlanar save = p->pl;
+    p->pl.fwd_refr = 1;
+    p->pl.ncmax = ncm;
+    p->pl.fwd_nc = ncmax_c;
+    p->pl.fwd_ab = 2;
+    p->pl.fwd_model = p->d_pl_fwd_model;
+    {
+        bool multi = false;
+        for (int z = 0; z < k.nz; ++z) multi |= off[z + 1] - off[z] > 1;
+        p->pl.fwd_multi = multi ? 1 : 0;
+    }
+    // clamp windows into the binned patterns' zero pads (bin_pad = ncmax on either side)
+    bool changed = false;
+    for (size_t i = 0; i < nm; ++i) {
+        int cb;
+        std::memcpy(&cb, &mdl[2 * i + 1].z, sizeof(int));
+        const int cl = std::min(std::max(cb, -ncm), (int)d.crop_x);
+        if (cl != cb) {
+            std::memcpy(&mdl[2 * i + 1].z, &cl, sizeof(int));
+            changed = true;
+        }
+    }
+    if (changed && (e = hipMemcpy(p->d_pl_fwd_model, mdl.data(), 2 * nm * sizeof(float4), hipMemcpyHostToDevice)) !=
+                       hipSuccess)
+        return hip_fail(e, "hipMemcpy");
+    if (!choose_fwd_z(p)) {
+        p->pl = save;
+        (void)hipFree(p->d_pl_fwd_model);
+        p->d_pl_fwd_model = nullptr;
+        return 0;
+    }
+    const int nq = (p->pl.ncmax * (p->planar_fz / 4) + 255) / 256;
+    p->pl.fwd_pf = nq;
+    p->planar_fwd = true;
+    if ((rc = fwd_buffers(p))) return rc;
+    if (!p->pl.fwd_bin) return fail(TVAM_ERR_INVALID, "refracted voxel-driven forward needs the binned patterns");
     return 0;
 }
 
@@ -524,21 +675,8 @@ static bool planar_fwd_setup(tvam_plan* p, const std::vector<float2>& cs, const 
         const int ab = env_int("TVAM_FWD_AB", 2);
         p->pl.fwd_ab = (ab >= 1 && ab <= 4) ? ab : 2;
     }
-    if (p->planar_fz == 0) {
-        // slices per workgroup: the fewest padded slice-passes ceil(nz / Z) * (Z + 4)
-        // (the +4 prices the per-angle candidate geometry shared by the Z slices)
-        int best = 8;
-        int64_t bcost = INT64_MAX;
-        for (int Z : {32, 28, 24, 16, 8}) {
-            if (!tvam_planar_fwd_fits(p->pl, Z)) continue;
-            const int64_t cost = (int64_t)((k.nz + Z - 1) / Z) * (Z + 4);
-            if (cost < bcost) bcost = cost, best = Z;
-        }
-        p->planar_fz = best;
-    }
-    while (p->planar_fz > 8 && !tvam_planar_fwd_fits(p->pl, p->planar_fz)) p->planar_fz /= 2;
+    if (!choose_fwd_z(p)) return false;
     p->pl.fwd_pf = (p->pl.ncmax * p->planar_fz + 255) / 256 <= 2 ? 2 : 4;
-    if (!tvam_planar_fwd_fits(p->pl, p->planar_fz)) return false;
     p->fwd_ang_h = std::move(fang);
     p->fwd_cb_h = std::move(fcb);
     return true;

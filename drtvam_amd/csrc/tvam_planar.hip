@@ -29,6 +29,8 @@
 // slice's.
 #include "tvam_internal.h"
 
+#include <algorithm>
+
 #define TVAM_PB 256
 
 __device__ __forceinline__ float pl_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
@@ -50,7 +52,8 @@ typedef float pl_f4 __attribute__((ext_vector_type(4)));
 __global__ __launch_bounds__(256) void tvam_planar_rays_kernel(TvamConsts k, const float2* __restrict__ cs, int ns,
                                                                float4* __restrict__ vox, float4* __restrict__ rec_f,
                                                                int32_t* __restrict__ rec_i,
-                                                               float4* __restrict__ rec_g) {
+                                                               float4* __restrict__ rec_g, float4* __restrict__ vox2,
+                                                               float4* __restrict__ chord) {
     const int64_t n = (int64_t)ns * k.crop_x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int al = (int)(i / k.crop_x), col = (int)(i - (int64_t)al * k.crop_x);
@@ -66,6 +69,8 @@ __global__ __launch_bounds__(256) void tvam_planar_rays_kernel(TvamConsts k, con
             rec_f[i] = make_float4(0.0f, -1.0f, 0.0f, 0.0f);
             rec_i[i] = -1;
             if (rec_g) rec_g[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (vox2) vox2[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            if (chord) chord[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
             continue;
         }
         if (rec_g)
@@ -75,12 +80,16 @@ __global__ __launch_bounds__(256) void tvam_planar_rays_kernel(TvamConsts k, con
             rec_i[i] = -2;                                  // falls back to the per-ray tile path
             continue;
         }
-        dx = d2x;  // the voxel-driven forward only serves straight rays (d2 == d)
+        dx = d2x;  // the medium chord's direction (the straight rays' own behind an index-matched vial)
         dy = d2y;
         const bool vx = fabsf(dx) > 1e-8f, vy = fabsf(dy) > 1e-8f;
         const float qx = vx ? -o2x * (1.0f / dx) : (float)q.sv[0];
         const float qy = vy ? -o2y * (1.0f / dy) : (float)q.sv[1];
         vox[i] = make_float4(qx, qy, q.t_start + q.tau_end, 0.0f);
+        if (vox2)  // refracted forward: the column's own 1 / d, axis flags and interface weight
+            vox2[i] = make_float4(vx ? 1.0f / dx : 0.0f, vy ? 1.0f / dy : 0.0f, __int_as_float((vx ? 1 : 0) | (vy ? 2 : 0)),
+                                  wgt);
+        if (chord) chord[i] = make_float4(o2x, o2y, d2x, d2y);
         rec_f[i] = make_float4(q.t_start, q.tau_end, q.dtm0[0], q.dtm0[1]);
         rec_i[i] = q.sv[0] | (q.sv[1] << 16);
     }
@@ -91,7 +100,7 @@ hipError_t tvam_launch_planar_rays(const TvamConsts& k, const TvamPlanar& pl, hi
     int64_t g = (n + 255) / 256;
     g = g > 65536 ? 65536 : (g < 1 ? 1 : g);
     hipLaunchKernelGGL(tvam_planar_rays_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, pl.cs, pl.ns, pl.vox,
-                       pl.rec_f, pl.rec_i, pl.rec_g);
+                       pl.rec_f, pl.rec_i, pl.rec_g, pl.vox2, pl.chord);
     return hipGetLastError();
 }
 
@@ -116,22 +125,29 @@ __host__ __device__ constexpr int tvam_fwd_zs(int Z) { return ((Z + 4) / 4) % 2 
 // some slice collects several DMD rows; PF: staged values per thread (BIN:
 // staged float4s); BIN: the window is staged from the slice-binned patterns
 // (pl.fwd_bin, [angle][column][slice]) with one 16-byte load and store per slot.
-template <int Z, int NC, bool MULTI, int PF, int AB, bool BIN = false>
+//
+// REFR (refracted rays, pl.fwd_refr): every staged column carries two records (its chord's
+// crossing-time offsets / end and its own 1 / d, axis flags and interface weight), the
+// per-angle constants are the (tile, angle) model of the chord index u (tvam_refr_model_kernel),
+// and each voxel visits a per-(tile, angle) number of candidates (the same for the whole
+// workgroup) from ceil(u - w).
+template <int Z, int NC, bool MULTI, int PF, int AB, bool BIN = false, bool REFR = false>
 __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, TvamPlanar pl,
                                                                   const float* __restrict__ pat,
                                                                   float* __restrict__ dose) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int ncm = pl.ncmax;
+    constexpr int RW = REFR ? 2 : 1;  // records (float4) per staged column
     // [2][AB][ncm * ZS + 4] (double buffer of AB angles per barrier), ZS = tvam_fwd_zs(Z);
     // the 4 words past a buffer's slab take the BIN staging's idle slots
     constexpr int ZS = tvam_fwd_zs(Z);
     const int bstride = ncm * ZS + 4;
     float* s_p = reinterpret_cast<float*>(smem);
-    float4* s_r = reinterpret_cast<float4*>(s_p + 2 * AB * bstride);  // [2][AB][ncm]
+    float4* s_r = reinterpret_cast<float4*>(s_p + 2 * AB * bstride);  // [2][AB][ncm * RW]
     // per-angle constants of TVAM_ACH (+2 look-ahead) angles, copied to LDS so the
     // angle loop issues no scalar loads (an s_load's lgkmcnt wait would also
     // drain every outstanding LDS read)
-    float4* s_ang = reinterpret_cast<float4*>(s_r + 2 * AB * ncm);  // [TVAM_ACH + 4][2]
+    float4* s_ang = reinterpret_cast<float4*>(s_r + 2 * AB * ncm * RW);  // [TVAM_ACH + 4][2]
     int* s_cb = reinterpret_cast<int*>(s_ang + 2 * (TVAM_ACH + 4)); // [TVAM_ACH + 4]
     int* s_row = s_cb + (TVAM_ACH + 4);                            // [Z]: the slice's row, -1 none, -2 several
 
@@ -175,13 +191,21 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
     }
     const int ns = pl.ns;
     int tbase = ab;
+    const float4* mdl = REFR ? pl.fwd_model + (size_t)tile * pl.ns * 2 : nullptr;  // this tile's models
     auto load_table = [&](int base) {
         for (int i = threadIdx.x; i < TVAM_ACH + 4; i += TVAM_PB) {
             const int a = base + i;
             if (a < ns) {
-                s_ang[2 * i] = pl.fwd_ang[2 * a];
-                s_ang[2 * i + 1] = pl.fwd_ang[2 * a + 1];
-                s_cb[i] = cbt[a];
+                if (REFR) {
+                    const float4 m1 = mdl[2 * a + 1];
+                    s_ang[2 * i] = mdl[2 * a];
+                    s_ang[2 * i + 1] = m1;
+                    s_cb[i] = __float_as_int(m1.z);
+                } else {
+                    s_ang[2 * i] = pl.fwd_ang[2 * a];
+                    s_ang[2 * i + 1] = pl.fwd_ang[2 * a + 1];
+                    s_cb[i] = cbt[a];
+                }
             }
         }
     };
@@ -250,10 +274,17 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
                 S.pv[q] = v;
             }
         }
-        const int col = cb + (int)threadIdx.x;
-        rv = pl_f4{0.0f, 0.0f, -1.0f, 0.0f};
-        if ((int)threadIdx.x < ncm && (unsigned)col < (unsigned)k.crop_x)
-            rv = reinterpret_cast<const pl_f4*>(pl.vox)[(size_t)al * k.crop_x + col];
+        if (REFR) {  // thread 2 j + h loads record h of window column j
+            const int col = cb + (int)(threadIdx.x >> 1);
+            rv = pl_f4{0.0f, 0.0f, (threadIdx.x & 1) ? 0.0f : -1.0f, 0.0f};
+            if ((int)threadIdx.x < 2 * ncm && (unsigned)col < (unsigned)k.crop_x)
+                rv = reinterpret_cast<const pl_f4*>((threadIdx.x & 1) ? pl.vox2 : pl.vox)[(size_t)al * k.crop_x + col];
+        } else {
+            const int col = cb + (int)threadIdx.x;
+            rv = pl_f4{0.0f, 0.0f, -1.0f, 0.0f};
+            if ((int)threadIdx.x < ncm && (unsigned)col < (unsigned)k.crop_x)
+                rv = reinterpret_cast<const pl_f4*>(pl.vox)[(size_t)al * k.crop_x + col];
+        }
     };
     // buffer b = (double-buffer half) * AB + (angle within the barrier group)
     auto store = [&](int buf, const Stage& S, const pl_f4& rv) {
@@ -266,14 +297,65 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
             for (int q = 0; q < PF; ++q)
                 if (st_jj[q] >= 0) sp[st_off[q]] = S.pv[q];
         }
-        if ((int)threadIdx.x < ncm) reinterpret_cast<pl_f4*>(s_r)[buf * ncm + threadIdx.x] = rv;
+        if ((int)threadIdx.x < ncm * RW) reinterpret_cast<pl_f4*>(s_r)[buf * ncm * RW + threadIdx.x] = rv;
     };
 
     float acc[Z];
 #pragma unroll
     for (int z = 0; z < Z; ++z) acc[z] = 0.0f;
 
+    auto compute_refr = [&](int al, int buf) {
+        const int cb = s_cb[al - tbase];
+        const float* sp = s_p + buf * bstride;
+        const float4* sr = s_r + buf * ncm * 2;
+        // u(lx, ly) = the chord index through the voxel centre (lattice coordinates from the tile corner)
+        const float4 m0 = s_ang[2 * (al - tbase)], m1 = s_ang[2 * (al - tbase) + 1];
+        const int nc = __float_as_int(m1.y);  // uniform over the workgroup
+        const float lx = (float)(threadIdx.x & 15) + 0.5f, ly = (float)(threadIdx.x >> 4) + 0.5f;
+        const float u = fmaf(lx * ly, m0.w, fmaf(ly, m0.z, fmaf(lx, m0.y, m0.x)));
+        int jj0 = (int)ceilf(u - m1.x) - cb;
+        jj0 = min(max(jj0, 0), ncm - nc);
+        for (int c = 0; c < nc; ++c) {
+            float4 q = sr[2 * (jj0 + c)], g = sr[2 * (jj0 + c) + 1];
+            asm volatile("" : "+v"(q.w));
+            const int fl = __float_as_int(g.z);
+            float tnx, tfx, tny, tfy;
+            if (fl & 1) {
+                const float xa = fmaf(X0, g.x, q.x), xb = fmaf(X1, g.x, q.x);
+                tnx = fminf(xa, xb);
+                tfx = fmaxf(xa, xb);
+            } else {  // |d.x| <= 1e-8: the DDA never steps x (q.x = its voxel index)
+                tnx = (float)ix == q.x ? -TVAM_INF : TVAM_INF;
+                tfx = TVAM_INF;
+            }
+            if (fl & 2) {
+                const float ya = fmaf(Y0, g.y, q.y), yb = fmaf(Y1, g.y, q.y);
+                tny = fminf(ya, yb);
+                tfy = fmaxf(ya, yb);
+            } else {
+                tny = (float)iy == q.y ? -TVAM_INF : TVAM_INF;
+                tfy = TVAM_INF;
+            }
+            const float tin = fmaxf(fmaxf(tnx, tny), 0.0f);
+            const float tout = fminf(fminf(tfx, tfy), q.z);
+            const float e = pl_exp2(k.nsig2 * tin) - pl_exp2(k.nsig2 * tout);
+            const float wgt = tout > tin ? e * g.w : 0.0f;  // x the interfaces' transmission (sensor.py:404)
+#pragma unroll
+            for (int z4 = 0; z4 < Z / 4; ++z4) {
+                const float4 p4 = reinterpret_cast<const float4*>(sp + (jj0 + c) * ZS)[z4];
+                acc[4 * z4 + 0] = fmaf(wgt, p4.x, acc[4 * z4 + 0]);
+                acc[4 * z4 + 1] = fmaf(wgt, p4.y, acc[4 * z4 + 1]);
+                acc[4 * z4 + 2] = fmaf(wgt, p4.z, acc[4 * z4 + 2]);
+                acc[4 * z4 + 3] = fmaf(wgt, p4.w, acc[4 * z4 + 3]);
+            }
+        }
+    };
+
     auto compute = [&](int al, int buf) {
+        if constexpr (REFR) {
+            compute_refr(al, buf);
+            return;
+        }
         const int cb = s_cb[al - tbase];
         const float* sp = s_p + buf * bstride;
         const float4* sr = s_r + buf * ncm;
@@ -448,18 +530,133 @@ __global__ __launch_bounds__(256) void tvam_slice_bin_kernel(TvamConsts k, TvamP
 
 size_t tvam_planar_fwd_lds(const TvamPlanar& pl, int Z) {
     const int ab = pl.fwd_ab > 1 ? pl.fwd_ab : 1;
-    return 2 * ab * (((size_t)pl.ncmax * tvam_fwd_zs(Z) + 4) * sizeof(float) + (size_t)pl.ncmax * sizeof(float4)) +
+    const size_t rw = pl.fwd_refr ? 2 : 1;
+    return 2 * ab * (((size_t)pl.ncmax * tvam_fwd_zs(Z) + 4) * sizeof(float) + rw * pl.ncmax * sizeof(float4)) +
            (size_t)(TVAM_ACH + 4) * (2 * sizeof(float4) + sizeof(int)) + (size_t)Z * sizeof(int);
 }
 
 bool tvam_planar_fwd_fits(const TvamPlanar& pl, int Z) {
+    if (pl.fwd_refr)  // two record loaders per window column; the binned staging only
+        return 2 * pl.ncmax <= TVAM_PB && pl.ncmax * (Z / 4) <= 2 * TVAM_PB && pl.fwd_nc >= 1 &&
+               pl.fwd_nc <= pl.ncmax && tvam_planar_fwd_lds(pl, Z) <= 64 * 1024;
     return pl.ncmax <= TVAM_PB && pl.ncmax * Z <= TVAM_PF * TVAM_PB && pl.fwd_nc >= 1 && pl.fwd_nc <= 4 &&
            pl.fwd_nc <= pl.ncmax;
+}
+
+// ---------------------------------------------------------------------------
+// Chord-index model of the refracted voxel-driven forward.  Behind a refracting
+// vial the medium chords of one angle's columns are no longer parallel, but they
+// do not cross inside the medium (the plan checks the bound that rests on it), so
+// the chord index u(p) -- c where chord c passes through p, linear between
+// neighbouring chords in their signed distances -- is monotone across the beam and
+// a line meets a voxel iff u at its corners brackets the line's index.  One thread
+// per (16x16 tile, angle) evaluates u exactly (bisection over the angle's chords)
+// at the tile's 17x17 voxel corners, fits the bilinear model through the tile
+// corners, and stores the half width w >= |u(corner) - model(centre)| of every
+// voxel (model error at the corners + the model's own half-voxel spread), the
+// candidate count and the staged window.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float refr_side(const float4* __restrict__ ch, int c, float px, float py) {
+    const float4 q = ch[c];
+    return (px - q.x) * q.w - (py - q.y) * q.z;
+}
+
+__device__ float refr_u(const float4* __restrict__ ch, int c0, int c1, float px, float py) {
+    const float s0 = refr_side(ch, c0, px, py), s1 = refr_side(ch, c1, px, py);
+    if ((s0 > 0.0f) == (s1 > 0.0f)) {  // outside the beam: extrapolate from the nearer edge pair
+        if (fabsf(s0) <= fabsf(s1)) {
+            const float sb = refr_side(ch, c0 + 1, px, py);
+            return (float)c0 + s0 / (s0 - sb);
+        }
+        const float sa = refr_side(ch, c1 - 1, px, py);
+        return (float)(c1 - 1) + sa / (sa - s1);
+    }
+    int lo = c0, hi = c1;
+    float slo = s0, shi = s1;
+    while (hi - lo > 1) {
+        const int mid = (lo + hi) >> 1;
+        const float sm = refr_side(ch, mid, px, py);
+        if ((sm > 0.0f) == (s0 > 0.0f)) {
+            lo = mid;
+            slo = sm;
+        } else {
+            hi = mid;
+            shi = sm;
+        }
+    }
+    return (float)lo + slo / (slo - shi);
+}
+
+__global__ __launch_bounds__(64) void tvam_refr_model_kernel(TvamConsts k, TvamPlanar pl, const int2* __restrict__ range,
+                                                             float4* __restrict__ model, int32_t* __restrict__ need) {
+    const int ntx = (k.res[0] + 15) >> 4, nty = (k.res[1] + 15) >> 4;
+    const int64_t n = (int64_t)ntx * nty * pl.ns;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const int tile = (int)(i / pl.ns), al = (int)(i - (int64_t)tile * pl.ns);
+        const int bx = tile % ntx, by = tile / ntx;
+        const int2 rg = range[al];
+        float4* m = model + 2 * i;
+        if (rg.y - rg.x < 1) {  // fewer than two chords reach the medium: no candidates
+            m[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            m[1] = make_float4(0.0f, __int_as_float(0), __int_as_float(0), 0.0f);
+            need[i] = 1;
+            continue;
+        }
+        const float4* ch = pl.chord + (size_t)al * k.crop_x;
+        auto uat = [&](int li, int lj) {
+            const float px = k.bmin[0] + (float)(bx * 16 + li) * k.h[0];
+            const float py = k.bmin[1] + (float)(by * 16 + lj) * k.h[1];
+            return refr_u(ch, rg.x, rg.y, px, py);
+        };
+        const float u00 = uat(0, 0), u10 = uat(16, 0), u01 = uat(0, 16), u11 = uat(16, 16);
+        const float4 m0 = make_float4(u00, (u10 - u00) * 0.0625f, (u01 - u00) * 0.0625f,
+                                      (u11 - u10 - u01 + u00) * 0.00390625f);
+        auto model_at = [&](float lx, float ly) { return fmaf(lx * ly, m0.w, fmaf(ly, m0.z, fmaf(lx, m0.y, m0.x))); };
+        float err = 0.0f;
+        for (int lj = 0; lj <= 16; ++lj)
+            for (int li = 0; li <= 16; ++li) err = fmaxf(err, fabsf(uat(li, lj) - model_at((float)li, (float)lj)));
+        // the model's spread from a voxel centre to its corners (half a voxel along each axis)
+        float spread = 0.0f;
+        for (int cy = 0; cy <= 16; cy += 16)
+            for (int cx = 0; cx <= 16; cx += 16)
+                spread = fmaxf(spread, fabsf(m0.y + m0.w * (float)cy) + fabsf(m0.z + m0.w * (float)cx));
+        const float w = err + 0.5f * spread + 2e-3f + 1e-4f * fabsf(u00);  // + fp32 rounding of u itself
+        const int nc = (int)floorf(2.0f * w + 1e-3f) + 1;
+        float umin = TVAM_INF, umax = -TVAM_INF;
+        for (int cy = 0; cy < 2; ++cy)
+            for (int cx = 0; cx < 2; ++cx) {
+                const float u = model_at(cx ? 15.5f : 0.5f, cy ? 15.5f : 0.5f);
+                umin = fminf(umin, u);
+                umax = fmaxf(umax, u);
+            }
+        int cb = (int)floorf(umin - w) - 1;
+        const int ce = (int)ceilf(umax + w) + 1;
+        need[i] = ce - cb + 1;
+        m[0] = m0;
+        m[1] = make_float4(w, __int_as_float(nc), __int_as_float(cb), 0.0f);
+    }
+}
+
+hipError_t tvam_launch_refr_model(const TvamConsts& k, const TvamPlanar& pl, const int2* range, float4* model,
+                                  int32_t* need, hipStream_t stream) {
+    const int64_t n = (int64_t)((k.res[0] + 15) / 16) * ((k.res[1] + 15) / 16) * pl.ns;
+    const unsigned g = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n + 63) / 64, 1 << 20));
+    hipLaunchKernelGGL(tvam_refr_model_kernel, dim3(g), dim3(64), 0, stream, k, pl, range, model, need);
+    return hipGetLastError();
 }
 
 template <int Z, int NC>
 static void launch_fwd(dim3 grid, size_t lds, hipStream_t stream, const TvamConsts& k, const TvamPlanar& pl,
                        const float* pat, float* dose) {
+    if (pl.fwd_refr) {  // refracted chords: binned staging, 2 angles per barrier, candidates per (tile, angle)
+        if (pl.fwd_pf == 1)
+            hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, 2, false, 1, 2, true, true>), grid, dim3(TVAM_PB), lds, stream,
+                               k, pl, pat, dose);
+        else
+            hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, 2, false, 2, 2, true, true>), grid, dim3(TVAM_PB), lds, stream,
+                               k, pl, pat, dose);
+        return;
+    }
     if (pl.fwd_bin && pl.fwd_pf == 1 && pl.fwd_ab == 1)
         hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 1, 1, true>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
     else if (pl.fwd_bin && pl.fwd_pf == 1)
@@ -483,6 +680,10 @@ static void launch_fwd(dim3 grid, size_t lds, hipStream_t stream, const TvamCons
 template <int Z>
 static hipError_t launch_fwd_z(dim3 grid, size_t lds, hipStream_t stream, const TvamConsts& k, const TvamPlanar& pl,
                                const float* pat, float* dose) {
+    if (pl.fwd_refr) {
+        launch_fwd<Z, 2>(grid, lds, stream, k, pl, pat, dose);
+        return hipGetLastError();
+    }
     switch (pl.fwd_nc) {
         case 1:
         case 2: launch_fwd<Z, 2>(grid, lds, stream, k, pl, pat, dose); break;

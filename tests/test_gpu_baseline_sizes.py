@@ -18,6 +18,7 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
+from drtvam_amd import _abi
 from drtvam_amd.configs import (benchy_index_matched, cylindrical_refraction, cylindrical_scattering,
                                 desc_from_config, square_occluded)
 from drtvam_amd.engine import Projection
@@ -52,10 +53,18 @@ def test_config2_every_angle(oracle):
 
 
 def test_config3_full_forward_fixed_point(oracle):
+    """Both planar forwards of config 3 against one oracle run: the voxel-driven one (per-(tile,
+    angle) chord-index models) and the ray-driven one, whose int32 fixed-point scale rests on a
+    beam-compression bound over all 400 angles."""
     N = 400
     d = desc_from_config(cylindrical_refraction(N=N, angles=N))
     n = N * N * N
     pat = np.random.default_rng(1).uniform(0.0, 0.1, n).astype(np.float32)
+    proj = Projection(d, DEV)
+    assert proj.planar and proj.planar_forward  # the voxel-driven forward over refracted chords
+    vox = proj.forward(torch.as_tensor(pat, device=DEV), None, 1, 0).cpu().numpy()[..., 0]
+    proj.close()
+    d.flags |= _abi.FLAG_RAY_FWD
     proj = Projection(d, DEV)
     assert proj.planar and not proj.planar_forward  # the ray-driven planar forward
     got = proj.forward(torch.as_tensor(pat, device=DEV), None, 1, 0).cpu().numpy()[..., 0]
@@ -66,6 +75,9 @@ def test_config3_full_forward_fixed_point(oracle):
     h = [(d.bbox_max[a] - d.bbox_min[a]) / d.film_res[a] for a in range(3)]
     inv_vol = 1.0 / (h[0] * h[1] * h[2])
     peak = float(np.abs(ref).max()) / inv_vol * scale
+    ev = rel_l2(vox, ref)
+    print(f"config 3 voxel-driven forward rel-L2 {ev:.3e}")
+    assert ev < RTOL
     e = rel_l2(got, ref)
     print(f"config 3 forward rel-L2 {e:.3e}, fixed-point scale 2^{np.log2(scale):.0f}, "
           f"largest sum {peak:.3e} of 2^31 ({peak / 2.0 ** 31:.3f}), visits {visits}")
@@ -86,7 +98,7 @@ def test_config3_adjoint_angle_shard(oracle):
     pix = (a0 * N * N + np.arange(n)).astype(np.uint32)
     proj = Projection(d, DEV)
     got = proj.forward(torch.as_tensor(pat, device=DEV), None, 1, 0).cpu().numpy()[..., 0]
-    assert proj.fwd_scale()[1]
+    assert proj.planar_forward
     ref, _ = oracle.forward(dfull, pat, active_pixels=pix, nthreads=THREADS)
     assert rel_l2(got, ref) < RTOL
     G = rng.uniform(-1, 1, (N, N, N)).astype(np.float32)

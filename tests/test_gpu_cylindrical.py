@@ -3,9 +3,11 @@
 The cylindrical container refracts every projector ray twice (air|glass at
 r_ext, glass|resin at r_int) before the medium segment, so rays of one angle
 are no longer parallel.  The kernels take each ray's refracted direction and
-interface weight from its record: the forward runs the per-ray tile kernel
-(slot lists from host-traced refracted chords), the adjoint the planar
-Z-sharing kernel under regular sampling.  Same tolerance as the index-matched
+interface weight from its record.  Under regular sampling the forward is
+voxel-driven (each voxel's candidate chords from the per-(tile, angle) chord-index
+model, tvam_refr_model_kernel) or, with FLAG_RAY_FWD, ray-driven with Z-slice
+sharing; jittered rays run the per-ray tile kernels (slot lists from host-traced
+refracted chords); the adjoint is the planar Z-sharing kernel under regular sampling.  Same tolerance as the index-matched
 parity tests (1e-4 relative L2 against the fp64-accumulating oracle).
 """
 import numpy as np
@@ -27,11 +29,13 @@ def rel_l2(a, b):
     return float(np.linalg.norm(a - b) / max(np.linalg.norm(b), 1e-300))
 
 
-def make(N, A, regular=True, spp=1, tile=0, planar=True, **kw):
+def make(N, A, regular=True, spp=1, tile=0, planar=True, ray_fwd=False, **kw):
     cfg = cylindrical_refraction(N=N, angles=A, regular_sampling=regular, spp=spp, **kw)
     d = desc_from_config(cfg, tile=tile)
     if not planar:
         d.flags |= _abi.FLAG_NO_PLANAR
+    if ray_fwd:
+        d.flags |= _abi.FLAG_RAY_FWD
     return d
 
 
@@ -45,6 +49,10 @@ CASES = [
     dict(N=33, A=17, r_int=5.5, r_ext=6.5),    # tube cuts the grid: grid corners outside the medium
     dict(N=32, A=16, r_int=5.5, r_ext=6.5, regular=False, spp=2),
     dict(N=24, A=12, vial_ior=1.9, medium_ior=1.33),  # strong refraction, total internal reflection at r_int
+    dict(N=33, A=24, ray_fwd=True),            # the ray-driven planar forward
+    dict(N=40, A=30, tile=7, ray_fwd=True),
+    dict(N=64, A=48, xres=32),                 # 2 DMD columns per voxel: wide candidate windows
+    dict(N=48, A=36, zres=24),                 # two DMD rows per slice (binned sums)
 ]
 
 
@@ -56,7 +64,12 @@ def _id(c):
 def test_forward_matches_oracle(oracle, case):
     case = dict(case)
     spp = case.get("spp", 1)
+    xres, zres = case.pop("xres", None), case.pop("zres", None)
     d = make(**case)
+    if xres:
+        d.film_res[0] = d.film_res[1] = xres
+    if zres:
+        d.film_res[2] = zres
     n = d.n_patterns * d.crop_y * d.crop_x
     pat = np.random.default_rng(0).uniform(0.0, 0.1, n).astype(np.float32)
     ref, visits = oracle.forward(d, pat, spp=spp, seed=5, nthreads=8)
@@ -65,7 +78,12 @@ def test_forward_matches_oracle(oracle, case):
     got = proj.forward(torch.as_tensor(pat, device="cuda:0"), None, spp, 5)
     torch.cuda.synchronize()
     got = got.cpu().numpy()[..., 0]
-    assert not proj.planar_forward  # refracted rays: per-ray tile forward
+    # the voxel-driven forward serves every planar plan but the ray-driven variant's
+    # (total internal reflection can leave a gap in an angle's chords: ray-driven then)
+    if proj.planar and not case.get("ray_fwd") and "vial_ior" not in case:
+        assert proj.planar_forward
+    if case.get("ray_fwd") or not proj.planar:
+        assert not proj.planar_forward
     # planar adjoint: regular sampling and every row's spawn offset row-independent (|z| <= 0.7 r_int)
     assert proj.planar == (case.get("regular", True) and case.get("planar", True) and 5.0 <= 0.7 * case.get("r_int", 8.0))
     assert rel_l2(got, ref) < RTOL_L2
@@ -78,7 +96,12 @@ def test_forward_matches_oracle(oracle, case):
 def test_adjoint_matches_oracle(oracle, case):
     case = dict(case)
     spp = case.get("spp", 1)
+    xres, zres = case.pop("xres", None), case.pop("zres", None)
     d = make(**case)
+    if xres:
+        d.film_res[0] = d.film_res[1] = xres
+    if zres:
+        d.film_res[2] = zres
     n = d.n_patterns * d.crop_y * d.crop_x
     G = np.random.default_rng(1).uniform(-1, 1, (d.film_res[2], d.film_res[1], d.film_res[0])).astype(np.float32)
     ref, _ = oracle.adjoint(d, G, spp=spp, seed=9, nthreads=8)
