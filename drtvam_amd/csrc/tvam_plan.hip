@@ -573,6 +573,21 @@ static int refr_fwd_setup(tvam_plan* p, const std::vector<int32_t>& off) {
         std::memcpy(&cb, &mdl[2 * i + 1].z, sizeof(int));
         (void)cb;
     }
+    if (env_int("TVAM_DEBUG_REFR", 0)) {
+        std::vector<int64_t> hist(16, 0);
+        double wsum = 0.0;
+        for (size_t i = 0; i < nm; ++i) {
+            int nc;
+            std::memcpy(&nc, &mdl[2 * i + 1].y, sizeof(int));
+            hist[std::min(nc, 15)]++;
+            wsum += mdl[2 * i + 1].x;
+        }
+        std::fprintf(stderr, "refr forward: window %d columns, candidates max %d, mean half width %.3f; nc histogram:", ncm,
+                     ncmax_c, wsum / (double)nm);
+        for (int i = 0; i < 16; ++i)
+            if (hist[i]) std::fprintf(stderr, " %d:%lld", i, (long long)hist[i]);
+        std::fprintf(stderr, "\n");
+    }
     TvamPlanar save = p->pl;
     p->pl.fwd_refr = 1;
     p->pl.ncmax = ncm;
