@@ -575,15 +575,17 @@ static int refr_fwd_setup(tvam_plan* p, const std::vector<int32_t>& off) {
     }
     if (env_int("TVAM_DEBUG_REFR", 0)) {
         std::vector<int64_t> hist(16, 0);
-        double wsum = 0.0;
+        double wsum = 0.0, esum = 0.0, emax = 0.0;
         for (size_t i = 0; i < nm; ++i) {
             int nc;
             std::memcpy(&nc, &mdl[2 * i + 1].y, sizeof(int));
             hist[std::min(nc, 15)]++;
             wsum += mdl[2 * i + 1].x;
+            esum += mdl[2 * i + 1].w;
+            emax = std::max(emax, (double)mdl[2 * i + 1].w);
         }
-        std::fprintf(stderr, "refr forward: window %d columns, candidates max %d, mean half width %.3f; nc histogram:", ncm,
-                     ncmax_c, wsum / (double)nm);
+        std::fprintf(stderr, "refr forward: window %d columns, candidates max %d, mean half width %.3f, model error "
+                     "mean %.3f max %.3f; nc histogram:", ncm, ncmax_c, wsum / (double)nm, esum / (double)nm, emax);
         for (int i = 0; i < 16; ++i)
             if (hist[i]) std::fprintf(stderr, " %d:%lld", i, (long long)hist[i]);
         std::fprintf(stderr, "\n");

@@ -274,11 +274,13 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
                 S.pv[q] = v;
             }
         }
-        if (REFR) {  // thread 2 j + h loads record h of window column j
-            const int col = cb + (int)(threadIdx.x >> 1);
-            rv = pl_f4{0.0f, 0.0f, (threadIdx.x & 1) ? 0.0f : -1.0f, 0.0f};
+        if (REFR) {  // thread h ncm + j loads record h of window column j (stored [2][ncm]: 16-byte
+                     // column stride in either half, so 16 neighbouring columns' reads hit distinct banks)
+            const int h = (int)threadIdx.x >= ncm ? 1 : 0;
+            const int col = cb + (int)threadIdx.x - h * ncm;
+            rv = pl_f4{0.0f, 0.0f, h ? 0.0f : -1.0f, 0.0f};
             if ((int)threadIdx.x < 2 * ncm && (unsigned)col < (unsigned)k.crop_x)
-                rv = reinterpret_cast<const pl_f4*>((threadIdx.x & 1) ? pl.vox2 : pl.vox)[(size_t)al * k.crop_x + col];
+                rv = reinterpret_cast<const pl_f4*>(h ? pl.vox2 : pl.vox)[(size_t)al * k.crop_x + col];
         } else {
             const int col = cb + (int)threadIdx.x;
             rv = pl_f4{0.0f, 0.0f, -1.0f, 0.0f};
@@ -310,45 +312,44 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
         const float4* sr = s_r + buf * ncm * 2;
         // u(lx, ly) = the chord index through the voxel centre (lattice coordinates from the tile corner)
         const float4 m0 = s_ang[2 * (al - tbase)], m1 = s_ang[2 * (al - tbase) + 1];
-        const int nc = __float_as_int(m1.y);  // uniform over the workgroup
+        const int nc = __builtin_amdgcn_readfirstlane(__float_as_int(m1.y));  // uniform over the workgroup, >= 2
         const float lx = (float)(threadIdx.x & 15) + 0.5f, ly = (float)(threadIdx.x >> 4) + 0.5f;
         const float u = fmaf(lx * ly, m0.w, fmaf(ly, m0.z, fmaf(lx, m0.y, m0.x)));
-        int jj0 = (int)ceilf(u - m1.x) - cb;
+        const float hv = 0.5f * (fabsf(fmaf(m0.w, ly, m0.y)) + fabsf(fmaf(m0.w, lx, m0.z))) + 0.25f * fabsf(m0.w);
+        int jj0 = (int)ceilf(u - hv - m1.x) - cb;  // the voxel's first candidate (m1.x: model error bound)
         jj0 = min(max(jj0, 0), ncm - nc);
-        for (int c = 0; c < nc; ++c) {
-            float4 q = sr[2 * (jj0 + c)], g = sr[2 * (jj0 + c) + 1];
-            asm volatile("" : "+v"(q.w));
+        // candidate c's weight (exact slab intersection with its own chord; 0 when it misses the voxel)
+        auto weight = [&](int jc) {
+            const float4 q = sr[jc], g = sr[ncm + jc];
             const int fl = __float_as_int(g.z);
-            float tnx, tfx, tny, tfy;
-            if (fl & 1) {
-                const float xa = fmaf(X0, g.x, q.x), xb = fmaf(X1, g.x, q.x);
-                tnx = fminf(xa, xb);
-                tfx = fmaxf(xa, xb);
-            } else {  // |d.x| <= 1e-8: the DDA never steps x (q.x = its voxel index)
-                tnx = (float)ix == q.x ? -TVAM_INF : TVAM_INF;
-                tfx = TVAM_INF;
-            }
-            if (fl & 2) {
-                const float ya = fmaf(Y0, g.y, q.y), yb = fmaf(Y1, g.y, q.y);
-                tny = fminf(ya, yb);
-                tfy = fmaxf(ya, yb);
-            } else {
-                tny = (float)iy == q.y ? -TVAM_INF : TVAM_INF;
-                tfy = TVAM_INF;
-            }
+            const float xa = fmaf(X0, g.x, q.x), xb = fmaf(X1, g.x, q.x);
+            const float ya = fmaf(Y0, g.y, q.y), yb = fmaf(Y1, g.y, q.y);
+            // |d| <= 1e-8 on an axis: the DDA never steps it (q = its voxel index)
+            const float tnx = (fl & 1) ? fminf(xa, xb) : ((float)ix == q.x ? -TVAM_INF : TVAM_INF);
+            const float tfx = (fl & 1) ? fmaxf(xa, xb) : TVAM_INF;
+            const float tny = (fl & 2) ? fminf(ya, yb) : ((float)iy == q.y ? -TVAM_INF : TVAM_INF);
+            const float tfy = (fl & 2) ? fmaxf(ya, yb) : TVAM_INF;
             const float tin = fmaxf(fmaxf(tnx, tny), 0.0f);
             const float tout = fminf(fminf(tfx, tfy), q.z);
             const float e = pl_exp2(k.nsig2 * tin) - pl_exp2(k.nsig2 * tout);
-            const float wgt = tout > tin ? e * g.w : 0.0f;  // x the interfaces' transmission (sensor.py:404)
+            return tout > tin ? e * g.w : 0.0f;  // x the interfaces' transmission (sensor.py:404)
+        };
+        auto accumulate = [&](int jc, float wgt) {
 #pragma unroll
             for (int z4 = 0; z4 < Z / 4; ++z4) {
-                const float4 p4 = reinterpret_cast<const float4*>(sp + (jj0 + c) * ZS)[z4];
+                const float4 p4 = reinterpret_cast<const float4*>(sp + jc * ZS)[z4];
                 acc[4 * z4 + 0] = fmaf(wgt, p4.x, acc[4 * z4 + 0]);
                 acc[4 * z4 + 1] = fmaf(wgt, p4.y, acc[4 * z4 + 1]);
                 acc[4 * z4 + 2] = fmaf(wgt, p4.z, acc[4 * z4 + 2]);
                 acc[4 * z4 + 3] = fmaf(wgt, p4.w, acc[4 * z4 + 3]);
             }
-        }
+        };
+        // every (tile, angle) has >= 2 candidates (the model kernel's floor): the first two run
+        // straight-line like the index-matched forward's pair, the rest in a (uniform) loop
+        const float w0 = weight(jj0), w1 = weight(jj0 + 1);
+        accumulate(jj0, w0);
+        accumulate(jj0 + 1, w1);
+        for (int c = 2; c < nc; ++c) accumulate(jj0 + c, weight(jj0 + c));
     };
 
     auto compute = [&](int al, int buf) {
@@ -620,8 +621,19 @@ __global__ __launch_bounds__(64) void tvam_refr_model_kernel(TvamConsts k, TvamP
         for (int cy = 0; cy <= 16; cy += 16)
             for (int cx = 0; cx <= 16; cx += 16)
                 spread = fmaxf(spread, fabsf(m0.y + m0.w * (float)cy) + fabsf(m0.z + m0.w * (float)cx));
-        const float w = err + 0.5f * spread + 2e-3f + 1e-4f * fabsf(u00);  // + fp32 rounding of u itself
-        const int nc = (int)floorf(2.0f * w + 1e-3f) + 1;
+        const float ue = err + 2e-3f + 1e-4f * fabsf(u00);  // model error + fp32 rounding of u itself
+        const float w = ue + 0.5f * spread;
+        // candidates of a voxel: the integers in [u - hv - ue, u + hv + ue], u the model at its centre and
+        // hv = 0.5 (|du/dlx| + |du/dly|) + |d2u/dlx dly| / 4 its half range at the corners; the forward
+        // runs the largest count of the tile's voxels (uniform over the workgroup)
+        int nc = 2;  // the forward runs two candidates straight-line
+        for (int vy = 0; vy < 16; ++vy)
+            for (int vx = 0; vx < 16; ++vx) {
+                const float lx = (float)vx + 0.5f, ly = (float)vy + 0.5f;
+                const float u = model_at(lx, ly);
+                const float hv = 0.5f * (fabsf(fmaf(m0.w, ly, m0.y)) + fabsf(fmaf(m0.w, lx, m0.z))) + 0.25f * fabsf(m0.w);
+                nc = max(nc, (int)floorf(u + hv + ue) - (int)ceilf(u - hv - ue) + 1);
+            }
         float umin = TVAM_INF, umax = -TVAM_INF;
         for (int cy = 0; cy < 2; ++cy)
             for (int cx = 0; cx < 2; ++cx) {
@@ -633,7 +645,7 @@ __global__ __launch_bounds__(64) void tvam_refr_model_kernel(TvamConsts k, TvamP
         const int ce = (int)ceilf(umax + w) + 1;
         need[i] = ce - cb + 1;
         m[0] = m0;
-        m[1] = make_float4(w, __int_as_float(nc), __int_as_float(cb), 0.0f);
+        m[1] = make_float4(ue, __int_as_float(nc), __int_as_float(cb), err);  // .w: diagnostics only
     }
 }
 

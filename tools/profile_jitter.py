@@ -1,6 +1,7 @@
-"""Forward + adjoint of a jittered BASELINE config on an angle shard (per-ray tile kernels), for
-rocprofv3 counter passes.  usage: python tools/profile_jitter.py CONFIG N ANGLES_IN_SHARD [reps]
-CONFIG 4: cylindrical scattering (16 spp); 5: square vial + occluder (4 spp); 3j: config 3 jittered."""
+"""Forward + adjoint of a BASELINE config on an angle shard, for rocprofv3 counter passes.
+usage: python tools/profile_jitter.py CONFIG N ANGLES_IN_SHARD [reps]
+CONFIG 2: index matched; 3: cylindrical vial (regular sampling, planar kernels); 4: cylindrical
+scattering (16 spp); 4a: its first segments only (albedo 0); 5: square vial + occluder (4 spp)."""
 import os
 import sys
 import time
@@ -10,7 +11,8 @@ import torch
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from drtvam_amd import _abi  # noqa: E402
-from drtvam_amd.configs import cylindrical_scattering, desc_from_config, square_occluded  # noqa: E402
+from drtvam_amd.configs import (benchy_index_matched, cylindrical_refraction, cylindrical_scattering,  # noqa: E402
+                                desc_from_config, square_occluded)
 from drtvam_amd.engine import Projection  # noqa: E402
 
 
@@ -19,6 +21,10 @@ def main():
     reps = int(sys.argv[4]) if len(sys.argv) > 4 else 1
     if cfgname == "5":
         cfg = square_occluded(N=N, angles=N)
+    elif cfgname == "2":
+        cfg = benchy_index_matched(N=N, angles=N)
+    elif cfgname == "3":
+        cfg = cylindrical_refraction(N=N, angles=N)
     else:  # "4": config 4; "4a": its first segments only (albedo 0)
         cfg = cylindrical_scattering(N=N, angles=N)
         if cfgname == "4a":
