@@ -348,7 +348,8 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     // adjoint slices per workgroup: 8 (one march gathers 8 slices: measured 5.2 -> 3.9 ms on
     // config 2 with 1024-thread workgroups and 45 x 45 tiles), 4 for films under 8 slices
     p->planar_az = env_int("TVAM_PLANAR_ADJ_Z", k.nz >= 8 ? 8 : 4);
-    if (p->planar_fz != 8 && p->planar_fz != 16 && p->planar_fz != 24 && p->planar_fz != 28 && p->planar_fz != 32)
+    if (p->planar_fz != 8 && p->planar_fz != 16 && p->planar_fz != 24 && p->planar_fz != 28 && p->planar_fz != 32 &&
+        p->planar_fz != 40 && p->planar_fz != 52)
         p->planar_fz = 0;
     if (p->planar_az != 4 && p->planar_az != 8 && p->planar_az != 16) p->planar_az = 4;
     const int ns = (int)cs.size();
@@ -501,20 +502,28 @@ static int fwd_buffers(tvam_plan* p) {
 
 // Slices per workgroup of the voxel-driven forward: the fewest padded slice-passes
 // ceil(nz / Z) * (Z + 4) (the +4 prices the per-angle candidate geometry shared by the Z
-// slices) among the depths whose staging fits.  Returns false when none fits.
+// slices; +10 % for the deep slabs' lower occupancy) among the depths whose staging fits:
+// Z = 32 on 400-slice films, 52 on the 50-slice slabs of 8 ranks (one chunk instead of two of
+// 28: forward 0.546 -> 0.477 ms per rank).  Returns false when none fits.
 static int choose_fwd_z(tvam_plan* p) {
     const TvamConsts& k = p->k;
     if (p->planar_fz == 0) {
         int best = 8;
         int64_t bcost = INT64_MAX;
-        for (int Z : {32, 28, 24, 16, 8}) {
-            if (!tvam_planar_fwd_fits(p->pl, Z)) continue;
-            const int64_t cost = (int64_t)((k.nz + Z - 1) / Z) * (Z + 4);
+        const bool deep = env_int("TVAM_FWD_BIN", 1) != 0 && env_int("TVAM_FWD_DEEP", 1) != 0;
+        for (int Z : {52, 40, 32, 28, 24, 16, 8}) {
+            if ((Z > 32 && !deep) || !tvam_planar_fwd_fits(p->pl, Z)) continue;
+            // deep slabs (Z > 32: 4 instead of 5 waves per SIMD) measured ~4 % slower per slice at 400^3
+            const int64_t cost = (int64_t)((k.nz + Z - 1) / Z) * (Z + 4) * (Z > 32 ? 11 : 10);
             if (cost < bcost) bcost = cost, best = Z;
         }
         p->planar_fz = best;
     }
-    while (p->planar_fz > 8 && !tvam_planar_fwd_fits(p->pl, p->planar_fz)) p->planar_fz /= 2;
+    for (int Z : {52, 40, 32, 28, 24, 16, 8})  // the deepest instantiated depth <= the choice that fits
+        if (Z <= p->planar_fz && tvam_planar_fwd_fits(p->pl, Z)) {
+            p->planar_fz = Z;
+            break;
+        }
     return tvam_planar_fwd_fits(p->pl, p->planar_fz) ? 1 : 0;
 }
 

@@ -540,6 +540,9 @@ bool tvam_planar_fwd_fits(const TvamPlanar& pl, int Z) {
     if (pl.fwd_refr)  // two record loaders per window column; the binned staging only
         return 2 * pl.ncmax <= TVAM_PB && pl.ncmax * (Z / 4) <= 2 * TVAM_PB && pl.fwd_nc >= 1 &&
                pl.fwd_nc <= pl.ncmax && tvam_planar_fwd_lds(pl, Z) <= 64 * 1024;
+    if (Z > 32)  // deep slabs: the binned staging only (at most 2 float4 per thread and angle)
+        return pl.ncmax <= TVAM_PB && pl.ncmax * (Z / 4) <= 2 * TVAM_PB && pl.fwd_nc >= 1 && pl.fwd_nc <= 4 &&
+               pl.fwd_nc <= pl.ncmax;
     return pl.ncmax <= TVAM_PB && pl.ncmax * Z <= TVAM_PF * TVAM_PB && pl.fwd_nc >= 1 && pl.fwd_nc <= 4 &&
            pl.fwd_nc <= pl.ncmax;
 }
@@ -669,6 +672,15 @@ static void launch_fwd(dim3 grid, size_t lds, hipStream_t stream, const TvamCons
                                k, pl, pat, dose);
         return;
     }
+    if constexpr (Z > 32) {  // deep slabs (thin-slab shards, 400-slice films in 10 chunks): binned staging only
+        if (pl.fwd_pf == 1)
+            hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 1, 2, true>), grid, dim3(TVAM_PB), lds, stream, k, pl,
+                               pat, dose);
+        else
+            hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 2, 2, true>), grid, dim3(TVAM_PB), lds, stream, k, pl,
+                               pat, dose);
+        return;
+    }
     if (pl.fwd_bin && pl.fwd_pf == 1 && pl.fwd_ab == 1)
         hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 1, 1, true>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
     else if (pl.fwd_bin && pl.fwd_pf == 1)
@@ -738,6 +750,8 @@ static hipError_t tvam_launch_fwd_planar_z(dim3 grid, size_t lds, hipStream_t st
         case 24: return launch_fwd_z<24>(grid, lds, stream, k, pl, pat, dose);
         case 28: return launch_fwd_z<28>(grid, lds, stream, k, pl, pat, dose);
         case 32: return launch_fwd_z<32>(grid, lds, stream, k, pl, pat, dose);
+        case 40: return pl.fwd_bin ? launch_fwd_z<40>(grid, lds, stream, k, pl, pat, dose) : hipErrorInvalidValue;
+        case 52: return pl.fwd_bin ? launch_fwd_z<52>(grid, lds, stream, k, pl, pat, dose) : hipErrorInvalidValue;
         default: return hipErrorInvalidValue;
     }
 }

@@ -287,3 +287,18 @@ def test_slab_plan_matches_full_film(planar, band):
     gs = ps.adjoint(torch.as_tensor(G[z0:z1].copy(), device="cuda:0"), pats.size, None, 1, 0).cpu().numpy()
     ref = gfull.reshape(A, N, N)[:, r0:r1, :].reshape(-1)
     assert rel_l2(gs, ref) < 1e-5
+
+
+@pytest.mark.parametrize("Z", [40, 52])
+def test_deep_slab_forward(oracle, monkeypatch, Z):
+    """The deep-slab voxel-driven forward (Z = 40 / 52 slices per workgroup, binned staging; the
+    plan picks 52 for the 50-slice slabs of 8 z-slab ranks) against the oracle, including a
+    partial last chunk (60 slices)."""
+    monkeypatch.setenv("TVAM_PLANAR_FWD_Z", str(Z))
+    d = make(N=60, A=30)
+    n = d.n_patterns * d.crop_y * d.crop_x
+    pat = np.random.default_rng(11).uniform(0.0, 0.1, n).astype(np.float32)
+    ref, _ = oracle.forward(d, pat, nthreads=8)
+    got, proj = gpu_forward(d, pat)
+    assert proj.planar_forward
+    assert rel_l2(got, ref) < RTOL_L2
