@@ -770,7 +770,8 @@ void mark_tiles(const TileGrid& g, const CylChord& ch, double m, F&& mark) {
                 t1 = std::min(t1, b);
                 return t0 <= t1;
             };
-            if (clip(ch.ax, dx, bx0, bx1) && clip(ch.ay, dy, by0, by1)) mark(ty * g.ntx + tx);
+            if (clip(ch.ax, dx, bx0, bx1) && clip(ch.ay, dy, by0, by1))
+                mark(ty * g.ntx + tx, (t1 - t0) * std::hypot(dx, dy));  // the chord's length in the (grown) tile
         }
 }
 }  // namespace
@@ -840,20 +841,32 @@ static float cyl_rays_per_voxel(const tvam_desc& d, const TvamConsts& k, const s
     return (float)((double)ns * worst * wmax * 1.01);
 }
 
+// Within each angle a tile's slots are ordered by decreasing predicted in-tile chord length
+// (the longest of the column's traced sub-pixel chords): the per-ray tile kernels' waves take 64
+// consecutive slots of one angle, which then march similar lengths (the columns of an angle
+// crossing a tile have a trapezoid of lengths; in column order every wave held both ramps and the
+// long middle), while neighbouring lanes still read neighbouring columns' records.
 static void cyl_slot_lists(const tvam_desc& d, const TvamConsts& k, const std::vector<float2>& cs, int tsx, int tsy,
                            int ntx, int nty, double marg, std::vector<std::vector<uint32_t>>& per_tile) {
     const TileGrid g{(double)k.bmin[0], (double)k.bmin[1], tsx * (double)k.h[0], tsy * (double)k.h[1], ntx, nty};
     const double hmin = std::min(k.h[0], k.h[1]);
     per_tile.assign((size_t)ntx * nty, {});
+    std::vector<std::vector<float>> len_of((size_t)ntx * nty);
     std::vector<uint32_t> last((size_t)ntx * nty, 0xffffffffu);
+    std::vector<size_t> angle_start((size_t)ntx * nty, 0);
     const int ns = (int)cs.size();
-    for (int i = 0; i < ns; ++i)
+    const bool sort_len = env_int("TVAM_SLOT_SORT", 1) != 0;
+    for (int i = 0; i < ns; ++i) {
+        for (size_t t = 0; t < per_tile.size(); ++t) angle_start[t] = per_tile[t].size();
         for (int col = 0; col < d.crop_x; ++col) {
             const uint32_t key = ((uint32_t)i << 16) | (uint32_t)col;
-            auto mark = [&](int t) {
+            auto mark = [&](int t, double len) {
                 if (last[t] != key) {
                     last[t] = key;
                     per_tile[t].push_back(key);
+                    len_of[t].push_back((float)len);
+                } else {
+                    len_of[t].back() = std::max(len_of[t].back(), (float)len);
                 }
             };
             const float c = cs[i].x, s = cs[i].y;
@@ -888,6 +901,19 @@ static void cyl_slot_lists(const tvam_desc& d, const TvamConsts& k, const std::v
                 if (v.b.hit) mark_tiles(g, v.b, m, mark);
             }
         }
+        if (!sort_len) continue;
+        for (size_t t = 0; t < per_tile.size(); ++t) {  // this angle's slots of tile t, longest first
+            const size_t b = angle_start[t], e = per_tile[t].size();
+            if (e - b < 2) continue;
+            std::vector<size_t> ord(e - b);
+            for (size_t j = 0; j < ord.size(); ++j) ord[j] = b + j;
+            std::stable_sort(ord.begin(), ord.end(), [&](size_t x, size_t y) { return len_of[t][x] > len_of[t][y]; });
+            std::vector<uint32_t> keys(ord.size());
+            for (size_t j = 0; j < ord.size(); ++j) keys[j] = per_tile[t][ord[j]];
+            std::copy(keys.begin(), keys.end(), per_tile[t].begin() + (std::ptrdiff_t)b);
+        }
+    }
+    for (auto& v : len_of) std::vector<float>().swap(v);
 }
 
 extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** out) {
