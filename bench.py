@@ -289,13 +289,23 @@ def main():
                "slices": [prob.z0, prob.z1], "rows": [prob.r0, prob.r1], "angles": [prob.a0, prob.a1]}
         if prob.shard == "angle" and ew > 1:
             # two ring all-reduces of the full dose per iteration (main forward + line-search forward):
-            # each moves 2 (W - 1) / W of the film per rank at the RCCL bus bandwidth --ar-gbs
+            # each moves 2 (W - 1) / W of the film per rank at the RCCL bus bandwidth --ar-gbs.  When the
+            # projection renders slice ranges (ShardedLoop.forward_chunks), range k's all-reduce runs on
+            # RCCL's stream under range k + 1's forward: only the last range's is exposed, unless the
+            # all-reduce of a range outlasts the forward of the next
             fr = prob.proj.desc.film_res
             film = 4.0 * fr[0] * fr[1] * fr[2]
             ar_ms = 2 * (2.0 * (ew - 1) / ew) * film / (args.ar_gbs * 1e9) * 1e3
+            zc = prob.proj.fwd_chunk
+            chunks = prob.forward_chunks() or [(0, fr[2])]
+            nchunk = len(chunks)
+            per_fwd_ar, per_fwd_fwd = ar_ms / 2, fwd_avg * 1e3
+            exposed = 2 * (per_fwd_ar / nchunk + max(0.0, (per_fwd_ar - per_fwd_fwd) * (nchunk - 1) / nchunk))
             rec.update({"allreduce_model": {"bytes_per_allreduce": film, "per_iteration": 2, "bus_gbs": args.ar_gbs,
-                                            "ms_per_iteration": ar_ms},
-                        "ms_per_step_with_allreduce": ms + ar_ms})
+                                            "ms_per_iteration": ar_ms, "slice_ranges": nchunk, "fwd_chunk": zc,
+                                            "exposed_ms_per_iteration": exposed},
+                        "ms_per_step_with_allreduce": ms + exposed,
+                        "ms_per_step_without_overlap": ms + ar_ms})
         print(json.dumps(rec), flush=True)
         return
     if rank != 0:

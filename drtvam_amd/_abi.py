@@ -131,6 +131,9 @@ EXPORTS = {
     "tvam_plan_destroy": (None, [_P]),
     "tvam_forward": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _P, _P]),
     "tvam_adjoint": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, _P, _P]),
+    "tvam_forward_slices": (ctypes.c_int, [_P, _P, _P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32,
+                                           ctypes.c_int32, ctypes.c_int32, _P, _P]),
+    "tvam_plan_fwd_chunk": (ctypes.c_int, [_P]),
     "tvam_lbfgs_history": (ctypes.c_int, [ctypes.c_uint64, _P, _P, _P, _P, ctypes.c_int32, _P, _P, _P, _P, _P, _P,
                                           _P]),
     "tvam_lbfgs_direction": (ctypes.c_int, [ctypes.c_uint64, _P, ctypes.c_int32, _P, _P, ctypes.c_float, _P, _P, _P,

@@ -30,6 +30,7 @@ struct TvamTiles {
     int64_t* frozen;              // ray indices marked frozen by the ray setup (ray_i.y <= -2), appended
     unsigned long long* frozen_n; // their count (beyond frozen_cap: the frozen kernel scans ray_i instead)
     int64_t frozen_cap;
+    int32_t kz0, kz1;             // forward launches: local film slices [kz0, kz1) (tvam_forward_slices)
 };
 
 // Planar fast path of regular sampling (tvam_planar.hip): one ray record per
@@ -71,6 +72,7 @@ struct TvamPlanar {
     // voxel-driven forward behind a refracting vial (fwd_refr = 1): every column's chord has its
     // own direction, and the candidate columns of a voxel come from a per-(16x16 tile, angle)
     // bilinear model of the chord index u(x, y) (tvam_refr_model_kernel)
+    int32_t fwd_zc0, fwd_nzc;  // voxel-driven forward launch: slice chunks [zc0, zc0 + nzc) of Z slices (0, 0: all)
     int32_t fwd_refr;
     float4* vox2;              // [ns][crop_x] {1/d.x, 1/d.y, axis flags (int bits), interface weight}
     float4* chord;             // plan creation only: [ns][crop_x] {o2.x, o2.y, d2.x, d2.y} of the medium chord

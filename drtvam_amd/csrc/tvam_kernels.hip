@@ -278,7 +278,7 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
     float* s_red = tile + tile_words;
     unsigned* s_amax = reinterpret_cast<unsigned*>(s_red + 16);  // forward: per-angle max |p|
 
-    const int tile_id = blockIdx.x, kz = blockIdx.y;
+    const int tile_id = blockIdx.x, kz = (int)blockIdx.y + (MODE == TVAM_MODE_FWD ? tp.kz0 : 0);
     const int x0 = (tile_id % tp.ntx) * tsx, y0 = (tile_id / tp.ntx) * tsy;
     const int x1 = min(x0 + tsx, k.res[0]), y1 = min(y0 + tsy, k.res[1]);
     const int wx = x1 - x0, wy = y1 - y0;
@@ -452,15 +452,19 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
 hipError_t tvam_launch_tiles(int mode, const TvamConsts& k, const TvamTiles& t, size_t lds_bytes,
                              const float* pat, const int32_t* idxmap, const float* gin, float* out,
                              unsigned long long* counter, hipStream_t stream) {
-    dim3 grid((unsigned)(t.ntx * t.nty), (unsigned)k.nz);
+    // forward launches may cover a slice range [kz0, kz1) (tvam_forward_slices); the others every slice
+    const int nzl = mode == TVAM_MODE_FWD && t.kz1 > t.kz0 ? t.kz1 - t.kz0 : k.nz;
+    TvamTiles tl = t;
+    if (!(mode == TVAM_MODE_FWD && t.kz1 > t.kz0)) tl.kz0 = 0;
+    dim3 grid((unsigned)(t.ntx * t.nty), (unsigned)nzl);
     dim3 block(TVAM_BLOCK);
     const bool w2 = k.vox_chord < TVAM_W2_MAX;
 #define TVAM_TILE_LAUNCH(M)                                                                                      \
     if (w2)                                                                                                      \
-        hipLaunchKernelGGL((tvam_tile_kernel<M, true>), grid, block, lds_bytes, stream, k, t, pat, idxmap, gin, out, \
+        hipLaunchKernelGGL((tvam_tile_kernel<M, true>), grid, block, lds_bytes, stream, k, tl, pat, idxmap, gin, out, \
                            counter);                                                                             \
     else                                                                                                         \
-        hipLaunchKernelGGL((tvam_tile_kernel<M, false>), grid, block, lds_bytes, stream, k, t, pat, idxmap, gin, out, \
+        hipLaunchKernelGGL((tvam_tile_kernel<M, false>), grid, block, lds_bytes, stream, k, tl, pat, idxmap, gin, out, \
                            counter);
     switch (mode) {
         case TVAM_MODE_FWD:

@@ -1238,8 +1238,38 @@ extern "C" int tvam_plan_set_active(tvam_plan* p, int64_t active_base, int64_t a
     return 0;
 }
 
+// Slice granularity of tvam_forward_slices: the voxel-driven forward's Z, 1 for the per-ray tile
+// kernels, 0 when the plan's forward cannot be split by slices (scattered paths and per-path
+// kernels add into every slice; the ray-driven planar forward).
+static int fwd_chunk(const tvam_plan* p) {
+    if (p->surface || p->general || p->desc.albedo != 0.0f) return 0;
+    if (p->planar_fwd) return p->planar_fz;
+    return p->planar ? 0 : 1;
+}
+
+extern "C" int tvam_plan_fwd_chunk(const tvam_plan* p) { return p ? fwd_chunk(p) : 0; }
+
+static int forward_impl(tvam_plan* p, const float* active_data, const uint32_t* active_pixels, uint64_t n_active,
+                        uint32_t spp, uint32_t seed, float* dose, void* stream_, int zb, int ze);
+
 extern "C" int tvam_forward(tvam_plan* p, const float* active_data, const uint32_t* active_pixels, uint64_t n_active,
                             uint32_t spp, uint32_t seed, float* dose, void* stream_) {
+    return forward_impl(p, active_data, active_pixels, n_active, spp, seed, dose, stream_, 0, -1);
+}
+
+extern "C" int tvam_forward_slices(tvam_plan* p, const float* active_data, const uint32_t* active_pixels,
+                                   uint64_t n_active, uint32_t spp, uint32_t seed, int32_t z_begin, int32_t z_end,
+                                   float* dose, void* stream) {
+    if (!p) return fail(TVAM_ERR_INVALID, "null argument");
+    const int ch = fwd_chunk(p), nz = p->k.nz;
+    if (ch == 0) return fail(TVAM_ERR_UNSUPPORTED, "this plan's forward cannot be split into slice ranges");
+    if (z_begin < 0 || z_end > nz || z_begin >= z_end || z_begin % ch != 0 || (z_end % ch != 0 && z_end != nz))
+        return fail(TVAM_ERR_INVALID, "slice range must lie in the film and on the forward's slice chunks");
+    return forward_impl(p, active_data, active_pixels, n_active, spp, seed, dose, stream, z_begin, z_end);
+}
+
+static int forward_impl(tvam_plan* p, const float* active_data, const uint32_t* active_pixels, uint64_t n_active,
+                        uint32_t spp, uint32_t seed, float* dose, void* stream_, int zb, int ze) {
     if (!p || !dose || (!active_data && n_active)) return fail(TVAM_ERR_INVALID, "null argument");
     hipStream_t stream = (hipStream_t)stream_;
     TvamConsts k;
@@ -1247,10 +1277,13 @@ extern "C" int tvam_forward(tvam_plan* p, const float* active_data, const uint32
     if (rc) return rc;
     const TvamConsts& kc = k;
     size_t V = (size_t)kc.res[0] * kc.res[1] * kc.nz * (p->surface ? 2 : 1);
+    const bool ranged = ze >= 0;  // tvam_forward_slices: only slices [zb, ze) of dose are written
     hipError_t e;
     if (p->surface && !p->vols) return fail(TVAM_ERR_INVALID, "surface-aware film: call tvam_plan_set_volumes first");
     if (p->empty || n_active == 0 || p->surface || p->general) {
-        e = hipMemsetAsync(dose, 0, V * sizeof(float), stream);
+        const size_t plane = (size_t)kc.res[0] * kc.res[1];
+        e = ranged ? hipMemsetAsync(dose + (size_t)zb * plane, 0, (size_t)(ze - zb) * plane * sizeof(float), stream)
+                   : hipMemsetAsync(dose, 0, V * sizeof(float), stream);
         if (e != hipSuccess) return hip_fail(e, "hipMemsetAsync");
         if (p->empty || n_active == 0) return 0;
     }
@@ -1287,7 +1320,12 @@ extern "C" int tvam_forward(tvam_plan* p, const float* active_data, const uint32
             if ((e = hipMemsetAsync(p->d_counter, 0, sizeof(unsigned long long), stream)) != hipSuccess)
                 return hip_fail(e, "hipMemsetAsync");
         }
-        e = tvam_launch_fwd_planar(kc, p->pl, p->planar_fz, pat, dose, stream);
+        TvamPlanar pl = p->pl;
+        if (ranged) {
+            pl.fwd_zc0 = zb / p->planar_fz;
+            pl.fwd_nzc = (ze - zb + p->planar_fz - 1) / p->planar_fz;
+        }
+        e = tvam_launch_fwd_planar(kc, pl, p->planar_fz, pat, dose, stream);
         if (e != hipSuccess) return hip_fail(e, "planar forward launch");
     } else if (p->planar) {
         e = tvam_launch_fwd_rays_planar(kc, p->pl, p->tiles, p->planar_rz, pat, p->d_amax, p->d_fscale, dose, stream);
@@ -1296,6 +1334,10 @@ extern "C" int tvam_forward(tvam_plan* p, const float* active_data, const uint32
         TvamTiles t = p->tiles;
         t.spp = spp;
         t.seed = seed;
+        if (ranged) {
+            t.kz0 = zb;
+            t.kz1 = ze;
+        }
         if ((rc = ensure_rays(p, kc, t, idxmap, stream))) return rc;
         unsigned long long* stats = nullptr;
         if (p->desc.flags & TVAM_FLAG_FWD_STATS) {

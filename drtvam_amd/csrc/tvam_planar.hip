@@ -152,7 +152,9 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
     int* s_row = s_cb + (TVAM_ACH + 4);                            // [Z]: the slice's row, -1 none, -2 several
 
     const int ntx = (k.res[0] + 15) >> 4, nty = (k.res[1] + 15) >> 4;
-    const int ntiles = ntx * nty, nwg1 = ntiles * ((k.nz + Z - 1) / Z);
+    // slice chunks of this launch: [fwd_zc0, fwd_zc0 + fwd_nzc) (tvam_forward_slices), else all
+    const int nzc = pl.fwd_nzc > 0 ? pl.fwd_nzc : (k.nz + Z - 1) / Z;
+    const int ntiles = ntx * nty, nwg1 = ntiles * nzc;
     const int parts = pl.fwd_parts > 1 ? pl.fwd_parts : 1, nwg = nwg1 * parts;
     // XCD-aware order: workgroup b runs on XCD b % 8; give each XCD a contiguous
     // run of (z-chunk, tile) pairs so the tiles sharing a z-chunk's pattern rows
@@ -171,7 +173,7 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
     const int tile = L % ntiles;
     const int bx = tile % ntx, by = tile / ntx;
     const int ix = bx * 16 + (threadIdx.x & 15), iy = by * 16 + (threadIdx.x >> 4);
-    const int z0 = (L / ntiles) * Z;
+    const int z0 = ((pl.fwd_nzc > 0 ? pl.fwd_zc0 : 0) + L / ntiles) * Z;
     const float hx = k.h[0], hy = k.h[1];
     // voxel edges exactly as the DDA places them (bmin + i * h, sensor.py:357)
     const float X0 = k.bmin[0] + (float)ix * hx, X1 = k.bmin[0] + (float)(ix + 1) * hx;
@@ -476,11 +478,12 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
 }
 
 // dose = sum of the angle parts' partial doses, in part order (deterministic)
-__global__ __launch_bounds__(256) void tvam_fwd_parts_kernel(int64_t n, int parts, const float* __restrict__ part,
+__global__ __launch_bounds__(256) void tvam_fwd_parts_kernel(int64_t n, int parts, int64_t pstride,
+                                                             const float* __restrict__ part,
                                                              float* __restrict__ dose) {
     for (int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (int64_t)gridDim.x * 256) {
         float v = part[i];
-        for (int q = 1; q < parts; ++q) v += part[(size_t)q * n + i];
+        for (int q = 1; q < parts; ++q) v += part[(size_t)q * pstride + i];
         dose[i] = v;
     }
 }
@@ -491,10 +494,10 @@ __global__ __launch_bounds__(256) void tvam_fwd_parts_kernel(int64_t n, int part
 // block goes through LDS, read along columns and written along slices.  Pads and
 // slices past nz stay 0 from the plan's memset.
 __global__ __launch_bounds__(256) void tvam_slice_bin_kernel(TvamConsts k, TvamPlanar pl,
-                                                            const float* __restrict__ pat) {
+                                                            const float* __restrict__ pat, int zblock0) {
     __shared__ float s_t[64][65];
     __shared__ int s_row[64];  // the slice's row x crop_x; -1: no row; -2: several rows
-    const int c0 = blockIdx.x * 64, z0 = blockIdx.y * 64, al = blockIdx.z;
+    const int c0 = blockIdx.x * 64, z0 = ((int)blockIdx.y + zblock0) * 64, al = blockIdx.z;
     if (threadIdx.x < 64) {
         const int z = z0 + (int)threadIdx.x;
         int r = -1;
@@ -726,19 +729,29 @@ hipError_t tvam_launch_fwd_planar(const TvamConsts& k, const TvamPlanar& pl, int
     const int ntx = (k.res[0] + 15) / 16, nty = (k.res[1] + 15) / 16;
     const int parts = pl.fwd_parts > 1 ? pl.fwd_parts : 1;
     if (parts > 1 && !pl.fwd_part) return hipErrorInvalidValue;
-    const unsigned nwg = (unsigned)(ntx * nty) * (unsigned)((k.nz + Z - 1) / Z) * (unsigned)parts;
+    const int nzc = pl.fwd_nzc > 0 ? pl.fwd_nzc : (k.nz + Z - 1) / Z;
+    const unsigned nwg = (unsigned)(ntx * nty) * (unsigned)nzc * (unsigned)parts;
     dim3 grid(pl.xcd_remap ? (nwg + 7) / 8 * 8 : nwg);
     const size_t lds = tvam_planar_fwd_lds(pl, Z);
     if (pl.fwd_bin) {
         if (pl.bin_nz % Z != 0 || pl.bin_nz < k.nz) return hipErrorInvalidValue;
-        const dim3 bg((unsigned)((k.crop_x + 63) / 64), (unsigned)((k.nz + 63) / 64), (unsigned)pl.ns);
-        hipLaunchKernelGGL(tvam_slice_bin_kernel, bg, dim3(256), 0, stream, k, pl, pat);
+        // bin only the 64-slice blocks of this launch's slices
+        const int zlo = pl.fwd_nzc > 0 ? pl.fwd_zc0 * Z : 0;
+        const int zhi = pl.fwd_nzc > 0 ? std::min(k.nz, (pl.fwd_zc0 + pl.fwd_nzc) * Z) : k.nz;
+        const int b0 = zlo / 64, b1 = (zhi + 63) / 64;
+        const dim3 bg((unsigned)((k.crop_x + 63) / 64), (unsigned)std::max(b1 - b0, 1), (unsigned)pl.ns);
+        hipLaunchKernelGGL(tvam_slice_bin_kernel, bg, dim3(256), 0, stream, k, pl, pat, b0);
     }
     hipError_t e = tvam_launch_fwd_planar_z(grid, lds, stream, k, pl, Z, pat, dose);
     if (e != hipSuccess || parts == 1) return e;
-    const int64_t n = (int64_t)k.nz * k.res[0] * k.res[1];
+    // sum the angle parts of this launch's slices
+    const int64_t plane = (int64_t)k.res[0] * k.res[1];
+    const int64_t zlo = pl.fwd_nzc > 0 ? (int64_t)pl.fwd_zc0 * Z : 0;
+    const int64_t zhi = pl.fwd_nzc > 0 ? std::min<int64_t>(k.nz, (int64_t)(pl.fwd_zc0 + pl.fwd_nzc) * Z) : k.nz;
+    const int64_t n = (zhi - zlo) * plane;
     const unsigned g = (unsigned)std::min<int64_t>((n + 255) / 256, 8192);
-    hipLaunchKernelGGL(tvam_fwd_parts_kernel, dim3(g), dim3(256), 0, stream, n, parts, pl.fwd_part, dose);
+    hipLaunchKernelGGL(tvam_fwd_parts_kernel, dim3(g), dim3(256), 0, stream, n, parts, (int64_t)k.nz * plane,
+                       pl.fwd_part + zlo * plane, dose + zlo * plane);
     return hipGetLastError();
 }
 

@@ -438,7 +438,10 @@ __global__ __launch_bounds__(256) void tvam_frozen_kernel(TvamConsts k, TvamTile
     uint64_t nvis = 0;
     for (int64_t j = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; j < n; j += (int64_t)gridDim.x * blockDim.x) {
         const int64_t i = list ? tp.frozen[j] : j;
-        if (tp.ray_i[i].y > -2) continue;
+        const int iy = tp.ray_i[i].y;
+        if (iy > -2) continue;
+        if (MODE == TVAM_MODE_FWD && tp.kz1 > tp.kz0 && !(-2 - iy >= k.z0 + tp.kz0 && -2 - iy < k.z0 + tp.kz1))
+            continue;  // a slice-range forward: another range's frozen ray (it stays in its slice)
         const int64_t n_local = (int64_t)tp.n_shard * per_angle;  // sample-major ray records
         const int smp = (int)(i / n_local);
         const int64_t local = i - (int64_t)smp * n_local;

@@ -82,6 +82,25 @@ class Projection:
                 active_data.numel(), spp, seed & 0xFFFFFFFF, out.data_ptr(), _stream_ptr(self.device)))
         return out
 
+    def forward_slices(self, active_data: torch.Tensor, active_pixels: Optional[torch.Tensor], spp: int, seed: int,
+                       z_begin: int, z_end: int, out: torch.Tensor) -> torch.Tensor:
+        """The forward of film slices [z_begin, z_end) into out (the other slices untouched)."""
+        self._check_tensor(active_data, torch.float32, "active_data")
+        if active_pixels is not None:
+            self._check_tensor(active_pixels, torch.int32, "active_pixels")
+        self._check_tensor(out, torch.float32, "dose")
+        with torch.cuda.device(self.device):
+            _abi.check(self.lib.tvam_forward_slices(
+                self._plan, active_data.data_ptr(), None if active_pixels is None else active_pixels.data_ptr(),
+                active_data.numel(), spp, seed & 0xFFFFFFFF, int(z_begin), int(z_end), out.data_ptr(),
+                _stream_ptr(self.device)))
+        return out
+
+    @property
+    def fwd_chunk(self) -> int:
+        """Slice granularity of forward_slices (0: not splittable)."""
+        return int(self.lib.tvam_plan_fwd_chunk(self._plan))
+
     def adjoint(self, grad_dose: torch.Tensor, n_active: int, active_pixels: Optional[torch.Tensor] = None,
                 spp: int = 1, seed: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         grad_dose = grad_dose.contiguous()

@@ -144,9 +144,35 @@ class ShardedLoop:
         return g / self.n_active_global() if lf.reduction_name == 'mean' else g
 
     # ---- projections ----------------------------------------------------------
+    allreduce_chunks = 4  # angle shards: slice ranges whose dose all-reduce overlaps the next range's forward
+
+    def forward_chunks(self):
+        """Film slice ranges [(z0, z1), ...] of an overlapped forward + all-reduce, or None."""
+        return None
+
+    def forward_local_slices(self, x, seed, z0, z1, out):
+        raise NotImplementedError
+
+    def dose_buffer(self):
+        raise NotImplementedError
+
     def forward(self, x, seed):
-        vol = self.forward_local(x, seed)
-        return vol if self.dose_sharded else self.allreduce_(vol)
+        """This rank's partial dose, all-reduced over the angle shards.  When the
+        projection can render slice ranges, range k's all-reduce (async: RCCL runs it on its own
+        stream) overlaps range k + 1's forward; the sum per voxel is the same."""
+        if self.dose_sharded:
+            return self.forward_local(x, seed)
+        chunks = self.forward_chunks() if self.dist is not None else None
+        if not chunks:
+            return self.allreduce_(self.forward_local(x, seed))
+        vol = self.dose_buffer()
+        works = []
+        for z0, z1 in chunks:
+            self.forward_local_slices(x, seed, z0, z1, vol)
+            works.append(self.dist.all_reduce(vol[z0:z1], async_op=True))
+        for w in works:
+            w.wait()
+        return vol
 
     def adjoint(self, grad_vol, seed):
         return self.adjoint_local(grad_vol, seed)
@@ -479,6 +505,21 @@ class TvamProblem(ShardedLoop):
 
     def forward_local(self, x, seed):
         return self.proj.forward(x.detach().contiguous(), self.active_pixels, self.spp, seed)
+
+    def forward_chunks(self):
+        n = int(self.config.get('allreduce_chunks', self.allreduce_chunks))
+        zc = self.proj.fwd_chunk
+        nz = self.proj.film_shape[0]
+        if n <= 1 or zc <= 0 or nz < 2 * zc:
+            return None
+        step = -(-(-(-nz // n)) // zc) * zc  # ceil(nz / n) rounded up to the forward's slice chunk
+        return [(z0, min(nz, z0 + step)) for z0 in range(0, nz, step)]
+
+    def forward_local_slices(self, x, seed, z0, z1, out):
+        return self.proj.forward_slices(x.detach().contiguous(), self.active_pixels, self.spp, seed, z0, z1, out)
+
+    def dose_buffer(self):
+        return torch.empty(self.proj.film_shape, dtype=torch.float32, device=self.device)
 
     def adjoint_local(self, grad_vol, seed):
         return self.proj.adjoint(grad_vol, self.n_local, self.active_pixels, self.spp_grad, derive_seed_grad(seed))

@@ -186,6 +186,21 @@ int tvam_forward(tvam_plan* plan, const float* active_data,
                  uint32_t spp, uint32_t seed, float* dose, void* hip_stream);
 
 /*
+ * Forward projection of film slices [z_begin, z_end) only (relative to the plan's slab): the
+ * same values tvam_forward writes there, the other slices of dose untouched.  Lets a caller
+ * all-reduce a finished slice range of an angle shard's partial dose while the next range is
+ * computed.  The range must lie on the forward's slice chunks
+ * (tvam_plan_fwd_chunk); TVAM_ERR_UNSUPPORTED when the plan's forward cannot be split (0).
+ */
+int tvam_forward_slices(tvam_plan* plan, const float* active_data,
+                        const uint32_t* active_pixels, uint64_t n_active,
+                        uint32_t spp, uint32_t seed, int32_t z_begin, int32_t z_end,
+                        float* dose, void* hip_stream);
+/* Slice granularity of tvam_forward_slices (0: the plan's forward covers every slice at once:
+   scattering media, per-path kernels, the ray-driven planar forward). */
+int tvam_plan_fwd_chunk(const tvam_plan* plan);
+
+/*
  * Adjoint projection (render_backward).  grad_active[i] (overwritten, f32,
  * n_active entries) = d<grad_dose, forward(active_data)>/d active_data[i],
  * i.e. the gradient Dr.TVAM accumulates into projector.active_data.grad.

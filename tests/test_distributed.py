@@ -32,7 +32,8 @@ def operator():
 
 
 class MatrixShard(ShardedLoop):
-    def __init__(self, rank, world):
+    def __init__(self, rank, world, chunked=False):
+        self.chunked = chunked
         M, target = operator()
         self.a0, self.a1 = angle_shard(A, rank, world)
         self.M = M[:, self.a0 * PER_ANGLE:self.a1 * PER_ANGLE]
@@ -54,9 +55,20 @@ class MatrixShard(ShardedLoop):
     def adjoint_local(self, grad_vol, seed):
         return self.M.T @ grad_vol.reshape(-1)
 
+    # slice-range forward: the overlapped chunk-by-chunk dose all-reduce (async gloo here)
+    def forward_chunks(self):
+        return [(0, 1), (1, 3), (3, 4)] if self.chunked else None
 
-def run(rank, world, steps):
-    prob = MatrixShard(rank, world)
+    def forward_local_slices(self, x, seed, z0, z1, out):
+        out[z0:z1] = self.forward_local(x, seed)[z0:z1]
+        return out
+
+    def dose_buffer(self):
+        return torch.empty(SHAPE, dtype=torch.float64)
+
+
+def run(rank, world, steps, chunked=False):
+    prob = MatrixShard(rank, world, chunked)
     for i in range(steps):
         prob.iteration(i)
     x = prob.patterns_local()
@@ -67,12 +79,12 @@ def run(rank, world, steps):
     return np.asarray(prob.loss_hist), x.numpy()
 
 
-def _worker(rank, world, port, steps, q):
+def _worker(rank, world, port, steps, q, chunked=False):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
-        loss, x = run(rank, world, steps)
+        loss, x = run(rank, world, steps, chunked)
         if rank == 0:
             q.put((loss, x))
     finally:
@@ -93,14 +105,15 @@ def test_angle_shard_partition():
         assert max(b[1] - b[0] for b in blocks) - min(b[1] - b[0] for b in blocks) <= 1
 
 
-def test_sharded_loop_matches_single_rank():
+@pytest.mark.parametrize("chunked", [False, True])
+def test_sharded_loop_matches_single_rank(chunked):
     steps = 6
     ref_loss, ref_x = run(0, 1, steps)
     assert ref_loss[-1] < ref_loss[0]
     ctx = mp.get_context("spawn")
     q = ctx.SimpleQueue()
     port = free_port()
-    procs = [ctx.Process(target=_worker, args=(r, 2, port, steps, q)) for r in range(2)]
+    procs = [ctx.Process(target=_worker, args=(r, 2, port, steps, q, chunked)) for r in range(2)]
     for p in procs:
         p.start()
     loss, x = q.get()

@@ -2,7 +2,9 @@
 tensors): the sharded optimisation loop with the real HIP projections (planar
 path) and the fused L-BFGS (one all-reduce of the dot vector per step) must
 reproduce the single-rank run.  Each rank owns a contiguous angle block and
-renders a partial dose that is all-reduced."""
+renders a partial dose that is all-reduced; under jittered
+sampling (per-ray tile kernels) the forward runs in 4 slice ranges whose async
+all-reduces overlap the next range's forward."""
 import os
 import socket
 
@@ -21,13 +23,17 @@ def _run(rank, world, steps, shard):
     from drtvam_amd.configs import benchy_index_matched
     from drtvam_amd.optimize import TvamProblem
 
-    cfg = benchy_index_matched(**CFG)
+    jitter = shard == "angle_jitter"  # the per-ray tile path: the dose all-reduce in 4 overlapped slice ranges
+    cfg = benchy_index_matched(**CFG, regular_sampling=not jitter, spp=2 if jitter else 1)
+    shard = "angle" if jitter else shard
     cfg["shard"] = shard
     prob = TvamProblem(cfg, device=torch.device("cuda", 0), rank=rank, world_size=world)
     assert prob.shard == shard
     g = torch.Generator().manual_seed(0)
     prob.x0 = prob.local_from_global(torch.rand(prob.n_global, generator=g) * 0.1)
-    assert prob.proj.planar
+    assert prob.proj.planar != jitter
+    if jitter and world > 1:
+        assert prob.forward_chunks() is not None and len(prob.forward_chunks()) == 4
     for i in range(steps):
         prob.iteration(i)
     x = prob.gather_patterns(prob.patterns_local().float())
@@ -57,7 +63,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("shard", ["slab", "angle"])
+@pytest.mark.parametrize("shard", ["slab", "angle", "angle_jitter"])
 def test_two_rank_gpu_loop_matches_single_rank(shard):
     steps = 4
     ctx = mp.get_context("spawn")

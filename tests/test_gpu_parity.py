@@ -302,3 +302,44 @@ def test_deep_slab_forward(oracle, monkeypatch, Z):
     got, proj = gpu_forward(d, pat)
     assert proj.planar_forward
     assert rel_l2(got, ref) < RTOL_L2
+
+
+@pytest.mark.parametrize("kind", ["planar", "refracted", "tile_jittered", "square_occluder"])
+def test_forward_slices_assemble_the_forward(kind):
+    """tvam_forward_slices (the overlapped angle-shard all-reduce): slice ranges on the
+    forward's chunks, rendered one after another into one buffer, give the whole forward."""
+    from drtvam_amd.configs import cylindrical_refraction, square_vial
+    if kind == "planar":
+        d = make(N=48, A=24)
+    elif kind == "refracted":
+        d = desc_from_config(cylindrical_refraction(N=40, angles=20))
+    elif kind == "tile_jittered":
+        d = make(N=32, A=16, regular=False, spp=2)
+    else:
+        import os
+        occ = os.path.join(os.path.dirname(__file__), "golden", "occlusion.ply")
+        d = desc_from_config(square_vial(N=40, angles=16, spp=2, regular_sampling=False, occluders=(occ,)))
+    proj = Projection(d, "cuda:0")
+    zc = proj.fwd_chunk
+    assert zc >= 1
+    n = d.n_patterns * d.crop_y * d.crop_x
+    x = torch.as_tensor(np.random.default_rng(12).uniform(0, 0.1, n).astype(np.float32), device="cuda:0")
+    spp = 1 if d.regular_sampling else 2
+    full = proj.forward(x, None, spp, 3).clone()
+    out = torch.full_like(full, float("nan"))
+    nz = full.shape[0]
+    edges = sorted({0, nz} | {min(nz, zc * q) for q in (1, 3)})
+    for z0, z1 in zip(edges[:-1], edges[1:]):
+        proj.forward_slices(x, None, spp, 3, z0, z1, out)
+    torch.cuda.synchronize()
+    assert not torch.isnan(out).any()
+    assert rel_l2(out.cpu().numpy(), full.cpu().numpy()) < 1e-6
+    with pytest.raises(ValueError):
+        proj.forward_slices(x, None, spp, 3, 0, nz + 1, out)
+
+
+def test_forward_slices_unsupported_for_scattering():
+    from drtvam_amd.configs import cylindrical_scattering
+    d = desc_from_config(cylindrical_scattering(N=24, angles=8, spp=2))
+    proj = Projection(d, "cuda:0")
+    assert proj.fwd_chunk == 0
