@@ -253,6 +253,22 @@ def main():
 
     prob.proj.forward = timed(orig_fwd, fwd_ms)
     prob.proj.adjoint = timed(orig_adj, adj_ms)
+    # overlapped angle shards render a forward as slice ranges (ShardedLoop.forward): one forward =
+    # the ranges from slice 0 on, timed together
+    fwd_slices, orig_slices = [], getattr(prob.proj, "forward_slices", None)
+
+    def timed_slices(*a, **k):
+        if not state["on"]:
+            return orig_slices(*a, **k)
+        s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        s.record()
+        out = orig_slices(*a, **k)
+        e.record()
+        fwd_slices.append((a[4] if len(a) > 4 else k.get("z0", 0), s, e))
+        return out
+
+    if orig_slices is not None:
+        prob.proj.forward_slices = timed_slices
 
     for i in range(args.warmup):
         prob.iteration(i)
@@ -271,6 +287,11 @@ def main():
     state["on"] = False
     elapsed = t1 - t0
     fwd = [s.elapsed_time(e) for s, e in fwd_ms]
+    if fwd_slices:  # per forward: the sum of its slice ranges' times
+        for z0, s, e in fwd_slices:
+            if z0 == 0 or not fwd:
+                fwd.append(0.0)
+            fwd[-1] += s.elapsed_time(e)
     adj = [s.elapsed_time(e) for s, e in adj_ms]
     fwd_avg = sum(fwd) / len(fwd) / 1e3
     adj_avg = sum(adj) / len(adj) / 1e3 if adj else float("nan")
