@@ -12,7 +12,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TVAM_LIB") or os.path.join(_HERE, "libtvam.so")  # TVAM_LIB: a variant build
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 TVAM_OK = 0
 TVAM_ERR_INVALID = -1
@@ -153,6 +153,11 @@ EXPORTS = {
         ctypes.c_int,
         [_P, _P, ctypes.c_float, _P, ctypes.c_uint64, ctypes.c_int32, ctypes.c_float, ctypes.c_float,
          ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, _P, _P],
+    ),
+    "tvam_loss_threshold_probes": (
+        ctypes.c_int,
+        [_P, _P, _P, ctypes.c_int32, _P, ctypes.c_uint64, ctypes.c_int32, ctypes.c_float, ctypes.c_float,
+         ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, _P],
     ),
     "tvam_last_error": (ctypes.c_char_p, []),
     "tvam_abi_version": (ctypes.c_int, []),

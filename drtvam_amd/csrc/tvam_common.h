@@ -257,7 +257,18 @@ TVAM_HD float tvam_tri_hit(const float* v, float ox, float oy, float oz, float d
 
 TVAM_HD float tvam_occ_hit(const TvamConsts& k, float ox, float oy, float oz, float dx, float dy, float dz) {
     float best = TVAM_INF;
-    for (int i = 0; i < k.n_occ; ++i) best = fminf(best, tvam_tri_hit(k.occ + 9 * i, ox, oy, oz, dx, dy, dz));
+    for (int i = 0; i < k.n_occ; ++i) {
+        const float* v = k.occ + 9 * i;
+        // a planar ray (d.z = 0) far outside the triangle's z range misses it: Moller-Trumbore's
+        // barycentric test fails there by orders of magnitude more than its rounding (the margin),
+        // so skipping the test returns the same t (most of a wave's rays pass below / above)
+        if (dz == 0.0f) {
+            const float zlo = fminf(fminf(v[2], v[5]), v[8]), zhi = fmaxf(fmaxf(v[2], v[5]), v[8]);
+            const float mg = 1e-3f * (1.0f + fabsf(zlo) + fabsf(zhi));
+            if (oz < zlo - mg || oz > zhi + mg) continue;
+        }
+        best = fminf(best, tvam_tri_hit(v, ox, oy, oz, dx, dy, dz));
+    }
     return best;
 }
 

@@ -191,6 +191,10 @@ hipError_t tvam_launch_scatter(const TvamConsts& k, const float* data, const uin
 hipError_t tvam_launch_gather(const TvamConsts& k, const float* dense, const uint32_t* pixels,
                               uint64_t n, float* out, hipStream_t stream);
 
+#define TVAM_MAX_PROBES 8
+hipError_t tvam_launch_loss_probes(const float* dose, const float* ddose, const float* alphas, int na,
+                                   const float* target, uint64_t n, int K, float tl, float tu, float w_object,
+                                   float w_void, float w_limit, float scale, double* out, hipStream_t stream);
 hipError_t tvam_launch_loss_threshold(const float* dose, const float* ddose, float alpha,
                                       const float* target, uint64_t n, int K, float tl, float tu,
                                       float w_object, float w_void, float w_limit, float scale,

@@ -575,6 +575,82 @@ __global__ __launch_bounds__(256) void tvam_loss_threshold_kernel(
     }
 }
 
+// Armijo probes of the linear line search (lbfgs.py:255-268): the loss of dose + alpha_j * ddose for
+// up to TVAM_MAX_PROBES step sizes in one pass over dose / ddose / target (per element the same
+// arithmetic as tvam_loss_threshold_kernel), out[j] += sum_j * scale.
+struct TvamProbeAlphas {
+    float a[TVAM_MAX_PROBES];
+};
+
+__device__ __forceinline__ float tvam_loss_elem(float x, bool obj, int K, float tl, float tu, float w_object,
+                                                float w_void, float w_limit) {
+    if (obj) {
+        const float zo = tu - x, zl = x - 1.0f;
+        const float ro = zo > 0.0f ? zo : 0.0f, rl = zl > 0.0f ? zl : 0.0f;
+        return w_object * tvam_powi(ro, K) + w_limit * tvam_powi(rl, K);
+    }
+    const float zv = x - tl;
+    const float rv = zv > 0.0f ? zv : 0.0f;
+    return w_void * tvam_powi(rv, K);
+}
+
+__global__ __launch_bounds__(256) void tvam_loss_probes_kernel(
+    const float* __restrict__ dose, const float* __restrict__ ddose, TvamProbeAlphas al, int na,
+    const float* __restrict__ target, uint64_t n, uint64_t n4, int K, float tl, float tu, float w_object,
+    float w_void, float w_limit, float scale, double* __restrict__ out) {
+    __shared__ double red[TVAM_MAX_PROBES][256 / 64];
+    double acc[TVAM_MAX_PROBES];
+#pragma unroll
+    for (int j = 0; j < TVAM_MAX_PROBES; ++j) acc[j] = 0.0;
+    auto elem = [&](float x0, float dx, float tg) {
+        const bool obj = tg > 0.0f;
+#pragma unroll
+        for (int j = 0; j < TVAM_MAX_PROBES; ++j)
+            if (j < na) acc[j] += (double)tvam_loss_elem(fmaf(al.a[j], dx, x0), obj, K, tl, tu, w_object, w_void, w_limit);
+    };
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
+    // n4: elements / 4 when all three arrays are 16-byte aligned (float4 loads), else 0
+    const float4* d4 = reinterpret_cast<const float4*>(dose);
+    const float4* dd4 = reinterpret_cast<const float4*>(ddose);
+    const float4* t4 = reinterpret_cast<const float4*>(target);
+    for (uint64_t i = tid; i < n4; i += stride) {
+        const float4 x = d4[i], dx = dd4[i], tg = t4[i];
+        elem(x.x, dx.x, tg.x);
+        elem(x.y, dx.y, tg.y);
+        elem(x.z, dx.z, tg.z);
+        elem(x.w, dx.w, tg.w);
+    }
+    for (uint64_t i = 4 * n4 + tid; i < n; i += stride) elem(dose[i], ddose[i], target[i]);
+#pragma unroll
+    for (int j = 0; j < TVAM_MAX_PROBES; ++j) {
+        double v = acc[j];
+        for (int off = 32; off > 0; off >>= 1) v += __shfl_down(v, off, 64);
+        if ((threadIdx.x & 63) == 0) red[j][threadIdx.x >> 6] = v;
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < na) {
+        double s = 0.0;
+        for (int w = 0; w < 256 / 64; ++w) s += red[threadIdx.x][w];
+        atomicAdd(out + threadIdx.x, s * (double)scale);
+    }
+}
+
+hipError_t tvam_launch_loss_probes(const float* dose, const float* ddose, const float* alphas, int na,
+                                   const float* target, uint64_t n, int K, float tl, float tu, float w_object,
+                                   float w_void, float w_limit, float scale, double* out, hipStream_t stream) {
+    TvamProbeAlphas al{};
+    for (int j = 0; j < na; ++j) al.a[j] = alphas[j];
+    const bool al16 = ((reinterpret_cast<uintptr_t>(dose) | reinterpret_cast<uintptr_t>(ddose) |
+                        reinterpret_cast<uintptr_t>(target)) & 15) == 0;
+    const uint64_t n4 = al16 ? n / 4 : 0;
+    unsigned g = (unsigned)(((al16 ? n4 : n) + 255) / 256);
+    if (g > 2048) g = 2048;
+    if (g == 0) g = 1;
+    hipLaunchKernelGGL(tvam_loss_probes_kernel, dim3(g), dim3(256), 0, stream, dose, ddose, al, na, target, n, n4, K,
+                       tl, tu, w_object, w_void, w_limit, scale, out);
+    return hipGetLastError();
+}
+
 hipError_t tvam_launch_loss_threshold(const float* dose, const float* ddose, float alpha, const float* target,
                                       uint64_t n, int K, float tl, float tu, float w_object, float w_void,
                                       float w_limit, float scale, double* out, float* grad, hipStream_t stream) {

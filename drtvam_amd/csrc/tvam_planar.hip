@@ -114,6 +114,9 @@ hipError_t tvam_launch_planar_rays(const TvamConsts& k, const TvamPlanar& pl, hi
 // in exact arithmetic), so the dose is the same sum of telescoped weights
 // the DDA forms, up to fp32 rounding of the crossing times.
 // ---------------------------------------------------------------------------
+#ifndef TVAM_FWD_SKIPZERO
+#define TVAM_FWD_SKIPZERO 0
+#endif
 #define TVAM_PF 4     // most staged pattern values per thread and angle (host: ncmax * Z <= TVAM_PF * TVAM_PB)
 // slab row stride (words) of Z slices: an odd number of 16-byte groups, so 16
 // consecutive columns' ds_read_b128 hit 16 different bank groups
@@ -314,7 +317,8 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
         const float4* sr = s_r + buf * ncm * 2;
         // u(lx, ly) = the chord index through the voxel centre (lattice coordinates from the tile corner)
         const float4 m0 = s_ang[2 * (al - tbase)], m1 = s_ang[2 * (al - tbase) + 1];
-        const int nc = __builtin_amdgcn_readfirstlane(__float_as_int(m1.y));  // uniform over the workgroup, >= 2
+        // this wave's candidate count (uniform over the wave, >= 2)
+        const int nc = __builtin_amdgcn_readfirstlane((__float_as_int(m1.w) >> (8 * (threadIdx.x >> 6))) & 0xff);
         const float lx = (float)(threadIdx.x & 15) + 0.5f, ly = (float)(threadIdx.x >> 4) + 0.5f;
         const float u = fmaf(lx * ly, m0.w, fmaf(ly, m0.z, fmaf(lx, m0.y, m0.x)));
         const float hv = 0.5f * (fabsf(fmaf(m0.w, ly, m0.y)) + fabsf(fmaf(m0.w, lx, m0.z))) + 0.25f * fabsf(m0.w);
@@ -394,6 +398,22 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
             const float e = pl_exp2(k.nsig2 * tin) - pl_exp2(k.nsig2 * tout);
             wgt[c] = tout > tin ? e : 0.0f;
         }
+#if TVAM_FWD_SKIPZERO  // experiment: a lane reads only the slabs of candidates that meet its voxel
+#pragma unroll
+        for (int c = 0; c < NC; ++c) {
+            if (wgt[c] != 0.0f) {
+#pragma unroll
+                for (int z4 = 0; z4 < Z / 4; ++z4) {
+                    const float4 p4 = reinterpret_cast<const float4*>(sp + (jj0 + c) * ZS)[z4];
+                    acc[4 * z4 + 0] = fmaf(wgt[c], p4.x, acc[4 * z4 + 0]);
+                    acc[4 * z4 + 1] = fmaf(wgt[c], p4.y, acc[4 * z4 + 1]);
+                    acc[4 * z4 + 2] = fmaf(wgt[c], p4.z, acc[4 * z4 + 2]);
+                    acc[4 * z4 + 3] = fmaf(wgt[c], p4.w, acc[4 * z4 + 3]);
+                }
+            }
+        }
+        if (false)
+#endif
 #pragma unroll
         for (int z4 = 0; z4 < Z / 4; ++z4) {
 #pragma unroll
@@ -631,15 +651,22 @@ __global__ __launch_bounds__(64) void tvam_refr_model_kernel(TvamConsts k, TvamP
         const float w = ue + 0.5f * spread;
         // candidates of a voxel: the integers in [u - hv - ue, u + hv + ue], u the model at its centre and
         // hv = 0.5 (|du/dlx| + |du/dly|) + |d2u/dlx dly| / 4 its half range at the corners; the forward
-        // runs the largest count of the tile's voxels (uniform over the workgroup)
-        int nc = 2;  // the forward runs two candidates straight-line
-        for (int vy = 0; vy < 16; ++vy)
-            for (int vx = 0; vx < 16; ++vx) {
-                const float lx = (float)vx + 0.5f, ly = (float)vy + 0.5f;
-                const float u = model_at(lx, ly);
-                const float hv = 0.5f * (fabsf(fmaf(m0.w, ly, m0.y)) + fabsf(fmaf(m0.w, lx, m0.z))) + 0.25f * fabsf(m0.w);
-                nc = max(nc, (int)floorf(u + hv + ue) - (int)ceilf(u - hv - ue) + 1);
-            }
+        // runs the largest count of a wave's voxels (wave w: tile rows 4w .. 4w + 3; packed one byte
+        // per wave), at least two (the forward runs two candidates straight-line)
+        int nc = 2, ncw = 0;
+        for (int wv = 0; wv < 4; ++wv) {
+            int n_w = 2;
+            for (int vy = 4 * wv; vy < 4 * wv + 4; ++vy)
+                for (int vx = 0; vx < 16; ++vx) {
+                    const float lx = (float)vx + 0.5f, ly = (float)vy + 0.5f;
+                    const float u = model_at(lx, ly);
+                    const float hv = 0.5f * (fabsf(fmaf(m0.w, ly, m0.y)) + fabsf(fmaf(m0.w, lx, m0.z))) + 0.25f * fabsf(m0.w);
+                    n_w = max(n_w, (int)floorf(u + hv + ue) - (int)ceilf(u - hv - ue) + 1);
+                }
+            n_w = min(n_w, 255);
+            nc = max(nc, n_w);
+            ncw |= n_w << (8 * wv);
+        }
         float umin = TVAM_INF, umax = -TVAM_INF;
         for (int cy = 0; cy < 2; ++cy)
             for (int cx = 0; cx < 2; ++cx) {
@@ -651,7 +678,7 @@ __global__ __launch_bounds__(64) void tvam_refr_model_kernel(TvamConsts k, TvamP
         const int ce = (int)ceilf(umax + w) + 1;
         need[i] = ce - cb + 1;
         m[0] = m0;
-        m[1] = make_float4(ue, __int_as_float(nc), __int_as_float(cb), err);  // .w: diagnostics only
+        m[1] = make_float4(ue, __int_as_float(nc), __int_as_float(cb), __int_as_float(ncw));
     }
 }
 

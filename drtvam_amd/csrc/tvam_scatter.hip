@@ -1110,8 +1110,8 @@ __global__ void tvam_bin_start_kernel(const uint32_t* __restrict__ keys, int64_t
 // added in LDS, then dose += tile (the brick is this launch's alone).
 // Adjoint (ACC 2): the brick's grad * inv_vol staged in LDS, each entry's
 // weighted gather written to part[entry] (no atomics; summed per path later).
-template <int ACC>
-__global__ __launch_bounds__(512) void tvam_bin_march_kernel(TvamConsts k, TvamSegBuf sb,
+template <int ACC, int NT>
+__global__ __launch_bounds__(NT) void tvam_bin_march_kernel(TvamConsts k, TvamSegBuf sb,
                                                              const uint32_t* __restrict__ vals,
                                                              const uint32_t* __restrict__ slot_of,
                                                              const uint32_t* __restrict__ bstart,
@@ -1119,7 +1119,7 @@ __global__ __launch_bounds__(512) void tvam_bin_march_kernel(TvamConsts k, TvamS
                                                              float* __restrict__ part) {
     constexpr int NV = TVAM_BX * TVAM_BY * TVAM_BZ;
     __shared__ __attribute__((aligned(16))) unsigned char smem[NV * (ACC == 0 ? 8 : 4)];
-    __shared__ float red[8];
+    __shared__ float red[NT / 64];
     long long* ltile = reinterpret_cast<long long*>(smem);
     float* ftile = reinterpret_cast<float*>(smem);
     const int nbx = sc_nbr(k, 0), nby = sc_nbr(k, 1);
@@ -1135,13 +1135,13 @@ __global__ __launch_bounds__(512) void tvam_bin_march_kernel(TvamConsts k, TvamS
     if (ACC == 0) {
         // per-add bound: each add rounds to int32 (one v_cvt), the int64 sums cannot overflow
         float sw = 0.0f;
-        for (uint32_t e = e0 + threadIdx.x; e < e1; e += 512) sw = fmaxf(sw, fabsf(sb.r[3 * vals[e] + 2].y));
+        for (uint32_t e = e0 + threadIdx.x; e < e1; e += NT) sw = fmaxf(sw, fabsf(sb.r[3 * vals[e] + 2].y));
         for (int o = 32; o > 0; o >>= 1) sw = fmaxf(sw, __shfl_xor(sw, o, 64));
         if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sw;
-        for (int i = threadIdx.x; i < NV; i += 512) ltile[i] = 0;
+        for (int i = threadIdx.x; i < NV; i += NT) ltile[i] = 0;
         __syncthreads();
         float tot = 0.0f;
-        for (int w = 0; w < 8; ++w) tot = fmaxf(tot, red[w]);
+        for (int w = 0; w < NT / 64; ++w) tot = fmaxf(tot, red[w]);
         const float hmax = fmaxf(fmaxf(k.h[0], k.h[1]), k.h[2]);
         const float bound = tot * fminf(1.0f, k.sig_t * 1.7320508f * hmax) * 1.001f;
         if (bound > 0.0f && isfinite(bound)) {
@@ -1152,20 +1152,20 @@ __global__ __launch_bounds__(512) void tvam_bin_march_kernel(TvamConsts k, TvamS
             scale = ldexpf(1.0f, ex);
         }
     } else if (ACC == 1) {
-        for (int i = threadIdx.x; i < NV; i += 512) ftile[i] = 0.0f;
+        for (int i = threadIdx.x; i < NV; i += NT) ftile[i] = 0.0f;
         __syncthreads();
     } else {
-        for (int i = threadIdx.x; i < wx * wy * wz; i += 512) {
+        for (int i = threadIdx.x; i < wx * wy * wz; i += NT) {
             const int x = i % wx, y = (i / wx) % wy, z = i / (wx * wy);
             const size_t g = ((size_t)(lo[2] + z) * k.res[1] + (lo[1] + y)) * k.res[0] + (lo[0] + x);
             ftile[z * sz + y * sy + x] = gin[g] * k.inv_vol;  // volume.py:130
         }
         __syncthreads();
     }
-    // Three-stage load pipeline over this thread's entries e, e + S, e + 2S, ... (S = 512): while
+    // Three-stage load pipeline over this thread's entries e, e + S, e + 2S, ... (S = NT): while
     // entry e marches, the record of e + S, the slot of e + 2S and the entry id of e + 3S are in
     // flight (the chain vals -> slot_of -> record is three dependent gathers).
-    constexpr uint32_t S = 512;
+    constexpr uint32_t S = NT;
     const uint32_t et = e0 + threadIdx.x;
     // forward (ACC 0 / 1): vals hold the slots themselves
     auto slot_at = [&](uint32_t v) { return ACC == 2 ? slot_of[v] : v; };
@@ -1208,7 +1208,7 @@ __global__ __launch_bounds__(512) void tvam_bin_march_kernel(TvamConsts k, TvamS
     if (ACC == 2) return;
     __syncthreads();
     const float inv = 1.0f / scale;
-    for (int i = threadIdx.x; i < wx * wy * wz; i += 512) {
+    for (int i = threadIdx.x; i < wx * wy * wz; i += NT) {
         const int x = i % wx, y = (i / wx) % wy, z = i / (wx * wy);
         const int li = z * sz + y * sy + x;
         const float v = ACC == 0 ? (float)ltile[li] * inv : ftile[li];
@@ -1283,6 +1283,12 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
     const int nbx = (k.res[0] + TVAM_BX - 1) / TVAM_BX, nby = (k.res[1] + TVAM_BY - 1) / TVAM_BY,
               nbz = (k.res[2] + TVAM_BZ - 1) / TVAM_BZ;
     const int nbricks = nbx * nby * nbz;
+    // brick-march workgroup: 1024 threads double the waves per SIMD under the one 128 KB int64
+    // tile per CU (forward) and the two 64 KB gradient tiles (adjoint); TVAM_BIN_NT=512 for A/B
+    static const int bin_nt = [] {
+        const char* v = getenv("TVAM_BIN_NT");
+        return v && atoi(v) == 512 ? 512 : 1024;
+    }();
     int bits = 1;
     while ((1 << bits) < nbricks) ++bits;
     bits += TVAM_BIN_CLASS_BITS;
@@ -1379,18 +1385,30 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
         hipLaunchKernelGGL(tvam_bin_start_kernel, dim3((unsigned)g), dim3(256), 0, stream, s.keys[1], (int64_t)total,
                            nbricks, s.bstart);
         if (adj) {
-            hipLaunchKernelGGL(tvam_bin_march_kernel<2>, dim3((unsigned)nbricks), dim3(512), 0, stream, k, sb,
-                               s.vals[1], s.slot_of, s.bstart, nullptr, gin, s.part);
+            if (bin_nt == 1024)
+                hipLaunchKernelGGL((tvam_bin_march_kernel<2, 1024>), dim3((unsigned)nbricks), dim3(1024), 0, stream, k,
+                                   sb, s.vals[1], s.slot_of, s.bstart, nullptr, gin, s.part);
+            else
+                hipLaunchKernelGGL((tvam_bin_march_kernel<2, 512>), dim3((unsigned)nbricks), dim3(512), 0, stream, k,
+                                   sb, s.vals[1], s.slot_of, s.bstart, nullptr, gin, s.part);
             const int64_t npix = (p1 - p0) / spp;
             g = std::min<int64_t>((npix + 255) / 256, 65536);
             hipLaunchKernelGGL(tvam_bin_reduce_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, sb, spp, s.off,
                                s.part, idxmap, out);
         } else if (s.acc_float) {
-            hipLaunchKernelGGL(tvam_bin_march_kernel<1>, dim3((unsigned)nbricks), dim3(512), 0, stream, k, sb,
-                               s.vals[1], s.slot_of, s.bstart, out, nullptr, nullptr);
+            if (bin_nt == 1024)
+                hipLaunchKernelGGL((tvam_bin_march_kernel<1, 1024>), dim3((unsigned)nbricks), dim3(1024), 0, stream, k,
+                                   sb, s.vals[1], s.slot_of, s.bstart, out, nullptr, nullptr);
+            else
+                hipLaunchKernelGGL((tvam_bin_march_kernel<1, 512>), dim3((unsigned)nbricks), dim3(512), 0, stream, k,
+                                   sb, s.vals[1], s.slot_of, s.bstart, out, nullptr, nullptr);
         } else {
-            hipLaunchKernelGGL(tvam_bin_march_kernel<0>, dim3((unsigned)nbricks), dim3(512), 0, stream, k, sb,
-                               s.vals[1], s.slot_of, s.bstart, out, nullptr, nullptr);
+            if (bin_nt == 1024)
+                hipLaunchKernelGGL((tvam_bin_march_kernel<0, 1024>), dim3((unsigned)nbricks), dim3(1024), 0, stream, k,
+                                   sb, s.vals[1], s.slot_of, s.bstart, out, nullptr, nullptr);
+            else
+                hipLaunchKernelGGL((tvam_bin_march_kernel<0, 512>), dim3((unsigned)nbricks), dim3(512), 0, stream, k,
+                                   sb, s.vals[1], s.slot_of, s.bstart, out, nullptr, nullptr);
         }
         if ((e = hipGetLastError()) != hipSuccess) return e;
     }

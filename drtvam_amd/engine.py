@@ -218,6 +218,28 @@ def render(proj: Projection, active_data: torch.Tensor, active_pixels: Optional[
     return TvamRender.apply(active_data, proj, active_pixels, spp, spp_grad, seed, seed_grad)
 
 
+def loss_threshold_probes(dose: torch.Tensor, ddose: torch.Tensor, alphas, target: torch.Tensor, K: int, tl: float,
+                          tu: float, w_object: float, w_void: float, w_limit: float, scale: float) -> torch.Tensor:
+    """Fused ThresholdedLoss of dose + a * ddose for each a in alphas (<= 8): f64 device vector, one pass."""
+    lib = _abi.load_library()
+    na = len(alphas)
+    if not 1 <= na <= 8:
+        raise ValueError("loss_threshold_probes: 1 to 8 step sizes")
+    for name, t in (("dose", dose), ("ddose", ddose), ("target", target)):
+        if t.dtype != torch.float32 or not t.is_contiguous() or t.device != dose.device:
+            raise ValueError(f"{name} must be a contiguous float32 tensor on {dose.device}")
+    n = dose.numel()
+    if target.numel() != n or ddose.numel() != n:
+        raise ValueError("loss_threshold_probes: size mismatch")
+    out = torch.zeros(na, dtype=torch.float64, device=dose.device)
+    a = (ctypes.c_float * na)(*[float(v) for v in alphas])
+    with torch.cuda.device(dose.device):
+        _abi.check(lib.tvam_loss_threshold_probes(
+            dose.data_ptr(), ddose.data_ptr(), a, na, target.data_ptr(), n, int(K), float(tl), float(tu),
+            float(w_object), float(w_void), float(w_limit), float(scale), out.data_ptr(), _stream_ptr(dose.device)))
+    return out
+
+
 def loss_threshold(dose: torch.Tensor, target: torch.Tensor, K: int, tl: float, tu: float, w_object: float,
                    w_void: float, w_limit: float, scale: float, ddose: Optional[torch.Tensor] = None,
                    alpha: float = 0.0, grad: Optional[torch.Tensor] = None) -> torch.Tensor:

@@ -157,12 +157,15 @@ class FusedLinearLBFGS(LinearLBFGS):
     the dot vector over angle shards (one collective per step).
     """
 
+    probe_batch = 4  # Armijo step sizes per loss_steps pass
+
     def __init__(self, lr=1.0, m=5, params=None, render_fn=None, loss_fn=None, search_it=20, loss_step=None,
-                 allreduce=None, clamp_min=None):
+                 allreduce=None, clamp_min=None, loss_steps=None):
         if m > 7:
             raise ValueError("FusedLinearLBFGS keeps at most 7 history pairs")
         self.allreduce = allreduce
         self.clamp_min = clamp_min
+        self.loss_steps = loss_steps  # (vol, dvol, alphas, patterns) -> losses: the probes batched
         self.state = {}
         super().__init__(lr=lr, m=m, params=params, render_fn=render_fn, loss_fn=loss_fn, search_it=search_it,
                          loss_step=loss_step)
@@ -301,15 +304,32 @@ class FusedLinearLBFGS(LinearLBFGS):
         key = 'projector.active_data' if 'projector.active_data' in params else next(iter(params))
         alpha = 1.0
         steps = 0
-        for _ in range(self.search_it):
-            steps += 1
-            if self.loss_step is not None:
-                f_new = self.loss_step(vol, dvol, alpha, params[key])
-            else:
-                f_new = self.loss_fn(vol + alpha * dvol, params[key])
-            if float(f_new) <= loss_v + c1 * alpha * gdz_total:
-                break
-            alpha *= 0.5
+        if self.loss_steps is not None:
+            # the same backtracking sequence (alpha = 1, 1/2, ...; first Armijo pass wins), its
+            # probes evaluated probe_batch at a time: one loss pass and one host read per batch
+            done = False
+            while steps < self.search_it and not done:
+                nb = min(self.probe_batch, self.search_it - steps)
+                alphas = [alpha * 0.5 ** j for j in range(nb)]
+                fv = self.loss_steps(vol, dvol, alphas, params[key]).cpu().tolist()
+                for a, f_new in zip(alphas, fv):
+                    steps += 1
+                    alpha = a
+                    if f_new <= loss_v + c1 * a * gdz_total:
+                        done = True
+                        break
+                if not done:
+                    alpha *= 0.5
+        else:
+            for _ in range(self.search_it):
+                steps += 1
+                if self.loss_step is not None:
+                    f_new = self.loss_step(vol, dvol, alpha, params[key])
+                else:
+                    f_new = self.loss_fn(vol + alpha * dvol, params[key])
+                if float(f_new) <= loss_v + c1 * alpha * gdz_total:
+                    break
+                alpha *= 0.5
         self.last_alpha = alpha
         self.last_search_steps = steps
 

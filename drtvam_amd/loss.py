@@ -141,6 +141,16 @@ class ThresholdedLoss(Loss):
         s = self._sparsity_value(patterns)
         return v if s is None else v + s
 
+    def fused_values(self, x, target, patterns, dx, alphas, count=None):
+        """Losses of x + a*dx for every a in alphas (<= 8) as an f64 device vector, one kernel
+        pass (the Armijo probes of the line search; ``patterns`` / ``count`` as in fused_value)."""
+        from .engine import loss_threshold_probes
+        scale = 1.0 / (count or x.numel()) if self.reduction_name == 'mean' else 1.0
+        v = loss_threshold_probes(x.reshape(-1), dx.reshape(-1), alphas, target.reshape(-1), int(self.K), self.tl,
+                                  self.tu, self.weight_object, self.weight_void, self.weight_limit, scale)
+        s = self._sparsity_value(patterns)
+        return v if s is None else v + s
+
     def fused_value_grad(self, x, target, patterns, grad_out, count=None):
         """Loss value (f64 device scalar) and dL/dx written into grad_out, one kernel pass
         (``patterns`` / ``count`` as in fused_value)."""

@@ -210,6 +210,15 @@ class ShardedLoop:
             v = self.allreduce_(v)
         return v if s is None else v + s
 
+    def loss_steps(self, vol, dvol, alphas, patterns):
+        """loss_step for several step sizes at once (fused loss only): f64 device vector, one
+        loss pass and, on a sharded dose, one all-reduce."""
+        s = self.sparsity(patterns)
+        v = self.loss_fn.fused_values(vol, self.target, None, dvol, alphas, count=self.n_vox)
+        if self.dose_sharded:
+            v = self.allreduce_(v)
+        return v if s is None else v + s
+
     # ---- optimisation -------------------------------------------------------------
     def make_optimizer(self):
         key = 'projector.active_data'
@@ -221,7 +230,8 @@ class ShardedLoop:
         if dev.type == 'cuda' and self.fused_lbfgs:
             # three fused HIP passes per step and one all-reduce of the dot vector
             opt = FusedLinearLBFGS(render_fn=render_fn, loss_fn=None, loss_step=self.loss_step,
-                                   allreduce=self.allreduce_ if self.dist is not None else None, clamp_min=0.0)
+                                   allreduce=self.allreduce_ if self.dist is not None else None, clamp_min=0.0,
+                                   loss_steps=self.loss_steps if self.fused else None)
         else:
             opt = LinearLBFGS(render_fn=render_fn, loss_fn=None, dot=self.dot, loss_step=self.loss_step)
         opt[key] = self.x0

@@ -25,6 +25,8 @@
  *   tvam_loss_threshold<- ThresholdedLoss.__call__ loss.py:28-59, :119-132 (fused
  *                         value + dL/dx, also used for the Armijo probes of
  *                         LinearLBFGS.step lbfgs.py:256-266)
+ *   tvam_loss_threshold_probes <- the same Armijo probes, up to 8 step sizes per pass
+ *                         (lbfgs.py:255-268: one loss pass and one host read per batch)
  *   tvam_plan_destroy, tvam_last_error  <- Python exception plumbing
  *
  * All buffers are caller-owned device pointers (e.g. torch tensors' data_ptr()).
@@ -43,7 +45,7 @@
 extern "C" {
 #endif
 
-#define TVAM_ABI_VERSION 8
+#define TVAM_ABI_VERSION 9
 
 /* error codes */
 #define TVAM_OK               0
@@ -308,6 +310,20 @@ int tvam_loss_threshold(const float* dose, const float* ddose, float alpha,
                         float tl, float tu, float w_object, float w_void,
                         float w_limit, float scale, double* out, float* grad,
                         void* hip_stream);
+
+/*
+ * Armijo probes of LinearLBFGS's line search (lbfgs.py:255-268), fused: the
+ * ThresholdedLoss of dose + alphas[j] * ddose for j < n_alpha (<= 8, alphas on
+ * the host) in one pass; out[j] += the sum for alphas[j] (f64, caller zeroes
+ * out[0..n_alpha)), scaled like tvam_loss_threshold.  Per element the same
+ * arithmetic as tvam_loss_threshold with that alpha.
+ */
+int tvam_loss_threshold_probes(const float* dose, const float* ddose,
+                               const float* alphas, int32_t n_alpha,
+                               const float* target, uint64_t n, int32_t K,
+                               float tl, float tu, float w_object, float w_void,
+                               float w_limit, float scale, double* out,
+                               void* hip_stream);
 
 /* Thread-local message describing the last error ("" if none). */
 const char* tvam_last_error(void);

@@ -52,3 +52,62 @@ def test_fused_lbfgs_matches_torch(n, clamp):
     rel = np.linalg.norm(xs['fused'] - xs['torch']) / np.linalg.norm(xs['torch'])
     assert rel < 2e-3, rel
     assert hist['fused'][-1] < 0.5 * hist['fused'][0]
+
+
+def test_loss_probes_match_single_alpha():
+    """tvam_loss_threshold_probes: every step size's value equals tvam_loss_threshold's (same
+    per-element arithmetic), on float4-aligned arrays and on views off the 16-byte grid."""
+    from drtvam_amd.engine import loss_threshold, loss_threshold_probes
+    g = torch.Generator().manual_seed(3)
+    n = 1_000_003
+    dose = (torch.rand(n + 1, generator=g) * 1.2).cuda()
+    ddose = (torch.randn(n + 1, generator=g) * 0.3).cuda()
+    target = (torch.rand(n + 1, generator=g) > 0.6).float().cuda()
+    alphas = [1.0, 0.5, 0.25, 0.125, 2.0 ** -7, 3.0, 0.0, -0.5]
+    args = (2, 0.85, 0.95, 1.0, 1.0, 0.5, 1.0 / n)
+    for off in (0, 1):  # aligned, then every pointer 4 bytes off
+        d, dd, t = dose[off:off + n], ddose[off:off + n], target[off:off + n]
+        got = loss_threshold_probes(d, dd, alphas, t, *args).cpu().numpy()
+        ref = np.array([float(loss_threshold(d, t, *args, ddose=dd, alpha=a)) for a in alphas])
+        np.testing.assert_allclose(got, ref, rtol=1e-11)
+        got3 = loss_threshold_probes(d, dd, alphas[:3], t, *args).cpu().numpy()
+        np.testing.assert_allclose(got3, ref[:3], rtol=1e-11)
+    with pytest.raises(Exception):
+        loss_threshold_probes(dose[:n], ddose[:n], [1.0] * 9, target[:n], *args)
+
+
+def test_batched_probes_same_search():
+    """FusedLinearLBFGS with loss_steps (probes batched 4 per pass) takes the same step sizes,
+    probe counts and losses as the one-probe-at-a-time line search (lbfgs.py:255-268), including
+    searches longer than one batch."""
+    A, b = _problem(4096, 256, seed=5)
+    A = A * 30.0  # the first steps overshoot by far: long backtracking
+    key = 'projector.active_data'
+
+    def render(vars_):
+        return A @ vars_[key]
+
+    def loss_step(vol, dvol, alpha, p):
+        r = vol + alpha * dvol - b
+        return (r * r).sum().to(torch.float64)
+
+    def loss_steps(vol, dvol, alphas, p):
+        return torch.stack([loss_step(vol, dvol, a, p) for a in alphas])
+
+    x0 = torch.rand(4096, device='cuda') * 0.1
+    runs = {}
+    for name, ls in (('one', None), ('batched', loss_steps)):
+        opt = FusedLinearLBFGS(render_fn=render, loss_step=loss_step, clamp_min=0.0, loss_steps=ls)
+        opt[key] = x0
+        trace = []
+        for _ in range(10):
+            x = opt[key]
+            vol = A @ x.detach()
+            r = vol - b
+            x.grad = 2.0 * (A.t() @ r)
+            opt.step(vol, (r * r).sum())
+            trace.append((opt.last_alpha, opt.last_search_steps, float(((A @ opt[key].detach() - b) ** 2).sum())))
+        runs[name] = trace
+    assert [t[:2] for t in runs['batched']] == [t[:2] for t in runs['one']]
+    np.testing.assert_allclose([t[2] for t in runs['batched']], [t[2] for t in runs['one']], rtol=1e-6)
+    assert max(t[1] for t in runs['one']) > FusedLinearLBFGS.probe_batch  # a search spanning batches
