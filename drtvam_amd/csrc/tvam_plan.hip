@@ -1135,7 +1135,9 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
             slot_off[(size_t)t + 1] = (int64_t)slots.size();
             max_nrt = std::max<int64_t>(max_nrt, (int64_t)per_tile[t].size());
         }
-    } else
+    } else {
+    const bool adj_order = env_int("TVAM_ADJ_ORDER", 0) != 0 && d.regular_sampling;
+    const int adj_tw = tsx + 2 + std::max(0, env_int("TVAM_ADJ_PITCH_PAD", 0));  // = pl.adj_pitch
     for (int ty = 0; ty < nty; ++ty)
         for (int tx = 0; tx < ntx; ++tx) {
             int tile = ty * ntx + tx;
@@ -1156,11 +1158,56 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
                 int ch = std::min((int)std::ceil(c_hi) + 1 - d.crop_offset_x, d.crop_x - 1);
                 // (column order: ordering by in-tile chord length, as behind refracting vials, made the
                 // planar adjoint slower, 3.82 -> 3.96 ms on config 2)
+                if (adj_order && cl <= ch) {
+                    // TVAM_ADJ_ORDER=1: the columns dealt round-robin over the 16 LDS bank groups of
+                    // their tile-entry voxel (the planar adjoint's [z/4][voxel][4] tile: a 16-lane
+                    // group of a ds_read_b128 is conflict-free when its voxels differ mod 16), so
+                    // that 16 consecutive lanes start in 16 different groups
+                    std::vector<int> bucket[16];
+                    const double dxr = -c, dyr = -s;
+                    for (int col = cl; col <= ch; ++col) {
+                        const double lat = ex * (0.5 - ((double)(col + d.crop_offset_x) + 0.5) / W);
+                        const double px0 = lat * s, py0 = -lat * c;
+                        double tin = -1e300, tout = 1e300;
+                        auto slab = [&](double o, double dd, double a, double b) {
+                            if (std::fabs(dd) < 1e-12) {
+                                if (o < a || o > b) tout = -1e300;
+                                return;
+                            }
+                            const double t1 = (a - o) / dd, t2 = (b - o) / dd;
+                            tin = std::max(tin, std::min(t1, t2));
+                            tout = std::min(tout, std::max(t1, t2));
+                        };
+                        slab(px0, dxr, X0, X1);
+                        slab(py0, dyr, Y0, Y1);
+                        int grp = 0;
+                        if (tin < tout) {
+                            const double te = tin + 1e-6 * std::min(k.h[0], k.h[1]);
+                            const int x0v = tx * tsx, y0v = ty * tsy;
+                            int ix = (int)std::floor((px0 + te * dxr - (double)k.bmin[0]) / k.h[0]);
+                            int iy = (int)std::floor((py0 + te * dyr - (double)k.bmin[1]) / k.h[1]);
+                            ix = std::min(std::max(ix, x0v), std::min(x0v + tsx, k.res[0]) - 1);
+                            iy = std::min(std::max(iy, y0v), std::min(y0v + tsy, k.res[1]) - 1);
+                            grp = ((iy - y0v + 1) * adj_tw + (ix - x0v + 1)) & 15;
+                        }
+                        bucket[grp].push_back(col);
+                    }
+                    for (size_t r = 0;; ++r) {
+                        bool any = false;
+                        for (int b = 0; b < 16; ++b)
+                            if (r < bucket[b].size()) {
+                                slots.push_back(((uint32_t)i << 16) | (uint32_t)bucket[b][r]);
+                                any = true;
+                            }
+                        if (!any) break;
+                    }
+                } else
                 for (int col = cl; col <= ch; ++col) slots.push_back(((uint32_t)i << 16) | (uint32_t)col);
             }
             slot_off[(size_t)tile + 1] = (int64_t)slots.size();
             max_nrt = std::max<int64_t>(max_nrt, (int64_t)(slots.size() - first));
         }
+    }
     // flat slot count per workgroup must fit int32 (rows * slots * spp)
     if ((int64_t)p->max_rows_per_slice * max_nrt * 64 > (int64_t)0x7fffffff) {
         plan_free(p);
