@@ -8,6 +8,8 @@
 // were bank-conflict stalls.
 #define TVAM_TILE_PITCH(tsx) (((tsx) + 2) | 1)
 
+#include <vector>
+
 #include "tvam_common.h"
 #include "../../include/tvam.h"
 
@@ -122,6 +124,22 @@ struct TvamSegBuf {
     uint32_t* m;
 };
 
+// One chunk of forward bins kept in HBM for the next forward of the same (seed, spp): an
+// optimiser iteration renders seed i twice (the forward and the line-search forward, the
+// paths' geometry does not depend on the pattern), so the second call skips the path replay,
+// the scan, the bin fill and the sort, rescales the records' weights to the new pattern and
+// marches.  c.z of each record holds the path attenuation for that rescale.
+struct TvamBinChunk {
+    float4* r = nullptr;          // [3 * cap_slots] records
+    int64_t cap_slots = 0;
+    uint32_t* vals = nullptr;     // [cap_vals] sorted segment slots
+    int64_t cap_vals = 0;
+    uint32_t* bstart = nullptr;   // [nbricks + 1]
+    int64_t cap_bricks = 0;
+    uint32_t total = 0;
+    bool valid = false;
+};
+
 // Scratch of the binned forward (owned by the plan, grown on demand).
 struct TvamBinScratch {
     TvamSegBuf sb;
@@ -137,6 +155,12 @@ struct TvamBinScratch {
     int acc_float = 0;            // 1: float LDS adds instead of int64 fixed point (TVAM_BIN_FLOAT)
     uint32_t* slot_of = nullptr;  // [cap_entries] segment slot of each (segment, brick) entry
     float* part = nullptr;        // [cap_entries] adjoint partial of each entry
+    // forward bin cache (TvamBinChunk), keyed on the call's constants, seed, spp and chunking
+    std::vector<TvamBinChunk> fc;
+    bool fc_key = false;
+    TvamConsts fc_k{};
+    uint32_t fc_seed = 0, fc_spp = 0;
+    int64_t fc_chunk = 0, fc_npaths = 0;
 };
 
 hipError_t tvam_launch_tiles(int mode, const TvamConsts& k, const TvamTiles& t, size_t lds_bytes,

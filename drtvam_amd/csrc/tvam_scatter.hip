@@ -376,7 +376,8 @@ __global__ __launch_bounds__(256) void tvam_scatter_kernel(TvamConsts k, TvamTil
                     sb.r[3 * slot] = make_float4(q.t_start, q.tau_end, q.dtm0[0], q.dtm0[1]);
                     sb.r[3 * slot + 1] = make_float4(q.dtm0[2], q.ts[0] * (float)q.step[0], q.ts[1] * (float)q.step[1],
                                              q.ts[2] * (float)q.step[2]);
-                    sb.r[3 * slot + 2] = make_float4(__int_as_float(q.sv[0] | (q.sv[1] << 11) | (q.sv[2] << 22)), em * att, 0.0f, 0.0f);
+                    // .z: the attenuation alone, for the cached forward's rescale (tvam_bin_reweight_kernel)
+                    sb.r[3 * slot + 2] = make_float4(__int_as_float(q.sv[0] | (q.sv[1] << 11) | (q.sv[2] << 22)), em * att, att, 0.0f);
                     sb.m[slot] = (uint32_t)sc_walk_bricks(k, q, [](int, float, float) {});
                 }
             } else if (seg > 0) {
@@ -1244,6 +1245,20 @@ __global__ __launch_bounds__(256) void tvam_bin_reduce_kernel(TvamConsts k, Tvam
     }
 }
 
+// Cached forward bins, new pattern: each record's weight em * att with em of the new pattern,
+// the same expression as tvam_scatter_kernel<EMIT> (bit-identical records).  Slots without a
+// segment (m = 0) are never gathered, so rescaling their undefined contents is harmless.
+__global__ __launch_bounds__(256) void tvam_bin_reweight_kernel(TvamConsts k, TvamSegBuf sb, int spp,
+                                                                const float* __restrict__ pat) {
+    const int64_t ns = (sb.p1 - sb.p0) * sb.slots;
+    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t local = (sb.p0 + s / sb.slots) / spp;
+        const float em = pat[local] * k.wscale * k.inv_vol;
+        float* c = reinterpret_cast<float*>(&sb.r[3 * s + 2]);
+        c[1] = em * c[2];
+    }
+}
+
 template <typename T>
 hipError_t grow(T** p, int64_t& cap, int64_t need) {
     if (need <= cap) return hipSuccess;
@@ -1269,6 +1284,11 @@ void tvam_bin_scratch_free(TvamBinScratch& s) {
     (void)hipFree(s.temp);
     (void)hipFree(s.slot_of);
     (void)hipFree(s.part);
+    for (auto& c : s.fc) {
+        (void)hipFree(c.r);
+        (void)hipFree(c.vals);
+        (void)hipFree(c.bstart);
+    }
     s = TvamBinScratch{};
 }
 
@@ -1295,7 +1315,9 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
     const int spp = (int)t.spp;
     const int64_t npaths = (int64_t)t.n_shard * k.crop_y * k.crop_x * spp;
     // chunk of paths: a whole number of pixels (the adjoint reduces a pixel's samples together)
-    int64_t chunk = std::max<int64_t>(1, (int64_t)(1 << 27) / slots);  // 128M slots
+    int64_t max_slots = (int64_t)1 << 27;  // 128M slots (TVAM_BIN_CHUNK_SLOTS: smaller, for tests)
+    if (const char* v = getenv("TVAM_BIN_CHUNK_SLOTS")) max_slots = std::max<int64_t>(1, atoll(v));
+    int64_t chunk = std::max<int64_t>(1, max_slots / slots);
     chunk = std::max<int64_t>(spp, chunk / spp * spp);
     chunk = std::min(npaths, chunk);
     const int64_t nsl = chunk * slots;
@@ -1313,6 +1335,46 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
     int64_t capb = s.cap_bricks;
     if ((e = grow(&s.bstart, capb, (int64_t)nbricks + 1)) != hipSuccess) return e;
     s.cap_bricks = (int32_t)capb;
+    // forward bin cache: dense pattern sets only (a sparse set's streams follow the set), and not
+    // with skip_zero (then the paths depend on the pattern); TVAM_BIN_CACHE=0 turns it off
+    const char* cache_env = getenv("TVAM_BIN_CACHE");
+    const bool cacheable = !adj && !idxmap && !k.skip_zero && !(cache_env && atoi(cache_env) == 0);
+    if (cacheable) {
+        const bool same = s.fc_key && s.fc_seed == t.seed && s.fc_spp == t.spp && s.fc_chunk == chunk &&
+                          s.fc_npaths == npaths && std::memcmp(&s.fc_k, &k, sizeof(TvamConsts)) == 0;
+        if (!same) {
+            for (auto& c : s.fc) c.valid = false;
+            s.fc_key = true;
+            s.fc_k = k;
+            s.fc_seed = t.seed;
+            s.fc_spp = t.spp;
+            s.fc_chunk = chunk;
+            s.fc_npaths = npaths;
+        }
+        const size_t nch = (size_t)((npaths + chunk - 1) / chunk);
+        if (s.fc.size() < nch) s.fc.resize(nch);
+    }
+    // a chunk is cached while a quarter of the device memory stays free after its buffers
+    auto room = [](size_t bytes) {
+        size_t fr = 0, tot = 0;
+        return hipMemGetInfo(&fr, &tot) == hipSuccess && fr > bytes + tot / 4 + ((size_t)256 << 20);
+    };
+    // forward brick march: int64 fixed point (default) or float LDS adds (TVAM_BIN_FLOAT)
+    auto march_fwd = [&](const TvamSegBuf& sb, const uint32_t* vals, const uint32_t* bstart) {
+        const dim3 grid((unsigned)nbricks), blk(bin_nt);
+        if (s.acc_float && bin_nt == 1024)
+            hipLaunchKernelGGL((tvam_bin_march_kernel<1, 1024>), grid, blk, 0, stream, k, sb, vals, nullptr, bstart, out,
+                               nullptr, nullptr);
+        else if (s.acc_float)
+            hipLaunchKernelGGL((tvam_bin_march_kernel<1, 512>), grid, blk, 0, stream, k, sb, vals, nullptr, bstart, out,
+                               nullptr, nullptr);
+        else if (bin_nt == 1024)
+            hipLaunchKernelGGL((tvam_bin_march_kernel<0, 1024>), grid, blk, 0, stream, k, sb, vals, nullptr, bstart, out,
+                               nullptr, nullptr);
+        else
+            hipLaunchKernelGGL((tvam_bin_march_kernel<0, 512>), grid, blk, 0, stream, k, sb, vals, nullptr, bstart, out,
+                               nullptr, nullptr);
+    };
     for (int64_t p0 = 0; p0 < npaths; p0 += chunk) {
         const int64_t p1 = std::min(npaths, p0 + chunk);
         const int64_t ns = (p1 - p0) * slots;
@@ -1321,6 +1383,28 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
         sb.p1 = p1;
         sb.slots = slots;
         sb.adj = adj ? 1 : 0;
+        TvamBinChunk* cc = cacheable ? &s.fc[(size_t)(p0 / chunk)] : nullptr;
+        if (cc && cc->valid) {  // same paths as the cached chunk: new weights, then the march
+            if (cc->total == 0) continue;
+            sb.r = cc->r;
+            int64_t g = std::min<int64_t>((ns + 255) / 256, 262144);
+            hipLaunchKernelGGL(tvam_bin_reweight_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, sb, spp, pat);
+            march_fwd(sb, cc->vals, cc->bstart);
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            continue;
+        }
+        if (cc && cc->cap_slots < nsl) {
+            (void)hipFree(cc->r);
+            cc->r = nullptr;
+            cc->cap_slots = 0;
+            if (room(3 * (size_t)nsl * sizeof(float4)) &&
+                hipMalloc((void**)&cc->r, 3 * (size_t)nsl * sizeof(float4)) == hipSuccess)
+                cc->cap_slots = nsl;
+            else
+                cc->r = nullptr;
+        }
+        if (cc && !cc->r) cc = nullptr;  // no room: this chunk runs from the scratch
+        if (cc) sb.r = cc->r;
         if ((e = hipMemsetAsync(sb.m, 0, (ns + 1) * sizeof(uint32_t), stream)) != hipSuccess) return e;
         int64_t g = std::min<int64_t>((p1 - p0 + 255) / 256, 262144);
         hipLaunchKernelGGL(tvam_scatter_kernel<TVAM_MODE_EMIT>, dim3((unsigned)g), dim3(256), 0, stream, k, t, pat,
@@ -1342,7 +1426,33 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
         if ((e = hipMemcpyAsync(&total, s.off + ns, sizeof(uint32_t), hipMemcpyDeviceToHost, stream)) != hipSuccess)
             return e;
         if ((e = hipStreamSynchronize(stream)) != hipSuccess) return e;
-        if (total == 0) continue;
+        if (cc && (int64_t)total > cc->cap_vals) {
+            (void)hipFree(cc->vals);
+            cc->vals = nullptr;
+            cc->cap_vals = 0;
+            const int64_t cap = (int64_t)total + total / 8;
+            if (room((size_t)cap * sizeof(uint32_t)) &&
+                hipMalloc((void**)&cc->vals, (size_t)cap * sizeof(uint32_t)) == hipSuccess)
+                cc->cap_vals = cap;
+            else
+                cc->vals = nullptr;
+        }
+        if (cc && cc->cap_bricks < (int64_t)nbricks + 1) {
+            (void)hipFree(cc->bstart);
+            cc->bstart = nullptr;
+            cc->cap_bricks = 0;
+            if (hipMalloc((void**)&cc->bstart, ((size_t)nbricks + 1) * sizeof(uint32_t)) == hipSuccess)
+                cc->cap_bricks = (int64_t)nbricks + 1;
+            else
+                cc->bstart = nullptr;
+        }
+        // a chunk whose sorted slots find no room runs from the scratch arrays, uncached
+        const bool keep = cc && (total == 0 || (cc->vals && cc->bstart));
+        if (keep) cc->total = total;
+        if (total == 0) {
+            if (keep) cc->valid = true;
+            continue;
+        }
         if ((int64_t)total > s.cap_entries) {
             for (int i = 0; i < 2; ++i) {
                 (void)hipFree(s.keys[i]);
@@ -1378,12 +1488,14 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
         g = std::min<int64_t>((ns + 255) / 256, 262144);
         hipLaunchKernelGGL(tvam_bin_fill_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, sb, s.off, ns, s.keys[0],
                            s.vals[0], adj ? s.slot_of : nullptr);
-        if ((e = hipcub::DeviceRadixSort::SortPairs(s.temp, tb2, s.keys[0], s.keys[1], s.vals[0], s.vals[1],
+        uint32_t* vals_out = keep ? cc->vals : s.vals[1];
+        uint32_t* bstart = keep ? cc->bstart : s.bstart;
+        if ((e = hipcub::DeviceRadixSort::SortPairs(s.temp, tb2, s.keys[0], s.keys[1], s.vals[0], vals_out,
                                                     (int)total, 0, bits, stream)) != hipSuccess)
             return e;
         g = std::min<int64_t>(((int64_t)total + 256) / 256, 65536);
         hipLaunchKernelGGL(tvam_bin_start_kernel, dim3((unsigned)g), dim3(256), 0, stream, s.keys[1], (int64_t)total,
-                           nbricks, s.bstart);
+                           nbricks, bstart);
         if (adj) {
             if (bin_nt == 1024)
                 hipLaunchKernelGGL((tvam_bin_march_kernel<2, 1024>), dim3((unsigned)nbricks), dim3(1024), 0, stream, k,
@@ -1395,22 +1507,11 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
             g = std::min<int64_t>((npix + 255) / 256, 65536);
             hipLaunchKernelGGL(tvam_bin_reduce_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, sb, spp, s.off,
                                s.part, idxmap, out);
-        } else if (s.acc_float) {
-            if (bin_nt == 1024)
-                hipLaunchKernelGGL((tvam_bin_march_kernel<1, 1024>), dim3((unsigned)nbricks), dim3(1024), 0, stream, k,
-                                   sb, s.vals[1], s.slot_of, s.bstart, out, nullptr, nullptr);
-            else
-                hipLaunchKernelGGL((tvam_bin_march_kernel<1, 512>), dim3((unsigned)nbricks), dim3(512), 0, stream, k,
-                                   sb, s.vals[1], s.slot_of, s.bstart, out, nullptr, nullptr);
         } else {
-            if (bin_nt == 1024)
-                hipLaunchKernelGGL((tvam_bin_march_kernel<0, 1024>), dim3((unsigned)nbricks), dim3(1024), 0, stream, k,
-                                   sb, s.vals[1], s.slot_of, s.bstart, out, nullptr, nullptr);
-            else
-                hipLaunchKernelGGL((tvam_bin_march_kernel<0, 512>), dim3((unsigned)nbricks), dim3(512), 0, stream, k,
-                                   sb, s.vals[1], s.slot_of, s.bstart, out, nullptr, nullptr);
+            march_fwd(sb, vals_out, bstart);
         }
         if ((e = hipGetLastError()) != hipSuccess) return e;
+        if (keep) cc->valid = true;
     }
     return hipSuccess;
 }

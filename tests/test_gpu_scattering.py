@@ -148,3 +148,25 @@ def test_binned_matches_per_path(case):
     ga = Projection(d, "cuda:0").adjoint(G, n, None, spp, 7)
     gb = Projection(d2, "cuda:0").adjoint(G, n, None, spp, 7)
     assert float(torch.linalg.norm(ga - gb) / torch.linalg.norm(gb)) < 1e-5
+
+
+@pytest.mark.parametrize("chunk_slots", [None, "3000"], ids=["one-chunk", "many-chunks"])
+def test_forward_bin_cache(monkeypatch, chunk_slots):
+    """A second forward of the same seed reuses the cached brick bins (records rescaled to the new
+    pattern): bit-identical to an uncached plan, for the cached seed, a new pattern and a new seed."""
+    if chunk_slots:
+        monkeypatch.setenv("TVAM_BIN_CHUNK_SLOTS", chunk_slots)
+    d = make(vial="cylindrical", regular=False, spp=2, N=24, A=8)
+    n = d.n_patterns * d.crop_y * d.crop_x
+    rng = np.random.default_rng(6)
+    p1, p2 = (torch.as_tensor(rng.uniform(0, 0.1, n).astype(np.float32), device="cuda:0") for _ in range(2))
+    cached = Projection(d, "cuda:0")
+    got = [cached.forward(p1, None, 2, 3), cached.forward(p2, None, 2, 3), cached.forward(p1, None, 2, 3),
+           cached.forward(p2, None, 2, 4)]
+    monkeypatch.setenv("TVAM_BIN_CACHE", "0")
+    plain = Projection(d, "cuda:0")
+    want = [plain.forward(p1, None, 2, 3), plain.forward(p2, None, 2, 3), plain.forward(p1, None, 2, 3),
+            plain.forward(p2, None, 2, 4)]
+    for a, b in zip(got, want):
+        assert torch.equal(a, b)
+    assert not torch.equal(got[1], got[3])
