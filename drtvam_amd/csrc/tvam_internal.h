@@ -153,7 +153,6 @@ struct TvamBinScratch {
     void* temp = nullptr;
     size_t temp_bytes = 0;
     int acc_float = 0;            // 1: float LDS adds instead of int64 fixed point (TVAM_BIN_FLOAT)
-    uint32_t* slot_of = nullptr;  // [cap_entries] segment slot of each (segment, brick) entry
     float* part = nullptr;        // [cap_entries] adjoint partial of each entry
     // forward bin cache (TvamBinChunk), keyed on the call's constants, seed, spp and chunking
     std::vector<TvamBinChunk> fc;

@@ -1062,17 +1062,20 @@ __device__ __forceinline__ void sc_unpack(const float4 a, const float4 b, const 
 }
 
 // (brick, entry) pairs; an entry is one (segment, brick) crossing, entries of
-// a segment are contiguous from off[slot] (slot_of maps them back).
+// a segment are contiguous from off[slot].  The value is the segment slot; the
+// adjoint (jshift > 0) also stores the crossing's index j along its segment in the
+// key bits above the sorted ones, so the brick kernel writes its partial to entry
+// off[slot] + j without a slot_of gather on the record's dependency chain.
 __global__ __launch_bounds__(256) void tvam_bin_fill_kernel(TvamConsts k, TvamSegBuf sb, const uint32_t* __restrict__ off,
                                                             int64_t nslots, uint32_t* __restrict__ keys,
-                                                            uint32_t* __restrict__ vals,
-                                                            uint32_t* __restrict__ slot_of) {
+                                                            uint32_t* __restrict__ vals, int jshift) {
     for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nslots; s += (int64_t)gridDim.x * blockDim.x) {
         if (sb.m[s] == 0) continue;
         SegDda q;
         float w;
         sc_unpack(sb.r[3 * s], sb.r[3 * s + 1], sb.r[3 * s + 2], q, w);
-        uint32_t o = off[s];
+        const uint32_t o0 = off[s];
+        uint32_t o = o0;
         // visits per unit length: one per voxel-face crossing of each moving axis
         float rate = 0.0f;
 #pragma unroll
@@ -1081,25 +1084,19 @@ __global__ __launch_bounds__(256) void tvam_bin_fill_kernel(TvamConsts k, TvamSe
             // low key bits: a class of the predicted in-brick visit count, so that the lanes of a
             // wave of the brick kernel march entries of similar length
             const int cls = (int)fminf((float)(TVAM_BIN_CLASSES - 1), fmaxf(t1 - t0, 0.0f) * rate * 0.25f);
-            keys[o] = ((uint32_t)bid << TVAM_BIN_CLASS_BITS) | (uint32_t)cls;
-            // forward: the value is the segment slot itself (the brick kernel reads the record
-            // without a slot_of gather); adjoint: the entry, whose partial the pixel reduce sums
-            if (slot_of) {
-                vals[o] = o;
-                slot_of[o] = (uint32_t)s;
-            } else {
-                vals[o] = (uint32_t)s;
-            }
+            const uint32_t jb = jshift > 0 ? (o - o0) << jshift : 0u;
+            keys[o] = ((uint32_t)bid << TVAM_BIN_CLASS_BITS) | (uint32_t)cls | jb;
+            vals[o] = (uint32_t)s;
             ++o;
         });
     }
 }
 
-__global__ void tvam_bin_start_kernel(const uint32_t* __restrict__ keys, int64_t n, int nbricks,
+__global__ void tvam_bin_start_kernel(const uint32_t* __restrict__ keys, int64_t n, int nbricks, uint32_t kmask,
                                       uint32_t* __restrict__ bstart) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += (int64_t)gridDim.x * blockDim.x) {
-        const int kc = i < n ? (int)(keys[i] >> TVAM_BIN_CLASS_BITS) : nbricks;
-        const int kp = i > 0 ? (int)(keys[i - 1] >> TVAM_BIN_CLASS_BITS) : -1;
+        const int kc = i < n ? (int)((keys[i] & kmask) >> TVAM_BIN_CLASS_BITS) : nbricks;
+        const int kp = i > 0 ? (int)((keys[i - 1] & kmask) >> TVAM_BIN_CLASS_BITS) : -1;
         for (int b = kp + 1; b <= kc; ++b) bstart[b] = (uint32_t)i;  // bricks (kp, kc] start here
     }
 }
@@ -1110,11 +1107,13 @@ __global__ void tvam_bin_start_kernel(const uint32_t* __restrict__ keys, int64_t
 // single add and the int64 sums cannot overflow; ACC 1: float adds): the brick's visits
 // added in LDS, then dose += tile (the brick is this launch's alone).
 // Adjoint (ACC 2): the brick's grad * inv_vol staged in LDS, each entry's
-// weighted gather written to part[entry] (no atomics; summed per path later).
+// weighted gather written to part[off[slot] + j] (no atomics; summed per path later;
+// j from the key bits above jshift).
 template <int ACC, int NT>
 __global__ __launch_bounds__(NT) void tvam_bin_march_kernel(TvamConsts k, TvamSegBuf sb,
                                                              const uint32_t* __restrict__ vals,
-                                                             const uint32_t* __restrict__ slot_of,
+                                                             const uint32_t* __restrict__ keys,
+                                                             const uint32_t* __restrict__ off, int jshift,
                                                              const uint32_t* __restrict__ bstart,
                                                              float* __restrict__ dose, const float* __restrict__ gin,
                                                              float* __restrict__ part) {
@@ -1163,32 +1162,32 @@ __global__ __launch_bounds__(NT) void tvam_bin_march_kernel(TvamConsts k, TvamSe
         }
         __syncthreads();
     }
-    // Three-stage load pipeline over this thread's entries e, e + S, e + 2S, ... (S = NT): while
-    // entry e marches, the record of e + S, the slot of e + 2S and the entry id of e + 3S are in
-    // flight (the chain vals -> slot_of -> record is three dependent gathers).
+    // Two-stage load pipeline over this thread's entries e, e + S, e + 2S, ... (S = NT): while
+    // entry e marches, the record (and the adjoint's entry base off[slot]) of e + S and the slot of
+    // e + 2S are in flight (vals -> record is two dependent gathers).
     constexpr uint32_t S = NT;
     const uint32_t et = e0 + threadIdx.x;
-    // forward (ACC 0 / 1): vals hold the slots themselves
-    auto slot_at = [&](uint32_t v) { return ACC == 2 ? slot_of[v] : v; };
-    uint32_t v2 = et + 2 * S < e1 ? vals[et + 2 * S] : 0u;
-    uint32_t s1 = et + S < e1 ? slot_at(vals[et + S]) : 0u;
-    uint32_t s0 = et < e1 ? slot_at(vals[et]) : 0u;
+    uint32_t s1 = et + S < e1 ? vals[et + S] : 0u;
+    const uint32_t s0 = et < e1 ? vals[et] : 0u;
     float4 na = make_float4(0.0f, 0.0f, 0.0f, 0.0f), nb = na;
     float4 nc = na;
+    uint32_t nof = 0u;
     if (et < e1) {
         na = sb.r[3 * s0];
         nb = sb.r[3 * s0 + 1];
         nc = sb.r[3 * s0 + 2];
+        if (ACC == 2) nof = off[s0];
     }
     for (uint32_t e = et; e < e1; e += S) {
         const float4 ca = na, cb = nb, cc = nc;
+        const uint32_t cof = nof;
         if (e + S < e1) {
             na = sb.r[3 * s1];
             nb = sb.r[3 * s1 + 1];
             nc = sb.r[3 * s1 + 2];
+            if (ACC == 2) nof = off[s1];
         }
-        s1 = e + 2 * S < e1 ? slot_at(v2) : 0u;
-        v2 = e + 3 * S < e1 ? vals[e + 3 * S] : 0u;
+        s1 = e + 2 * S < e1 ? vals[e + 2 * S] : 0u;
         SegDda q;
         float w;
         sc_unpack(ca, cb, cc, q, w);
@@ -1204,7 +1203,7 @@ __global__ __launch_bounds__(NT) void tvam_bin_march_kernel(TvamConsts k, TvamSe
             else
                 acc = fmaf(c, ftile[li], acc);
         });
-        if (ACC == 2) part[vals[e]] = w * acc;
+        if (ACC == 2) part[cof + (keys[e] >> jshift)] = w * acc;
     }
     if (ACC == 2) return;
     __syncthreads();
@@ -1282,7 +1281,6 @@ void tvam_bin_scratch_free(TvamBinScratch& s) {
     }
     (void)hipFree(s.bstart);
     (void)hipFree(s.temp);
-    (void)hipFree(s.slot_of);
     (void)hipFree(s.part);
     for (auto& c : s.fc) {
         (void)hipFree(c.r);
@@ -1312,6 +1310,13 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
     int bits = 1;
     while ((1 << bits) < nbricks) ++bits;
     bits += TVAM_BIN_CLASS_BITS;
+    // adjoint keys carry the crossing index along the segment above the sorted bits (a straight
+    // segment crosses fewer than nbx + nby + nbz bricks)
+    int jbits = 1;
+    while ((1 << jbits) < nbx + nby + nbz) ++jbits;
+    if (bits + jbits > 32) return hipErrorNotSupported;
+    const int jshift = adj ? bits : 0;
+    const uint32_t kmask = bits >= 32 ? 0xffffffffu : ((1u << bits) - 1u);
     const int spp = (int)t.spp;
     const int64_t npaths = (int64_t)t.n_shard * k.crop_y * k.crop_x * spp;
     // chunk of paths: a whole number of pixels (the adjoint reduces a pixel's samples together)
@@ -1363,16 +1368,16 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
     auto march_fwd = [&](const TvamSegBuf& sb, const uint32_t* vals, const uint32_t* bstart) {
         const dim3 grid((unsigned)nbricks), blk(bin_nt);
         if (s.acc_float && bin_nt == 1024)
-            hipLaunchKernelGGL((tvam_bin_march_kernel<1, 1024>), grid, blk, 0, stream, k, sb, vals, nullptr, bstart, out,
+            hipLaunchKernelGGL((tvam_bin_march_kernel<1, 1024>), grid, blk, 0, stream, k, sb, vals, nullptr, nullptr, 0, bstart, out,
                                nullptr, nullptr);
         else if (s.acc_float)
-            hipLaunchKernelGGL((tvam_bin_march_kernel<1, 512>), grid, blk, 0, stream, k, sb, vals, nullptr, bstart, out,
+            hipLaunchKernelGGL((tvam_bin_march_kernel<1, 512>), grid, blk, 0, stream, k, sb, vals, nullptr, nullptr, 0, bstart, out,
                                nullptr, nullptr);
         else if (bin_nt == 1024)
-            hipLaunchKernelGGL((tvam_bin_march_kernel<0, 1024>), grid, blk, 0, stream, k, sb, vals, nullptr, bstart, out,
+            hipLaunchKernelGGL((tvam_bin_march_kernel<0, 1024>), grid, blk, 0, stream, k, sb, vals, nullptr, nullptr, 0, bstart, out,
                                nullptr, nullptr);
         else
-            hipLaunchKernelGGL((tvam_bin_march_kernel<0, 512>), grid, blk, 0, stream, k, sb, vals, nullptr, bstart, out,
+            hipLaunchKernelGGL((tvam_bin_march_kernel<0, 512>), grid, blk, 0, stream, k, sb, vals, nullptr, nullptr, 0, bstart, out,
                                nullptr, nullptr);
     };
     for (int64_t p0 = 0; p0 < npaths; p0 += chunk) {
@@ -1459,9 +1464,7 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
                 (void)hipFree(s.vals[i]);
                 s.keys[i] = s.vals[i] = nullptr;
             }
-            (void)hipFree(s.slot_of);
             (void)hipFree(s.part);
-            s.slot_of = nullptr;
             s.part = nullptr;
             s.cap_entries = 0;
             const int64_t cap = (int64_t)total + total / 4;
@@ -1469,9 +1472,7 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
                 if ((e = hipMalloc((void**)&s.keys[i], cap * sizeof(uint32_t))) != hipSuccess ||
                     (e = hipMalloc((void**)&s.vals[i], cap * sizeof(uint32_t))) != hipSuccess)
                     return e;
-            if ((e = hipMalloc((void**)&s.slot_of, cap * sizeof(uint32_t))) != hipSuccess ||
-                (e = hipMalloc((void**)&s.part, cap * sizeof(float))) != hipSuccess)
-                return e;
+            if ((e = hipMalloc((void**)&s.part, cap * sizeof(float))) != hipSuccess) return e;
             s.cap_entries = cap;
         }
         size_t tb2 = 0;
@@ -1487,7 +1488,7 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
         }
         g = std::min<int64_t>((ns + 255) / 256, 262144);
         hipLaunchKernelGGL(tvam_bin_fill_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, sb, s.off, ns, s.keys[0],
-                           s.vals[0], adj ? s.slot_of : nullptr);
+                           s.vals[0], jshift);
         uint32_t* vals_out = keep ? cc->vals : s.vals[1];
         uint32_t* bstart = keep ? cc->bstart : s.bstart;
         if ((e = hipcub::DeviceRadixSort::SortPairs(s.temp, tb2, s.keys[0], s.keys[1], s.vals[0], vals_out,
@@ -1495,14 +1496,14 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
             return e;
         g = std::min<int64_t>(((int64_t)total + 256) / 256, 65536);
         hipLaunchKernelGGL(tvam_bin_start_kernel, dim3((unsigned)g), dim3(256), 0, stream, s.keys[1], (int64_t)total,
-                           nbricks, bstart);
+                           nbricks, kmask, bstart);
         if (adj) {
             if (bin_nt == 1024)
                 hipLaunchKernelGGL((tvam_bin_march_kernel<2, 1024>), dim3((unsigned)nbricks), dim3(1024), 0, stream, k,
-                                   sb, s.vals[1], s.slot_of, s.bstart, nullptr, gin, s.part);
+                                   sb, s.vals[1], s.keys[1], s.off, jshift, s.bstart, nullptr, gin, s.part);
             else
                 hipLaunchKernelGGL((tvam_bin_march_kernel<2, 512>), dim3((unsigned)nbricks), dim3(512), 0, stream, k,
-                                   sb, s.vals[1], s.slot_of, s.bstart, nullptr, gin, s.part);
+                                   sb, s.vals[1], s.keys[1], s.off, jshift, s.bstart, nullptr, gin, s.part);
             const int64_t npix = (p1 - p0) / spp;
             g = std::min<int64_t>((npix + 255) / 256, 65536);
             hipLaunchKernelGGL(tvam_bin_reduce_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, sb, spp, s.off,
