@@ -122,6 +122,7 @@ struct TvamSegBuf {
     int32_t adj;                  // records for the adjoint (weight att * wscale)
     float4* r;                    // [slots][3] segment records (48 B, one cache-line span per gather)
     uint32_t* m;
+    uint32_t* wmax;               // forward: max |record weight| of the chunk (float bits, atomicMax)
 };
 
 // One chunk of forward bins kept in HBM for the next forward of the same (seed, spp): an

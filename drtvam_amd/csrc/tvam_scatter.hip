@@ -314,7 +314,10 @@ __global__ __launch_bounds__(256) void tvam_scatter_kernel(TvamConsts k, TvamTil
     const float st = k.sig_t, ss = k.sig_s;
     const int nsurf = k.vial_type == 0 ? 1 : 2;  // glass vials: two surfaces before the medium
     uint64_t nvis = 0;
+    float wmax = 0.0f;  // EMIT (forward): largest |record weight| of this thread's paths
     for (int64_t i = i0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        if (MODE == TVAM_MODE_EMIT && !sb.adj)  // slots without a segment: attenuation 0 (the cache's rescale)
+            for (int q = 0; q < sb.slots; ++q) reinterpret_cast<float*>(&sb.r[3 * ((i - sb.p0) * sb.slots + q) + 2])[2] = 0.0f;
         const int64_t local = i / spp;
         const int smp = (int)(i - local * spp);
         float em = 1.0f;
@@ -379,6 +382,7 @@ __global__ __launch_bounds__(256) void tvam_scatter_kernel(TvamConsts k, TvamTil
                     // .z: the attenuation alone, for the cached forward's rescale (tvam_bin_reweight_kernel)
                     sb.r[3 * slot + 2] = make_float4(__int_as_float(q.sv[0] | (q.sv[1] << 11) | (q.sv[2] << 22)), em * att, att, 0.0f);
                     sb.m[slot] = (uint32_t)sc_walk_bricks(k, q, [](int, float, float) {});
+                    wmax = fmaxf(wmax, fabsf(em * att));
                 }
             } else if (seg > 0) {
                 const float r = sc_dda<MODE>(k, px, py, pz, vx, vy, vz, tsi, em * att, out, gin, nvis);
@@ -409,6 +413,10 @@ __global__ __launch_bounds__(256) void tvam_scatter_kernel(TvamConsts k, TvamTil
     if (MODE == TVAM_MODE_COUNT) {
         for (int off = 32; off > 0; off >>= 1) nvis += __shfl_down(nvis, off, 64);
         if ((threadIdx.x & 63) == 0 && nvis) atomicAdd(counter, (unsigned long long)nvis);
+    }
+    if (MODE == TVAM_MODE_EMIT && !sb.adj) {
+        for (int off = 32; off > 0; off >>= 1) wmax = fmaxf(wmax, __shfl_xor(wmax, off, 64));
+        if ((threadIdx.x & 63) == 0 && wmax > 0.0f) atomicMax(sb.wmax, __float_as_uint(wmax));
     }
 }
 
@@ -1119,7 +1127,6 @@ __global__ __launch_bounds__(NT) void tvam_bin_march_kernel(TvamConsts k, TvamSe
                                                              float* __restrict__ part) {
     constexpr int NV = TVAM_BX * TVAM_BY * TVAM_BZ;
     __shared__ __attribute__((aligned(16))) unsigned char smem[NV * (ACC == 0 ? 8 : 4)];
-    __shared__ float red[NT / 64];
     long long* ltile = reinterpret_cast<long long*>(smem);
     float* ftile = reinterpret_cast<float*>(smem);
     const int nbx = sc_nbr(k, 0), nby = sc_nbr(k, 1);
@@ -1133,15 +1140,11 @@ __global__ __launch_bounds__(NT) void tvam_bin_march_kernel(TvamConsts k, TvamSe
     const int sy = TVAM_BX, sz = TVAM_BX * TVAM_BY;
     float scale = 1.0f;
     if (ACC == 0) {
-        // per-add bound: each add rounds to int32 (one v_cvt), the int64 sums cannot overflow
-        float sw = 0.0f;
-        for (uint32_t e = e0 + threadIdx.x; e < e1; e += NT) sw = fmaxf(sw, fabsf(sb.r[3 * vals[e] + 2].y));
-        for (int o = 32; o > 0; o >>= 1) sw = fmaxf(sw, __shfl_xor(sw, o, 64));
-        if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = sw;
+        // per-add bound: each add rounds to int32 (one v_cvt), the int64 sums cannot overflow; the
+        // chunk's largest |weight| (from the record writer: no gather pass over the brick's entries)
         for (int i = threadIdx.x; i < NV; i += NT) ltile[i] = 0;
         __syncthreads();
-        float tot = 0.0f;
-        for (int w = 0; w < NT / 64; ++w) tot = fmaxf(tot, red[w]);
+        const float tot = __uint_as_float(*sb.wmax);
         const float hmax = fmaxf(fmaxf(k.h[0], k.h[1]), k.h[2]);
         const float bound = tot * fminf(1.0f, k.sig_t * 1.7320508f * hmax) * 1.001f;
         if (bound > 0.0f && isfinite(bound)) {
@@ -1245,17 +1248,22 @@ __global__ __launch_bounds__(256) void tvam_bin_reduce_kernel(TvamConsts k, Tvam
 }
 
 // Cached forward bins, new pattern: each record's weight em * att with em of the new pattern,
-// the same expression as tvam_scatter_kernel<EMIT> (bit-identical records).  Slots without a
-// segment (m = 0) are never gathered, so rescaling their undefined contents is harmless.
+// the same expression as tvam_scatter_kernel<EMIT> (bit-identical records), and the chunk's
+// largest |weight| (slots without a segment carry attenuation 0: the same max as EMIT's).
 __global__ __launch_bounds__(256) void tvam_bin_reweight_kernel(TvamConsts k, TvamSegBuf sb, int spp,
                                                                 const float* __restrict__ pat) {
     const int64_t ns = (sb.p1 - sb.p0) * sb.slots;
+    float wmax = 0.0f;
     for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += (int64_t)gridDim.x * blockDim.x) {
         const int64_t local = (sb.p0 + s / sb.slots) / spp;
         const float em = pat[local] * k.wscale * k.inv_vol;
         float* c = reinterpret_cast<float*>(&sb.r[3 * s + 2]);
-        c[1] = em * c[2];
+        const float w = em * c[2];  // c[2] = 0 for slots without a segment
+        c[1] = w;
+        wmax = fmaxf(wmax, fabsf(w));
     }
+    for (int off = 32; off > 0; off >>= 1) wmax = fmaxf(wmax, __shfl_xor(wmax, off, 64));
+    if ((threadIdx.x & 63) == 0 && wmax > 0.0f) atomicMax(sb.wmax, __float_as_uint(wmax));
 }
 
 template <typename T>
@@ -1274,6 +1282,7 @@ hipError_t grow(T** p, int64_t& cap, int64_t need) {
 void tvam_bin_scratch_free(TvamBinScratch& s) {
     (void)hipFree(s.sb.r);
     (void)hipFree(s.sb.m);
+    (void)hipFree(s.sb.wmax);
     (void)hipFree(s.off);
     for (int i = 0; i < 2; ++i) {
         (void)hipFree(s.keys[i]);
@@ -1333,7 +1342,8 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
         s.acc_float = keep_float;
         if ((e = hipMalloc((void**)&s.sb.r, 3 * nsl * sizeof(float4))) != hipSuccess ||
             (e = hipMalloc((void**)&s.sb.m, (nsl + 1) * sizeof(uint32_t))) != hipSuccess ||
-            (e = hipMalloc((void**)&s.off, (nsl + 1) * sizeof(uint32_t))) != hipSuccess)
+            (e = hipMalloc((void**)&s.off, (nsl + 1) * sizeof(uint32_t))) != hipSuccess ||
+            (e = hipMalloc((void**)&s.sb.wmax, sizeof(uint32_t))) != hipSuccess)
             return e;
         s.cap_slots = nsl;
     }
@@ -1388,6 +1398,7 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
         sb.p1 = p1;
         sb.slots = slots;
         sb.adj = adj ? 1 : 0;
+        if (!adj && (e = hipMemsetAsync(sb.wmax, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
         TvamBinChunk* cc = cacheable ? &s.fc[(size_t)(p0 / chunk)] : nullptr;
         if (cc && cc->valid) {  // same paths as the cached chunk: new weights, then the march
             if (cc->total == 0) continue;
