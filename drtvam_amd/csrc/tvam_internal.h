@@ -111,7 +111,6 @@ enum TvamMode { TVAM_MODE_FWD = 0, TVAM_MODE_ADJ = 1, TVAM_MODE_COUNT = 2, TVAM_
 // brick-bin sort keys: brick id << TVAM_BIN_CLASS_BITS | class of the entry's predicted in-brick
 // visit count (entries of one brick run in class order: similar march lengths per wave)
 #define TVAM_BIN_CLASS_BITS 4
-#define TVAM_BIN_CLASSES (1 << TVAM_BIN_CLASS_BITS)
 
 // Scattered segments of paths [p0, p1): `slots` records per path
 // (a = {t_start, tau_end, dtm0_x, dtm0_y}, b = {dtm0_z, +-ts_x, +-ts_y, +-ts_z},

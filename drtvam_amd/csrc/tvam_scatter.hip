@@ -1076,7 +1076,7 @@ __device__ __forceinline__ void sc_unpack(const float4 a, const float4 b, const 
 // off[slot] + j without a slot_of gather on the record's dependency chain.
 __global__ __launch_bounds__(256) void tvam_bin_fill_kernel(TvamConsts k, TvamSegBuf sb, const uint32_t* __restrict__ off,
                                                             int64_t nslots, uint32_t* __restrict__ keys,
-                                                            uint32_t* __restrict__ vals, int jshift) {
+                                                            uint32_t* __restrict__ vals, int jshift, int cbits) {
     for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nslots; s += (int64_t)gridDim.x * blockDim.x) {
         if (sb.m[s] == 0) continue;
         SegDda q;
@@ -1091,9 +1091,10 @@ __global__ __launch_bounds__(256) void tvam_bin_fill_kernel(TvamConsts k, TvamSe
         sc_walk_bricks(k, q, [&](int bid, float t0, float t1) {
             // low key bits: a class of the predicted in-brick visit count, so that the lanes of a
             // wave of the brick kernel march entries of similar length
-            const int cls = (int)fminf((float)(TVAM_BIN_CLASSES - 1), fmaxf(t1 - t0, 0.0f) * rate * 0.25f);
+            // classes of 4 visits (16 classes) or 8 (8 classes)
+            const int cls = (int)fminf((float)((1 << cbits) - 1), fmaxf(t1 - t0, 0.0f) * rate * (0.015625f * (float)(1 << cbits)));
             const uint32_t jb = jshift > 0 ? (o - o0) << jshift : 0u;
-            keys[o] = ((uint32_t)bid << TVAM_BIN_CLASS_BITS) | (uint32_t)cls | jb;
+            keys[o] = ((uint32_t)bid << cbits) | (uint32_t)cls | jb;
             vals[o] = (uint32_t)s;
             ++o;
         });
@@ -1101,10 +1102,10 @@ __global__ __launch_bounds__(256) void tvam_bin_fill_kernel(TvamConsts k, TvamSe
 }
 
 __global__ void tvam_bin_start_kernel(const uint32_t* __restrict__ keys, int64_t n, int nbricks, uint32_t kmask,
-                                      uint32_t* __restrict__ bstart) {
+                                      int cbits, uint32_t* __restrict__ bstart) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += (int64_t)gridDim.x * blockDim.x) {
-        const int kc = i < n ? (int)((keys[i] & kmask) >> TVAM_BIN_CLASS_BITS) : nbricks;
-        const int kp = i > 0 ? (int)((keys[i - 1] & kmask) >> TVAM_BIN_CLASS_BITS) : -1;
+        const int kc = i < n ? (int)((keys[i] & kmask) >> cbits) : nbricks;
+        const int kp = i > 0 ? (int)((keys[i - 1] & kmask) >> cbits) : -1;
         for (int b = kp + 1; b <= kc; ++b) bstart[b] = (uint32_t)i;  // bricks (kp, kc] start here
     }
 }
@@ -1318,7 +1319,11 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
     }();
     int bits = 1;
     while ((1 << bits) < nbricks) ++bits;
-    bits += TVAM_BIN_CLASS_BITS;
+    // length classes: 16, or 8 where that keeps the sort key within 16 bits (two radix passes
+    // instead of three; config 4: 4225 bricks); TVAM_BIN_CBITS overrides (2..4)
+    int cbits = bits <= 12 ? 4 : (bits == 13 ? 3 : TVAM_BIN_CLASS_BITS);
+    if (const char* v = getenv("TVAM_BIN_CBITS")) cbits = std::min(4, std::max(2, atoi(v)));
+    bits += cbits;
     // adjoint keys carry the crossing index along the segment above the sorted bits (a straight
     // segment crosses fewer than nbx + nby + nbz bricks)
     int jbits = 1;
@@ -1499,7 +1504,7 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
         }
         g = std::min<int64_t>((ns + 255) / 256, 262144);
         hipLaunchKernelGGL(tvam_bin_fill_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, sb, s.off, ns, s.keys[0],
-                           s.vals[0], jshift);
+                           s.vals[0], jshift, cbits);
         uint32_t* vals_out = keep ? cc->vals : s.vals[1];
         uint32_t* bstart = keep ? cc->bstart : s.bstart;
         if ((e = hipcub::DeviceRadixSort::SortPairs(s.temp, tb2, s.keys[0], s.keys[1], s.vals[0], vals_out,
@@ -1507,7 +1512,7 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
             return e;
         g = std::min<int64_t>(((int64_t)total + 256) / 256, 65536);
         hipLaunchKernelGGL(tvam_bin_start_kernel, dim3((unsigned)g), dim3(256), 0, stream, s.keys[1], (int64_t)total,
-                           nbricks, kmask, bstart);
+                           nbricks, kmask, cbits, bstart);
         if (adj) {
             if (bin_nt == 1024)
                 hipLaunchKernelGGL((tvam_bin_march_kernel<2, 1024>), dim3((unsigned)nbricks), dim3(1024), 0, stream, k,
