@@ -18,6 +18,7 @@ contiguous blocks, dose all-reduced over RCCL twice per iteration, L-BFGS
 dots all-reduced.  Rank 0 prints one JSON line.
 """
 import argparse
+import gc
 import json
 import os
 import sys
@@ -155,7 +156,7 @@ def make_roofline(args, N, A, world, prob, visits, rays, fwd_s):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=2,
                     help="BASELINE.json configs[1] (2: index-matched, the metric's workload), configs[2] "
@@ -273,6 +274,9 @@ def main():
     for i in range(args.warmup):
         prob.iteration(i)
         log(f"[rank {rank}] warmup {i} loss {prob.loss_hist[-1]:.6e}")
+    # as drtvam_amd.optimize.main's loop: long-lived setup objects out of the cyclic GC
+    gc.collect()
+    gc.freeze()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()

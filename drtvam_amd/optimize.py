@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import argparse
 import ctypes
+import gc
 import json
 import os
 import time
@@ -574,6 +575,10 @@ def optimize(config, patterns_fwd=None, device=None):
         return psf_analysis(prob, config, output)
     else:
         print("Optimizing patterns...")
+        # the scene, plan and tensors live for the whole loop: keep them out of the cyclic GC's
+        # generations (a full collection mid-loop stalls the host between two launches)
+        gc.collect()
+        gc.freeze()
         for i in range(prob.n_steps):
             t0 = time.perf_counter()
             loss = prob.iteration(i)
