@@ -158,6 +158,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--prewarm", type=float, default=1.0,
+                    help="seconds of untimed forward projections before the warmup iterations (GPU and host "
+                         "clocks of a fresh box ramp up; the optimiser state is not touched)")
     ap.add_argument("--config", type=int, choices=[2, 3, 4, 5], default=2,
                     help="BASELINE.json configs[1] (2: index-matched, the metric's workload), configs[2] "
                          "(3: cylindrical vial, refraction) or configs[3] (4: cylindrical vial, scattering "
@@ -271,6 +274,14 @@ def main():
     if orig_slices is not None:
         prob.proj.forward_slices = timed_slices
 
+    t_pre = time.perf_counter()
+    n_pre = 0
+    while n_pre == 0 or time.perf_counter() - t_pre < args.prewarm:
+        prob.forward_local(prob.x0, 0)  # this rank's projection only: no collective, state untouched
+        torch.cuda.synchronize()
+        n_pre += 1
+        if args.prewarm <= 0:
+            break
     for i in range(args.warmup):
         prob.iteration(i)
         log(f"[rank {rank}] warmup {i} loss {prob.loss_hist[-1]:.6e}")
@@ -372,7 +383,7 @@ def main():
                             f"z-slab x{world} (film slabs + DMD row bands, scalar all-reduces only)"
                             if prob.shard == "slab" else
                             f"angle-shard x{world} + {'RCCL' if args.backend == 'nccl' else 'gloo'} dose all-reduce"),
-            "zero_skip": bool(args.zero_skip), "tile": prob.proj.desc.tile,
+            "zero_skip": bool(args.zero_skip), "prewarm_forwards": n_pre, "tile": prob.proj.desc.tile,
             "filter_radon": ({"active": prob.n_filtered, "of": prob.n_global} if prob.active_pixels is not None
                              else None),
             "fwd_ms": fwd_avg * 1e3, "adj_ms": adj_avg * 1e3, "visits_per_pass": visits, "rays_per_pass": rays,
