@@ -1027,10 +1027,11 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
 
     // tile geometry: LDS-resident xy tile of one z-slice
     auto pick = [&](int res) {
-        // measured optimum (400^3 / 400 angles): the planar adjoint (regular sampling, 8
-        // interleaved slices in LDS) at <= 48 (45 at 400: two 71 KB tiles per CU), the
-        // per-ray tile kernels at 64
-        int ts = d.tile > 0 ? d.tile : (d.regular_sampling && !(d.flags & TVAM_FLAG_NO_PLANAR) ? 48 : 64);
+        // measured optima: the planar adjoint (regular sampling, 8 interleaved slices in LDS) at
+        // <= 48 (45 at 400^3: two 71 KB tiles per CU); the per-ray tile kernels of the jittered
+        // configs at 73 (config 5, 800^3: 11 tiles of 73 -> 3.15 s per iteration vs 3.35 s at 13
+        // tiles of 62, 3.24 s at 80, 3.50 s at 89; config 4: 6 tiles of 67 within 1 % of 5 of 80)
+        int ts = d.tile > 0 ? d.tile : (d.regular_sampling && !(d.flags & TVAM_FLAG_NO_PLANAR) ? 48 : 73);
         int nt = (res + ts - 1) / ts;
         return (res + nt - 1) / nt;
     };
