@@ -105,9 +105,15 @@ hipError_t tvam_launch_fwd_rays_planar(const TvamConsts& k, const TvamPlanar& pl
 enum TvamMode { TVAM_MODE_FWD = 0, TVAM_MODE_ADJ = 1, TVAM_MODE_COUNT = 2, TVAM_MODE_EMIT = 3 };
 
 // Brick of the binned scattered-segment forward (LDS int64 tile: 128 KB)
+#ifndef TVAM_BX
 #define TVAM_BX 32
+#endif
+#ifndef TVAM_BY
 #define TVAM_BY 32
+#endif
+#ifndef TVAM_BZ
 #define TVAM_BZ 16
+#endif
 // brick-bin sort keys: brick id << TVAM_BIN_CLASS_BITS | class of the entry's predicted in-brick
 // visit count (entries of one brick run in class order: similar march lengths per wave)
 #define TVAM_BIN_CLASS_BITS 4

@@ -1319,9 +1319,9 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
     }();
     int bits = 1;
     while ((1 << bits) < nbricks) ++bits;
-    // length classes: 16, or 8 where that keeps the sort key within 16 bits (two radix passes
+    // length classes: 16, or 8 / 4 where that keeps the sort key within 16 bits (two radix passes
     // instead of three; config 4: 4225 bricks); TVAM_BIN_CBITS overrides (2..4)
-    int cbits = bits <= 12 ? 4 : (bits == 13 ? 3 : TVAM_BIN_CLASS_BITS);
+    int cbits = bits <= 14 ? std::min(4, 16 - bits) : TVAM_BIN_CLASS_BITS;
     if (const char* v = getenv("TVAM_BIN_CBITS")) cbits = std::min(4, std::max(2, atoi(v)));
     bits += cbits;
     // adjoint keys carry the crossing index along the segment above the sorted bits (a straight
