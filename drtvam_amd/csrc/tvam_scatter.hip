@@ -1197,16 +1197,24 @@ __global__ __launch_bounds__(NT) void tvam_bin_march_kernel(TvamConsts k, TvamSe
         sc_unpack(ca, cb, cc, q, w);
         const float ws = w * scale;
         float acc = 0.0f;
+        // adjoint: each visit's LDS value is consumed one visit later, so its read latency overlaps
+        // the next DDA step (the sum keeps its order: bit-identical)
+        float pc = 0.0f, pv = 0.0f;
         sc_box_march(k, q, lo, hi, [&](int x, int y, int z, float c) {
             const int li = z * sz + y * sy + x;
-            if (ACC == 0)
+            if (ACC == 0) {
                 __hip_atomic_fetch_add(&ltile[li], (long long)__float2int_rn(ws * c), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
-            else if (ACC == 1)
+            } else if (ACC == 1) {
                 __hip_atomic_fetch_add(&ftile[li], w * c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            else
-                acc = fmaf(c, ftile[li], acc);
+            } else {
+                const float v = ftile[li];
+                acc = fmaf(pc, pv, acc);
+                pc = c;
+                pv = v;
+            }
         });
+        if (ACC == 2) acc = fmaf(pc, pv, acc);
         if (ACC == 2) part[cof + (keys[e] >> jshift)] = w * acc;
     }
     if (ACC == 2) return;
