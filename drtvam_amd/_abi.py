@@ -12,7 +12,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TVAM_LIB") or os.path.join(_HERE, "libtvam.so")  # TVAM_LIB: a variant build
 
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 TVAM_OK = 0
 TVAM_ERR_INVALID = -1
@@ -149,6 +149,7 @@ EXPORTS = {
     "tvam_plan_stats": (ctypes.c_int, [_P, ctypes.POINTER(ctypes.c_uint64)]),
     "tvam_discretize": (ctypes.c_int, [ctypes.POINTER(TvamDesc), _P, _P]),
     "tvam_plan_fwd_scale": (ctypes.c_int, [_P, _P]),
+    "tvam_plan_bin_stats": (ctypes.c_int, [_P, _P]),
     "tvam_loss_threshold": (
         ctypes.c_int,
         [_P, _P, ctypes.c_float, _P, ctypes.c_uint64, ctypes.c_int32, ctypes.c_float, ctypes.c_float,

@@ -166,6 +166,9 @@ struct TvamBinScratch {
     TvamConsts fc_k{};
     uint32_t fc_seed = 0, fc_spp = 0;
     int64_t fc_chunk = 0, fc_npaths = 0;
+    // last call's chunking (tvam_plan_bin_stats): chunks, chunks served from the cache,
+    // chunks stored into it, brick entries sorted, paths per chunk
+    int64_t st[5] = {0, 0, 0, 0, 0};
 };
 
 hipError_t tvam_launch_tiles(int mode, const TvamConsts& k, const TvamTiles& t, size_t lds_bytes,

@@ -1712,6 +1712,12 @@ extern "C" int tvam_plan_stats(tvam_plan* p, uint64_t* fallback_tiles) {
     return 0;
 }
 
+extern "C" int tvam_plan_bin_stats(tvam_plan* p, int64_t* stats) {
+    if (!p || !stats) return fail(TVAM_ERR_INVALID, "null argument");
+    for (int i = 0; i < 5; ++i) stats[i] = p->bins.st[i];
+    return 0;
+}
+
 extern "C" int tvam_loss_threshold(const float* dose, const float* ddose, float alpha, const float* target, uint64_t n,
                                    int32_t K, float tl, float tu, float w_object, float w_void, float w_limit,
                                    float scale, double* out, float* grad, void* stream) {

@@ -1403,9 +1403,12 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
             hipLaunchKernelGGL((tvam_bin_march_kernel<0, 512>), grid, blk, 0, stream, k, sb, vals, nullptr, nullptr, 0, bstart, out,
                                nullptr, nullptr);
     };
+    for (int i = 0; i < 5; ++i) s.st[i] = 0;
+    s.st[4] = chunk;
     for (int64_t p0 = 0; p0 < npaths; p0 += chunk) {
         const int64_t p1 = std::min(npaths, p0 + chunk);
         const int64_t ns = (p1 - p0) * slots;
+        ++s.st[0];
         TvamSegBuf sb = s.sb;
         sb.p0 = p0;
         sb.p1 = p1;
@@ -1414,6 +1417,8 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
         if (!adj && (e = hipMemsetAsync(sb.wmax, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
         TvamBinChunk* cc = cacheable ? &s.fc[(size_t)(p0 / chunk)] : nullptr;
         if (cc && cc->valid) {  // same paths as the cached chunk: new weights, then the march
+            ++s.st[1];
+            s.st[3] += cc->total;
             if (cc->total == 0) continue;
             sb.r = cc->r;
             int64_t g = std::min<int64_t>((ns + 255) / 256, 262144);
@@ -1478,6 +1483,8 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
         // a chunk whose sorted slots find no room runs from the scratch arrays, uncached
         const bool keep = cc && (total == 0 || (cc->vals && cc->bstart));
         if (keep) cc->total = total;
+        if (keep) ++s.st[2];
+        s.st[3] += total;
         if (total == 0) {
             if (keep) cc->valid = true;
             continue;

@@ -576,17 +576,21 @@ def optimize(config, patterns_fwd=None, device=None):
     else:
         print("Optimizing patterns...")
         # the scene, plan and tensors live for the whole loop: keep them out of the cyclic GC's
-        # generations (a full collection mid-loop stalls the host between two launches)
+        # generations (a full collection mid-loop stalls the host between two launches); unfrozen
+        # afterwards, so the problem's prob <-> opt cycle and its plans are collected on return
         gc.collect()
         gc.freeze()
-        for i in range(prob.n_steps):
-            t0 = time.perf_counter()
-            loss = prob.iteration(i)
-            torch.cuda.synchronize()
-            prob.timing.append(time.perf_counter() - t0)
-            if loss == 0.0:
-                print("Converged")
-                break
+        try:
+            for i in range(prob.n_steps):
+                t0 = time.perf_counter()
+                loss = prob.iteration(i)
+                torch.cuda.synchronize()
+                prob.timing.append(time.perf_counter() - t0)
+                if loss == 0.0:
+                    print("Converged")
+                    break
+        finally:
+            gc.unfreeze()
     print("Rendering final state...")
     vol_final = prob.final_render()
     pats = prob.gather_patterns(prob.patterns_local().float())

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define TVAM_ABI_VERSION 9
+#define TVAM_ABI_VERSION 10
 
 /* error codes */
 #define TVAM_OK               0
@@ -253,6 +253,13 @@ int tvam_discretize(const tvam_desc* desc, float* occ, void* hip_stream);
    |every voxel's scaled sum| < 2^30 guaranteed, scale[1] = 1 (exact int32 fixed point)
    or 0 (the bound was not finite: float LDS adds). */
 int tvam_plan_fwd_scale(tvam_plan* plan, float* scale);
+
+/* Diagnostics (host-synchronous): the chunking of the last brick-binned call of a plan with
+   a scattering medium (the later segments of every path, tvam_scatter.hip).  stats[0] =
+   chunks of paths, [1] = chunks served from the forward bin cache (weights rescaled to the
+   new pattern, no replay / sort), [2] = chunks stored into the cache, [3] = brick entries
+   marched, [4] = paths per chunk.  All 0 when the plan's last call binned nothing.  (ABI v10) */
+int tvam_plan_bin_stats(tvam_plan* plan, int64_t* stats);
 
 /* Surface-aware plans: the per-channel voxel volumes the forward divides by and the
    adjoint multiplies the incoming gradient with (inv_vol = 1/volume, 0 where volume

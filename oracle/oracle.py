@@ -57,6 +57,11 @@ def lib():
         L.oracle_frozen_axes.argtypes = [ctypes.c_int]
         L.oracle_discretize.restype = ctypes.c_int
         L.oracle_discretize.argtypes = [D, P, ctypes.c_int]
+        L.oracle_forward_streams.restype = ctypes.c_int
+        L.oracle_forward_streams.argtypes = [D, P, P, P, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_uint32, P, P,
+                                             ctypes.c_int]
+        L.oracle_adjoint_streams.restype = ctypes.c_int
+        L.oracle_adjoint_streams.argtypes = L.oracle_forward_streams.argtypes
         L.oracle_dda_ray.restype = ctypes.c_int
         L.oracle_dda_ray.argtypes = [D, P, P, ctypes.c_float, ctypes.c_double, P, P]
         _lib = L
@@ -72,13 +77,23 @@ def film_shape(desc):
     return (rz, ry, rx)
 
 
-def forward(desc, active_data, active_pixels=None, spp=1, seed=0, nthreads=1, part=-1):
+def forward(desc, active_data, active_pixels=None, spp=1, seed=0, nthreads=1, part=-1, streams=None):
     """Dose [z, y, x] (float64) and the DDA visit count of one forward pass.
-    Scattering media: part=1 keeps only each path's first medium segment, part=0 the rest."""
+    Scattering media: part=1 keeps only each path's first medium segment, part=0 the rest.
+    streams: per active entry, its position in a larger set (sampler streams streams[i] * spp + k):
+    a subset of a plan's dense shard traced with the shard's own streams."""
     data = np.ascontiguousarray(active_data, dtype=np.float32)
     pix = None if active_pixels is None else np.ascontiguousarray(active_pixels, dtype=np.uint32)
     dose = np.zeros(film_shape(desc), dtype=np.float64)
     visits = ctypes.c_uint64(0)
+    if streams is not None:
+        st = np.ascontiguousarray(streams, dtype=np.uint64)
+        assert pix is not None and st.size == data.size == pix.size and part == -1
+        rc = lib().oracle_forward_streams(ctypes.byref(desc), _ptr(data), _ptr(pix), _ptr(st), data.size, spp, seed,
+                                          _ptr(dose), ctypes.cast(ctypes.byref(visits), ctypes.c_void_p), nthreads)
+        if rc:
+            raise ValueError(f"oracle_forward_streams failed ({rc})")
+        return dose, visits.value
     rc = lib().oracle_forward_part(ctypes.byref(desc), _ptr(data), _ptr(pix), data.size, spp, seed, _ptr(dose),
                                    ctypes.cast(ctypes.byref(visits), ctypes.c_void_p), nthreads, part)
     if rc:
@@ -86,14 +101,22 @@ def forward(desc, active_data, active_pixels=None, spp=1, seed=0, nthreads=1, pa
     return dose, visits.value
 
 
-def adjoint(desc, grad_dose, active_pixels=None, n_active=None, spp=1, seed=0, nthreads=1):
-    """Gradient w.r.t. active_data (float64) of <grad_dose, forward(.)>."""
+def adjoint(desc, grad_dose, active_pixels=None, n_active=None, spp=1, seed=0, nthreads=1, streams=None):
+    """Gradient w.r.t. active_data (float64) of <grad_dose, forward(.)>.  streams: as in forward()."""
     g = np.ascontiguousarray(grad_dose, dtype=np.float32).reshape(film_shape(desc))
     pix = None if active_pixels is None else np.ascontiguousarray(active_pixels, dtype=np.uint32)
     if n_active is None:
         n_active = pix.size if pix is not None else desc.n_patterns * desc.crop_y * desc.crop_x
     out = np.zeros(n_active, dtype=np.float64)
     visits = ctypes.c_uint64(0)
+    if streams is not None:
+        st = np.ascontiguousarray(streams, dtype=np.uint64)
+        assert pix is not None and st.size == pix.size == n_active
+        rc = lib().oracle_adjoint_streams(ctypes.byref(desc), _ptr(g), _ptr(pix), _ptr(st), n_active, spp, seed,
+                                          _ptr(out), ctypes.cast(ctypes.byref(visits), ctypes.c_void_p), nthreads)
+        if rc:
+            raise ValueError(f"oracle_adjoint_streams failed ({rc})")
+        return out, visits.value
     rc = lib().oracle_adjoint(ctypes.byref(desc), _ptr(g), _ptr(pix), n_active, spp, seed, _ptr(out),
                               ctypes.cast(ctypes.byref(visits), ctypes.c_void_p), nthreads)
     if rc:

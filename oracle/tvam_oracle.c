@@ -1198,7 +1198,7 @@ int oracle_radon(const tvam_desc* d, const float* tgt, int ntgt, uint32_t spp, u
 /* ------------------------------------------------------------------------ */
 static int or_forward_impl(const tvam_desc* d, const float* active_data, const uint32_t* active_pixels,
                            uint64_t n_active, uint32_t spp, uint32_t seed, double* dose, uint64_t* visits,
-                           int nthreads, int part, const float* inv_volumes) {
+                           int nthreads, int part, const float* inv_volumes, const uint64_t* streams) {
     int rc = or_check(d);
     if (rc) return rc;
     if (d->regular_sampling) spp = 1;
@@ -1233,7 +1233,7 @@ static int or_forward_impl(const tvam_desc* d, const float* active_data, const u
             for (int64_t i = 0; i < (int64_t)n_active; ++i) {
                 uint32_t pixel = or_pixel(d, active_pixels, (uint64_t)i);
                 double em = (double)active_data[i] * wr;
-                uint64_t st = or_stream(d, active_pixels, (uint64_t)i);
+                uint64_t st = streams ? streams[i] : or_stream(d, active_pixels, (uint64_t)i);
                 for (uint32_t k = 0; k < spp; ++k)
                     or_trace(&s, pixel, st * spp + k, seed, em, priv ? 0 : 3, mine, NULL, -1, &nv_total);
             }
@@ -1247,7 +1247,7 @@ static int or_forward_impl(const tvam_desc* d, const float* active_data, const u
         for (uint64_t i = 0; i < n_active; ++i) {
             uint32_t pixel = or_pixel(d, active_pixels, i);
             double em = (double)active_data[i] * wr;
-            uint64_t st = or_stream(d, active_pixels, (uint64_t)i);
+            uint64_t st = streams ? streams[i] : or_stream(d, active_pixels, (uint64_t)i);
             for (uint32_t k = 0; k < spp; ++k)
                 or_trace(&s, pixel, st * spp + k, seed, em, 0, dose, NULL, -1, &nv_total);
         }
@@ -1292,7 +1292,7 @@ static int or_forward_impl(const tvam_desc* d, const float* active_data, const u
                     uint64_t i = row_idx[j];
                     uint32_t pixel = or_pixel(d, active_pixels, i);
                     double em = (double)active_data[i] * wr;
-                    uint64_t st = or_stream(d, active_pixels, (uint64_t)i);
+                    uint64_t st = streams ? streams[i] : or_stream(d, active_pixels, (uint64_t)i);
                     for (uint32_t q = 0; q < spp; ++q)
                         or_trace(&s, pixel, st * spp + q, seed, em, 0, dose, NULL, k, &nv_total);
                 }
@@ -1312,7 +1312,7 @@ static int or_forward_impl(const tvam_desc* d, const float* active_data, const u
 int oracle_forward_part(const tvam_desc* d, const float* active_data, const uint32_t* active_pixels,
                         uint64_t n_active, uint32_t spp, uint32_t seed, double* dose, uint64_t* visits,
                         int nthreads, int part) {
-    return or_forward_impl(d, active_data, active_pixels, n_active, spp, seed, dose, visits, nthreads, part, NULL);
+    return or_forward_impl(d, active_data, active_pixels, n_active, spp, seed, dose, visits, nthreads, part, NULL, NULL);
 }
 
 /* Surface-aware forward: dose [V][2] = film / volume per channel (inv_volumes [V][2]). */
@@ -1320,7 +1320,7 @@ int oracle_forward_surface(const tvam_desc* d, const float* active_data, const u
                            uint64_t n_active, uint32_t spp, uint32_t seed, const float* inv_volumes, double* dose,
                            uint64_t* visits, int nthreads) {
     return or_forward_impl(d, active_data, active_pixels, n_active, spp, seed, dose, visits, nthreads, -1,
-                           inv_volumes);
+                           inv_volumes, NULL);
 }
 
 int oracle_forward(const tvam_desc* d, const float* active_data, const uint32_t* active_pixels,
@@ -1337,7 +1337,7 @@ int oracle_phase(const tvam_desc* d, const float* dd, float u1, float u2, float*
 
 static int or_adjoint_impl(const tvam_desc* d, const float* grad_dose, const uint32_t* active_pixels,
                            uint64_t n_active, uint32_t spp, uint32_t seed, double* grad, uint64_t* visits,
-                           int nthreads, const float* inv_volumes) {
+                           int nthreads, const float* inv_volumes, const uint64_t* streams) {
     int rc = or_check(d);
     if (rc) return rc;
     if (d->regular_sampling) spp = 1;
@@ -1360,7 +1360,7 @@ static int or_adjoint_impl(const tvam_desc* d, const float* grad_dose, const uin
     for (int64_t i = 0; i < (int64_t)n_active; ++i) {
         uint32_t pixel = or_pixel(d, active_pixels, (uint64_t)i);
         double g = 0.0;
-        uint64_t st = or_stream(d, active_pixels, (uint64_t)i);
+        uint64_t st = streams ? streams[i] : or_stream(d, active_pixels, (uint64_t)i);
         for (uint32_t k = 0; k < spp; ++k)
             g += or_trace(&s, pixel, st * spp + k, seed, 1.0, 1, NULL, dl, -1, &nv_total);
         grad[i] = wr * g;
@@ -1373,13 +1373,30 @@ static int or_adjoint_impl(const tvam_desc* d, const float* grad_dose, const uin
 int oracle_adjoint(const tvam_desc* d, const float* grad_dose, const uint32_t* active_pixels,
                    uint64_t n_active, uint32_t spp, uint32_t seed, double* grad, uint64_t* visits,
                    int nthreads) {
-    return or_adjoint_impl(d, grad_dose, active_pixels, n_active, spp, seed, grad, visits, nthreads, NULL);
+    return or_adjoint_impl(d, grad_dose, active_pixels, n_active, spp, seed, grad, visits, nthreads, NULL, NULL);
 }
 
 int oracle_adjoint_surface(const tvam_desc* d, const float* grad_dose, const uint32_t* active_pixels,
                            uint64_t n_active, uint32_t spp, uint32_t seed, const float* inv_volumes, double* grad,
                            uint64_t* visits, int nthreads) {
-    return or_adjoint_impl(d, grad_dose, active_pixels, n_active, spp, seed, grad, visits, nthreads, inv_volumes);
+    return or_adjoint_impl(d, grad_dose, active_pixels, n_active, spp, seed, grad, visits, nthreads, inv_volumes, NULL);
+}
+
+/* Test infrastructure: the forward / adjoint of a subset of a larger set's pixels, each
+   active entry i drawing the sampler streams streams[i]*spp .. +spp-1 of its position in the
+   larger set (common.py:57-67, :81).  A test can thus check the pixels it picks out of a
+   plan's whole dense shard without the oracle tracing every path of the shard. */
+int oracle_forward_streams(const tvam_desc* d, const float* active_data, const uint32_t* active_pixels,
+                           const uint64_t* streams, uint64_t n_active, uint32_t spp, uint32_t seed, double* dose,
+                           uint64_t* visits, int nthreads) {
+    return or_forward_impl(d, active_data, active_pixels, n_active, spp, seed, dose, visits, nthreads, -1, NULL,
+                           streams);
+}
+
+int oracle_adjoint_streams(const tvam_desc* d, const float* grad_dose, const uint32_t* active_pixels,
+                           const uint64_t* streams, uint64_t n_active, uint32_t spp, uint32_t seed, double* grad,
+                           uint64_t* visits, int nthreads) {
+    return or_adjoint_impl(d, grad_dose, active_pixels, n_active, spp, seed, grad, visits, nthreads, NULL, streams);
 }
 
 /* ------------------------------------------------------------------------ */

@@ -156,17 +156,30 @@ def test_forward_bin_cache(monkeypatch, chunk_slots):
     pattern): bit-identical to an uncached plan, for the cached seed, a new pattern and a new seed."""
     if chunk_slots:
         monkeypatch.setenv("TVAM_BIN_CHUNK_SLOTS", chunk_slots)
+    import gc
+    gc.collect()  # plans of earlier tests (their bin caches) and torch's cached blocks: the cache
+    torch.cuda.empty_cache()  # stores a chunk only while a quarter of the device memory stays free
     d = make(vial="cylindrical", regular=False, spp=2, N=24, A=8)
+    d.flags |= _abi.FLAG_NO_ZERO_SKIP  # the cache serves dense sets without zero skipping (as bench.py)
     n = d.n_patterns * d.crop_y * d.crop_x
     rng = np.random.default_rng(6)
     p1, p2 = (torch.as_tensor(rng.uniform(0, 0.1, n).astype(np.float32), device="cuda:0") for _ in range(2))
     cached = Projection(d, "cuda:0")
     got = [cached.forward(p1, None, 2, 3), cached.forward(p2, None, 2, 3), cached.forward(p1, None, 2, 3),
            cached.forward(p2, None, 2, 4)]
+    st = cached.bin_stats()
+    assert st["chunks"] >= (2 if chunk_slots else 1) and st["cached"] == 0 and st["stored"] == st["chunks"]
+    # a cached call after the seed change: seed 4's records overwrote seed 3's in the same cache
+    # buffers, and slots without a seed-4 segment must carry attenuation 0, not seed 3's (ADVICE r2)
+    got.append(cached.forward(p1, None, 2, 4))
+    st = cached.bin_stats()
+    assert st["cached"] == st["chunks"] >= 1, st
+    print("bin stats", st)
     monkeypatch.setenv("TVAM_BIN_CACHE", "0")
     plain = Projection(d, "cuda:0")
     want = [plain.forward(p1, None, 2, 3), plain.forward(p2, None, 2, 3), plain.forward(p1, None, 2, 3),
-            plain.forward(p2, None, 2, 4)]
+            plain.forward(p2, None, 2, 4), plain.forward(p1, None, 2, 4)]
+    assert plain.bin_stats()["cached"] == 0
     for a, b in zip(got, want):
         assert torch.equal(a, b)
     assert not torch.equal(got[1], got[3])

@@ -211,3 +211,27 @@ def test_scattered_part_matches_analog_mc(oracle):
     pz = np.mean(prof, axis=0)
     pa = analog.sum(axis=(1, 2)) / (1 - d.albedo)
     assert np.linalg.norm(pz - pa) / np.linalg.norm(pa) < 0.1
+
+
+def test_subset_streams_match_whole_set(oracle):
+    """oracle.forward / adjoint with `streams` (the subset entries' positions in the whole dense
+    set) reproduce the whole set's per-pixel adjoint and, for patterns that vanish off the
+    subset, its forward exactly: the checker of tests/test_gpu_bin_chunks.py."""
+    d = scene(N=16, A=6, regular=False, spp=2, vial="cylindrical", max_depth=6)
+    n = d.n_patterns * d.crop_y * d.crop_x
+    sub = np.arange(3, n, 7)
+    pix = np.arange(n, dtype=np.uint32)[sub]  # crop = the whole DMD here
+    pat = np.zeros(n, np.float32)
+    pat[sub] = np.random.default_rng(1).uniform(0.0, 0.1, sub.size)
+    G = np.random.default_rng(2).uniform(-1, 1, (16, 16, 16)).astype(np.float32)
+    d.active_total = n  # the subset's rays are weighted by the whole set's size
+    whole, _ = oracle.forward(d, pat, spp=2, seed=9, nthreads=1)
+    part, _ = oracle.forward(d, pat[sub], active_pixels=pix, spp=2, seed=9, nthreads=1, streams=sub)
+    assert whole.sum() > 0
+    np.testing.assert_allclose(part, whole, rtol=0, atol=1e-12 * np.abs(whole).max())
+    gw, _ = oracle.adjoint(d, G, spp=2, seed=9, nthreads=2)
+    gs, _ = oracle.adjoint(d, G, active_pixels=pix, spp=2, seed=9, nthreads=2, streams=sub)
+    np.testing.assert_array_equal(gs, gw[sub])
+    # without streams the subset would draw the streams of positions 0 .. |sub| - 1
+    g0, _ = oracle.adjoint(d, G, active_pixels=pix, spp=2, seed=9, nthreads=2)
+    assert not np.array_equal(g0, gw[sub])
