@@ -320,9 +320,12 @@ def main():
     if args.emulate:
         ew = int(args.emulate.split("/")[1])
         ms = elapsed / args.steps * 1e3
-        rec = {"emulate": args.emulate, "shard": prob.shard, "ms_per_step": ms,
-               "fwd_ms": fwd_avg * 1e3, "adj_ms": adj_avg * 1e3, "visits_per_pass": visits,
-               "slices": [prob.z0, prob.z1], "rows": [prob.r0, prob.r1], "angles": [prob.a0, prob.a1]}
+        rec = {"emulate": args.emulate, "shard": prob.shard, "config": args.config, "n": N,
+               "ms_per_step": ms, "fwd_ms": fwd_avg * 1e3, "adj_ms": adj_avg * 1e3, "visits_per_pass": visits,
+               "slices": [prob.z0, prob.z1], "rows": [prob.r0, prob.r1], "angles": [prob.a0, prob.a1],
+               "device_mem_used_bytes": (lambda fr_tot: fr_tot[1] - fr_tot[0])(torch.cuda.mem_get_info(dev))}
+        if prob.proj.desc.albedo != 0.0:  # scattering: the brick-bin chunking and its device memory
+            rec["bins"] = prob.proj.bin_stats()
         if prob.shard == "angle" and ew > 1:
             # two ring all-reduces of the full dose per iteration (main forward + line-search forward):
             # each moves 2 (W - 1) / W of the film per rank at the RCCL bus bandwidth --ar-gbs.  When the

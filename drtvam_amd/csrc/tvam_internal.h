@@ -63,6 +63,17 @@ struct TvamPlanar {
     int32_t adj_nt;            // adjoint: threads per workgroup (256 or 512)
     int32_t adj_planes;        // adjoint: gradient tile as Z/4 planes [z/4][voxel][4] (else interleaved [voxel][z])
     int32_t adj_w2;            // adjoint: degree-2 visit weights where vox_chord < TVAM_W2_MAX
+    // adjoint: per (tile, step quadrant) ray lists (adj_quad = 1, tvam_plan.hip adj_quadrant_lists).
+    // With the gradient tile's row pitch = +1 (mod 16) for rays whose x and y steps have equal
+    // signs and -1 (mod 16) for opposite signs, every visit moves a lane's 16-byte LDS chunk by
+    // the same +-1, so the lanes of a wave keep their entry chunks' differences: each 16-lane group
+    // of a ds_read_b128 is dealt rays of distinct entry chunks mod 16 (conflict-free throughout)
+    // and similar in-tile lengths.  Lists padded to whole waves with 0xffffffff.
+    const uint32_t* adj_qslots;
+    const int64_t* adj_qoff;   // [ntiles * 4 + 1]
+    int32_t adj_quad;
+    int32_t adj_pitch2;        // row pitch of quadrants 1, 2 (opposite step signs); adj_pitch: 0, 3
+    int32_t rayfwd_pitch;      // ray-driven forward: LDS row pitch of its dose tile (>= tile + 2)
     int32_t rayfwd_nt;         // ray-driven forward: threads per workgroup (256 or 512)
     int32_t fwd_parts;         // forward: angle parts per (tile, slice chunk) (thin slabs; 1 = none)
     int32_t fwd_ab;            // forward: angles per barrier (1 or 2)
@@ -169,6 +180,7 @@ struct TvamBinScratch {
     // last call's chunking (tvam_plan_bin_stats): chunks, chunks served from the cache,
     // chunks stored into it, brick entries sorted, paths per chunk
     int64_t st[5] = {0, 0, 0, 0, 0};
+    int64_t temp_cap() const { return (int64_t)temp_bytes; }
 };
 
 hipError_t tvam_launch_tiles(int mode, const TvamConsts& k, const TvamTiles& t, size_t lds_bytes,

@@ -85,6 +85,8 @@ struct tvam_plan {
     float4* d_pl_rec_f = nullptr;
     int32_t* d_pl_rec_i = nullptr;
     float4* d_pl_rec_g = nullptr;
+    uint32_t* d_adjq_slots = nullptr;  // planar adjoint: per (tile, quadrant) ray lists
+    int64_t* d_adjq_off = nullptr;
     float* d_pl_part = nullptr;  // voxel-driven forward: partial doses of the angle parts
     float* d_pl_bin = nullptr;   // voxel-driven forward: slice-binned patterns
     float4* d_pl_vox2 = nullptr;      // refracted voxel-driven forward: per-column 1/d, flags, weight
@@ -164,6 +166,8 @@ static void plan_free(tvam_plan* p) {
     (void)hipFree(p->d_pl_rec_f);
     (void)hipFree(p->d_pl_rec_i);
     (void)hipFree(p->d_pl_rec_g);
+    (void)hipFree(p->d_adjq_slots);
+    (void)hipFree(p->d_adjq_off);
     (void)hipFree(p->d_pl_part);
     (void)hipFree(p->d_pl_bin);
     (void)hipFree(p->d_pl_vox2);
@@ -332,6 +336,131 @@ static int fwd_buffers(tvam_plan* p);
 static int choose_fwd_z(tvam_plan* p);
 static int refr_fwd_setup(tvam_plan* p, const std::vector<int32_t>& off);
 
+// Planar adjoint ray lists per (tile, step quadrant) (TvamPlanar::adj_quad).  The gradient tile
+// is [z/4][voxel][4] with voxel = (y + 1) * pitch + x + 1, one 16-byte chunk per voxel and read;
+// a ds_read_b128 is served in four 16-lane groups ({0-3, 12-15, 20-27}, {4-11, 16-19, 28-31},
+// + 32), each conflict-free when its lanes' chunks differ mod 16.  With pitch = +1 (mod 16) for
+// quadrants whose x and y steps have equal signs and -1 (mod 16) otherwise, every step moves a
+// lane's chunk by the same +-1 in one quadrant, so lanes that enter a tile at distinct chunks mod
+// 16 stay distinct for the whole march.  Per (tile, quadrant): the rays in (angle, column) order,
+// blocks of 256 sorted by predicted in-tile visits (lane balance), each block dealt into waves
+// whose 16-lane groups take rays of distinct entry chunks first.  The entry voxel and the visit
+// count come from the plan's own ray records with the kernel's closed-form resume
+// (tvam_axis_window / tvam_axis_steps), so the residues are exact.  Host model of the gain:
+// tools/lds_bank_model2.py (config 2: LDS cycles 2.65 -> 1.45 x the conflict-free full-wave cost).
+static int adj_quadrant_lists(tvam_plan* p) {
+    const TvamConsts& k = p->k;
+    const TvamTiles& t = p->tiles;
+    const int ns = p->pl.ns, ntiles = t.ntx * t.nty;
+    const size_t nrec = (size_t)ns * k.crop_x;
+    std::vector<float4> rf(nrec), rg, ang((size_t)std::max(ns, 1));
+    std::vector<int32_t> ri(nrec);
+    std::vector<int64_t> off((size_t)ntiles + 1);
+    hipError_t e;
+    if ((e = hipMemcpy(rf.data(), p->d_pl_rec_f, nrec * sizeof(float4), hipMemcpyDeviceToHost)) != hipSuccess ||
+        (e = hipMemcpy(ri.data(), p->d_pl_rec_i, nrec * sizeof(int32_t), hipMemcpyDeviceToHost)) != hipSuccess ||
+        (e = hipMemcpy(off.data(), p->d_slot_off, off.size() * sizeof(int64_t), hipMemcpyDeviceToHost)) != hipSuccess ||
+        (ns > 0 && (e = hipMemcpy(ang.data(), p->d_ang, (size_t)ns * sizeof(float4), hipMemcpyDeviceToHost)) != hipSuccess))
+        return hip_fail(e, "hipMemcpy (adjoint lists)");
+    if (p->d_pl_rec_g) {
+        rg.resize(nrec);
+        if ((e = hipMemcpy(rg.data(), p->d_pl_rec_g, nrec * sizeof(float4), hipMemcpyDeviceToHost)) != hipSuccess)
+            return hip_fail(e, "hipMemcpy (adjoint lists)");
+    }
+    std::vector<uint32_t> slots((size_t)off[ntiles]);
+    if (!slots.empty() &&
+        (e = hipMemcpy(slots.data(), p->d_slot_off ? p->d_slots : nullptr, slots.size() * sizeof(uint32_t),
+                       hipMemcpyDeviceToHost)) != hipSuccess)
+        return hip_fail(e, "hipMemcpy (adjoint lists)");
+    const int tw1 = p->pl.adj_pitch, tw2 = p->pl.adj_pitch2;
+    static const int G[4][16] = {{0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
+                                 {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31},
+                                 {32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59},
+                                 {36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63}};
+    constexpr uint32_t PAD = 0xffffffffu;
+    const int W = std::max(64, env_int("TVAM_ADJ_QBLOCK", 256)) / 64 * 64;
+    const bool qsort = env_int("TVAM_ADJ_QSORT", 1) != 0, qdeal = env_int("TVAM_ADJ_QDEAL", 1) != 0;
+    struct Ray { uint32_t e; int len, res; };
+    std::vector<uint32_t> out;
+    std::vector<int64_t> qoff((size_t)ntiles * 4 + 1, 0);
+    std::vector<Ray> q[4];
+    for (int tile = 0; tile < ntiles; ++tile) {
+        const int x0 = (tile % t.ntx) * t.tsx, y0 = (tile / t.ntx) * t.tsy;
+        const int x1 = std::min(x0 + t.tsx, k.res[0]), y1 = std::min(y0 + t.tsy, k.res[1]);
+        for (auto& v : q) v.clear();
+        for (int64_t j = off[tile]; j < off[tile + 1]; ++j) {
+            const uint32_t ev = slots[(size_t)j];
+            const int al = (int)(ev >> 16), colc = (int)(ev & 0xffffu);
+            const size_t r = (size_t)al * k.crop_x + colc;
+            const int rv = ri[r];
+            if (rv < 0) continue;  // misses the vial / grid (the kernel skips it)
+            const float4 ff = rf[r];
+            float4 an = ang[(size_t)al];
+            if (!rg.empty()) {
+                const float4 gg = rg[r];
+                an = make_float4(std::fabs(gg.x), std::fabs(gg.y), gg.x < 0.0f ? -1.0f : 1.0f, gg.y < 0.0f ? -1.0f : 1.0f);
+            }
+            const int svx = rv & 0xffff, svy = rv >> 16, stx = (int)an.z, sty = (int)an.w;
+            float tin0, tout0, tin1, tout1;
+            int nin0, nout0, nin1, nout1;
+            tvam_axis_window(svx, stx, ff.z, an.x, x0, x1, tin0, tout0, nin0, nout0);
+            tvam_axis_window(svy, sty, ff.w, an.y, y0, y1, tin1, tout1, nin1, nout1);
+            const float tau_e = std::max(std::max(tin0, tin1), 0.0f);
+            const float tau_x = std::min(std::min(tout0, tout1), ff.y);
+            if (!(tau_e < tau_x)) continue;  // does not cross this tile (the kernel skips it)
+            const int n0 = tvam_axis_steps(tau_e, ff.z, an.x, nin0, nout0);
+            const int n1 = tvam_axis_steps(tau_e, ff.w, an.y, nin1, nout1);
+            const int m0 = tvam_axis_steps(tau_x, ff.z, an.x, nin0, nout0);
+            const int m1 = tvam_axis_steps(tau_x, ff.w, an.y, nin1, nout1);
+            const int vx = svx + stx * n0, vy = svy + sty * n1;
+            const int qd = (stx < 0 ? 2 : 0) + (sty < 0 ? 1 : 0);
+            const int tw = (qd == 0 || qd == 3) ? tw1 : tw2;
+            const int res = ((vy - y0 + 1) * tw + (vx - x0 + 1)) & 15;
+            q[qd].push_back({ev, std::abs(m0 - n0) + std::abs(m1 - n1) + 1, res});
+        }
+        for (int qd = 0; qd < 4; ++qd) {
+            std::vector<Ray>& v = q[qd];
+            for (size_t b0 = 0; b0 < v.size(); b0 += (size_t)W) {
+                std::vector<Ray> blk(v.begin() + (std::ptrdiff_t)b0, v.begin() + (std::ptrdiff_t)std::min(v.size(), b0 + (size_t)W));
+                if (qsort)
+                    std::stable_sort(blk.begin(), blk.end(), [](const Ray& a, const Ray& b) { return a.len > b.len; });
+                std::vector<char> used(blk.size(), 0);
+                size_t left = blk.size(), first = 0;
+                while (left > 0) {
+                    uint32_t wave[64];
+                    for (int l = 0; l < 64; ++l) wave[l] = PAD;
+                    for (int g = 0; g < 4 && left > 0; ++g) {
+                        int pick[16], np = 0;
+                        unsigned seen = 0;
+                        for (size_t i = first; i < blk.size() && np < 16; ++i)
+                            if (qdeal && !used[i] && !(seen >> blk[i].res & 1u)) {
+                                seen |= 1u << blk[i].res;
+                                pick[np++] = (int)i;
+                                used[i] = 1;
+                            }
+                        for (size_t i = first; i < blk.size() && np < 16; ++i)
+                            if (!used[i]) {
+                                pick[np++] = (int)i;
+                                used[i] = 1;
+                            }
+                        for (int j = 0; j < np; ++j) wave[G[g][j]] = blk[(size_t)pick[j]].e;
+                        left -= (size_t)np;
+                        while (first < blk.size() && used[first]) ++first;
+                    }
+                    out.insert(out.end(), wave, wave + 64);
+                }
+            }
+            qoff[(size_t)tile * 4 + qd + 1] = (int64_t)out.size();
+        }
+    }
+    int rc;
+    if ((rc = upload(&p->d_adjq_slots, out)) || (rc = upload(&p->d_adjq_off, qoff))) return rc;
+    p->pl.adj_qslots = p->d_adjq_slots;
+    p->pl.adj_qoff = p->d_adjq_off;
+    p->pl.adj_quad = 1;
+    return 0;
+}
+
 static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     const tvam_desc& d = p->desc;
     const TvamConsts& k = p->k;
@@ -371,6 +500,16 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     p->planar_rz = env_int("TVAM_RAY_FWD_Z", 4);
     if (p->planar_rz != 4 && p->planar_rz != 8) p->planar_rz = 4;
     p->pl.adj_pitch = p->tiles.tsx + 2 + std::max(0, env_int("TVAM_ADJ_PITCH_PAD", 0));
+    // quadrant lists (adj_quadrant_lists, TVAM_ADJ_QUAD=0: one list in (angle, column) order): row
+    // pitches = +1 / -1 (mod 16), at least the tile + guard band
+    p->pl.adj_quad = env_int("TVAM_ADJ_QUAD", 0) != 0 && env_int("TVAM_ADJ_PLANES", 1) != 0;
+    p->pl.adj_pitch2 = p->pl.adj_pitch;
+    p->pl.rayfwd_pitch = p->pl.adj_pitch;
+    if (p->pl.adj_quad) {
+        const int w = p->tiles.tsx + 2;
+        p->pl.adj_pitch = w + ((1 - w) % 16 + 16) % 16;    // = 1 (mod 16)
+        p->pl.adj_pitch2 = w + ((15 - w) % 16 + 16) % 16;  // = 15 (mod 16)
+    }
     p->pl.adj_planes = env_int("TVAM_ADJ_PLANES", 1);
     p->pl.adj_w2 = env_int("TVAM_ADJ_W2", 1);
     p->pl.xcd_remap = env_int("TVAM_XCD_REMAP", 1);
@@ -393,7 +532,8 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
         const int ant = env_int("TVAM_ADJ_NT", p->planar_az >= 8 ? 1024 : 512);
         p->pl.adj_nt = ant == 256 || ant == 1024 ? ant : 512;
         const int64_t want = p->pl.adj_nt >= 1024 ? 8192 : 16384;
-        const int64_t nwg = (int64_t)p->tiles.ntx * p->tiles.nty * ((k.nz + p->planar_az - 1) / p->planar_az);
+        const int64_t nwg = (int64_t)p->tiles.ntx * p->tiles.nty * ((k.nz + p->planar_az - 1) / p->planar_az) *
+                            (p->pl.adj_quad ? 4 : 1);  // quadrant lists: one workgroup per quadrant
         int split = (int)std::min<int64_t>(8, std::max<int64_t>(1, (want + nwg - 1) / std::max<int64_t>(nwg, 1)));
         const int es = env_int("TVAM_ADJ_SPLIT", 0);
         if (es >= 1 && es <= 64) split = es;
@@ -462,6 +602,7 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
         p->pl.chord = nullptr;
         if (rc) return rc;
     }
+    if (p->pl.adj_quad && (rc = adj_quadrant_lists(p))) return rc;
     p->planar = true;
     return 0;
 }
@@ -1714,7 +1855,16 @@ extern "C" int tvam_plan_stats(tvam_plan* p, uint64_t* fallback_tiles) {
 
 extern "C" int tvam_plan_bin_stats(tvam_plan* p, int64_t* stats) {
     if (!p || !stats) return fail(TVAM_ERR_INVALID, "null argument");
-    for (int i = 0; i < 5; ++i) stats[i] = p->bins.st[i];
+    const TvamBinScratch& b = p->bins;
+    for (int i = 0; i < 5; ++i) stats[i] = b.st[i];
+    int64_t cache = 0;  // device bytes the forward bin cache holds
+    for (const TvamBinChunk& c : b.fc)
+        cache += c.cap_slots * 3 * (int64_t)sizeof(float4) + (c.cap_vals + c.cap_bricks) * (int64_t)sizeof(uint32_t);
+    stats[5] = cache;
+    // the chunk scratch: records, brick counts and offsets, sort keys / values, adjoint partials
+    stats[6] = b.cap_slots * (3 * (int64_t)sizeof(float4) + 2 * (int64_t)sizeof(uint32_t)) +
+               b.cap_entries * (int64_t)(4 * sizeof(uint32_t) + sizeof(float)) + b.cap_bricks * 4 + b.temp_cap();
+    stats[7] = 0;
     return 0;
 }
 

@@ -821,12 +821,34 @@ __global__ __launch_bounds__(NT) void tvam_adj_planar_kernel(TvamConsts k, TvamP
                                                                   float* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tsx = tp.tsx, tsy = tp.tsy;
-    const int tw = pl.adj_pitch, th = tsy + 2;  // row pitch >= tsx + 2 (padded against bank conflicts)
+    const int tile_id = blockIdx.x, z0 = blockIdx.y * Z;
+    // this workgroup's part of the tile's ray list: with quadrant lists (pl.adj_quad) blockIdx.z =
+    // split part * 4 + step quadrant, parts of whole waves, and the row pitch of the quadrant;
+    // else a part of the one (angle, column)-ordered list (a thin slab has few slice chunks:
+    // several workgroups then share one tile's rays, each ray once)
+    int tw = pl.adj_pitch;  // row pitch >= tsx + 2
+    const uint32_t* slots;
+    int gb, nrt;
+    if (pl.adj_quad) {
+        const int qd = (int)(blockIdx.z & 3u), part = (int)(blockIdx.z >> 2), nparts = (int)(gridDim.z >> 2);
+        if (qd == 1 || qd == 2) tw = pl.adj_pitch2;
+        const int64_t q0 = pl.adj_qoff[(size_t)tile_id * 4 + qd], q1 = pl.adj_qoff[(size_t)tile_id * 4 + qd + 1];
+        slots = pl.adj_qslots + q0;
+        const int nwv = (int)((q1 - q0) >> 6);
+        gb = (int)(((int64_t)nwv * part) / nparts) * 64;
+        nrt = (int)(((int64_t)nwv * (part + 1)) / nparts) * 64;
+    } else {
+        slots = tp.slots + tp.slot_off[tile_id];
+        const int nall = (int)(tp.slot_off[tile_id + 1] - tp.slot_off[tile_id]);
+        gb = (int)(((int64_t)nall * blockIdx.z) / gridDim.z);
+        nrt = (int)(((int64_t)nall * (blockIdx.z + 1)) / gridDim.z);
+    }
+    if (gb >= nrt) return;  // (uniform over the workgroup)
+    const int th = tsy + 2;
     float* tile = reinterpret_cast<float*>(smem);
-    int* s_roff = reinterpret_cast<int*>(tile + (size_t)tw * th * Z);  // [Z + 1] CSR of the chunk's rows
+    int* s_roff = reinterpret_cast<int*>(tile + (size_t)max(pl.adj_pitch, pl.adj_pitch2) * th * Z);  // [Z + 1] CSR
     int* s_rows = s_roff + Z + 1;                                       // [pl.max_rows_chunk]
 
-    const int tile_id = blockIdx.x, z0 = blockIdx.y * Z;
     const int x0 = (tile_id % tp.ntx) * tsx, y0 = (tile_id / tp.ntx) * tsy;
     const int x1 = min(x0 + tsx, k.res[0]), y1 = min(y0 + tsy, k.res[1]);
     const int wx = x1 - x0, wy = y1 - y0;
@@ -857,12 +879,6 @@ __global__ __launch_bounds__(NT) void tvam_adj_planar_kernel(TvamConsts k, TvamP
     __syncthreads();
     if (s_roff[Z] == 0) return;  // no DMD row lies in these slices
 
-    // this workgroup's part of the tile's ray list (a thin slab has few slice
-    // chunks: several workgroups then share one tile's rays, each ray once)
-    const uint32_t* slots = tp.slots + tp.slot_off[tile_id];
-    const int nall = (int)(tp.slot_off[tile_id + 1] - tp.slot_off[tile_id]);
-    const int gb = (int)(((int64_t)nall * blockIdx.z) / gridDim.z);
-    const int nrt = (int)(((int64_t)nall * (blockIdx.z + 1)) / gridDim.z);
     // PF: a two-stage software pipeline over this lane's rays -- the slot of ray
     // k + 2 and the records of ray k + 1 are loaded while ray k marches
     int g = gb + (int)threadIdx.x;
@@ -871,6 +887,12 @@ __global__ __launch_bounds__(NT) void tvam_adj_planar_kernel(TvamConsts k, TvamP
     float4 ff_n = make_float4(0.0f, 0.0f, 0.0f, 0.0f), an_n = ff_n;
     float w_n = 1.0f;
     auto records = [&](uint32_t e, int& ri, float4& ff, float4& an, float& wray) {
+        if (e == 0xffffffffu) {  // padding slot of a quadrant list
+            ri = -1;
+            ff = an = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            wray = 1.0f;
+            return;
+        }
         const int al = (int)(e >> 16), colc = (int)(e & 0xffffu);
         ri = pl.rec_i[(size_t)al * k.crop_x + colc];
         ff = pl.rec_f[(size_t)al * k.crop_x + colc];
@@ -970,19 +992,25 @@ __global__ __launch_bounds__(NT) void tvam_adj_planar_kernel(TvamConsts k, TvamP
                     act = idxmap[act];
                     if (act < 0) continue;
                 }
+#ifdef TVAM_ADJ_NOATOMIC_DEBUG  // timing experiment only (wrong results): no gradient atomics
+                if (v == 1.2345e-30f) out[act] = v;
+#else
                 atomicAdd(&out[act], v);  // backward_from(Le * em_grad), volume.py:274-276
+#endif
             }
         }
     }
 }
 
 size_t tvam_planar_adj_lds(const TvamPlanar& pl, const TvamTiles& t, int Z) {
-    return (size_t)pl.adj_pitch * (t.tsy + 2) * Z * sizeof(float) + (size_t)(Z + 1 + pl.max_rows_chunk) * sizeof(int);
+    return (size_t)std::max(pl.adj_pitch, pl.adj_pitch2) * (t.tsy + 2) * Z * sizeof(float) +
+           (size_t)(Z + 1 + pl.max_rows_chunk) * sizeof(int);
 }
 
 hipError_t tvam_launch_adj_planar(const TvamConsts& k, const TvamPlanar& pl, const TvamTiles& t, int Z,
                                   const int32_t* idxmap, const float* gin, float* out, hipStream_t stream) {
-    dim3 grid((unsigned)(t.ntx * t.nty), (unsigned)((k.nz + Z - 1) / Z), (unsigned)std::max(pl.adj_split, 1));
+    dim3 grid((unsigned)(t.ntx * t.nty), (unsigned)((k.nz + Z - 1) / Z),
+              (unsigned)std::max(pl.adj_split, 1) * (pl.adj_quad ? 4u : 1u));
     const size_t lds = tvam_planar_adj_lds(pl, t, Z);
     const bool pf = pl.adj_prefetch != 0;
     // 512-thread workgroups (adj_nt): the LDS tile (28 KB at 40 x 40 x 4) admits 5
@@ -1098,7 +1126,7 @@ __global__ __launch_bounds__(256) void tvam_fwd_scale_kernel(TvamConsts k, int n
 static __host__ __device__ inline int tvam_ray_fwd_plane(int tw, int th) { return (tw * th + 31) / 32 * 32 + 8; }
 
 size_t tvam_planar_rayfwd_lds(const TvamPlanar& pl, const TvamTiles& t, int Z) {
-    return (size_t)tvam_ray_fwd_plane(pl.adj_pitch, t.tsy + 2) * Z * sizeof(float) +
+    return (size_t)tvam_ray_fwd_plane(pl.rayfwd_pitch, t.tsy + 2) * Z * sizeof(float) +
            (size_t)(Z + 1 + pl.max_rows_chunk) * sizeof(int);
 }
 
@@ -1199,7 +1227,7 @@ __global__ __launch_bounds__(NT) void tvam_fwd_rays_planar_kernel(TvamConsts k, 
                                                                        float* __restrict__ dose) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tsx = tp.tsx, tsy = tp.tsy;
-    const int tw = pl.adj_pitch, th = tsy + 2;
+    const int tw = pl.rayfwd_pitch, th = tsy + 2;
     const int pw = tvam_ray_fwd_plane(tw, th);  // plane pitch in words
     int* itile = reinterpret_cast<int*>(smem);
     int* s_roff = itile + (size_t)pw * Z;

@@ -186,14 +186,15 @@ class Projection:
 
     def bin_stats(self):
         """Chunking of the last brick-binned call (scattering media): a dict with the chunks of
-        paths, those served from / stored into the forward bin cache, the brick entries marched
-        and the paths per chunk (tvam_plan_bin_stats)."""
+        paths, those served from / stored into the forward bin cache, the brick entries marched,
+        the paths per chunk and the device bytes of the bin cache and scratch (tvam_plan_bin_stats)."""
         import numpy as np
-        v = np.zeros(5, dtype=np.int64)
+        v = np.zeros(8, dtype=np.int64)
         with torch.cuda.device(self.device):
             torch.cuda.synchronize(self.device)
             _abi.check(self.lib.tvam_plan_bin_stats(self._plan, v.ctypes.data))
-        return dict(zip(("chunks", "cached", "stored", "entries", "chunk_paths"), (int(x) for x in v)))
+        return dict(zip(("chunks", "cached", "stored", "entries", "chunk_paths", "cache_bytes", "scratch_bytes"),
+                        (int(x) for x in v)))
 
     def count_visits(self, spp: int = 1, seed: int = 0) -> int:
         v = ctypes.c_uint64(0)

@@ -258,7 +258,9 @@ int tvam_plan_fwd_scale(tvam_plan* plan, float* scale);
    a scattering medium (the later segments of every path, tvam_scatter.hip).  stats[0] =
    chunks of paths, [1] = chunks served from the forward bin cache (weights rescaled to the
    new pattern, no replay / sort), [2] = chunks stored into the cache, [3] = brick entries
-   marched, [4] = paths per chunk.  All 0 when the plan's last call binned nothing.  (ABI v10) */
+   marched, [4] = paths per chunk (all 0 when the plan's last call binned nothing), [5] = device
+   bytes the forward bin cache holds, [6] = device bytes of the chunk scratch, [7] = 0
+   (reserved).  stats has 8 entries.  (ABI v10) */
 int tvam_plan_bin_stats(tvam_plan* plan, int64_t* stats);
 
 /* Surface-aware plans: the per-channel voxel volumes the forward divides by and the
