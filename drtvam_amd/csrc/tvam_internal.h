@@ -115,6 +115,11 @@ hipError_t tvam_launch_fwd_rays_planar(const TvamConsts& k, const TvamPlanar& pl
 
 enum TvamMode { TVAM_MODE_FWD = 0, TVAM_MODE_ADJ = 1, TVAM_MODE_COUNT = 2, TVAM_MODE_EMIT = 3 };
 
+// float4s per brick-bin segment record (3: 48 B; 4: 64-B aligned records, one line fetch per
+// random gather; build-time A/B)
+#ifndef TVAM_REC_F4
+#define TVAM_REC_F4 3
+#endif
 // Brick of the binned scattered-segment forward (LDS int64 tile: 128 KB)
 #ifndef TVAM_BX
 #define TVAM_BX 32

@@ -1859,10 +1859,10 @@ extern "C" int tvam_plan_bin_stats(tvam_plan* p, int64_t* stats) {
     for (int i = 0; i < 5; ++i) stats[i] = b.st[i];
     int64_t cache = 0;  // device bytes the forward bin cache holds
     for (const TvamBinChunk& c : b.fc)
-        cache += c.cap_slots * 3 * (int64_t)sizeof(float4) + (c.cap_vals + c.cap_bricks) * (int64_t)sizeof(uint32_t);
+        cache += c.cap_slots * TVAM_REC_F4 * (int64_t)sizeof(float4) + (c.cap_vals + c.cap_bricks) * (int64_t)sizeof(uint32_t);
     stats[5] = cache;
     // the chunk scratch: records, brick counts and offsets, sort keys / values, adjoint partials
-    stats[6] = b.cap_slots * (3 * (int64_t)sizeof(float4) + 2 * (int64_t)sizeof(uint32_t)) +
+    stats[6] = b.cap_slots * (TVAM_REC_F4 * (int64_t)sizeof(float4) + 2 * (int64_t)sizeof(uint32_t)) +
                b.cap_entries * (int64_t)(4 * sizeof(uint32_t) + sizeof(float)) + b.cap_bricks * 4 + b.temp_cap();
     stats[7] = 0;
     return 0;

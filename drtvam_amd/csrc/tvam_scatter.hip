@@ -269,6 +269,71 @@ __device__ __forceinline__ void sc_box_march(const TvamConsts& k, const SegDda& 
     }
 }
 
+// sc_box_march for the brick kernels: the same visits (the same crossing times fmaf(n, ts, dtm0)
+// and axis choices), stepped without divergent branches (every axis' candidate next crossing is
+// formed and selected), with the visit's index into a TVAM_BX x TVAM_BY x TVAM_BZ tile carried
+// incrementally.  W2: the degree-2 visit weight of tvam_common.h on E = st e^{-st t} (used when
+// st * sqrt(3) * max h < TVAM_W2_MAX3, a relative weight error < 4.2e-6), restarted from exp2 at
+// every brick entry; else tvam_omexp as sc_box_march.  F(tile index, weight).
+#define TVAM_W2_MAX3 5.0e-3f
+template <bool W2, typename F>
+__device__ __forceinline__ void sc_brick_march(const TvamConsts& k, const SegDda& q, const int lo[3], const int hi[3],
+                                               F&& f) {
+    float tin[3], tout[3];
+    int nin[3], nout[3];
+#pragma unroll
+    for (int a = 0; a < 3; ++a)
+        tvam_axis_window(q.sv[a], q.step[a], q.dtm0[a], q.ts[a], lo[a], hi[a], tin[a], tout[a], nin[a], nout[a]);
+    const float tau_e = fmaxf(fmaxf(fmaxf(tin[0], tin[1]), tin[2]), 0.0f);
+    const float tau_x = fminf(fminf(fminf(tout[0], tout[1]), tout[2]), q.tau_end);
+    if (!(tau_e < tau_x)) return;
+    int n0 = tvam_axis_steps(tau_e, q.dtm0[0], q.ts[0], nin[0], nout[0]);
+    int n1 = tvam_axis_steps(tau_e, q.dtm0[1], q.ts[1], nin[1], nout[1]);
+    int n2 = tvam_axis_steps(tau_e, q.dtm0[2], q.ts[2], nin[2], nout[2]);
+    constexpr int SY = TVAM_BX, SZ = TVAM_BX * TVAM_BY;
+    int li = (q.sv[0] + q.step[0] * n0 - lo[0]) + (q.sv[1] + q.step[1] * n1 - lo[1]) * SY +
+             (q.sv[2] + q.step[2] * n2 - lo[2]) * SZ;
+    const int dl0 = q.step[0], dl1 = q.step[1] * SY, dl2 = q.step[2] * SZ;
+    const float ts0 = q.ts[0], ts1 = q.ts[1], ts2 = q.ts[2];
+    const float d0 = q.dtm0[0], d1 = q.dtm0[1], d2 = q.dtm0[2];
+    // a frozen axis (dtm0 = inf) never steps: its T stays inf
+    const bool f0 = d0 < TVAM_INF, f1 = d1 < TVAM_INF, f2 = d2 < TVAM_INF;
+    float T0 = f0 ? fmaf((float)n0, ts0, d0) : TVAM_INF;
+    float T1 = f1 ? fmaf((float)n1, ts1, d1) : TVAM_INF;
+    float T2 = f2 ? fmaf((float)n2, ts2, d2) : TVAM_INF;
+    const float stop = tau_x - 1e-6f;
+    const float base = k.nsig2 * q.t_start;
+    const float e_in = sc_exp2(fmaf(k.nsig2, tau_e, base));
+    float ea = W2 ? k.sig_t * e_in : e_in, tp = tau_e;
+    const float mhs = -0.5f * k.sig_t, msig = -k.sig_t;
+    for (int guard = 0; guard < 3 * 4096; ++guard) {
+        const bool m0 = T0 <= T1 && T0 <= T2;
+        const bool m1 = !m0 && T1 <= T2;
+        const float tmin = m0 ? T0 : (m1 ? T1 : T2);
+        const float tn = tmin < tau_x ? tmin : tau_x;
+        const float dt = fmaxf(tn - tp, 0.0f);
+        float c;
+        if (W2) {
+            c = ea * dt * fmaf(mhs, dt, 1.0f);
+            ea = fmaf(msig, c, ea);
+        } else {
+            c = ea * tvam_omexp(k.sig_t * dt);
+            ea = ea - c;
+        }
+        tp = tn;
+        f(li, c);
+        if (!(tn < stop)) break;
+        const bool m2 = !m0 && !m1;
+        n0 += m0 ? 1 : 0;
+        n1 += m1 ? 1 : 0;
+        n2 += m2 ? 1 : 0;
+        li += m0 ? dl0 : (m1 ? dl1 : dl2);
+        T0 = m0 ? fmaf((float)n0, ts0, d0) : T0;
+        T1 = m1 ? fmaf((float)n1, ts1, d1) : T1;
+        T2 = m2 ? fmaf((float)n2, ts2, d2) : T2;
+    }
+}
+
 // The whole segment, brick by brick (the binned forward's visits exactly).
 template <typename F>
 __device__ __forceinline__ void sc_seg_march(const TvamConsts& k, const SegDda& q, F&& f) {
@@ -317,7 +382,7 @@ __global__ __launch_bounds__(256) void tvam_scatter_kernel(TvamConsts k, TvamTil
     float wmax = 0.0f;  // EMIT (forward): largest |record weight| of this thread's paths
     for (int64_t i = i0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         if (MODE == TVAM_MODE_EMIT && !sb.adj)  // slots without a segment: attenuation 0 (the cache's rescale)
-            for (int q = 0; q < sb.slots; ++q) reinterpret_cast<float*>(&sb.r[3 * ((i - sb.p0) * sb.slots + q) + 2])[2] = 0.0f;
+            for (int q = 0; q < sb.slots; ++q) reinterpret_cast<float*>(&sb.r[TVAM_REC_F4 * ((i - sb.p0) * sb.slots + q) + 2])[2] = 0.0f;
         const int64_t local = i / spp;
         const int smp = (int)(i - local * spp);
         float em = 1.0f;
@@ -376,11 +441,11 @@ __global__ __launch_bounds__(256) void tvam_scatter_kernel(TvamConsts k, TvamTil
                 SegDda q;
                 if (seg <= sb.slots && sc_dda_init(k, o, dv, tsi, q)) {
                     const int64_t slot = (i - sb.p0) * sb.slots + (seg - 1);
-                    sb.r[3 * slot] = make_float4(q.t_start, q.tau_end, q.dtm0[0], q.dtm0[1]);
-                    sb.r[3 * slot + 1] = make_float4(q.dtm0[2], q.ts[0] * (float)q.step[0], q.ts[1] * (float)q.step[1],
+                    sb.r[TVAM_REC_F4 * slot] = make_float4(q.t_start, q.tau_end, q.dtm0[0], q.dtm0[1]);
+                    sb.r[TVAM_REC_F4 * slot + 1] = make_float4(q.dtm0[2], q.ts[0] * (float)q.step[0], q.ts[1] * (float)q.step[1],
                                              q.ts[2] * (float)q.step[2]);
                     // .z: the attenuation alone, for the cached forward's rescale (tvam_bin_reweight_kernel)
-                    sb.r[3 * slot + 2] = make_float4(__int_as_float(q.sv[0] | (q.sv[1] << 11) | (q.sv[2] << 22)), em * att, att, 0.0f);
+                    sb.r[TVAM_REC_F4 * slot + 2] = make_float4(__int_as_float(q.sv[0] | (q.sv[1] << 11) | (q.sv[2] << 22)), em * att, att, 0.0f);
                     sb.m[slot] = (uint32_t)sc_walk_bricks(k, q, [](int, float, float) {});
                     wmax = fmaxf(wmax, fabsf(em * att));
                 }
@@ -1081,9 +1146,12 @@ __global__ __launch_bounds__(256) void tvam_bin_fill_kernel(TvamConsts k, TvamSe
         if (sb.m[s] == 0) continue;
         SegDda q;
         float w;
-        sc_unpack(sb.r[3 * s], sb.r[3 * s + 1], sb.r[3 * s + 2], q, w);
+        sc_unpack(sb.r[TVAM_REC_F4 * s], sb.r[TVAM_REC_F4 * s + 1], sb.r[TVAM_REC_F4 * s + 2], q, w);
         const uint32_t o0 = off[s];
         uint32_t o = o0;
+        // adjoint: the segment's first entry in the record's spare word, so the brick kernel's
+        // partial store needs no off[slot] gather (the record line was just read)
+        if (jshift > 0) reinterpret_cast<uint32_t*>(&sb.r[TVAM_REC_F4 * s + 2])[3] = o0;
         // visits per unit length: one per voxel-face crossing of each moving axis
         float rate = 0.0f;
 #pragma unroll
@@ -1139,6 +1207,7 @@ __global__ __launch_bounds__(NT) void tvam_bin_march_kernel(TvamConsts k, TvamSe
     const int hi[3] = {min(lo[0] + TVAM_BX, k.res[0]), min(lo[1] + TVAM_BY, k.res[1]), min(lo[2] + TVAM_BZ, k.res[2])};
     const int wx = hi[0] - lo[0], wy = hi[1] - lo[1], wz = hi[2] - lo[2];
     const int sy = TVAM_BX, sz = TVAM_BX * TVAM_BY;
+    const bool w2 = k.sig_t * 1.7320508f * fmaxf(fmaxf(k.h[0], k.h[1]), k.h[2]) < TVAM_W2_MAX3;
     float scale = 1.0f;
     if (ACC == 0) {
         // per-add bound: each add rounds to int32 (one v_cvt), the int64 sums cannot overflow; the
@@ -1166,42 +1235,38 @@ __global__ __launch_bounds__(NT) void tvam_bin_march_kernel(TvamConsts k, TvamSe
         }
         __syncthreads();
     }
-    // Two-stage load pipeline over this thread's entries e, e + S, e + 2S, ... (S = NT): while
-    // entry e marches, the record (and the adjoint's entry base off[slot]) of e + S and the slot of
-    // e + 2S are in flight (vals -> record is two dependent gathers).
+    // Load pipeline over this thread's entries e, e + S, e + 2S, ... (S = NT), unrolled by two with
+    // two record register sets: while one entry marches, the records (and the adjoint's entry base
+    // off[slot] and key) of the next are in flight and the slot of the one after (vals -> record is
+    // two dependent gathers).  Indices are clamped to the brick's last entry, so every load is
+    // issued unconditionally (no branch around it: the compiler's vmcnt waits then count only the
+    // loads a use needs; a single register set with conditional loads had it wait for the next
+    // entry's records at the top of every entry).
     constexpr uint32_t S = NT;
-    const uint32_t et = e0 + threadIdx.x;
-    uint32_t s1 = et + S < e1 ? vals[et + S] : 0u;
-    const uint32_t s0 = et < e1 ? vals[et] : 0u;
-    float4 na = make_float4(0.0f, 0.0f, 0.0f, 0.0f), nb = na;
-    float4 nc = na;
-    uint32_t nof = 0u;
-    if (et < e1) {
-        na = sb.r[3 * s0];
-        nb = sb.r[3 * s0 + 1];
-        nc = sb.r[3 * s0 + 2];
-        if (ACC == 2) nof = off[s0];
-    }
-    for (uint32_t e = et; e < e1; e += S) {
-        const float4 ca = na, cb = nb, cc = nc;
-        const uint32_t cof = nof;
-        if (e + S < e1) {
-            na = sb.r[3 * s1];
-            nb = sb.r[3 * s1 + 1];
-            nc = sb.r[3 * s1 + 2];
-            if (ACC == 2) nof = off[s1];
+    const uint32_t et = e0 + threadIdx.x, el = e1 - 1;
+    struct Ent {
+        float4 a, b, c;
+        uint32_t of, key;
+    };
+    auto load = [&](uint32_t slot, uint32_t e, Ent& r) {
+        r.a = sb.r[TVAM_REC_F4 * slot];
+        r.b = sb.r[TVAM_REC_F4 * slot + 1];
+        r.c = sb.r[TVAM_REC_F4 * slot + 2];
+        if (ACC == 2) {
+            r.of = __float_as_uint(r.c.w);  // off[slot], stored by tvam_bin_fill_kernel
+            r.key = keys[min(e, el)];
         }
-        s1 = e + 2 * S < e1 ? vals[e + 2 * S] : 0u;
+    };
+    auto run = [&](const Ent& r) {
         SegDda q;
         float w;
-        sc_unpack(ca, cb, cc, q, w);
+        sc_unpack(r.a, r.b, r.c, q, w);
         const float ws = w * scale;
         float acc = 0.0f;
         // adjoint: each visit's LDS value is consumed one visit later, so its read latency overlaps
         // the next DDA step (the sum keeps its order: bit-identical)
         float pc = 0.0f, pv = 0.0f;
-        sc_box_march(k, q, lo, hi, [&](int x, int y, int z, float c) {
-            const int li = z * sz + y * sy + x;
+        auto visit = [&](int li, float c) {
             if (ACC == 0) {
                 __hip_atomic_fetch_add(&ltile[li], (long long)__float2int_rn(ws * c), __ATOMIC_RELAXED,
                                        __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -1213,9 +1278,27 @@ __global__ __launch_bounds__(NT) void tvam_bin_march_kernel(TvamConsts k, TvamSe
                 pc = c;
                 pv = v;
             }
-        });
-        if (ACC == 2) acc = fmaf(pc, pv, acc);
-        if (ACC == 2) part[cof + (keys[e] >> jshift)] = w * acc;
+        };
+        if (w2)
+            sc_brick_march<true>(k, q, lo, hi, visit);
+        else
+            sc_brick_march<false>(k, q, lo, hi, visit);
+        if (ACC == 2) part[r.of + (r.key >> jshift)] = w * fmaf(pc, pv, acc);
+    };
+    if (et < e1) {
+        uint32_t sB = vals[min(et + S, el)];
+        Ent rA, rB;
+        load(vals[et], et, rA);
+        for (uint32_t e = et;; e += 2 * S) {
+            load(sB, e + S, rB);
+            const uint32_t sC = vals[min(e + 2 * S, el)];
+            run(rA);
+            if (e + S >= e1) break;
+            load(sC, e + 2 * S, rA);
+            sB = vals[min(e + 3 * S, el)];
+            run(rB);
+            if (e + 2 * S >= e1) break;
+        }
     }
     if (ACC == 2) return;
     __syncthreads();
@@ -1266,7 +1349,7 @@ __global__ __launch_bounds__(256) void tvam_bin_reweight_kernel(TvamConsts k, Tv
     for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += (int64_t)gridDim.x * blockDim.x) {
         const int64_t local = (sb.p0 + s / sb.slots) / spp;
         const float em = pat[local] * k.wscale * k.inv_vol;
-        float* c = reinterpret_cast<float*>(&sb.r[3 * s + 2]);
+        float* c = reinterpret_cast<float*>(&sb.r[TVAM_REC_F4 * s + 2]);
         const float w = em * c[2];  // c[2] = 0 for slots without a segment
         c[1] = w;
         wmax = fmaxf(wmax, fabsf(w));
@@ -1353,7 +1436,7 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
         const int keep_float = s.acc_float;
         tvam_bin_scratch_free(s);
         s.acc_float = keep_float;
-        if ((e = hipMalloc((void**)&s.sb.r, 3 * nsl * sizeof(float4))) != hipSuccess ||
+        if ((e = hipMalloc((void**)&s.sb.r, TVAM_REC_F4 * nsl * sizeof(float4))) != hipSuccess ||
             (e = hipMalloc((void**)&s.sb.m, (nsl + 1) * sizeof(uint32_t))) != hipSuccess ||
             (e = hipMalloc((void**)&s.off, (nsl + 1) * sizeof(uint32_t))) != hipSuccess ||
             (e = hipMalloc((void**)&s.sb.wmax, sizeof(uint32_t))) != hipSuccess)
@@ -1431,8 +1514,8 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
             (void)hipFree(cc->r);
             cc->r = nullptr;
             cc->cap_slots = 0;
-            if (room(3 * (size_t)nsl * sizeof(float4)) &&
-                hipMalloc((void**)&cc->r, 3 * (size_t)nsl * sizeof(float4)) == hipSuccess)
+            if (room(TVAM_REC_F4 * (size_t)nsl * sizeof(float4)) &&
+                hipMalloc((void**)&cc->r, TVAM_REC_F4 * (size_t)nsl * sizeof(float4)) == hipSuccess)
                 cc->cap_slots = nsl;
             else
                 cc->r = nullptr;
