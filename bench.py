@@ -27,7 +27,6 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 
 
 def log(*a):
@@ -109,48 +108,40 @@ def cpu_baseline(config, N, seconds, threads):
                       f"+ 23 vector passes over {N}^3 floats (numpy, {t_pass * 1e3:.0f} ms each) = {t_vec:.2f}s"}
 
 
-# Peaks (MI355X_MICROARCH.md): HBM3E 8 TB/s; LDS 256 B/clk/CU for ds_read_b128 (64 banks x 4 B) on
-# 256 CUs; VALU: a wave64 instruction occupies a SIMD-32 for 2 cycles (F32 157.3 TF = 1024 SIMDs x
-# 32 lanes x 2 flop x 2.4 GHz); clock 2.4 GHz (spec peak engine clock).
-CLOCK_GHZ = 2.4
-LDS_PEAK_GBS = 256 * 256 * CLOCK_GHZ  # 157,286 GB/s
-VALU_PEAK_WAVE_INSTR = 1024 * CLOCK_GHZ * 1e9 / 2  # wave64 VALU instructions / s
-PMC_SUMMARY = os.path.join(ROOT, "profiles", "r02", "pmc_config2.json")
+# Roofline of the dominant kernel, from the committed counter summary of the current build
+# (tools/pmc_bench.sh + tools/roofline_summary.py -> profiles/r03/roofline_config<K>.json): the
+# binding resource's bytes per launch (LDS-array cycles x 256 B, or HBM FETCH x 2 + WRITE) over
+# the launch duration of the counter run itself, against the 2.4 GHz spec peak (LDS 157.3 TB/s,
+# HBM 8 TB/s; MI355X_MICROARCH.md).  Every field can be recomputed from that one file; the bench's
+# own HIP-event time of the projection call that contains the kernel is reported beside it.
+ROOFLINE_DIR = os.path.join(ROOT, "profiles", "r03")
+DOMINANT = {2: "forward: voxel-driven planar forward (two per iteration)",
+            3: "forward: voxel-driven planar forward over refracted chords (two per iteration)",
+            4: "adjoint brick march of the scattered segments (23 launches per adjoint)",
+            5: "forward: per-ray tile kernel of the jittered first segments (two per iteration)"}
 
 
-def make_roofline(args, N, A, world, prob, visits, rays, fwd_s):
-    """Roofline of the dominant kernel, the forward projection (two per iteration): the voxel-driven
-    tvam_fwd_planar_kernel (+ its slice-binning pass) on config 2.  Its binding resource is the LDS
-    array (staged pattern slabs, 16-B reads), not HBM: per launch the LDS-array cycles and VALU
-    instructions come from the committed rocprofv3 counters of the same kernels
-    (profiles/r02/pmc_config2.json, tools/pmc_round.sh + tools/summarize_pmc.py), the duration is this
-    run's HIP-event time of the forward call (binning pass included, so the fractions are slightly
-    conservative)."""
+def make_roofline(args, N, A, world, prob, visits, rays, fwd_s, adj_s):
     alg_bytes = 8.0 * visits + 4.0 * rays  # SURVEY.md 8(d): forward = 8 B per visit + 4 B per ray
-    info = {"kernel": "tvam_fwd_planar_kernel" if prob.proj.planar_forward else "forward projection",
-            "fwd_call_s": fwd_s,
-            "survey_8d_model": {"alg_bytes_per_launch": alg_bytes, "rate_gbs": alg_bytes / fwd_s / 1e9,
-                                "note": "per-visit dose read-modify-write model of SURVEY 8(d); the kernel keeps "
-                                        "the dose in registers, so this rate exceeds HBM and is not a roofline"}}
-    if not (args.config == 2 and N == 400 and A == 400 and world == 1 and os.path.exists(PMC_SUMMARY)
-            and prob.proj.planar_forward):
-        return {"bound": "lds", "achieved": None, "peak": LDS_PEAK_GBS, "unit": "GB/s", "frac": None,
-                "traffic": None, "note": "counters committed for config 2 at 400^3 only", **info}
-    pmc = json.load(open(PMC_SUMMARY))["kernels"]["forward"]
-    c = pmc["sum"]
-    lds_bytes = c["SQ_LDS_IDX_ACTIVE"] * 256.0  # LDS-array cycles (summed over CUs) x 256 B per cycle
-    achieved = lds_bytes / fwd_s / 1e9
-    traffic = 2.0 * c["FETCH_SIZE"] * 1024 + c["WRITE_SIZE"] * 1024  # KiB; FETCH x2: gfx950 wide reads
-    valu = c["SQ_INSTS_VALU"] / fwd_s / VALU_PEAK_WAVE_INSTR
-    main = pmc["launches"][pmc["main"]]
-    return {"bound": "lds", "achieved": achieved, "peak": LDS_PEAK_GBS, "unit": "GB/s",
-            "frac": achieved / LDS_PEAK_GBS, "traffic": traffic,
-            "secondary": {"valu_issue_frac": valu, "hbm_gbs": traffic / fwd_s / 1e9,
-                          "hbm_frac": traffic / fwd_s / 1e9 / HBM_PEAK_GBS,
-                          "lds_bank_conflict_cycles": c["SQ_LDS_BANK_CONFLICT"],
-                          "clock_ghz_measured": main.get("clock_ghz"),
-                          "rocprof_avg_ns": c["avg_ns"]},
-            "counters": os.path.relpath(PMC_SUMMARY, ROOT), **info}
+    info = {"fwd_call_ms": fwd_s * 1e3, "adj_call_ms": adj_s * 1e3,
+            "survey_8d_model": {"alg_bytes_per_forward": alg_bytes, "rate_gbs": alg_bytes / fwd_s / 1e9,
+                                "note": "per-visit dose read-modify-write model of SURVEY 8(d); the gather-form "
+                                        "kernels keep the dose in registers / LDS, so this rate is no roofline"}}
+    path = os.path.join(ROOFLINE_DIR, f"roofline_config{args.config}.json")
+    full = N == (800 if args.config == 5 else 400) and A == N and world == 1 and not args.filter_radon
+    if not (full and os.path.exists(path)):
+        return {"bound": None, "achieved": None, "peak": None, "unit": "GB/s", "frac": None, "traffic": None,
+                "note": "counter summaries are committed for the BASELINE sizes on one GPU", **info}
+    summ = json.load(open(path))
+    r = summ["roofline"]
+    return {"bound": r["bound"], "achieved": r["achieved"], "peak": r["peak"], "unit": "GB/s", "frac": r["frac"],
+            "traffic": r["traffic"], "traffic_over_min": r["traffic_over_min"], "min_bytes": r["min_bytes"],
+            "kernel": summ["kernel"], "role": DOMINANT[args.config], "launch_ns_counter_run": summ["avg_ns"],
+            "clock_ghz_counter_run": summ["clock_ghz_measured"],
+            "secondary": {"valu_issue_frac": r["valu_issue_frac"], "hbm_frac": r["hbm_frac"],
+                          "lds_bank_conflict_frac": r["lds_bank_conflict_frac"],
+                          "frac_at_measured_clock": r["frac_at_measured_clock"]},
+            "counters": os.path.relpath(path, ROOT), "counters_build": summ["build"], **info}
 
 
 def main():
@@ -353,7 +344,7 @@ def main():
             dist.destroy_process_group()
         return
 
-    roofline = make_roofline(args, N, A, world, prob, visits, rays, fwd_avg)
+    roofline = make_roofline(args, N, A, world, prob, visits, rays, fwd_avg, adj_avg)
     cpu = None
     if args.cpu_baseline == "auto" and world == 1:
         threads = host_info()["threads"]

@@ -199,9 +199,11 @@ static int validate(const tvam_desc& d) {
         return fail(TVAM_ERR_INVALID, "Tried to render a purely absorptive volume with a delta tracking sensor. This is not supported.");
     if (d.sensor_type == TVAM_SENSOR_RATIO && !(d.majorant > 0.0f))
         return fail(TVAM_ERR_INVALID, "the 'ratio' sensor needs a positive majorant");
+    if (d.sample_time && d.film_channels != 1)
+        return fail(TVAM_ERR_UNSUPPORTED, "sample_time needs a one-channel film");
     if ((d.sensor_type != TVAM_SENSOR_DDA || d.sample_time) &&
-        (d.film_channels != 1 || d.slab_begin != 0 || (d.slab_end >= 0 && d.slab_end != d.film_res[2])))
-        return fail(TVAM_ERR_UNSUPPORTED, "sample_time and the ratio / delta sensors need a one-channel film without slabs");
+        (d.slab_begin != 0 || (d.slab_end >= 0 && d.slab_end != d.film_res[2])))
+        return fail(TVAM_ERR_UNSUPPORTED, "sample_time and the ratio / delta sensors need a film without slabs");
     if (d.vial_type != TVAM_VIAL_INDEX_MATCHED && d.vial_type != TVAM_VIAL_CYLINDRICAL &&
         d.vial_type != TVAM_VIAL_SQUARE)
         return fail(TVAM_ERR_UNSUPPORTED, "only the 'index_matched', 'cylindrical' and 'square' containers are implemented on the GPU path");
@@ -211,8 +213,6 @@ static int validate(const tvam_desc& d) {
     if (d.film_channels == 2) {
         if (d.n_target_tris <= 0 || !d.target_tris)
             return fail(TVAM_ERR_INVALID, "No target shape found in the scene");  // sensor.py:60-61
-        if (d.albedo != 0.0f)
-            return fail(TVAM_ERR_UNSUPPORTED, "surface-aware films are implemented for non-scattering media");
         if (d.slab_begin != 0 || (d.slab_end >= 0 && d.slab_end != d.film_res[2]))
             return fail(TVAM_ERR_UNSUPPORTED, "surface-aware films cannot be split into slabs");
     }
@@ -1740,7 +1740,7 @@ extern "C" int tvam_count_visits(tvam_plan* p, uint32_t spp, uint32_t seed, uint
             e = tvam_launch_frozen(TVAM_MODE_COUNT, k, t, nullptr, nullptr, nullptr, nullptr, p->d_counter, nullptr);
     }
     if (e != hipSuccess) return hip_fail(e, "count launch");
-    if (p->desc.albedo != 0.0f && !p->general) {
+    if (p->desc.albedo != 0.0f && !p->general && !p->surface) {  // (the surface kernel runs whole paths)
         e = tvam_launch_scatter_paths(TVAM_MODE_COUNT, k, t, nullptr, nullptr, nullptr, nullptr, p->d_counter, nullptr);
         if (e != hipSuccess) return hip_fail(e, "scatter count launch");
     }

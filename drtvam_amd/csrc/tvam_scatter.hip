@@ -613,7 +613,34 @@ __device__ float sf_dda(const TvamConsts& k, float ox, float oy, float oz, float
     return acc;
 }
 
+// A point deposit of the ratio / delta sensors on a surface-aware film (sensor.py:143-151,
+// :248-260): voxel floor((p - bbox.min) / h), skipped outside the grid, index 2 voxel + channel.
 template <int MODE>
+__device__ __forceinline__ float sf_point(const TvamConsts& k, float px, float py, float pz, float w, int ch,
+                                          float* __restrict__ film, const float* __restrict__ gin,
+                                          const float* __restrict__ vols, uint64_t& nvis) {
+    const int vx = (int)floorf((px - k.bmin[0]) / k.h[0]);
+    const int vy = (int)floorf((py - k.bmin[1]) / k.h[1]);
+    const int vz = (int)floorf((pz - k.bmin[2]) / k.h[2]);
+    if (vx < 0 || vy < 0 || vz < 0 || vx >= k.res[0] || vy >= k.res[1] || vz >= k.res[2]) return 0.0f;
+    const int64_t idx = 2 * (vx + (int64_t)vy * k.res[0] + (int64_t)vz * k.res[0] * k.res[1]) + ch;
+    ++nvis;
+    if (MODE == TVAM_MODE_FWD) atomicAdd(&film[idx], w);
+    else if (MODE == TVAM_MODE_ADJ) {
+        const float v = vols[idx];
+        return w * (gin[idx] * (v != 0.0f ? 1.0f / v : 0.0f));
+    }
+    return 0.0f;
+}
+
+// RNG (a scattering medium or the ratio / delta sensor; oracle or_trace_surface_scatter /
+// or_trace_estimator): the path loop of tvam_scatter_kernel in which each segment ends at the
+// nearer of the target mesh and the container; the draws per iteration are RR, the medium's
+// (scattering media), the ratio sensor's steps, then BSDF 1d + 2d at a surface or the phase
+// function's 1d + 2d at a medium event.  A target hit before the free flight ends passes the null
+// BSDF with weight tr / pdf (pdf = tr, volume.py:206-208; e^{-st t} without scattering, :263),
+// toggles the channel and does not count towards max_depth.
+template <int MODE, bool RNG>
 __global__ __launch_bounds__(256) void tvam_surface_kernel(TvamConsts k, TvamTiles tp, const float* __restrict__ pat,
                                                            const int32_t* __restrict__ idxmap,
                                                            const float* __restrict__ gin,
@@ -622,6 +649,8 @@ __global__ __launch_bounds__(256) void tvam_surface_kernel(TvamConsts k, TvamTil
     const int spp = (int)tp.spp;
     const int64_t per_angle = (int64_t)k.crop_y * k.crop_x;
     const int64_t n = (int64_t)tp.n_shard * per_angle * spp;
+    const float st = k.sig_t, ss = k.sig_s, mj = k.majorant;
+    const bool has_sc = ss != 0.0f;
     uint64_t nvis = 0;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const int64_t local = i / spp;
@@ -640,11 +669,13 @@ __global__ __launch_bounds__(256) void tvam_surface_kernel(TvamConsts k, TvamTil
         const int64_t pix = local - (int64_t)al * per_angle;
         const int rowc = (int)(pix / k.crop_x), colc = (int)(pix - (int64_t)rowc * k.crop_x);
         float jx = 0.5f, jy = 0.5f;
-        if (!k.regular) {
-            TvamPcg rng;
+        TvamPcg rng;
+        if (!k.regular || RNG) {
             rng.seed(tp.seed, tvam_stream(k, idxmap, local, (uint32_t)spp, smp));
-            jx = rng.next_float();
-            jy = rng.next_float();
+            if (!k.regular) {
+                jx = rng.next_float();
+                jy = rng.next_float();
+            }
         }
         const float2 csv = tp.cs[al];
         float xc, yc, ox, oy, oz, dx, dy;
@@ -652,21 +683,92 @@ __global__ __launch_bounds__(256) void tvam_surface_kernel(TvamConsts k, TvamTil
         tvam_ray_world(k, csv.x, csv.y, xc, yc, ox, oy, oz, dx, dy);
         float o2x, o2y, d2x, d2y, maxt, wgt;
         if (!tvam_segment(k, ox, oy, oz, dx, dy, o2x, o2y, d2x, d2y, maxt, wgt)) continue;
+        const int nsurf = k.vial_type == 0 ? 1 : 2;
+        if (RNG) {
+            (void)rng.next_float();  // aperture sample (projector.py:160)
+            (void)rng.next_float();
+            for (int q = 0; q < (has_sc ? 5 : 4) * nsurf; ++q) (void)rng.next_float();  // RR, (medium), BSDF
+        }
         float px = o2x, py = o2y, pz = oz;
-        const float vx = d2x, vy = d2y, vz = 0.0f;
+        float vx = d2x, vy = d2y, vz = 0.0f;
         float att = wgt, tcont = maxt, acc = 0.0f;
-        int inside = 0;
+        int inside = 0, depth = nsurf;
         for (int it = 0; it < 4096; ++it) {
+            if (RNG) {
+                const float q = fminf(0.99f, att);
+                const float u_rr = rng.next_float();
+                if (depth > k.rr_depth) {  // Russian roulette (volume.py:182-185)
+                    if (!(u_rr < q)) break;
+                    att = att * (1.0f / q);
+                }
+                if (!(att != 0.0f)) break;
+            }
             int tri;
             const float tt = sf_target_hit(k, px, py, pz, vx, vy, vz, tri);
             const bool hit = tt < tcont;
             const float tsi = hit ? tt : tcont;
-            const float r = sf_dda<MODE>(k, px, py, pz, vx, vy, vz, tsi, em * att, inside ? 0 : 1, out, gin, vols, nvis);
-            if (MODE == TVAM_MODE_ADJ) acc = fmaf(att, r, acc);
-            att = att * expf(-k.sig_t * tsi);
-            if (!hit) break;
+            float tmi = TVAM_INF;
+            if (RNG && has_sc) tmi = -logf(1.0f - rng.next_float()) / st;
+            const bool reached = !(tmi <= tsi);
+            const int ch = inside ? 0 : 1;
+            if (k.sensor_type == TVAM_SENSOR_DDA) {
+                const float r = sf_dda<MODE>(k, px, py, pz, vx, vy, vz, tsi, em * att, ch, out, gin, vols, nvis);
+                if (MODE == TVAM_MODE_ADJ) acc = fmaf(att, r, acc);
+            } else if (RNG && k.sensor_type == TVAM_SENSOR_RATIO) {
+                const float ratio = st / mj, keep = 1.0f - ratio;
+                float t = 0.0f, pk = 1.0f;
+                for (int s2 = 0; s2 < (1 << 20); ++s2) {
+                    t = t + (-logf(1.0f - rng.next_float()) / mj);
+                    if (!(t < tsi)) break;
+                    const float w = att * pk * ratio;
+                    const float r = sf_point<MODE>(k, fmaf(vx, t, px), fmaf(vy, t, py), fmaf(vz, t, pz), em * w, ch, out,
+                                                   gin, vols, nvis);
+                    if (MODE == TVAM_MODE_ADJ) acc += r;
+                    pk = pk * keep;
+                }
+            } else if (RNG && !reached) {  // delta: the medium interaction ray(mei.t)
+                const float r = sf_point<MODE>(k, fmaf(vx, tmi, px), fmaf(vy, tmi, py), fmaf(vz, tmi, pz), em * att, ch,
+                                               out, gin, vols, nvis);
+                if (MODE == TVAM_MODE_ADJ) acc += r;
+            }
+            if (RNG && !reached) {  // a medium event before the surface: phase sampling
+                const float tr = expf(-tmi * st);
+                const float pdf = tr * st;
+                const float inv = pdf > 0.0f ? 1.0f / pdf : 0.0f;
+                float w = tr * inv;
+                w = w * ss;
+                (void)rng.next_float();  // phase next_1d
+                const float u1 = rng.next_float(), u2 = rng.next_float();
+                float wx, wy, wz;
+                sc_phase(k, vx, vy, vz, u1, u2, wx, wy, wz);
+                px = fmaf(vx, tmi, px);
+                py = fmaf(vy, tmi, py);
+                pz = fmaf(vz, tmi, pz);
+                vx = wx;
+                vy = wy;
+                vz = wz;
+                att = att * w;
+                ++depth;
+                if (depth >= k.max_depth) break;
+                tcont = sc_container_hit(k, px, py, pz, vx, vy, vz);
+                if (!(tcont < TVAM_INF)) break;  // escapes through an open end
+                continue;
+            }
+            if (!hit) break;  // the container or an occluder: leaves the medium for good
+            if (RNG && has_sc) {
+                const float tr = expf(-tsi * st);
+                const float inv = tr > 0.0f ? 1.0f / tr : 0.0f;
+                att = att * (tr * inv);
+            } else {
+                att = att * expf(-k.sig_t * tsi);
+            }
+            if (RNG) {
+                (void)rng.next_float();  // BSDF next_1d + next_2d (null BSDF)
+                (void)rng.next_float();
+                (void)rng.next_float();
+            }
             inside ^= 1;
-            // spawn_ray at the target hit: offset_p along the geometric normal (oracle or_trace_surface)
+            // spawn_ray at the target hit: offset_p along the geometric normal (oracle or_spawn_target)
             const float* v = k.tgt + 9 * tri;
             const float e1x = v[3] - v[0], e1y = v[4] - v[1], e1z = v[5] - v[2];
             const float e2x = v[6] - v[0], e2y = v[7] - v[1], e2z = v[8] - v[2];
@@ -959,19 +1061,21 @@ hipError_t tvam_launch_surface_paths(int mode, const TvamConsts& k, const TvamTi
     int64_t g = (n + 255) / 256;
     if (g > 262144) g = 262144;
     if (g < 1) g = 1;
+    // draws beyond the ray's own: a scattering medium (volume.py:159) or the ratio / delta sensor
+    const bool scat = k.sig_s != 0.0f || k.sensor_type != TVAM_SENSOR_DDA;
+#define TVAM_SF_LAUNCH(M)                                                                                          \
+    if (scat)                                                                                                      \
+        hipLaunchKernelGGL((tvam_surface_kernel<M, true>), dim3((unsigned)g), dim3(256), 0, stream, k, t, pat, idxmap, \
+                           gin, vols, out, counter);                                                               \
+    else                                                                                                           \
+        hipLaunchKernelGGL((tvam_surface_kernel<M, false>), dim3((unsigned)g), dim3(256), 0, stream, k, t, pat, idxmap, \
+                           gin, vols, out, counter);
     switch (mode) {
-        case TVAM_MODE_FWD:
-            hipLaunchKernelGGL(tvam_surface_kernel<TVAM_MODE_FWD>, dim3((unsigned)g), dim3(256), 0, stream, k, t, pat,
-                               idxmap, gin, vols, out, counter);
-            break;
-        case TVAM_MODE_ADJ:
-            hipLaunchKernelGGL(tvam_surface_kernel<TVAM_MODE_ADJ>, dim3((unsigned)g), dim3(256), 0, stream, k, t, pat,
-                               idxmap, gin, vols, out, counter);
-            break;
-        default:
-            hipLaunchKernelGGL(tvam_surface_kernel<TVAM_MODE_COUNT>, dim3((unsigned)g), dim3(256), 0, stream, k, t,
-                               pat, idxmap, gin, vols, out, counter);
+        case TVAM_MODE_FWD: TVAM_SF_LAUNCH(TVAM_MODE_FWD) break;
+        case TVAM_MODE_ADJ: TVAM_SF_LAUNCH(TVAM_MODE_ADJ) break;
+        default: TVAM_SF_LAUNCH(TVAM_MODE_COUNT)
     }
+#undef TVAM_SF_LAUNCH
     return hipGetLastError();
 }
 

@@ -824,10 +824,8 @@ static int or_check(const tvam_desc* d) {
     if (d->projector_type != TVAM_PROJECTOR_COLLIMATED) return TVAM_ERR_UNSUPPORTED;
     if (d->film_channels != 1 && d->film_channels != 2) return TVAM_ERR_UNSUPPORTED;
     if (d->film_channels == 2 && (d->n_target_tris <= 0 || !d->target_tris)) return TVAM_ERR_INVALID;
-    if (d->film_channels == 2 && d->albedo != 0.0f) return TVAM_ERR_UNSUPPORTED;
     if (d->sensor_type != TVAM_SENSOR_DDA && d->sensor_type != TVAM_SENSOR_RATIO && d->sensor_type != TVAM_SENSOR_DELTA)
         return TVAM_ERR_INVALID;
-    if (d->sensor_type != TVAM_SENSOR_DDA && d->film_channels == 2) return TVAM_ERR_UNSUPPORTED;
     if (d->sensor_type == TVAM_SENSOR_DELTA && d->albedo == 0.0f) return TVAM_ERR_INVALID; /* volume.py:160-161 */
     if (d->sensor_type == TVAM_SENSOR_RATIO && !(d->majorant > 0.0f)) return TVAM_ERR_INVALID;
     if (d->albedo < 0.0f || d->albedo > 1.0f) return TVAM_ERR_INVALID;
@@ -861,6 +859,26 @@ static double or_point(const or_scene* s, const float p[3], double w, int mode, 
     } else if (mode == 1) return w * (double)grad[idx];
     return 0.0;
 }
+
+/* spawn_ray at a target hit (t along (o, dd), triangle tri): offset_p along the geometric
+   normal, away from the side the ray came from; o becomes the new origin. */
+static void or_spawn_target(const tvam_desc* d, int tri, float t, float o[3], const float dd[3]) {
+    const float* v = d->target_tris + 9 * tri;
+    float e1[3] = {v[3] - v[0], v[4] - v[1], v[5] - v[2]}, e2[3] = {v[6] - v[0], v[7] - v[1], v[8] - v[2]};
+    float c[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+    float ninv = 1.0f / sqrtf(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+    float n[3], p[3];
+    for (int k = 0; k < 3; ++k) {
+        n[k] = c[k] * ninv;
+        p[k] = fmaf(dd[k], t, o[k]);
+    }
+    float m = fmaxf(fmaxf(fabsf(p[0]), fabsf(p[1])), fabsf(p[2]));
+    float mag = (1.0f + m) * OR_RAY_EPS;
+    if (signbit(n[0] * dd[0] + n[1] * dd[1] + n[2] * dd[2])) mag = -mag;
+    for (int k = 0; k < 3; ++k) o[k] = fmaf(mag, n[k], p[k]);
+}
+
+static float or_target_hit(const tvam_desc* d, const float o[3], const float dd[3], int* tri);
 
 /* The path loop (volume.py:179-272) with the 'ratio' or 'delta' sensor (sensor.py:112-295):
    every medium segment [0, si.t) of the path either
@@ -899,6 +917,10 @@ static double or_trace_estimator(const or_scene* s, uint32_t pixel, uint64_t wav
     const float st = d->sigma_t, ss = d->albedo * d->sigma_t;
     const float mj = d->majorant;
     double acc = 0.0;
+    /* surface-aware film (C = 2): the target mesh cuts the segments as in or_trace_surface_scatter;
+       the deposits go to channel 0 inside the target, 1 outside (sensor.py:148-151, :257-260) */
+    const int sa = s->C == 2;
+    int inside = 0, cut = 0;
     for (int seg = 0;; ++seg) {
         const float q = fminf(0.99f, att);
         const float u_rr = or_pcg_float(&rng);
@@ -908,11 +930,20 @@ static double or_trace_estimator(const or_scene* s, uint32_t pixel, uint64_t wav
         }
         if (!(att != 0.0f)) break;
         float tsi = maxt;
-        if (seg > 0) {
+        if (seg > 0 || cut) {
             int which;
             tsi = or_container_hit(s, o, dd, &which);
             if (!(tsi < INFINITY)) break;
         }
+        int tri = -1, hit = 0;
+        float tt = INFINITY;
+        if (sa) {
+            tt = or_target_hit(d, o, dd, &tri);
+            hit = tt < tsi;
+            if (hit) tsi = tt;
+        }
+        double* film_c = film ? film + (inside ? 0 : 1) * sa : NULL;
+        const float* grad_c = grad ? grad + (inside ? 0 : 1) * sa : NULL;
         float tmi = INFINITY;
         if (has_sc) {
             const float u_m = or_pcg_float(&rng);
@@ -931,15 +962,29 @@ static double or_trace_estimator(const or_scene* s, uint32_t pixel, uint64_t wav
                 float p[3];
                 for (int k = 0; k < 3; ++k) p[k] = fmaf(dd[k], t, o[k]);
                 const double w = wseg * pk * ratio;
-                if (mode == 1) acc += or_point(s, p, w, 1, NULL, grad, visits);
-                else or_point(s, p, w * em, mode, film, NULL, visits);
+                if (mode == 1) acc += or_point(s, p, w, 1, NULL, grad_c, visits);
+                else or_point(s, p, w * em, mode, film_c, NULL, visits);
                 pk *= 1.0 - ratio;
             }
         } else if (!reached) { /* delta: the medium interaction */
             float p[3];
             for (int k = 0; k < 3; ++k) p[k] = fmaf(dd[k], tmi, o[k]);
-            if (mode == 1) acc += or_point(s, p, wseg, 1, NULL, grad, visits);
-            else or_point(s, p, wseg * em, mode, film, NULL, visits);
+            if (mode == 1) acc += or_point(s, p, wseg, 1, NULL, grad_c, visits);
+            else or_point(s, p, wseg * em, mode, film_c, NULL, visits);
+        }
+        if (reached && hit) { /* the target's null BSDF: pass through, depth unchanged (volume.py:271) */
+            if (has_sc) {
+                const float tr = expf(-tsi * st);
+                const float inv = tr > 0.0f ? 1.0f / tr : 0.0f;
+                att = att * (tr * inv); /* transmittance_eval_pdf: tr / pdf, pdf = tr */
+            } else {
+                att = att * expf(-st * tsi); /* volume.py:263 */
+            }
+            for (int i = 0; i < 3; ++i) (void)or_pcg_float(&rng); /* BSDF next_1d + next_2d */
+            inside = !inside;
+            cut = 1;
+            or_spawn_target(d, tri, tt, o, dd);
+            continue;
         }
         if (reached) break;
         const float tr = expf(-tmi * st);
@@ -1038,12 +1083,118 @@ static double or_trace_surface(const or_scene* s, uint32_t pixel, uint64_t wave_
     return acc;
 }
 
+/* Surface-aware film in a scattering medium (film_channels 2, has_scattering; volume.py:179-272
+   with the target mesh in the scene, null BSDF).  The loop of or_trace_scatter in which the
+   nearest surface of every medium segment is the nearer of the target mesh and the container
+   (or an occluder); every segment deposits from its origin up to that surface (sensor.py with
+   maxt = si.t) into channel 0 while inside the target, 1 outside (sensor.py:405-409;
+   inside_target starts outside and toggles at each target hit, volume.py:175, :218).  Per loop
+   iteration the draws are RR next_1d, the medium next_1d (volume.py:200), then BSDF next_1d +
+   next_2d at a surface (:225-226) or the phase function's next_1d + next_2d at a medium event
+   (:247-251).  A target hit before the free flight ends (reached_surface) passes the null BSDF:
+   the attenuation takes transmittance_eval_pdf's tr / pdf with pdf = tr (:206-208), the next
+   segment starts at the hit point offset along the face normal (spawn_ray), and depth is not
+   incremented (:271); the container or an occluder ends the path (transmission only, convex). */
+static double or_trace_surface_scatter(const or_scene* s, uint32_t pixel, uint64_t wave_index, uint32_t seed,
+                                       double em, int mode, double* film, const float* grad, uint64_t* visits) {
+    const tvam_desc* d = s->d;
+    or_ray ray;
+    or_pcg32 rng;
+    or_gen_ray_rng(s, pixel, wave_index, seed, &ray, &rng);
+    float o[3], dd[3], maxt;
+    double attd = 1.0;
+    int nsurf;
+    if (d->vial_type == TVAM_VIAL_CYLINDRICAL || d->vial_type == TVAM_VIAL_SQUARE) {
+        if (!(d->vial_type == TVAM_VIAL_SQUARE ? or_segment_square(s, &ray, o, dd, &maxt, &attd)
+                                               : or_segment_cylindrical(s, &ray, o, dd, &maxt, &attd)))
+            return 0.0;
+        nsurf = 2;
+    } else {
+        if (d->max_depth < 2 || !or_segment_index_matched(s, &ray, o, &maxt)) return 0.0;
+        for (int k = 0; k < 3; ++k) dd[k] = ray.d[k];
+        nsurf = 1;
+    }
+    for (int i = 0; i < 5 * nsurf; ++i) (void)or_pcg_float(&rng); /* the surface iterations before the medium */
+    float att = (float)attd;
+    int depth = nsurf, inside = 0;
+    const float st = d->sigma_t, ss = d->albedo * d->sigma_t;
+    double acc = 0.0;
+    float tcont = maxt;
+    for (int it = 0; it < 4096; ++it) {
+        const float q = fminf(0.99f, att);
+        const float u_rr = or_pcg_float(&rng);
+        if (depth > d->rr_depth) { /* volume.py:182-185 */
+            if (!(u_rr < q)) break;
+            att = att * (1.0f / q);
+        }
+        if (!(att != 0.0f)) break;
+        int tri;
+        const float tt = or_target_hit(d, o, dd, &tri);
+        const int hit = tt < tcont;
+        const float tsi = hit ? tt : tcont;
+        const float u_m = or_pcg_float(&rng);
+        const float tmi = -logf(1.0f - u_m) / st;
+        const int reached = tsi < tmi;
+        const int ch = inside ? 0 : 1;
+        if (mode == 0 || mode == 3)
+            (void)or_dda(s, o, dd, tsi, em * (double)att, mode, film + ch, NULL, -1, visits);
+        else if (mode == 1)
+            acc += (double)att * or_dda(s, o, dd, tsi, em, mode, NULL, grad + ch, -1, visits);
+        else
+            (void)or_dda(s, o, dd, tsi, em, mode, NULL, NULL, -1, visits);
+        if (reached) {
+            if (!hit) break; /* the container or an occluder: leaves the medium for good */
+            const float tr = expf(-tsi * st);
+            const float inv = tr > 0.0f ? 1.0f / tr : 0.0f;
+            att = att * (tr * inv);
+            for (int i = 0; i < 3; ++i) (void)or_pcg_float(&rng); /* BSDF next_1d + next_2d */
+            inside = !inside;
+            const float* v = d->target_tris + 9 * tri;
+            float e1[3] = {v[3] - v[0], v[4] - v[1], v[5] - v[2]}, e2[3] = {v[6] - v[0], v[7] - v[1], v[8] - v[2]};
+            float c[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+            float ninv = 1.0f / sqrtf(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+            float n[3], p[3];
+            for (int k = 0; k < 3; ++k) {
+                n[k] = c[k] * ninv;
+                p[k] = fmaf(dd[k], tt, o[k]);
+            }
+            float m = fmaxf(fmaxf(fabsf(p[0]), fabsf(p[1])), fabsf(p[2]));
+            float mag = (1.0f + m) * OR_RAY_EPS;
+            if (signbit(n[0] * dd[0] + n[1] * dd[1] + n[2] * dd[2])) mag = -mag;
+            for (int k = 0; k < 3; ++k) o[k] = fmaf(mag, n[k], p[k]);
+        } else {
+            const float tr = expf(-tmi * st);
+            const float pdf = tr * st;
+            const float inv = pdf > 0.0f ? 1.0f / pdf : 0.0f;
+            float w = tr * inv;
+            w = w * ss;
+            (void)or_pcg_float(&rng); /* phase next_1d (unused) */
+            const float u1 = or_pcg_float(&rng), u2 = or_pcg_float(&rng);
+            float wo[3];
+            or_phase_sample(d, dd, u1, u2, wo);
+            for (int k = 0; k < 3; ++k) {
+                o[k] = fmaf(dd[k], tmi, o[k]);
+                dd[k] = wo[k];
+            }
+            att = att * w;
+            ++depth;
+            if (depth >= d->max_depth) break;
+        }
+        int which;
+        tcont = or_container_hit(s, o, dd, &which);
+        if (!(tcont < INFINITY)) break; /* escapes through an open end: no surface, no deposit */
+    }
+    return acc;
+}
+
 /* one ray: generate + segment + DDA.  Returns the adjoint sum (mode 1).
    mode 0: forward, 3: forward with atomic film adds (shared film). */
 static double or_trace(const or_scene* s, uint32_t pixel, uint64_t wave_index, uint32_t seed, double em,
                        int mode, double* film, const float* grad, int only_slice, uint64_t* visits) {
     if (s->d->sensor_type != TVAM_SENSOR_DDA)
         return or_trace_estimator(s, pixel, wave_index, seed, em, mode, film, grad, visits);
+    if (s->d->albedo != 0.0f && s->C == 2)  /* has_scattering, surface-aware film */
+        return or_trace_surface_scatter(s, pixel, wave_index, seed, em, mode, film, grad, visits);
     if (s->d->albedo != 0.0f)  /* has_scattering (volume.py:159) */
         return or_trace_scatter(s, pixel, wave_index, seed, em, mode, film, grad, visits, s->part);
     if (s->C == 2) return or_trace_surface(s, pixel, wave_index, seed, em, mode, film, grad, only_slice, visits);
@@ -1214,8 +1365,9 @@ static int or_forward_impl(const tvam_desc* d, const float* active_data, const u
     if ((d->albedo != 0.0f || d->sensor_type != TVAM_SENSOR_DDA) && nthreads > 1) {
         /* scattered paths leave their slice: per-thread films (static
            schedule, fixed-order reduction), or atomics when those would not fit */
-        const int priv = (double)V * (double)nthreads * 8.0 <= 2.0e9;
-        double* films = priv ? (double*)calloc(V * (size_t)nthreads, sizeof(double)) : NULL;
+        const size_t VC = V * (size_t)s.C;  /* film entries (2 channels on surface-aware films) */
+        const int priv = (double)VC * (double)nthreads * 8.0 <= 2.0e9;
+        double* films = priv ? (double*)calloc(VC * (size_t)nthreads, sizeof(double)) : NULL;
         if (priv && !films) return TVAM_ERR_INVALID;
 #ifdef _OPENMP
 #pragma omp parallel num_threads(nthreads) reduction(+ : nv_total)
@@ -1226,7 +1378,7 @@ static int or_forward_impl(const tvam_desc* d, const float* active_data, const u
 #else
             const int tid = 0;
 #endif
-            double* mine = priv ? films + (size_t)tid * V : dose;
+            double* mine = priv ? films + (size_t)tid * VC : dose;
 #ifdef _OPENMP
 #pragma omp for schedule(static)
 #endif
@@ -1240,7 +1392,7 @@ static int or_forward_impl(const tvam_desc* d, const float* active_data, const u
         }
         if (priv) {
             for (int t = 0; t < nthreads; ++t)
-                for (size_t v = 0; v < V; ++v) dose[v] += films[(size_t)t * V + v];
+                for (size_t v = 0; v < VC; ++v) dose[v] += films[(size_t)t * VC + v];
             free(films);
         }
     } else if (nthreads <= 1) {

@@ -31,7 +31,9 @@ def test_single_gpu_line():
     assert r["metric"] == "optimizer iterations/sec (fwd+adjoint), 64³ voxels × 64 angles"
     assert r["n_gpus"] == 1 and r["steps"] == 3 and r["value"] > 0
     assert r["cpu_baseline"]["kind"] == "port" and r["cpu_baseline"]["host"]["threads"] >= 1
-    assert r["roofline"]["bound"] == "lds"
+    # counter summaries are committed for the BASELINE sizes only (profiles/r03/roofline_config<K>.json)
+    assert set(r["roofline"]) >= {"bound", "achieved", "peak", "unit", "frac", "traffic"}
+    assert r["roofline"]["frac"] is None and r["roofline"]["fwd_call_ms"] > 0
 
 
 @pytest.mark.parametrize("shard,port", [("slab", 29651), ("angle", 29653)])

@@ -136,12 +136,103 @@ def test_adjoint_dot_product(oracle):
     assert lhs == pytest.approx(rhs, rel=1e-6)  # delta_L = grad * inv_vol rounds to fp32 (volume.py:130)
 
 
-def test_rejects_scattering_and_missing_mesh(oracle):
+def test_rejects_missing_mesh(oracle):
     d = sa_desc(N=8, tris=cube_tris([-1, -1, -1], [1, 1, 1]))
-    d.albedo = 0.5
-    with pytest.raises(ValueError):
-        oracle.forward_surface(d, np.ones(8 * 8 * 8, np.float32), np.ones((8, 8, 8, 2), np.float32))
-    d.albedo = 0.0
     d.n_target_tris = 0
     with pytest.raises(ValueError):
         oracle.forward_surface(d, np.ones(8 * 8 * 8, np.float32), np.ones((8, 8, 8, 2), np.float32))
+
+
+# ---------------------------------------------------------------------------
+# Surface-aware films in a scattering medium (or_trace_surface_scatter; the README.md:135 run)
+# ---------------------------------------------------------------------------
+def sa_scatter_desc(tris, N=16, A=8, albedo=0.7, sigma_t=0.6, spp=2, max_depth=8):
+    cfg = benchy_index_matched(N=N, angles=A, size_mm=4.0, r=2.9, regular_sampling=False, spp=spp, sigma_t=sigma_t)
+    cfg["vial"]["medium"]["albedo"] = albedo
+    cfg["vial"]["medium"]["phase"] = {"type": "rayleigh"}
+    cfg["max_depth"] = max_depth
+    cfg["rr_depth"] = max_depth
+    d = desc_from_config(cfg)
+    plain = desc_from_config(cfg)
+    d.film_channels = 2
+    d.set_target(tris)
+    return d, plain
+
+
+def test_scatter_target_never_hit_equals_scattering_film(oracle):
+    """A target no path reaches (above the grid and the vial's open ends): every segment deposits
+    into channel 1 exactly as the one-channel scattering path (same draws, same segments)."""
+    N, A = 16, 8
+    d, plain = sa_scatter_desc(cube_tris([-0.5, -0.5, 30.0], [0.5, 0.5, 31.0]), N=N, A=A)
+    n = A * N * N
+    pat = np.random.default_rng(0).uniform(0, 0.1, n).astype(np.float32)
+    ones = np.ones((N, N, N, 2), np.float32)
+    sa, v2 = oracle.forward_surface(d, pat, ones, spp=2, seed=3, nthreads=8)
+    ref, v1 = oracle.forward(plain, pat, spp=2, seed=3, nthreads=8)
+    scat, _ = oracle.forward(plain, pat, spp=2, seed=3, nthreads=8, part=0)
+    assert scat.sum() > 0.05 * ref.sum()  # the scattered part is exercised
+    vv = float(np.prod((np.asarray(plain.bbox_max) - np.asarray(plain.bbox_min)) / N))
+    assert v1 == v2
+    assert np.all(sa[..., 0] == 0)
+    np.testing.assert_allclose(sa[..., 1] / vv, ref, rtol=1e-9, atol=1e-12 * np.abs(ref).max())
+    G = np.random.default_rng(1).uniform(-1, 1, (N, N, N)).astype(np.float32)
+    inv_vol = np.float32(1.0 / vv)
+    G2 = np.stack([np.zeros_like(G), G * inv_vol], -1)  # the plain adjoint scales G by inv_vol in fp32
+    g2, _ = oracle.adjoint_surface(d, G2, ones, spp=2, seed=3, nthreads=8)
+    g1, _ = oracle.adjoint(plain, G, spp=2, seed=3, nthreads=8)
+    np.testing.assert_allclose(g2, g1, rtol=1e-9, atol=1e-12 * np.abs(g1).max())
+
+
+def test_scatter_channels_follow_target_side(oracle):
+    """Segments deposit into channel 0 only inside the target and 1 only outside: voxels deep
+    inside the box get nothing in channel 1, voxels far outside nothing in channel 0."""
+    N, A = 16, 8
+    lo, hi = [-1.1, -0.7, -0.9], [0.8, 1.3, 0.6]
+    d, _ = sa_scatter_desc(cube_tris(lo, hi), N=N, A=A)
+    n = A * N * N
+    pat = np.random.default_rng(2).uniform(0, 0.1, n).astype(np.float32)
+    sa, _ = oracle.forward_surface(d, pat, np.ones((N, N, N, 2), np.float32), spp=2, seed=7, nthreads=8)
+    h = 4.0 / N
+    c = -2.0 + h * (np.arange(N) + 0.5)
+    z, y, x = np.meshgrid(c, c, c, indexing="ij")
+    deep_in = (x > lo[0] + h) & (x < hi[0] - h) & (y > lo[1] + h) & (y < hi[1] - h) & (z > lo[2] + h) & (z < hi[2] - h)
+    far_out = (x < lo[0] - h) | (x > hi[0] + h) | (y < lo[1] - h) | (y > hi[1] + h) | (z < lo[2] - h) | (z > hi[2] + h)
+    assert np.all(sa[..., 1][deep_in] == 0) and np.all(sa[..., 0][far_out] == 0)
+    assert np.all(sa[..., 0][deep_in] > 0)
+
+
+def test_scatter_channels_unbiased_vs_scattering_film(oracle):
+    """The channels add up, in expectation, to the one-channel scattering film: a target pass-through
+    weighs tr / pdf = 1 (volume.py:206-208) and restarts the track-length deposit from the hit
+    point.  Totals over 24 seeds agree within 3 standard errors."""
+    N, A = 12, 6
+    d, plain = sa_scatter_desc(cube_tris([-1.1, -0.7, -0.9], [0.8, 1.3, 0.6]), N=N, A=A, spp=4)
+    n = A * N * N
+    pat = np.random.default_rng(3).uniform(0, 0.1, n).astype(np.float32)
+    ones = np.ones((N, N, N, 2), np.float32)
+    vv = float(np.prod((np.asarray(plain.bbox_max) - np.asarray(plain.bbox_min)) / N))
+    ts, tp = [], []
+    for seed in range(24):
+        sa, _ = oracle.forward_surface(d, pat, ones, spp=4, seed=seed, nthreads=8)
+        ref, _ = oracle.forward(plain, pat, spp=4, seed=seed, nthreads=8)
+        ts.append(sa.sum())
+        tp.append(ref.sum() * vv)
+    ts, tp = np.asarray(ts), np.asarray(tp)
+    se = np.sqrt(ts.var(ddof=1) / ts.size + tp.var(ddof=1) / tp.size)
+    assert abs(ts.mean() - tp.mean()) < 3 * se + 1e-12, (ts.mean(), tp.mean(), se)
+    assert se < 0.02 * tp.mean()  # the check has teeth
+
+
+def test_scatter_adjoint_dot_product(oracle):
+    N, A = 12, 6
+    d, _ = sa_scatter_desc(cube_tris([-1.0, -0.8, -0.5], [0.9, 1.1, 0.7]), N=N, A=A)
+    vol = oracle.compute_volume(d, sample_count=32, nthreads=8)
+    rng = np.random.default_rng(4)
+    n = A * N * N
+    p = rng.uniform(0, 1, n).astype(np.float32)
+    G = rng.uniform(-1, 1, (N, N, N, 2)).astype(np.float32)
+    Ap, _ = oracle.forward_surface(d, p, vol, spp=2, seed=5, nthreads=8)
+    AtG, _ = oracle.adjoint_surface(d, G, vol, spp=2, seed=5, nthreads=8)
+    lhs = float(np.sum(Ap * G.astype(np.float64)))
+    rhs = float(np.dot(p.astype(np.float64), AtG))
+    assert lhs == pytest.approx(rhs, rel=1e-6)

@@ -1,0 +1,95 @@
+"""Committed roofline summary of one config's dominant kernel from a tools/pmc_bench.sh directory.
+
+usage: python tools/roofline_summary.py PMC_DIR CONFIG KERNEL_PREFIX BOUND OUT.json [MIN_BYTES]
+
+KERNEL_PREFIX selects the kernel by the start of its name as rocprofv3 prints it (template
+arguments included, e.g. "void tvam_fwd_planar_kernel<32, 2, false, 1, 2, true, false>"); every
+launch of it in the four counter passes is averaged.  The launch duration is the counter run's
+own (End_Timestamp - Start_Timestamp of the same dispatches, median over the passes), so every
+derived number can be recomputed from this one file; the --kernel-trace --stats pass of the same
+command is recorded beside it (avg_ns_trace) as the cross-check.  BOUND is the resource the
+roofline is taken on: "lds" (SQ_LDS_IDX_ACTIVE LDS-array cycles x 256 B, MI355X_MICROARCH.md
+section LDS: 64 dwords per clock per CU) or "hbm" (FETCH_SIZE x 2, the gfx950 correction for wide
+reads, + WRITE_SIZE, both in KiB).  Peaks at the 2.4 GHz spec clock: LDS 256 CUs x 256 B = 157.3
+TB/s, HBM 8 TB/s.  MIN_BYTES: the launch's least HBM traffic (its inputs read once, its outputs
+written once), for traffic / minimum."""
+import csv
+import json
+import os
+import statistics
+import subprocess
+import sys
+from collections import defaultdict
+
+CLOCK_GHZ, CUS = 2.4, 256
+PEAK = {"lds": CUS * 256 * CLOCK_GHZ, "hbm": 8000.0}  # GB/s
+
+
+def main():
+    src, config, prefix, bound, dst = sys.argv[1:6]
+    min_bytes = float(sys.argv[6]) if len(sys.argv) > 6 else None
+    counters = defaultdict(list)
+    durs = []
+    names = set()
+    for p in sorted(os.listdir(src)):
+        f = os.path.join(src, p, "p_counter_collection.csv")
+        if not os.path.exists(f):
+            continue
+        seen = {}
+        for r in csv.DictReader(open(f)):
+            if not r["Kernel_Name"].startswith(prefix):
+                continue
+            names.add(r["Kernel_Name"].split("(")[0])
+            counters[r["Counter_Name"]].append(float(r["Counter_Value"]))
+            seen[r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
+        if seen:
+            durs.append(statistics.mean(seen.values()))
+    assert len(names) == 1, names
+    kname = names.pop()
+    c = {k: statistics.mean(v) for k, v in counters.items()}
+    avg_ns = statistics.median(durs)
+    trace = None
+    ts = os.path.join(src, "trace", "k_kernel_stats.csv")
+    if os.path.exists(ts):
+        for r in csv.DictReader(open(ts)):
+            if r["Name"].startswith(prefix):
+                trace = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"])}
+    lds_bytes = c.get("SQ_LDS_IDX_ACTIVE", 0.0) * 256.0
+    hbm_bytes = 2.0 * c.get("FETCH_SIZE", 0.0) * 1024.0 + c.get("WRITE_SIZE", 0.0) * 1024.0
+    res_bytes = lds_bytes if bound == "lds" else hbm_bytes
+    achieved = res_bytes / avg_ns  # GB/s
+    clock = c["GRBM_GUI_ACTIVE"] / 8.0 / avg_ns if "GRBM_GUI_ACTIVE" in c else None
+    out = {
+        "config": int(config),
+        "command": open(os.path.join(src, "command.txt")).read().strip(),
+        "build": subprocess.run(["git", "rev-parse", "--short=12", "HEAD"], capture_output=True, text=True).stdout.strip(),
+        "kernel": kname,
+        "launches_per_pass": len(counters.get("SQ_WAVES", counters.get("FETCH_SIZE", []))),
+        "avg_ns": avg_ns,
+        "avg_ns_source": "counter passes' own dispatch timestamps (median over the passes)",
+        "avg_ns_trace": trace,
+        "clock_ghz_measured": clock,
+        "counters_per_launch": c,
+        "roofline": {
+            "bound": bound,
+            "achieved": achieved,
+            "peak": PEAK[bound],
+            "unit": "GB/s",
+            "frac": achieved / PEAK[bound],
+            "frac_at_measured_clock": (achieved / (PEAK[bound] * clock / CLOCK_GHZ)) if (bound == "lds" and clock) else None,
+            "resource_bytes_per_launch": res_bytes,
+            "traffic": hbm_bytes,
+            "traffic_over_min": (hbm_bytes / min_bytes) if min_bytes else None,
+            "min_bytes": min_bytes,
+            "valu_issue_frac": c.get("SQ_INSTS_VALU", 0.0) * 2.0 / (4 * CUS * CLOCK_GHZ * avg_ns),
+            "hbm_frac": hbm_bytes / avg_ns / PEAK["hbm"],
+            "lds_bank_conflict_frac": (c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"]) if c.get("SQ_LDS_IDX_ACTIVE") else None,
+        },
+    }
+    json.dump(out, open(dst, "w"), indent=1)
+    print(json.dumps({k: out[k] for k in ("kernel", "avg_ns", "avg_ns_trace", "clock_ghz_measured")}))
+    print(json.dumps(out["roofline"]))
+
+
+if __name__ == "__main__":
+    main()
