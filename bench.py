@@ -117,7 +117,7 @@ def cpu_baseline(config, N, seconds, threads):
 ROOFLINE_DIR = os.path.join(ROOT, "profiles", "r03")
 DOMINANT = {2: "forward: voxel-driven planar forward (two per iteration)",
             3: "forward: voxel-driven planar forward over refracted chords (two per iteration)",
-            4: "adjoint brick march of the scattered segments (23 launches per adjoint)",
+            4: "forward brick march of the scattered segments (23 launches per forward, two forwards per iteration)",
             5: "forward: per-ray tile kernel of the jittered first segments (two per iteration)"}
 
 
@@ -134,11 +134,11 @@ def make_roofline(args, N, A, world, prob, visits, rays, fwd_s, adj_s):
                 "note": "counter summaries are committed for the BASELINE sizes on one GPU", **info}
     summ = json.load(open(path))
     r = summ["roofline"]
-    return {"bound": r["bound"], "achieved": r["achieved"], "peak": r["peak"], "unit": "GB/s", "frac": r["frac"],
+    return {"bound": r["bound"], "achieved": r["achieved"], "peak": r["peak"], "unit": r["unit"], "frac": r["frac"],
             "traffic": r["traffic"], "traffic_over_min": r["traffic_over_min"], "min_bytes": r["min_bytes"],
             "kernel": summ["kernel"], "role": DOMINANT[args.config], "launch_ns_counter_run": summ["avg_ns"],
             "clock_ghz_counter_run": summ["clock_ghz_measured"],
-            "secondary": {"valu_issue_frac": r["valu_issue_frac"], "hbm_frac": r["hbm_frac"],
+            "secondary": {"valu_issue_frac": r["valu_issue_frac"], "hbm_frac": r["hbm_frac"], "lds_frac": r["lds_frac"],
                           "lds_bank_conflict_frac": r["lds_bank_conflict_frac"],
                           "frac_at_measured_clock": r["frac_at_measured_clock"]},
             "counters": os.path.relpath(path, ROOT), "counters_build": summ["build"], **info}

@@ -9,9 +9,10 @@ own (End_Timestamp - Start_Timestamp of the same dispatches, median over the pas
 derived number can be recomputed from this one file; the --kernel-trace --stats pass of the same
 command is recorded beside it (avg_ns_trace) as the cross-check.  BOUND is the resource the
 roofline is taken on: "lds" (SQ_LDS_IDX_ACTIVE LDS-array cycles x 256 B, MI355X_MICROARCH.md
-section LDS: 64 dwords per clock per CU) or "hbm" (FETCH_SIZE x 2, the gfx950 correction for wide
-reads, + WRITE_SIZE, both in KiB).  Peaks at the 2.4 GHz spec clock: LDS 256 CUs x 256 B = 157.3
-TB/s, HBM 8 TB/s.  MIN_BYTES: the launch's least HBM traffic (its inputs read once, its outputs
+section LDS: 64 dwords per clock per CU), "hbm" (FETCH_SIZE x 2, the gfx950 correction for wide
+reads, + WRITE_SIZE, both in KiB) or "valu" (SQ_INSTS_VALU wave64 instructions, issued one per 2
+cycles per SIMD-32).  Peaks at the 2.4 GHz spec clock: LDS 256 CUs x 256 B = 157.3 TB/s, HBM
+8 TB/s, VALU 1,228.8 G wave instructions / s.  MIN_BYTES: the launch's least HBM traffic (its inputs read once, its outputs
 written once), for traffic / minimum."""
 import csv
 import json
@@ -22,7 +23,8 @@ import sys
 from collections import defaultdict
 
 CLOCK_GHZ, CUS = 2.4, 256
-PEAK = {"lds": CUS * 256 * CLOCK_GHZ, "hbm": 8000.0}  # GB/s
+# GB/s; "valu": wave64 VALU instructions (G/s): 1024 SIMD-32 issuing one every 2 cycles
+PEAK = {"lds": CUS * 256 * CLOCK_GHZ, "hbm": 8000.0, "valu": 4 * CUS * CLOCK_GHZ / 2}
 
 
 def main():
@@ -39,13 +41,13 @@ def main():
         for r in csv.DictReader(open(f)):
             if not r["Kernel_Name"].startswith(prefix):
                 continue
-            names.add(r["Kernel_Name"].split("(")[0])
+            names.add(r["Kernel_Name"][:len(prefix)])
             counters[r["Counter_Name"]].append(float(r["Counter_Value"]))
             seen[r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
         if seen:
             durs.append(statistics.mean(seen.values()))
     assert len(names) == 1, names
-    kname = names.pop()
+    kname = names.pop().rstrip("(")
     c = {k: statistics.mean(v) for k, v in counters.items()}
     avg_ns = statistics.median(durs)
     trace = None
@@ -56,8 +58,8 @@ def main():
                 trace = {"calls": int(r["Calls"]), "avg_ns": float(r["AverageNs"])}
     lds_bytes = c.get("SQ_LDS_IDX_ACTIVE", 0.0) * 256.0
     hbm_bytes = 2.0 * c.get("FETCH_SIZE", 0.0) * 1024.0 + c.get("WRITE_SIZE", 0.0) * 1024.0
-    res_bytes = lds_bytes if bound == "lds" else hbm_bytes
-    achieved = res_bytes / avg_ns  # GB/s
+    res_bytes = {"lds": lds_bytes, "hbm": hbm_bytes, "valu": c.get("SQ_INSTS_VALU", 0.0)}[bound]
+    achieved = res_bytes / avg_ns  # GB/s (valu: G instructions / s)
     clock = c["GRBM_GUI_ACTIVE"] / 8.0 / avg_ns if "GRBM_GUI_ACTIVE" in c else None
     out = {
         "config": int(config),
@@ -74,14 +76,15 @@ def main():
             "bound": bound,
             "achieved": achieved,
             "peak": PEAK[bound],
-            "unit": "GB/s",
+            "unit": "Ginstr/s" if bound == "valu" else "GB/s",
             "frac": achieved / PEAK[bound],
-            "frac_at_measured_clock": (achieved / (PEAK[bound] * clock / CLOCK_GHZ)) if (bound == "lds" and clock) else None,
+            "frac_at_measured_clock": (achieved / (PEAK[bound] * clock / CLOCK_GHZ)) if (bound != "hbm" and clock) else None,
             "resource_bytes_per_launch": res_bytes,
             "traffic": hbm_bytes,
             "traffic_over_min": (hbm_bytes / min_bytes) if min_bytes else None,
             "min_bytes": min_bytes,
-            "valu_issue_frac": c.get("SQ_INSTS_VALU", 0.0) * 2.0 / (4 * CUS * CLOCK_GHZ * avg_ns),
+            "valu_issue_frac": c.get("SQ_INSTS_VALU", 0.0) / avg_ns / PEAK["valu"],
+            "lds_frac": lds_bytes / avg_ns / PEAK["lds"],
             "hbm_frac": hbm_bytes / avg_ns / PEAK["hbm"],
             "lds_bank_conflict_frac": (c["SQ_LDS_BANK_CONFLICT"] / c["SQ_LDS_IDX_ACTIVE"]) if c.get("SQ_LDS_IDX_ACTIVE") else None,
         },
