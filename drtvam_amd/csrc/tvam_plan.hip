@@ -1225,12 +1225,14 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
             if (s >= 0 && s < k.nz) rows_of[s].push_back(rc);
         } else {
             // jittered rows: a ray's height yc(jy) is monotone in jy in fp32 (tvam_ray_camera), and so is
-            // its slice (int)((yc - bmin) / h) (tvam_slice_of), so the slices of jy in [0, 1) lie between
-            // those of jy = 1 and jy = 0, computed with the kernels' own fp32 expressions (a slice list
-            // with a +-1 margin made two of every three row slots of the tile kernels idle at 1:1 rows)
+            // its slice (int)((yc - bmin) / h) (tvam_slice_of), so the slices of the sampler's jy in
+            // [0, 1 - 2^-23] (TvamPcg::next_float) lie between those of its two ends, computed with the
+            // kernels' own fp32 expressions (a slice list with a +-1 margin made two of every three row
+            // slots of the tile kernels idle at 1:1 rows; jy = 1 itself, never drawn, listed a row in
+            // the next slice wherever row and slice boundaries coincide)
             float xc, ytop, ybot;
             tvam_ray_camera(k, 0, row, 0.5f, 0.0f, xc, ytop);
-            tvam_ray_camera(k, 0, row, 0.5f, 1.0f, xc, ybot);
+            tvam_ray_camera(k, 0, row, 0.5f, 0.99999988f, xc, ybot);
             if (!(ytop > k.bmin[2] && ybot < k.bmax[2])) continue;  // every jittered ray misses the grid
             const float zlo = ybot > k.bmin[2] ? ybot : k.bmin[2], zhi = ytop < k.bmax[2] ? ytop : k.bmax[2];
             int s0 = (int)((zlo - k.bmin[2]) / k.h[2]), s1 = (int)((zhi - k.bmin[2]) / k.h[2]);
