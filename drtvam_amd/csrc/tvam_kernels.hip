@@ -24,6 +24,45 @@
 #ifndef TVAM_FWD_ACC64
 #define TVAM_FWD_ACC64 0  // 1: forward accumulates 64-bit fixed point (8 B per voxel of LDS)
 #endif
+#ifndef TVAM_TILE_DIAG
+#define TVAM_TILE_DIAG 0  // 1 (diagnostic builds only): per-wave slot / visit / cycle counters
+#endif
+
+#if TVAM_TILE_DIAG
+// [0] waves, [1] loop iterations, [2] lane slots, [3] zero-pattern skips, [4] inactive pixels,
+// [5] other slice / no segment, [6] misses the tile window, [7] marched lanes, [8] visits,
+// [9] sum over iterations of the wave's largest visit count, [10] cycles before the loop,
+// [11] setup cycles, [12] march cycles, [13] / [14] loop end / start times, [16 + b] marched lanes
+// whose visits are in [b/8, (b+1)/8) of their wave's largest count (b = 0..7)
+__device__ unsigned long long tvam_tile_diag[24];
+extern "C" int tvam_tile_diag_read(unsigned long long* host, int reset) {
+    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(tvam_tile_diag), sizeof(tvam_tile_diag)) != hipSuccess) return -1;
+    if (reset) {
+        static const unsigned long long zero[24] = {};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(tvam_tile_diag), zero, sizeof(zero)) != hipSuccess) return -1;
+    }
+    return 0;
+}
+// per-slot visit counts of one (tile, slice) workgroup (0xffffffff: nothing marched)
+__device__ unsigned tvam_tile_dslot[1 << 21];
+__device__ int tvam_tile_dsel[2] = {-1, -1};
+extern "C" int tvam_tile_diag_slots(int tile, int slice, unsigned* host, int n) {
+    const int sel[2] = {tile, slice};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(tvam_tile_dsel), sel, sizeof(sel)) != hipSuccess) return -1;
+    if (host && n > 0 &&
+        hipMemcpyFromSymbol(host, HIP_SYMBOL(tvam_tile_dslot), sizeof(unsigned) * (size_t)min(n, 1 << 21)) != hipSuccess)
+        return -1;
+    return 0;
+}
+__device__ __forceinline__ unsigned tvam_wave_umax(unsigned v) {
+    for (int off = 32; off > 0; off >>= 1) v = max(v, (unsigned)__shfl_xor((int)v, off, 64));
+    return v;
+}
+__device__ __forceinline__ unsigned long long tvam_wave_usum(unsigned long long v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+    return v;
+}
+#endif
 
 __device__ __forceinline__ float tvam_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
@@ -94,6 +133,7 @@ __device__ __forceinline__ void tvam_march(TvamMarchRay a, const float tsx, cons
             const int li = (int)(a.pv - tile) / ESZ, ly = li / tw, lx = li - ly * tw;
             nvis += (tn > tp && lx >= 1 && lx <= wx && ly >= 1 && ly <= wy) ? 1 : 0;
         }
+        if (TVAM_TILE_DIAG && ACC != ACC_COUNT) ++nvis;  // diagnostic builds: every visit
         tp = tn;
         const bool mx = a.Tx <= a.Ty;
         a.Tx = mx ? a.Tx + tsx : a.Tx;
@@ -130,6 +170,7 @@ struct TvamTileRay {
     int lidx, sx, sy;
     float t, rem, dtx, dty, tsx, tsy;
     float weight;  // interfaces' transmission weight (refracting vials; 1 otherwise)
+    int why;       // diagnostic builds: why the ray does not reach the tile (1 inactive, 2 slice, 3 window)
 };
 
 // Ray record pre-pass (one thread per ray of the shard): ray generation
@@ -205,10 +246,12 @@ __device__ __forceinline__ bool tvam_tile_ray(const TvamConsts& k, const TvamTil
     r.act = r.local;
     if (idxmap) {
         r.act = idxmap[r.local];
+        r.why = 1;
         if (r.act < 0) return false;  // inactive pixel
     }
     const int64_t ri = (int64_t)smp * ((int64_t)tp.n_shard * k.crop_y * k.crop_x) + r.local;  // sample-major records
     const int2 ii = tp.ray_i[ri];
+    r.why = 2;
     if (ii.y != kz + k.z0) return false;  // misses the grid / vial, or lies in another z-slice
     const float4 ff = tp.ray_f[ri];
     float4 an;
@@ -228,6 +271,7 @@ __device__ __forceinline__ bool tvam_tile_ray(const TvamConsts& k, const TvamTil
     tvam_axis_window(svy, sty, ff.w, an.y, y0, y1, tin1, tout1, nin1, nout1);
     const float tau_e = fmaxf(fmaxf(tin0, tin1), 0.0f);
     const float tau_x = fminf(fminf(tout0, tout1), ff.y);
+    r.why = 3;
     if (!(tau_e < tau_x)) return false;
     const int n0 = tvam_axis_steps(tau_e, ff.z, an.x, nin0, nout0);
     const int n1 = tvam_axis_steps(tau_e, ff.w, an.y, nin1, nout1);
@@ -266,6 +310,37 @@ __device__ __forceinline__ float tvam_block_sum(float v, float* red) {
     return m;
 }
 
+// Slot setup of the per-ray tile kernels: slot f -> (sample, slice row, list entry) -> the ray's
+// resumed march state in this tile.  false: nothing to march (zero pattern under skip_zero,
+// inactive pixel, other slice, or the ray misses the tile).
+template <int MODE, bool W2>
+__device__ __forceinline__ bool tvam_tile_slot(const TvamConsts& k, const TvamTiles& tp, const float* __restrict__ pat,
+                                               const int32_t* __restrict__ idxmap, int kz, int x0, int x1, int y0,
+                                               int y1, const uint32_t* __restrict__ slots, int rbeg, int nrows,
+                                               int smp, int ri, int rrem, int acc_mode, float fscale, TvamTileRay& r,
+                                               float& e0, int& why) {
+    const uint32_t e = slots[rrem];
+    const int al = (int)(e >> 16), colc = (int)(e & 0xffffu);
+    const int rowc = tp.slice_rows[rbeg + ri];
+    float em = 1.0f;
+    if (MODE == TVAM_MODE_FWD && k.skip_zero) {
+        const int64_t local = ((int64_t)(k.a0 + al) * k.crop_y + rowc) * k.crop_x + colc - k.shard_base;
+        why = 4;
+        if (pat[local] == 0.0f) return false;  // contributes exactly zero dose
+    }
+    const bool reach = tvam_tile_ray(k, tp, kz, x0, x1, y0, y1, rowc, al, colc, smp, idxmap, r);
+    why = reach ? 0 : r.why;
+    if (!reach) return false;
+    if (MODE == TVAM_MODE_FWD) {  // (after the slice test: half of config 5's slots lie in another slice)
+        em = pat[r.local] * k.wscale;  // Le * weight (common.py:108-111, volume.py:49)
+        if (acc_mode != ACC_FLOAT) em *= fscale;
+        em *= r.weight;  // attenuation of the vial's interfaces (sensor.py:404)
+    }
+    e0 = (W2 ? em * k.sig_t : em) * tvam_exp2(k.nsig2 * r.t);
+    return true;
+}
+
+// One workgroup per (xy tile, z-slice); the tile (+ guard band) resident in LDS.
 template <int MODE, bool W2>
 __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
     TvamConsts k, TvamTiles tp, const float* __restrict__ pat, const int32_t* __restrict__ idxmap,
@@ -278,6 +353,9 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
     float* s_red = tile + tile_words;
     unsigned* s_amax = reinterpret_cast<unsigned*>(s_red + 16);  // forward: per-angle max |p|
 
+#if TVAM_TILE_DIAG
+    const unsigned long long dg_t0 = __builtin_amdgcn_s_memtime();
+#endif
     const int tile_id = blockIdx.x, kz = (int)blockIdx.y + (MODE == TVAM_MODE_FWD ? tp.kz0 : 0);
     const int x0 = (tile_id % tp.ntx) * tsx, y0 = (tile_id / tp.ntx) * tsy;
     const int x1 = min(x0 + tsx, k.res[0]), y1 = min(y0 + tsy, k.res[1]);
@@ -385,50 +463,97 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
 
     constexpr int ESZ = (MODE == TVAM_MODE_FWD && TVAM_FWD_ACC64) ? 8 : 4;
     unsigned long long nvis = 0;
+    // one march from a resumed state, into the tile (forward / count) or gathering from it (adjoint)
+    auto march = [&](TvamMarchRay& m, float rtsx, float rtsy, int sxb, int syb) -> float {
+        float acc = 0.0f;
+        if (MODE == TVAM_MODE_FWD) {
+            if (TVAM_FWD_ACC64 && acc_mode == ACC_FIXED64)
+                tvam_march<ACC_FIXED64, W2>(m, rtsx, rtsy, sxb, syb, k.sig_t, acc, nvis);
+            else if (!TVAM_FWD_ACC64 && acc_mode == ACC_FIXED)
+                tvam_march<ACC_FIXED, W2>(m, rtsx, rtsy, sxb, syb, k.sig_t, acc, nvis);
+            else
+                tvam_march<ACC_FLOAT, W2>(m, rtsx, rtsy, sxb, syb, k.sig_t, acc, nvis);
+        } else if (MODE == TVAM_MODE_ADJ) {
+            tvam_march<ACC_GATHER, W2>(m, rtsx, rtsy, sxb, syb, k.sig_t, acc, nvis);
+        } else {
+            tvam_march<ACC_COUNT, W2>(m, rtsx, rtsy, sxb, syb, k.sig_t, acc, nvis, reinterpret_cast<const char*>(tile),
+                                      tw, wx, wy);
+        }
+        return acc;
+    };
+#if TVAM_TILE_DIAG
+    unsigned long long dg[16] = {};
+    unsigned hist[8] = {};
+    const unsigned long long tk0 = __builtin_amdgcn_s_memtime();
+    dg[10] = tk0 - dg_t0;
+    unsigned long long vis_prev = 0;
+    // per march round: visits of this lane, the wave's largest count, the lanes' histogram
+    auto diag_round = [&]() {
+        const unsigned v = (unsigned)(nvis - vis_prev);
+        vis_prev = nvis;
+        dg[8] += v;
+        const unsigned vm = tvam_wave_umax(v);
+        dg[9] += vm;
+        if (v > 0) ++hist[min(7, (int)(8u * v / vm))];
+    };
+#endif
+
     TvamSlot sl;
     tvam_slot_init(sl, threadIdx.x, max(per_row, 1));
     for (int f = threadIdx.x; f < total; f += TVAM_BLOCK, tvam_slot_next(sl, per_row)) {
         const int smp = spp == 1 ? 0 : sl.ri / nrows;
-        const uint32_t e = slots[sl.rrem];
-        const int al = (int)(e >> 16), colc = (int)(e & 0xffffu);
-        const int rowc = tp.slice_rows[rbeg + sl.ri - smp * nrows];
-        float em = 1.0f;
-        if (MODE == TVAM_MODE_FWD) {
-            const int64_t local = ((int64_t)(k.a0 + al) * k.crop_y + rowc) * k.crop_x + colc - k.shard_base;
-            const float p = pat[local];
-            if (p == 0.0f && k.skip_zero) continue;  // contributes exactly zero dose
-            em = p * k.wscale;                        // Le * weight (common.py:108-111, volume.py:49)
-            if (acc_mode != ACC_FLOAT) em *= fscale;
-        }
         TvamTileRay r;
-        if (!tvam_tile_ray(k, tp, kz, x0, x1, y0, y1, rowc, al, colc, smp, idxmap, r)) continue;
-        if (MODE == TVAM_MODE_FWD) em *= r.weight;  // attenuation of the vial's interfaces (sensor.py:404)
-        TvamMarchRay m;
-        m.pv = reinterpret_cast<char*>(tile) + r.lidx * ESZ;
-        m.Tx = r.dtx;
-        m.Ty = r.dty;
-        m.rem = r.rem;
-        m.stop = r.rem - 1e-6f;
-        m.nt0 = k.nsig2 * r.t;
-        m.ems = em;
-        m.e0 = (W2 ? em * k.sig_t : em) * tvam_exp2(m.nt0);
-        const int sxb = r.sx * ESZ, syb = r.sy * ESZ;
-        float acc = 0.0f;
-        if (MODE == TVAM_MODE_FWD) {
-            if (TVAM_FWD_ACC64 && acc_mode == ACC_FIXED64)
-                tvam_march<ACC_FIXED64, W2>(m, r.tsx, r.tsy, sxb, syb, k.sig_t, acc, nvis);
-            else if (!TVAM_FWD_ACC64 && acc_mode == ACC_FIXED)
-                tvam_march<ACC_FIXED, W2>(m, r.tsx, r.tsy, sxb, syb, k.sig_t, acc, nvis);
-            else
-                tvam_march<ACC_FLOAT, W2>(m, r.tsx, r.tsy, sxb, syb, k.sig_t, acc, nvis);
-        } else if (MODE == TVAM_MODE_ADJ) {
-            tvam_march<ACC_GATHER, W2>(m, r.tsx, r.tsy, sxb, syb, k.sig_t, acc, nvis);
-            atomicAdd(&out[r.act], acc * (k.wscale * r.weight));  // backward_from(Le * em_grad), volume.py:274-276
-        } else {
-            tvam_march<ACC_COUNT, W2>(m, r.tsx, r.tsy, sxb, syb, k.sig_t, acc, nvis, reinterpret_cast<const char*>(tile),
-                                  tw, wx, wy);
+        float e0;
+        int why = 5;
+        if (tvam_tile_slot<MODE, W2>(k, tp, pat, idxmap, kz, x0, x1, y0, y1, slots, rbeg, nrows, smp,
+                                     sl.ri - smp * nrows, sl.rrem, acc_mode, fscale, r, e0, why)) {
+            TvamMarchRay m;
+            m.pv = reinterpret_cast<char*>(tile) + r.lidx * ESZ;
+            m.Tx = r.dtx;
+            m.Ty = r.dty;
+            m.rem = r.rem;
+            m.stop = r.rem - 1e-6f;
+            m.e0 = e0;
+            const float acc = march(m, r.tsx, r.tsy, r.sx * ESZ, r.sy * ESZ);
+            if (MODE == TVAM_MODE_ADJ)
+                atomicAdd(&out[r.act], acc * (k.wscale * r.weight));  // backward_from(Le * em_grad), volume.py:274-276
+        }
+#if TVAM_TILE_DIAG
+        if ((int)blockIdx.x == tvam_tile_dsel[0] && (int)blockIdx.y == tvam_tile_dsel[1] && f < (1 << 21))
+            tvam_tile_dslot[f] = why == 0 ? (unsigned)(nvis - vis_prev) : 0xffffffffu;
+        dg[1] += 1;
+        dg[2] += 1;
+        dg[3] += why == 4;
+        dg[4] += why == 1;
+        dg[5] += why == 2;
+        dg[6] += why == 3;
+        dg[7] += why == 0;
+        diag_round();
+#endif
+    }
+#if TVAM_TILE_DIAG
+    {
+        const unsigned long long tk1 = __builtin_amdgcn_s_memtime();
+        // per-lane counts summed over the wave; iteration / cycle / max counts are wave-uniform (lane 0's)
+        unsigned long long sums[7];
+        for (int i = 2; i <= 8; ++i) sums[i - 2] = tvam_wave_usum(dg[i]);
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(&tvam_tile_diag[0], 1ull);
+            atomicAdd(&tvam_tile_diag[1], dg[1]);
+            for (int i = 2; i <= 8; ++i) atomicAdd(&tvam_tile_diag[i], sums[i - 2]);
+            atomicAdd(&tvam_tile_diag[9], dg[9]);
+            atomicAdd(&tvam_tile_diag[10], dg[10]);
+            atomicAdd(&tvam_tile_diag[11], dg[11]);
+            atomicAdd(&tvam_tile_diag[12], dg[12]);
+            atomicAdd(&tvam_tile_diag[13], tk1);  // minus tk0 below
+            atomicAdd(&tvam_tile_diag[14], tk0);
+        }
+        for (int b = 0; b < 8; ++b) {
+            const unsigned long long hb = tvam_wave_usum((unsigned long long)hist[b]);
+            if ((threadIdx.x & 63) == 0) atomicAdd(&tvam_tile_diag[16 + b], hb);
         }
     }
+#endif
 
     if (MODE == TVAM_MODE_FWD) {
         __syncthreads();
