@@ -33,6 +33,20 @@ struct TvamTiles {
     unsigned long long* frozen_n; // their count (beyond frozen_cap: the frozen kernel scans ray_i instead)
     int64_t frozen_cap;
     int32_t kz0, kz1;             // forward launches: local film slices [kz0, kz1) (tvam_forward_slices)
+    // Jittered rows whose rays reach neighbouring slices only at the sampler's extreme jitters
+    // (config 4 / 5: 1:1 rows, one ray in ~10^4 elsewhere; tvam_plan.hip): each slice then enumerates
+    // its main rows (row_main: the slice of the row's centre ray), and the few rays outside their
+    // row's main slice ("strays", listed by the ray setup, sorted by slice per record set) join the
+    // workgroup of their slice.  slice_moff = nullptr: every slice enumerates its full row list.
+    const int32_t* slice_moff;    // [res_z + 1] CSR offsets into slice_mrows
+    const int32_t* slice_mrows;
+    const int32_t* row_main;      // [crop_y] local main slice of each crop row (-1: none)
+    uint32_t* stray_idx;          // ray setup: stray record indices, appended (capacity stray_cap)
+    uint32_t* stray_cnt;          // [res_z + 1] strays per local slice (the scan's cursor afterwards)
+    uint32_t* stray_off;          // [res_z + 1] CSR offsets into stray_list
+    uint32_t* stray_list;         // stray record indices by slice
+    unsigned long long* stray_n;  // strays found (beyond stray_cap: the workgroups use the full row lists)
+    uint32_t stray_cap;
 };
 
 // Planar fast path of regular sampling (tvam_planar.hip): one ray record per
@@ -231,6 +245,7 @@ hipError_t tvam_launch_radon(const TvamConsts& k, const TvamTiles& t, const floa
 
 // Per-ray pre-pass: ray generation, vial segment and DDA initialisation of
 // every ray of the shard, stored as the records the tile kernels resume from.
+hipError_t tvam_launch_stray_lists(const TvamConsts& k, const TvamTiles& t, hipStream_t stream);
 hipError_t tvam_launch_ray_setup(const TvamConsts& k, const TvamTiles& t, float4* ray_f, int2* ray_i,
                                  float4* ray_g, const int32_t* idxmap, hipStream_t stream);
 

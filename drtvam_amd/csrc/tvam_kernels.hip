@@ -222,6 +222,16 @@ __global__ __launch_bounds__(256) void tvam_ray_setup_kernel(TvamConsts k, TvamT
             const unsigned long long j = atomicAdd(tp.frozen_n, 1ull);
             if ((int64_t)j < tp.frozen_cap) tp.frozen[j] = i;
         }
+        if (tp.row_main && !frozen) {  // a ray outside its row's main slice (TvamTiles::slice_moff)
+            const int zl = slice - k.z0;
+            if (zl >= 0 && zl < k.nz && zl != tp.row_main[rowc]) {
+                const unsigned long long j = atomicAdd(tp.stray_n, 1ull);
+                if (j < tp.stray_cap) {
+                    tp.stray_idx[j] = (uint32_t)i;
+                    atomicAdd(&tp.stray_cnt[zl], 1u);
+                }
+            }
+        }
         if (ray_g)
             ray_g[i] = make_float4(q.step[0] > 0 ? q.ts[0] : -q.ts[0], q.step[1] > 0 ? q.ts[1] : -q.ts[1], wgt, 0.0f);
     }
@@ -234,6 +244,52 @@ hipError_t tvam_launch_ray_setup(const TvamConsts& k, const TvamTiles& t, float4
     if (g > 65536) g = 65536;
     if (g < 1) g = 1;
     hipLaunchKernelGGL(tvam_ray_setup_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, t, ray_f, ray_i, ray_g, idxmap);
+    return hipGetLastError();
+}
+
+// Stray rays by slice (one workgroup): offsets from the ray setup's counts, then every stray
+// record index into its slice's range (order inside a slice: atomic; the tile kernels' sums do
+// not depend on it).  Beyond stray_cap the lists stay unused (the tile kernels test stray_n).
+__global__ __launch_bounds__(1024) void tvam_stray_lists_kernel(TvamTiles tp, int nz, int z0) {
+    __shared__ uint32_t s_part[1024];
+    const unsigned long long n_all = *tp.stray_n;
+    if (n_all > tp.stray_cap) return;
+    const int n = (int)n_all;
+    // exclusive scan of stray_cnt[0, nz): per-thread chunks, then the chunk totals
+    const int per = (nz + 1023) / 1024, b = (int)threadIdx.x * per;
+    uint32_t sum = 0;
+    for (int z = b; z < min(b + per, nz); ++z) sum += tp.stray_cnt[z];
+    s_part[threadIdx.x] = sum;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        uint32_t acc = 0;
+        for (int t = 0; t < 1024; ++t) {
+            const uint32_t v = s_part[t];
+            s_part[t] = acc;
+            acc += v;
+        }
+    }
+    __syncthreads();
+    uint32_t acc = s_part[threadIdx.x];
+    for (int z = b; z < min(b + per, nz); ++z) {
+        const uint32_t c = tp.stray_cnt[z];
+        tp.stray_off[z] = acc;
+        tp.stray_cnt[z] = 0;  // the fill's cursor
+        acc += c;
+    }
+    if (b < nz && b + per >= nz) tp.stray_off[nz] = acc;
+    if (nz == 0 && threadIdx.x == 0) tp.stray_off[0] = 0;
+    __syncthreads();
+    for (int j = threadIdx.x; j < n; j += 1024) {
+        const uint32_t i = tp.stray_idx[j];
+        const int zl = tp.ray_i[i].y - z0;
+        const uint32_t pos = atomicAdd(&tp.stray_cnt[zl], 1u);
+        tp.stray_list[tp.stray_off[zl] + pos] = i;
+    }
+}
+
+hipError_t tvam_launch_stray_lists(const TvamConsts& k, const TvamTiles& t, hipStream_t stream) {
+    hipLaunchKernelGGL(tvam_stray_lists_kernel, dim3(1), dim3(1024), 0, stream, t, k.nz, k.z0);
     return hipGetLastError();
 }
 
@@ -310,18 +366,27 @@ __device__ __forceinline__ float tvam_block_sum(float v, float* red) {
     return m;
 }
 
+// Record index (sample-major, tvam_ray_setup_kernel) -> (shard angle, crop row, crop column, sample).
+__device__ __forceinline__ void tvam_ray_of(const TvamConsts& k, const TvamTiles& tp, uint32_t i, int& al, int& rowc,
+                                            int& colc, int& smp) {
+    const int64_t n_local = (int64_t)tp.n_shard * k.crop_y * k.crop_x;
+    smp = (int)((int64_t)i / n_local);
+    const int64_t g = (int64_t)i - (int64_t)smp * n_local + k.shard_base;
+    const int64_t t = g / k.crop_x;
+    colc = (int)(g - t * k.crop_x);
+    const int64_t a = t / k.crop_y;
+    rowc = (int)(t - a * k.crop_y);
+    al = (int)a - k.a0;
+}
+
 // Slot setup of the per-ray tile kernels: slot f -> (sample, slice row, list entry) -> the ray's
 // resumed march state in this tile.  false: nothing to march (zero pattern under skip_zero,
 // inactive pixel, other slice, or the ray misses the tile).
 template <int MODE, bool W2>
 __device__ __forceinline__ bool tvam_tile_slot(const TvamConsts& k, const TvamTiles& tp, const float* __restrict__ pat,
                                                const int32_t* __restrict__ idxmap, int kz, int x0, int x1, int y0,
-                                               int y1, const uint32_t* __restrict__ slots, int rbeg, int nrows,
-                                               int smp, int ri, int rrem, int acc_mode, float fscale, TvamTileRay& r,
-                                               float& e0, int& why) {
-    const uint32_t e = slots[rrem];
-    const int al = (int)(e >> 16), colc = (int)(e & 0xffffu);
-    const int rowc = tp.slice_rows[rbeg + ri];
+                                               int y1, int al, int colc, int rowc, int smp, int acc_mode, float fscale,
+                                               TvamTileRay& r, float& e0, int& why) {
     float em = 1.0f;
     if (MODE == TVAM_MODE_FWD && k.skip_zero) {
         const int64_t local = ((int64_t)(k.a0 + al) * k.crop_y + rowc) * k.crop_x + colc - k.shard_base;
@@ -378,8 +443,14 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
     // this tile's (angle, column) slots, longest predicted in-tile march first
     const uint32_t* slots = tp.slots + tp.slot_off[tile_id];
     const int nrt = (int)(tp.slot_off[tile_id + 1] - tp.slot_off[tile_id]);
-    const int rbeg = tp.slice_off[kz], rend = tp.slice_off[kz + 1];
+    // rows: the slice's main rows plus its stray rays (TvamTiles::slice_moff), else its full row list
+    const bool main_rows = tp.slice_moff && *tp.stray_n <= (unsigned long long)tp.stray_cap;
+    const int32_t* rows = main_rows ? tp.slice_mrows : tp.slice_rows;
+    const int rbeg = main_rows ? tp.slice_moff[kz] : tp.slice_off[kz];
+    const int rend = main_rows ? tp.slice_moff[kz + 1] : tp.slice_off[kz + 1];
     const int nrows = rend - rbeg;
+    const int nrows_all = tp.slice_off[kz + 1] - tp.slice_off[kz];  // (every marched ray comes from these)
+    const int sbeg = main_rows ? (int)tp.stray_off[kz] : 0, send = main_rows ? (int)tp.stray_off[kz + 1] : 0;
     const int spp = (int)tp.spp;
     // slot f -> (sample, slice row, list entry) with the sample slowest: the lanes of a wave march
     // different pixels.  With the sample fastest, spp neighbouring lanes marched one pixel's
@@ -408,12 +479,23 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
         for (int f = threadIdx.x; f < first; f += TVAM_BLOCK, tvam_slot_next(sl, per_row)) {  // one look per (angle, column)
             const uint32_t e = slots[sl.rrem];
             const int al = (int)(e >> 16), colc = (int)(e & 0xffffu);
-            const int rowc = tp.slice_rows[rbeg + sl.ri];
+            const int rowc = rows[rbeg + sl.ri];
             const int64_t local = ((int64_t)(k.a0 + al) * k.crop_y + rowc) * k.crop_x + colc - k.shard_base;
             if (idxmap && idxmap[local] < 0) continue;
             const float v = fabsf(pat[local]);
             if (v > 0.0f) {
                 atomicMax(&s_amax[al], __float_as_uint(v));  // non-negative floats order like their bits
+                nz += 1.0f;
+            }
+        }
+        for (int f = sbeg + (int)threadIdx.x; f < send; f += TVAM_BLOCK) {  // the stray rays
+            int al, rowc, colc, smp;
+            tvam_ray_of(k, tp, tp.stray_list[f], al, rowc, colc, smp);
+            const int64_t local = ((int64_t)(k.a0 + al) * k.crop_y + rowc) * k.crop_x + colc - k.shard_base;
+            if (idxmap && idxmap[local] < 0) continue;
+            const float v = fabsf(pat[local]);
+            if (v > 0.0f) {
+                atomicMax(&s_amax[al], __float_as_uint(v));
                 nz += 1.0f;
             }
         }
@@ -435,7 +517,14 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
             for (int f = threadIdx.x; f < first; f += TVAM_BLOCK, tvam_slot_next(sl, per_row)) {
                 const uint32_t e = slots[sl.rrem];
                 const int al = (int)(e >> 16), colc = (int)(e & 0xffffu);
-                const int rowc = tp.slice_rows[rbeg + sl.ri];
+                const int rowc = rows[rbeg + sl.ri];
+                const int64_t local = ((int64_t)(k.a0 + al) * k.crop_y + rowc) * k.crop_x + colc - k.shard_base;
+                if (idxmap && idxmap[local] < 0) continue;
+                nbig += fabsf(pat[local]) >= thr ? 1.0f : 0.0f;
+            }
+            for (int f = sbeg + (int)threadIdx.x; f < send; f += TVAM_BLOCK) {
+                int al, rowc, colc, smp;
+                tvam_ray_of(k, tp, tp.stray_list[f], al, rowc, colc, smp);
                 const int64_t local = ((int64_t)(k.a0 + al) * k.crop_y + rowc) * k.crop_x + colc - k.shard_base;
                 if (idxmap && idxmap[local] < 0) continue;
                 nbig += fabsf(pat[local]) >= thr ? 1.0f : 0.0f;
@@ -443,7 +532,7 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
             nbig = tvam_block_sum(nbig, s_red);
         }
         const float per_angle = k.rays_per_voxel / (float)ns;
-        const float bound = amax_sum * fabsf(k.wscale) * k.vox_chord * per_angle * (float)(nrows * spp);
+        const float bound = amax_sum * fabsf(k.wscale) * k.vox_chord * per_angle * (float)(nrows_all * spp);
         const int headroom = TVAM_FWD_ACC64 ? 62 : 30;
         if (!(amax_sum > 0.0f)) {
             acc_mode = TVAM_FWD_ACC64 ? ACC_FIXED64 : ACC_FIXED;  // all-zero tile: every contribution is 0
@@ -502,11 +591,12 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
     tvam_slot_init(sl, threadIdx.x, max(per_row, 1));
     for (int f = threadIdx.x; f < total; f += TVAM_BLOCK, tvam_slot_next(sl, per_row)) {
         const int smp = spp == 1 ? 0 : sl.ri / nrows;
+        const uint32_t e = slots[sl.rrem];
         TvamTileRay r;
         float e0;
         int why = 5;
-        if (tvam_tile_slot<MODE, W2>(k, tp, pat, idxmap, kz, x0, x1, y0, y1, slots, rbeg, nrows, smp,
-                                     sl.ri - smp * nrows, sl.rrem, acc_mode, fscale, r, e0, why)) {
+        if (tvam_tile_slot<MODE, W2>(k, tp, pat, idxmap, kz, x0, x1, y0, y1, (int)(e >> 16), (int)(e & 0xffffu),
+                                     rows[rbeg + sl.ri - smp * nrows], smp, acc_mode, fscale, r, e0, why)) {
             TvamMarchRay m;
             m.pv = reinterpret_cast<char*>(tile) + r.lidx * ESZ;
             m.Tx = r.dtx;
@@ -530,6 +620,25 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
         dg[7] += why == 0;
         diag_round();
 #endif
+    }
+    for (int f = sbeg + (int)threadIdx.x; f < send; f += TVAM_BLOCK) {  // the slice's stray rays
+        int al, rowc, colc, smp;
+        tvam_ray_of(k, tp, tp.stray_list[f], al, rowc, colc, smp);
+        TvamTileRay r;
+        float e0;
+        int why = 5;
+        if (tvam_tile_slot<MODE, W2>(k, tp, pat, idxmap, kz, x0, x1, y0, y1, al, colc, rowc, smp, acc_mode, fscale, r,
+                                     e0, why)) {
+            TvamMarchRay m;
+            m.pv = reinterpret_cast<char*>(tile) + r.lidx * ESZ;
+            m.Tx = r.dtx;
+            m.Ty = r.dty;
+            m.rem = r.rem;
+            m.stop = r.rem - 1e-6f;
+            m.e0 = e0;
+            const float acc = march(m, r.tsx, r.tsy, r.sx * ESZ, r.sy * ESZ);
+            if (MODE == TVAM_MODE_ADJ) atomicAdd(&out[r.act], acc * (k.wscale * r.weight));
+        }
     }
 #if TVAM_TILE_DIAG
     {

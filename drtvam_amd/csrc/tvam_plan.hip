@@ -50,6 +50,9 @@ struct tvam_plan {
     float2* d_cs = nullptr;
     int32_t* d_slice_off = nullptr;
     int32_t* d_slice_rows = nullptr;
+    int32_t* d_slice_moff = nullptr;   // main-row lists (TvamTiles::slice_moff)
+    int32_t* d_slice_mrows = nullptr;
+    int32_t* d_row_main = nullptr;
     uint32_t* d_slots = nullptr;
     int64_t* d_slot_off = nullptr;
     unsigned long long* d_counter = nullptr;
@@ -63,6 +66,9 @@ struct tvam_plan {
         float4* g = nullptr;
         int64_t* frozen = nullptr;  // frozen-axis rays of the ray records (tvam_frozen_kernel)
         unsigned long long* frozen_n = nullptr;
+        uint32_t* stray = nullptr;  // stray rays (TvamTiles::stray_*): [cap] appended, [cap] by slice,
+        uint32_t* stray_cs = nullptr;  // [2 (nz + 1)] counts / cursors, offsets
+        unsigned long long* stray_n = nullptr;
         uint64_t cap = 0;
         bool valid = false;
         uint32_t spp = 0, seed = 0;
@@ -144,6 +150,9 @@ static void plan_free(tvam_plan* p) {
     (void)hipFree(p->d_cs);
     (void)hipFree(p->d_slice_off);
     (void)hipFree(p->d_slice_rows);
+    (void)hipFree(p->d_slice_moff);
+    (void)hipFree(p->d_slice_mrows);
+    (void)hipFree(p->d_row_main);
     (void)hipFree(p->d_slots);
     (void)hipFree(p->d_slot_off);
     (void)hipFree(p->d_counter);
@@ -154,6 +163,9 @@ static void plan_free(tvam_plan* p) {
         (void)hipFree(r.g);
         (void)hipFree(r.frozen);
         (void)hipFree(r.frozen_n);
+        (void)hipFree(r.stray);
+        (void)hipFree(r.stray_cs);
+        (void)hipFree(r.stray_n);
         if (r.ready) (void)hipEventDestroy(r.ready);
     }
     (void)hipFree(p->d_dense);
@@ -1249,6 +1261,37 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
             for (int s = s0; s <= s1; ++s) rows_of[s - k.z0].push_back(rc);
         }
     }
+    // Main rows of jittered plans (TvamTiles::slice_moff): a row's main slice is its centre ray's;
+    // used when the row lists hold rows that only the extreme jitters take into a slice (config 5:
+    // 1:1 rows list two per slice, and half of the tile kernels' slots were rays of the other
+    // slice, tools/tile_diag.py) and 32 interior jitters of every row stay in its main slice.
+    std::vector<int32_t> row_main(d.crop_y, -1), slice_moff(k.nz + 1, 0), slice_mrows;
+    bool main_rows = false;
+    if (!d.regular_sampling && env_int("TVAM_TILE_MAIN", 1) != 0) {
+        std::vector<std::vector<int32_t>> mrows(k.nz);
+        bool split = false;
+        for (int rc = 0; rc < d.crop_y && !split; ++rc) {
+            float xc, yc;
+            tvam_ray_camera(k, 0, d.crop_offset_y + rc, 0.5f, 0.5f, xc, yc);
+            const int sg = tvam_slice_of(k, yc);
+            for (int j = 0; j < 32 && !split; ++j) {
+                tvam_ray_camera(k, 0, d.crop_offset_y + rc, 0.5f, ((float)j + 0.5f) / 32.0f, xc, yc);
+                split = tvam_slice_of(k, yc) != sg;
+            }
+            if (sg >= k.z0 && sg < k.z0 + k.nz) {
+                row_main[rc] = sg - k.z0;
+                mrows[sg - k.z0].push_back(rc);
+            }
+        }
+        bool gain = false;
+        for (int z = 0; z < k.nz; ++z) gain = gain || mrows[z].size() < rows_of[z].size();
+        main_rows = gain && !split;
+        for (int z = 0; z < k.nz && main_rows; ++z) {
+            slice_moff[z] = (int32_t)slice_mrows.size();
+            slice_mrows.insert(slice_mrows.end(), mrows[z].begin(), mrows[z].end());
+        }
+        slice_moff[k.nz] = (int32_t)slice_mrows.size();
+    }
     std::vector<int32_t> slice_off(k.nz + 1, 0), slice_rows;
     p->max_rows_per_slice = 0;
     for (int s = 0; s < k.nz; ++s) {
@@ -1383,6 +1426,17 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
     p->tiles.slots = p->d_slots;
     p->tiles.slot_off = p->d_slot_off;
     p->tiles.ang = p->d_ang;
+    if (main_rows) {
+        if (slice_mrows.empty()) slice_mrows.push_back(0);
+        if ((rc = upload(&p->d_slice_moff, slice_moff)) || (rc = upload(&p->d_slice_mrows, slice_mrows)) ||
+            (rc = upload(&p->d_row_main, row_main))) {
+            plan_free(p);
+            return rc;
+        }
+        p->tiles.slice_moff = p->d_slice_moff;
+        p->tiles.slice_mrows = p->d_slice_mrows;
+        p->tiles.row_main = p->d_row_main;
+    }
     for (auto& r : p->rs)
         if ((e = hipEventCreateWithFlags(&r.ready, hipEventDisableTiming)) != hipSuccess) {
             plan_free(p);
@@ -1444,6 +1498,7 @@ static int ensure_dense(tvam_plan* p) {
 // buffer grows on demand (first call with a larger spp); the pre-pass runs
 // only when the cached records do not match the call.
 #define TVAM_FROZEN_CAP (1 << 20)
+#define TVAM_STRAY_CAP (1 << 22)  // stray rays per record set (more: the tile kernels use the full row lists)
 
 static int ensure_rays(tvam_plan* p, const TvamConsts& k, TvamTiles& t, const int32_t* idxmap, hipStream_t stream) {
     const uint64_t n = (uint64_t)(k.a1 - k.a0) * k.crop_y * k.crop_x * t.spp;
@@ -1455,6 +1510,14 @@ static int ensure_rays(tvam_plan* p, const TvamConsts& k, TvamTiles& t, const in
         t.frozen = r.frozen;
         t.frozen_n = r.frozen_n;
         t.frozen_cap = TVAM_FROZEN_CAP;
+        if (t.slice_moff) {
+            t.stray_idx = r.stray;
+            t.stray_list = r.stray + TVAM_STRAY_CAP;
+            t.stray_cnt = r.stray_cs;
+            t.stray_off = r.stray_cs + (k.nz + 1);
+            t.stray_n = r.stray_n;
+            t.stray_cap = TVAM_STRAY_CAP;
+        }
         r.used = ++p->ray_tick;
     };
     // jittered records of a sparse active set depend on the set (sampler streams by active
@@ -1483,6 +1546,11 @@ static int ensure_rays(tvam_plan* p, const TvamConsts& k, TvamTiles& t, const in
             ((e = hipMalloc((void**)&r.frozen, (size_t)TVAM_FROZEN_CAP * sizeof(int64_t))) != hipSuccess ||
              (e = hipMalloc((void**)&r.frozen_n, sizeof(unsigned long long))) != hipSuccess))
             return hip_fail(e, "hipMalloc (frozen-ray list)");
+        if (t.slice_moff && !r.stray &&
+            ((e = hipMalloc((void**)&r.stray, (size_t)2 * TVAM_STRAY_CAP * sizeof(uint32_t))) != hipSuccess ||
+             (e = hipMalloc((void**)&r.stray_cs, (size_t)2 * (k.nz + 1) * sizeof(uint32_t))) != hipSuccess ||
+             (e = hipMalloc((void**)&r.stray_n, sizeof(unsigned long long))) != hipSuccess))
+            return hip_fail(e, "hipMalloc (stray-ray lists)");
         r.cap = n;
         return 0;
     };
@@ -1508,8 +1576,13 @@ static int ensure_rays(tvam_plan* p, const TvamConsts& k, TvamTiles& t, const in
     bind(*r);
     if ((e = hipMemsetAsync(r->frozen_n, 0, sizeof(unsigned long long), stream)) != hipSuccess)
         return hip_fail(e, "hipMemsetAsync");
+    if (t.slice_moff && ((e = hipMemsetAsync(r->stray_n, 0, sizeof(unsigned long long), stream)) != hipSuccess ||
+                         (e = hipMemsetAsync(r->stray_cs, 0, (size_t)(k.nz + 1) * sizeof(uint32_t), stream)) != hipSuccess))
+        return hip_fail(e, "hipMemsetAsync");
     if ((e = tvam_launch_ray_setup(k, t, r->f, r->i, r->g, idxmap, stream)) != hipSuccess)
         return hip_fail(e, "ray setup launch");
+    if (t.slice_moff && (e = tvam_launch_stray_lists(k, t, stream)) != hipSuccess)
+        return hip_fail(e, "stray list launch");
     if ((e = hipEventRecord(r->ready, stream)) != hipSuccess) return hip_fail(e, "hipEventRecord");
     r->valid = true;
     r->spp = t.spp;
