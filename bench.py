@@ -382,6 +382,8 @@ def main():
                              else None),
             "fwd_ms": fwd_avg * 1e3, "adj_ms": adj_avg * 1e3, "visits_per_pass": visits, "rays_per_pass": rays,
             "final_loss": prob.loss_hist[-1],
+            # scattering: the last (line-search) forward's brick-bin chunks, how many the cache served
+            "bins": prob.proj.bin_stats() if prob.proj.desc.albedo != 0.0 else None,
         },
         "roofline": roofline,
         "cpu_baseline": cpu,

@@ -367,6 +367,20 @@ __device__ float sc_dda(const TvamConsts& k, float ox, float oy, float oz, float
     return acc;
 }
 
+// The largest of a 256-thread workgroup's non-negative values into *dst (float bits, which order
+// like the floats): one device atomic per workgroup (one per wave put ~10^6 atomics on a single
+// address per chunk)
+__device__ __forceinline__ void sc_block_max(float v, uint32_t* dst) {
+    __shared__ float s_max[4];
+    for (int off = 32; off > 0; off >>= 1) v = fmaxf(v, __shfl_xor(v, off, 64));
+    if ((threadIdx.x & 63) == 0) s_max[threadIdx.x >> 6] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        v = fmaxf(fmaxf(s_max[0], s_max[1]), fmaxf(s_max[2], s_max[3]));
+        if (v > 0.0f) atomicMax(dst, __float_as_uint(v));
+    }
+}
+
 template <int MODE>
 __global__ __launch_bounds__(256) void tvam_scatter_kernel(TvamConsts k, TvamTiles tp, const float* __restrict__ pat,
                                                            const int32_t* __restrict__ idxmap,
@@ -479,10 +493,7 @@ __global__ __launch_bounds__(256) void tvam_scatter_kernel(TvamConsts k, TvamTil
         for (int off = 32; off > 0; off >>= 1) nvis += __shfl_down(nvis, off, 64);
         if ((threadIdx.x & 63) == 0 && nvis) atomicAdd(counter, (unsigned long long)nvis);
     }
-    if (MODE == TVAM_MODE_EMIT && !sb.adj) {
-        for (int off = 32; off > 0; off >>= 1) wmax = fmaxf(wmax, __shfl_xor(wmax, off, 64));
-        if ((threadIdx.x & 63) == 0 && wmax > 0.0f) atomicMax(sb.wmax, __float_as_uint(wmax));
-    }
+    if (MODE == TVAM_MODE_EMIT && !sb.adj) sc_block_max(wmax, sb.wmax);
 }
 
 // ---------------------------------------------------------------------------
@@ -1445,21 +1456,22 @@ __global__ __launch_bounds__(256) void tvam_bin_reduce_kernel(TvamConsts k, Tvam
 
 // Cached forward bins, new pattern: each record's weight em * att with em of the new pattern,
 // the same expression as tvam_scatter_kernel<EMIT> (bit-identical records), and the chunk's
-// largest |weight| (slots without a segment carry attenuation 0: the same max as EMIT's).
+// largest |weight| (EMIT clears the attenuation of slots without a segment: the same max as
+// EMIT's).  32-bit slot indices (a chunk holds < 2^31 slots; chunks are whole pixels, so a slot's
+// pixel is the chunk's first pixel + s / (spp * slots)), one block-max atomic per workgroup.
 __global__ __launch_bounds__(256) void tvam_bin_reweight_kernel(TvamConsts k, TvamSegBuf sb, int spp,
                                                                 const float* __restrict__ pat) {
-    const int64_t ns = (sb.p1 - sb.p0) * sb.slots;
+    const uint32_t ns = (uint32_t)((sb.p1 - sb.p0) * sb.slots), per = (uint32_t)spp * (uint32_t)sb.slots;
+    const float* __restrict__ pc = pat + sb.p0 / spp;
     float wmax = 0.0f;
-    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t local = (sb.p0 + s / sb.slots) / spp;
-        const float em = pat[local] * k.wscale * k.inv_vol;
-        float* c = reinterpret_cast<float*>(&sb.r[TVAM_REC_F4 * s + 2]);
+    for (uint32_t s = blockIdx.x * blockDim.x + threadIdx.x; s < ns; s += gridDim.x * blockDim.x) {
+        const float em = pc[s / per] * k.wscale * k.inv_vol;
+        float* c = reinterpret_cast<float*>(&sb.r[TVAM_REC_F4 * (size_t)s + 2]);
         const float w = em * c[2];  // c[2] = 0 for slots without a segment
         c[1] = w;
         wmax = fmaxf(wmax, fabsf(w));
     }
-    for (int off = 32; off > 0; off >>= 1) wmax = fmaxf(wmax, __shfl_xor(wmax, off, 64));
-    if ((threadIdx.x & 63) == 0 && wmax > 0.0f) atomicMax(sb.wmax, __float_as_uint(wmax));
+    sc_block_max(wmax, sb.wmax);
 }
 
 template <typename T>
@@ -1535,6 +1547,7 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
     chunk = std::max<int64_t>(spp, chunk / spp * spp);
     chunk = std::min(npaths, chunk);
     const int64_t nsl = chunk * slots;
+    if (nsl >= ((int64_t)1 << 31)) return hipErrorNotSupported;  // 32-bit slot indices (reweight)
     hipError_t e;
     if (nsl > s.cap_slots) {
         const int keep_float = s.acc_float;
@@ -1569,10 +1582,11 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
         const size_t nch = (size_t)((npaths + chunk - 1) / chunk);
         if (s.fc.size() < nch) s.fc.resize(nch);
     }
-    // a chunk is cached while a quarter of the device memory stays free after its buffers
+    // a chunk is cached while an eighth of the device memory (+ 1 GB) stays free after its buffers
+    // (the call's other buffers, e.g. the ray records and this scratch, are allocated before)
     auto room = [](size_t bytes) {
         size_t fr = 0, tot = 0;
-        return hipMemGetInfo(&fr, &tot) == hipSuccess && fr > bytes + tot / 4 + ((size_t)256 << 20);
+        return hipMemGetInfo(&fr, &tot) == hipSuccess && fr > bytes + tot / 8 + ((size_t)1 << 30);
     };
     // forward brick march: int64 fixed point (default) or float LDS adds (TVAM_BIN_FLOAT)
     auto march_fwd = [&](const TvamSegBuf& sb, const uint32_t* vals, const uint32_t* bstart) {
@@ -1608,7 +1622,7 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
             s.st[3] += cc->total;
             if (cc->total == 0) continue;
             sb.r = cc->r;
-            int64_t g = std::min<int64_t>((ns + 255) / 256, 262144);
+            int64_t g = std::min<int64_t>((ns + 255) / 256, 8192);
             hipLaunchKernelGGL(tvam_bin_reweight_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, sb, spp, pat);
             march_fwd(sb, cc->vals, cc->bstart);
             if ((e = hipGetLastError()) != hipSuccess) return e;

@@ -112,7 +112,7 @@ def _default_chunks(s, min_chunks):
     got = proj.forward(_dense(s, p1), None, SPP4, SEED4).cpu().numpy()[..., 0]
     st = proj.bin_stats()
     print("forward bin stats", st)
-    # chunks are cached while a quarter of the device memory stays free: the rest (if any) run
+    # chunks are cached while an eighth of the device memory stays free: the rest (if any) run
     # uncached again in the second forward, next to the cached ones
     assert st["chunks"] >= min_chunks and st["cached"] == 0 and st["stored"] >= 1, st
     stored = st["stored"]
