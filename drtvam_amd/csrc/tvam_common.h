@@ -67,6 +67,7 @@ struct TvamConsts {
     float vial_hz_int;   // square: half height of the inner cuboid (0.45 height, geometry.py:207)
     const float* occ;    // occluder triangles [n_occ][3][3] (device; geometry.py:55-72), nullptr if none
     int32_t n_occ;
+    float occ_lo[3], occ_hi[3];  // the occluder triangles' bounding box (tvam_occ_hit's early out)
     const float* tgt;    // surface-aware films: target mesh triangles [n_tgt][3][3] (device), else nullptr
     int32_t n_tgt;
     int32_t sensor_type; // TVAM_SENSOR_* (dda / ratio / delta)
@@ -257,6 +258,26 @@ TVAM_HD float tvam_tri_hit(const float* v, float ox, float oy, float oz, float d
 
 TVAM_HD float tvam_occ_hit(const TvamConsts& k, float ox, float oy, float oz, float dx, float dy, float dz) {
     float best = TVAM_INF;
+    if (dz == 0.0f) {
+        // a planar ray that passes the occluders' bounding box, grown by the per-triangle skip's
+        // margin below, misses every triangle (same argument): most rays never test one
+        const float o[2] = {ox, oy}, d[2] = {dx, dy};
+        const float mz = 1e-3f * (1.0f + fabsf(k.occ_lo[2]) + fabsf(k.occ_hi[2]));
+        if (oz < k.occ_lo[2] - mz || oz > k.occ_hi[2] + mz) return TVAM_INF;
+        float t0 = 0.0f, t1 = TVAM_INF;  // tvam_tri_hit reports t >= 0 only
+        for (int a = 0; a < 2; ++a) {
+            const float m = 1e-3f * (1.0f + fabsf(k.occ_lo[a]) + fabsf(k.occ_hi[a]));
+            const float lo = k.occ_lo[a] - m, hi = k.occ_hi[a] + m;
+            if (d[a] == 0.0f) {
+                if (o[a] < lo || o[a] > hi) return TVAM_INF;
+                continue;
+            }
+            const float ta = (lo - o[a]) / d[a], tb = (hi - o[a]) / d[a];
+            t0 = fmaxf(t0, fminf(ta, tb));
+            t1 = fminf(t1, fmaxf(ta, tb));
+        }
+        if (t0 > t1) return TVAM_INF;
+    }
     for (int i = 0; i < k.n_occ; ++i) {
         const float* v = k.occ + 9 * i;
         // a planar ray (d.z = 0) far outside the triangle's z range misses it: Moller-Trumbore's

@@ -173,6 +173,32 @@ struct TvamTileRay {
     int why;       // diagnostic builds: why the ray does not reach the tile (1 inactive, 2 slice, 3 window)
 };
 
+// Appends this wave's stray rays (s: the lane's ray lies outside its row's main slice zl) to the
+// stray list with one atomic per wave, and adds the per-slice counts with one atomic per distinct
+// slice among them (a wave's lanes are neighbouring pixels of one row, so its strays share one or
+// two slices).  One atomic per stray on the single list counter serialised: config 5's ray setup
+// spent most of its time there.  List order is the atomics' (the tile kernels' sums ignore it).
+__device__ __forceinline__ void tvam_append_strays(const TvamTiles& tp, bool s, int zl, uint32_t idx) {
+    const unsigned long long m = __ballot(s);
+    if (m == 0) return;
+    const int lane = (int)__lane_id(), leader = __ffsll((long long)m) - 1;
+    unsigned long long base = 0;
+    if (lane == leader) base = atomicAdd(tp.stray_n, (unsigned long long)__popcll(m));
+    base = ((unsigned long long)(unsigned)__shfl((int)(base >> 32), leader, 64) << 32) |
+           (unsigned long long)(unsigned)__shfl((int)(unsigned)base, leader, 64);
+    const unsigned long long j = base + (unsigned long long)__popcll(m & ((1ull << lane) - 1ull));
+    const bool kept = s && j < (unsigned long long)tp.stray_cap;
+    if (kept) tp.stray_idx[j] = idx;
+    unsigned long long left = __ballot(kept);
+    while (left) {  // per-slice counts of the kept strays
+        const int l0 = __ffsll((long long)left) - 1;
+        const int z0 = __shfl(zl, l0, 64);
+        const unsigned long long same = __ballot(kept && zl == z0) & left;
+        if (lane == l0) atomicAdd(&tp.stray_cnt[z0], (unsigned)__popcll(same));
+        left &= ~same;
+    }
+}
+
 // Ray record pre-pass (one thread per ray of the shard): ray generation
 // (common.py:81-108), index-matched vial segment (volume.py:179-216) and DDA
 // initialisation (sensor.py:327-365).  Record index = sample * n_local + local.
@@ -186,11 +212,24 @@ __global__ __launch_bounds__(256) void tvam_ray_setup_kernel(TvamConsts k, TvamT
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         // record i = smp * n_local + local (sample-major: the tile kernels' lanes, which enumerate
         // the sample slowest, read consecutive records of neighbouring pixels)
-        const int smp = (int)(i / n_local);
-        const int64_t local = i - (int64_t)smp * n_local;
-        const int al = (int)(local / per_angle);
-        const int64_t pix = local - (int64_t)al * per_angle;
-        const int rowc = (int)(pix / k.crop_x), colc = (int)(pix - (int64_t)rowc * k.crop_x);
+        int smp, al, rowc, colc;
+        int64_t local;
+        if (n <= (int64_t)0xffffffff) {  // 32-bit index arithmetic (a 64-bit division is ~3x the code)
+            const uint32_t ii = (uint32_t)i, nl = (uint32_t)n_local, pa = (uint32_t)per_angle, cx = (uint32_t)k.crop_x;
+            const uint32_t s32 = ii / nl, l32 = ii - s32 * nl, a32 = l32 / pa, p32 = l32 - a32 * pa, r32 = p32 / cx;
+            smp = (int)s32;
+            local = (int64_t)l32;
+            al = (int)a32;
+            rowc = (int)r32;
+            colc = (int)(p32 - r32 * cx);
+        } else {
+            smp = (int)(i / n_local);
+            local = i - (int64_t)smp * n_local;
+            al = (int)(local / per_angle);
+            const int64_t pix = local - (int64_t)al * per_angle;
+            rowc = (int)(pix / k.crop_x);
+            colc = (int)(pix - (int64_t)rowc * k.crop_x);
+        }
         float jx = 0.5f, jy = 0.5f;
         if (!k.regular) {
             TvamPcg rng;
@@ -222,18 +261,14 @@ __global__ __launch_bounds__(256) void tvam_ray_setup_kernel(TvamConsts k, TvamT
             const unsigned long long j = atomicAdd(tp.frozen_n, 1ull);
             if ((int64_t)j < tp.frozen_cap) tp.frozen[j] = i;
         }
+        bool stray = false;
+        const int zl = slice - k.z0;
         if (tp.row_main && !frozen) {  // a ray outside its row's main slice (TvamTiles::slice_moff)
-            const int zl = slice - k.z0;
-            if (zl >= 0 && zl < k.nz && zl != tp.row_main[rowc]) {
-                const unsigned long long j = atomicAdd(tp.stray_n, 1ull);
-                if (j < tp.stray_cap) {
-                    tp.stray_idx[j] = (uint32_t)i;
-                    atomicAdd(&tp.stray_cnt[zl], 1u);
-                }
-            }
+            stray = zl >= 0 && zl < k.nz && zl != tp.row_main[rowc];
         }
         if (ray_g)
             ray_g[i] = make_float4(q.step[0] > 0 ? q.ts[0] : -q.ts[0], q.step[1] > 0 ? q.ts[1] : -q.ts[1], wgt, 0.0f);
+        if (tp.row_main) tvam_append_strays(tp, stray, zl, (uint32_t)i);
     }
 }
 

@@ -1182,6 +1182,14 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
         }
         p->k.occ = p->d_occ;
         p->k.n_occ = d.n_occluder_tris;
+        for (int a = 0; a < 3; ++a) {
+            p->k.occ_lo[a] = TVAM_INF;
+            p->k.occ_hi[a] = -TVAM_INF;
+        }
+        for (size_t i = 0; i < tri.size(); ++i) {
+            p->k.occ_lo[i % 3] = std::min(p->k.occ_lo[i % 3], tri[i]);
+            p->k.occ_hi[i % 3] = std::max(p->k.occ_hi[i % 3], tri[i]);
+        }
     }
     const TvamConsts& k = p->k;
     const int ns = a1 - a0;

@@ -397,8 +397,24 @@ __global__ __launch_bounds__(256) void tvam_scatter_kernel(TvamConsts k, TvamTil
     for (int64_t i = i0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         if (MODE == TVAM_MODE_EMIT && !sb.adj)  // slots without a segment: attenuation 0 (the cache's rescale)
             for (int q = 0; q < sb.slots; ++q) reinterpret_cast<float*>(&sb.r[TVAM_REC_F4 * ((i - sb.p0) * sb.slots + q) + 2])[2] = 0.0f;
-        const int64_t local = i / spp;
-        const int smp = (int)(i - local * spp);
+        int64_t local;
+        int smp, al, rowc, colc;
+        if (n <= (int64_t)0xffffffff) {  // 32-bit index arithmetic (a 64-bit division is ~3x the code)
+            const uint32_t ii = (uint32_t)i, sp = (uint32_t)spp, pa = (uint32_t)per_angle, cx = (uint32_t)k.crop_x;
+            const uint32_t l32 = ii / sp, a32 = l32 / pa, p32 = l32 - a32 * pa, r32 = p32 / cx;
+            local = (int64_t)l32;
+            smp = (int)(ii - l32 * sp);
+            al = (int)a32;
+            rowc = (int)r32;
+            colc = (int)(p32 - r32 * cx);
+        } else {
+            local = i / spp;
+            smp = (int)(i - local * spp);
+            al = (int)(local / per_angle);
+            const int64_t pix = local - (int64_t)al * per_angle;
+            rowc = (int)(pix / k.crop_x);
+            colc = (int)(pix - (int64_t)rowc * k.crop_x);
+        }
         float em = 1.0f;
         int64_t act = local;
         if (MODE == TVAM_MODE_FWD || (MODE == TVAM_MODE_EMIT && !sb.adj)) {
@@ -412,9 +428,6 @@ __global__ __launch_bounds__(256) void tvam_scatter_kernel(TvamConsts k, TvamTil
             act = idxmap[local];
             if (act < 0) continue;
         }
-        const int al = (int)(local / per_angle);
-        const int64_t pix = local - (int64_t)al * per_angle;
-        const int rowc = (int)(pix / k.crop_x), colc = (int)(pix - (int64_t)rowc * k.crop_x);
         TvamPcg rng;
         rng.seed(tp.seed, tvam_stream(k, idxmap, local, (uint32_t)spp, smp));
         float jx = 0.5f, jy = 0.5f;
