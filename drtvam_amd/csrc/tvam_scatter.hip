@@ -1263,23 +1263,16 @@ __device__ __forceinline__ void sc_unpack(const float4 a, const float4 b, const 
 }
 
 // (brick, entry) pairs; an entry is one (segment, brick) crossing, entries of
-// a segment are contiguous from off[slot].  The value is the segment slot; the
-// adjoint (jshift > 0) also stores the crossing's index j along its segment in the
-// key bits above the sorted ones, so the brick kernel writes its partial to entry
-// off[slot] + j without a slot_of gather on the record's dependency chain.
+// a segment are contiguous from off[slot].  The value is the segment slot.
 __global__ __launch_bounds__(256) void tvam_bin_fill_kernel(TvamConsts k, TvamSegBuf sb, const uint32_t* __restrict__ off,
                                                             int64_t nslots, uint32_t* __restrict__ keys,
-                                                            uint32_t* __restrict__ vals, int jshift, int cbits) {
+                                                            uint32_t* __restrict__ vals, int cbits) {
     for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nslots; s += (int64_t)gridDim.x * blockDim.x) {
         if (sb.m[s] == 0) continue;
         SegDda q;
         float w;
         sc_unpack(sb.r[TVAM_REC_F4 * s], sb.r[TVAM_REC_F4 * s + 1], sb.r[TVAM_REC_F4 * s + 2], q, w);
-        const uint32_t o0 = off[s];
-        uint32_t o = o0;
-        // adjoint: the segment's first entry in the record's spare word, so the brick kernel's
-        // partial store needs no off[slot] gather (the record line was just read)
-        if (jshift > 0) reinterpret_cast<uint32_t*>(&sb.r[TVAM_REC_F4 * s + 2])[3] = o0;
+        uint32_t o = off[s];
         // visits per unit length: one per voxel-face crossing of each moving axis
         float rate = 0.0f;
 #pragma unroll
@@ -1289,8 +1282,7 @@ __global__ __launch_bounds__(256) void tvam_bin_fill_kernel(TvamConsts k, TvamSe
             // wave of the brick kernel march entries of similar length
             // classes of 4 visits (16 classes) or 8 (8 classes)
             const int cls = (int)fminf((float)((1 << cbits) - 1), fmaxf(t1 - t0, 0.0f) * rate * (0.015625f * (float)(1 << cbits)));
-            const uint32_t jb = jshift > 0 ? (o - o0) << jshift : 0u;
-            keys[o] = ((uint32_t)bid << cbits) | (uint32_t)cls | jb;
+            keys[o] = ((uint32_t)bid << cbits) | (uint32_t)cls;
             vals[o] = (uint32_t)s;
             ++o;
         });
@@ -1311,16 +1303,18 @@ __global__ void tvam_bin_start_kernel(const uint32_t* __restrict__ keys, int64_t
 // per-visit weight min(1, st sqrt3 h), so the step is 2^-30 of the largest
 // single add and the int64 sums cannot overflow; ACC 1: float adds): the brick's visits
 // added in LDS, then dose += tile (the brick is this launch's alone).
-// Adjoint (ACC 2): the brick's grad * inv_vol staged in LDS, each entry's
-// weighted gather written to part[off[slot] + j] (no atomics; summed per path later;
-// j from the key bits above jshift).
+// Adjoint (ACC 2): the brick's grad * inv_vol staged in LDS, each entry's weighted gather
+// written at its own sorted position e with its DMD pixel (the chunk-local pixel of its slot,
+// slot / pslots): coalesced stores, no atomics.  tvam_scatter_binned then sorts the
+// (pixel, partial) pairs by pixel and sums each pixel's run (a partial stored at the
+// segment's own entry index instead -- one random 4-byte store per entry -- took 57 % of
+// this kernel's time on config 4).
 template <int ACC, int NT>
 __global__ __launch_bounds__(NT) void tvam_bin_march_kernel(TvamConsts k, TvamSegBuf sb,
                                                              const uint32_t* __restrict__ vals,
-                                                             const uint32_t* __restrict__ keys,
-                                                             const uint32_t* __restrict__ off, int jshift,
                                                              const uint32_t* __restrict__ bstart,
                                                              float* __restrict__ dose, const float* __restrict__ gin,
+                                                             uint32_t pslots, uint32_t* __restrict__ ppix,
                                                              float* __restrict__ part) {
     constexpr int NV = TVAM_BX * TVAM_BY * TVAM_BZ;
     __shared__ __attribute__((aligned(16))) unsigned char smem[NV * (ACC == 0 ? 8 : 4)];
@@ -1364,9 +1358,8 @@ __global__ __launch_bounds__(NT) void tvam_bin_march_kernel(TvamConsts k, TvamSe
         __syncthreads();
     }
     // Load pipeline over this thread's entries e, e + S, e + 2S, ... (S = NT), unrolled by two with
-    // two record register sets: while one entry marches, the records (and the adjoint's entry base
-    // off[slot] and key) of the next are in flight and the slot of the one after (vals -> record is
-    // two dependent gathers).  Indices are clamped to the brick's last entry, so every load is
+    // two record register sets: while one entry marches, the records of the next are in flight and
+    // the slot of the one after (vals -> record is two dependent gathers).  Indices are clamped to the brick's last entry, so every load is
     // issued unconditionally (no branch around it: the compiler's vmcnt waits then count only the
     // loads a use needs; a single register set with conditional loads had it wait for the next
     // entry's records at the top of every entry).
@@ -1374,18 +1367,16 @@ __global__ __launch_bounds__(NT) void tvam_bin_march_kernel(TvamConsts k, TvamSe
     const uint32_t et = e0 + threadIdx.x, el = e1 - 1;
     struct Ent {
         float4 a, b, c;
-        uint32_t of, key;
+        uint32_t slot;
     };
     auto load = [&](uint32_t slot, uint32_t e, Ent& r) {
+        (void)e;
         r.a = sb.r[TVAM_REC_F4 * slot];
         r.b = sb.r[TVAM_REC_F4 * slot + 1];
         r.c = sb.r[TVAM_REC_F4 * slot + 2];
-        if (ACC == 2) {
-            r.of = __float_as_uint(r.c.w);  // off[slot], stored by tvam_bin_fill_kernel
-            r.key = keys[min(e, el)];
-        }
+        r.slot = slot;
     };
-    auto run = [&](const Ent& r) {
+    auto run = [&](const Ent& r, uint32_t e) {
         SegDda q;
         float w;
         sc_unpack(r.a, r.b, r.c, q, w);
@@ -1411,7 +1402,10 @@ __global__ __launch_bounds__(NT) void tvam_bin_march_kernel(TvamConsts k, TvamSe
             sc_brick_march<true>(k, q, lo, hi, visit);
         else
             sc_brick_march<false>(k, q, lo, hi, visit);
-        if (ACC == 2) part[r.of + (r.key >> jshift)] = w * fmaf(pc, pv, acc);
+        if (ACC == 2) {
+            part[e] = w * fmaf(pc, pv, acc);
+            ppix[e] = r.slot / pslots;
+        }
     };
     if (et < e1) {
         uint32_t sB = vals[min(et + S, el)];
@@ -1420,11 +1414,11 @@ __global__ __launch_bounds__(NT) void tvam_bin_march_kernel(TvamConsts k, TvamSe
         for (uint32_t e = et;; e += 2 * S) {
             load(sB, e + S, rB);
             const uint32_t sC = vals[min(e + 2 * S, el)];
-            run(rA);
+            run(rA, e);
             if (e + S >= e1) break;
             load(sC, e + 2 * S, rA);
             sB = vals[min(e + 3 * S, el)];
-            run(rB);
+            run(rB, e + S);
             if (e + 2 * S >= e1) break;
         }
     }
@@ -1442,28 +1436,32 @@ __global__ __launch_bounds__(NT) void tvam_bin_march_kernel(TvamConsts k, TvamSe
     }
 }
 
-// Adjoint: per DMD pixel of the chunk, the sum of its samples' segment-brick
-// partials (contiguous from off[first slot]), added to the pattern gradient
-// after the first-segment kernels (same stream, one writer per entry).
-__global__ __launch_bounds__(256) void tvam_bin_reduce_kernel(TvamConsts k, TvamSegBuf sb, int spp,
-                                                              const uint32_t* __restrict__ off,
+// Adjoint: per DMD pixel of the chunk, the sum of its samples' segment-brick partials (its
+// run [pstart[i], pstart[i + 1]) of the pixel-sorted partials; one wave per pixel, coalesced
+// reads, a fixed butterfly order), added to the pattern gradient after the first-segment
+// kernels (same stream, one writer per pixel).
+__global__ __launch_bounds__(256) void tvam_bin_reduce_kernel(TvamSegBuf sb, int spp, const uint32_t* __restrict__ pstart,
                                                               const float* __restrict__ part,
                                                               const int32_t* __restrict__ idxmap,
                                                               float* __restrict__ grad) {
     const int64_t l0 = sb.p0 / spp, l1 = sb.p1 / spp;
-    for (int64_t local = l0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; local < l1;
-         local += (int64_t)gridDim.x * blockDim.x) {
-        const int64_t s0 = (local * spp - sb.p0) * sb.slots, s1 = s0 + (int64_t)spp * sb.slots;
-        const uint32_t a = off[s0], b = off[s1];
-        if (a == b) continue;
+    const int lane = (int)(threadIdx.x & 63);
+    const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, ws = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t local = l0 + w0; local < l1; local += ws) {
+        const int64_t i = local - l0;
+        const uint32_t a = pstart[i], b = pstart[i + 1];
+        if (a == b) continue;  // (uniform over the wave)
         float acc = 0.0f;
-        for (uint32_t e = a; e < b; ++e) acc += part[e];
-        int64_t act = local;
-        if (idxmap) {
-            act = idxmap[local];
-            if (act < 0) continue;
+        for (uint32_t e = a + (uint32_t)lane; e < b; e += 64) acc += part[e];
+        for (int off = 32; off > 0; off >>= 1) acc += __shfl_xor(acc, off, 64);
+        if (lane == 0) {
+            int64_t act = local;
+            if (idxmap) {
+                act = idxmap[local];
+                if (act < 0) continue;
+            }
+            grad[act] += acc;
         }
-        grad[act] += acc;
     }
 }
 
@@ -1544,12 +1542,6 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
     int cbits = bits <= 14 ? std::min(4, 16 - bits) : TVAM_BIN_CLASS_BITS;
     if (const char* v = getenv("TVAM_BIN_CBITS")) cbits = std::min(4, std::max(2, atoi(v)));
     bits += cbits;
-    // adjoint keys carry the crossing index along the segment above the sorted bits (a straight
-    // segment crosses fewer than nbx + nby + nbz bricks)
-    int jbits = 1;
-    while ((1 << jbits) < nbx + nby + nbz) ++jbits;
-    if (bits + jbits > 32) return hipErrorNotSupported;
-    const int jshift = adj ? bits : 0;
     const uint32_t kmask = bits >= 32 ? 0xffffffffu : ((1u << bits) - 1u);
     const int spp = (int)t.spp;
     const int64_t npaths = (int64_t)t.n_shard * k.crop_y * k.crop_x * spp;
@@ -1605,17 +1597,17 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
     auto march_fwd = [&](const TvamSegBuf& sb, const uint32_t* vals, const uint32_t* bstart) {
         const dim3 grid((unsigned)nbricks), blk(bin_nt);
         if (s.acc_float && bin_nt == 1024)
-            hipLaunchKernelGGL((tvam_bin_march_kernel<1, 1024>), grid, blk, 0, stream, k, sb, vals, nullptr, nullptr, 0, bstart, out,
-                               nullptr, nullptr);
+            hipLaunchKernelGGL((tvam_bin_march_kernel<1, 1024>), grid, blk, 0, stream, k, sb, vals, bstart, out,
+                               nullptr, 0u, nullptr, nullptr);
         else if (s.acc_float)
-            hipLaunchKernelGGL((tvam_bin_march_kernel<1, 512>), grid, blk, 0, stream, k, sb, vals, nullptr, nullptr, 0, bstart, out,
-                               nullptr, nullptr);
+            hipLaunchKernelGGL((tvam_bin_march_kernel<1, 512>), grid, blk, 0, stream, k, sb, vals, bstart, out,
+                               nullptr, 0u, nullptr, nullptr);
         else if (bin_nt == 1024)
-            hipLaunchKernelGGL((tvam_bin_march_kernel<0, 1024>), grid, blk, 0, stream, k, sb, vals, nullptr, nullptr, 0, bstart, out,
-                               nullptr, nullptr);
+            hipLaunchKernelGGL((tvam_bin_march_kernel<0, 1024>), grid, blk, 0, stream, k, sb, vals, bstart, out,
+                               nullptr, 0u, nullptr, nullptr);
         else
-            hipLaunchKernelGGL((tvam_bin_march_kernel<0, 512>), grid, blk, 0, stream, k, sb, vals, nullptr, nullptr, 0, bstart, out,
-                               nullptr, nullptr);
+            hipLaunchKernelGGL((tvam_bin_march_kernel<0, 512>), grid, blk, 0, stream, k, sb, vals, bstart, out,
+                               nullptr, 0u, nullptr, nullptr);
     };
     for (int i = 0; i < 5; ++i) s.st[i] = 0;
     s.st[4] = chunk;
@@ -1733,7 +1725,7 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
         }
         g = std::min<int64_t>((ns + 255) / 256, 262144);
         hipLaunchKernelGGL(tvam_bin_fill_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, sb, s.off, ns, s.keys[0],
-                           s.vals[0], jshift, cbits);
+                           s.vals[0], cbits);
         uint32_t* vals_out = keep ? cc->vals : s.vals[1];
         uint32_t* bstart = keep ? cc->bstart : s.bstart;
         if ((e = hipcub::DeviceRadixSort::SortPairs(s.temp, tb2, s.keys[0], s.keys[1], s.vals[0], vals_out,
@@ -1743,16 +1735,41 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
         hipLaunchKernelGGL(tvam_bin_start_kernel, dim3((unsigned)g), dim3(256), 0, stream, s.keys[1], (int64_t)total,
                            nbricks, kmask, cbits, bstart);
         if (adj) {
+            // partials at their sorted positions with their pixel (s.keys[1]: read by the start
+            // kernel above, free now), sorted by pixel into keys[0] / vals[0] (free since the
+            // sort), each pixel's run start in s.off (free since the fill), summed per pixel
+            uint32_t* ppix = s.keys[1];
+            const uint32_t pslots = (uint32_t)spp * (uint32_t)slots;
             if (bin_nt == 1024)
                 hipLaunchKernelGGL((tvam_bin_march_kernel<2, 1024>), dim3((unsigned)nbricks), dim3(1024), 0, stream, k,
-                                   sb, s.vals[1], s.keys[1], s.off, jshift, s.bstart, nullptr, gin, s.part);
+                                   sb, s.vals[1], s.bstart, nullptr, gin, pslots, ppix, s.part);
             else
                 hipLaunchKernelGGL((tvam_bin_march_kernel<2, 512>), dim3((unsigned)nbricks), dim3(512), 0, stream, k,
-                                   sb, s.vals[1], s.keys[1], s.off, jshift, s.bstart, nullptr, gin, s.part);
+                                   sb, s.vals[1], s.bstart, nullptr, gin, pslots, ppix, s.part);
             const int64_t npix = (p1 - p0) / spp;
-            g = std::min<int64_t>((npix + 255) / 256, 65536);
-            hipLaunchKernelGGL(tvam_bin_reduce_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, sb, spp, s.off,
-                               s.part, idxmap, out);
+            int pbits = 1;
+            while (((int64_t)1 << pbits) < npix) ++pbits;
+            float* psort = reinterpret_cast<float*>(s.vals[0]);
+            size_t tb3 = 0;
+            if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb3, ppix, s.keys[0], s.part, psort, (int)total, 0,
+                                                        pbits, stream)) != hipSuccess)
+                return e;
+            if (tb3 > s.temp_bytes) {
+                (void)hipFree(s.temp);
+                s.temp = nullptr;
+                s.temp_bytes = 0;
+                if ((e = hipMalloc(&s.temp, tb3)) != hipSuccess) return e;
+                s.temp_bytes = tb3;
+            }
+            if ((e = hipcub::DeviceRadixSort::SortPairs(s.temp, tb3, ppix, s.keys[0], s.part, psort, (int)total, 0,
+                                                        pbits, stream)) != hipSuccess)
+                return e;
+            g = std::min<int64_t>(((int64_t)total + 256) / 256, 65536);
+            hipLaunchKernelGGL(tvam_bin_start_kernel, dim3((unsigned)g), dim3(256), 0, stream, s.keys[0],
+                               (int64_t)total, (int)npix, 0xffffffffu, 0, s.off);
+            g = std::min<int64_t>((npix + 3) / 4, 65536);  // a wave per pixel
+            hipLaunchKernelGGL(tvam_bin_reduce_kernel, dim3((unsigned)g), dim3(256), 0, stream, sb, spp, s.off, psort,
+                               idxmap, out);
         } else {
             march_fwd(sb, vals_out, bstart);
         }
