@@ -1264,28 +1264,80 @@ __device__ __forceinline__ void sc_unpack(const float4 a, const float4 b, const 
 
 // (brick, entry) pairs; an entry is one (segment, brick) crossing, entries of
 // a segment are contiguous from off[slot].  The value is the segment slot.
+// Lane balance: a workgroup takes TVAM_FILL_T consecutive slots, orders them in LDS by their
+// brick count (counting sort, longest first; empty slots last) and its lanes walk them in that
+// order, so the lanes of a wave walk segments of similar length.  In slot order the lanes of a
+// wave idled on empty slots and on the wave's longest walk (lane utilisation 0.12).  Every
+// slot writes its own entries [off[slot], off[slot] + m[slot]): the order does not change the
+// output.
+#define TVAM_FILL_T 1024
 __global__ __launch_bounds__(256) void tvam_bin_fill_kernel(TvamConsts k, TvamSegBuf sb, const uint32_t* __restrict__ off,
                                                             int64_t nslots, uint32_t* __restrict__ keys,
                                                             uint32_t* __restrict__ vals, int cbits) {
-    for (int64_t s = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; s < nslots; s += (int64_t)gridDim.x * blockDim.x) {
-        if (sb.m[s] == 0) continue;
-        SegDda q;
-        float w;
-        sc_unpack(sb.r[TVAM_REC_F4 * s], sb.r[TVAM_REC_F4 * s + 1], sb.r[TVAM_REC_F4 * s + 2], q, w);
-        uint32_t o = off[s];
-        // visits per unit length: one per voxel-face crossing of each moving axis
-        float rate = 0.0f;
+    constexpr int U = TVAM_FILL_T / 256;
+    __shared__ uint32_t s_cnt[256];
+    __shared__ uint32_t s_ord[TVAM_FILL_T];
+    for (int64_t t0 = (int64_t)blockIdx.x * TVAM_FILL_T; t0 < nslots; t0 += (int64_t)gridDim.x * TVAM_FILL_T) {
+        s_cnt[threadIdx.x] = 0;
+        __syncthreads();
+        uint32_t bin[U], rk[U];
 #pragma unroll
-        for (int a = 0; a < 3; ++a) rate += q.ts[a] < TVAM_INF ? 1.0f / q.ts[a] : 0.0f;
-        sc_walk_bricks(k, q, [&](int bid, float t0, float t1) {
-            // low key bits: a class of the predicted in-brick visit count, so that the lanes of a
-            // wave of the brick kernel march entries of similar length
-            // classes of 4 visits (16 classes) or 8 (8 classes)
-            const int cls = (int)fminf((float)((1 << cbits) - 1), fmaxf(t1 - t0, 0.0f) * rate * (0.015625f * (float)(1 << cbits)));
-            keys[o] = ((uint32_t)bid << cbits) | (uint32_t)cls;
-            vals[o] = (uint32_t)s;
-            ++o;
-        });
+        for (int u = 0; u < U; ++u) {
+            const int64_t s = t0 + threadIdx.x + u * 256;
+            const uint32_t m = s < nslots ? sb.m[s] : 0u;
+            bin[u] = m == 0 ? 255u : 254u - min(m - 1u, 254u);  // longest first, empty slots last (bin 255)
+            rk[u] = atomicAdd(&s_cnt[bin[u]], 1u);
+        }
+        __syncthreads();
+        if (threadIdx.x < 64) {  // exclusive scan of the 256 bin counts (one wave, 4 bins per lane)
+            const int l = threadIdx.x;
+            uint32_t c[4], tot = 0;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                c[j] = s_cnt[4 * l + j];
+                tot += c[j];
+            }
+            uint32_t inc = tot;
+            for (int d = 1; d < 64; d <<= 1) {
+                const uint32_t v = __shfl_up(inc, d, 64);
+                if (l >= d) inc += v;
+            }
+            uint32_t run = inc - tot;
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const uint32_t cj = c[j];
+                s_cnt[4 * l + j] = run;
+                run += cj;
+            }
+        }
+        __syncthreads();
+        // non-empty slots: those before bin 255's start
+        const uint32_t nne = s_cnt[255];
+#pragma unroll
+        for (int u = 0; u < U; ++u) s_ord[s_cnt[bin[u]] + rk[u]] = threadIdx.x + u * 256;
+        __syncthreads();
+        for (uint32_t r = threadIdx.x; r < nne; r += 256) {
+            const int64_t s = t0 + s_ord[r];
+            SegDda q;
+            float w;
+            sc_unpack(sb.r[TVAM_REC_F4 * s], sb.r[TVAM_REC_F4 * s + 1], sb.r[TVAM_REC_F4 * s + 2], q, w);
+            uint32_t o = off[s];
+            // visits per unit length: one per voxel-face crossing of each moving axis
+            float rate = 0.0f;
+#pragma unroll
+            for (int a = 0; a < 3; ++a) rate += q.ts[a] < TVAM_INF ? 1.0f / q.ts[a] : 0.0f;
+            sc_walk_bricks(k, q, [&](int bid, float ta, float tb) {
+                // low key bits: a class of the predicted in-brick visit count, so that the lanes of a
+                // wave of the brick kernel march entries of similar length
+                // classes of 4 visits (16 classes) or 8 (8 classes)
+                const int cls = (int)fminf((float)((1 << cbits) - 1),
+                                           fmaxf(tb - ta, 0.0f) * rate * (0.015625f * (float)(1 << cbits)));
+                keys[o] = ((uint32_t)bid << cbits) | (uint32_t)cls;
+                vals[o] = (uint32_t)s;
+                ++o;
+            });
+        }
+        __syncthreads();
     }
 }
 
@@ -1723,7 +1775,7 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
             if ((e = hipMalloc(&s.temp, tb2)) != hipSuccess) return e;
             s.temp_bytes = tb2;
         }
-        g = std::min<int64_t>((ns + 255) / 256, 262144);
+        g = std::min<int64_t>((ns + TVAM_FILL_T - 1) / TVAM_FILL_T, 65536);
         hipLaunchKernelGGL(tvam_bin_fill_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, sb, s.off, ns, s.keys[0],
                            s.vals[0], cbits);
         uint32_t* vals_out = keep ? cc->vals : s.vals[1];
