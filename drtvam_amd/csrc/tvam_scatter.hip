@@ -166,11 +166,22 @@ __device__ __forceinline__ int sc_nbr(const TvamConsts& k, int a) {
     return (k.res[a] + B - 1) / B;
 }
 
+// tvam_axis_window's exit time of one axis' window [lo, hi), without branches (the same values)
+__device__ __forceinline__ float sc_axis_tout(int sv, int step, float dtm0, float ts, int lo, int hi) {
+    const int nout = step > 0 ? hi - sv : sv - lo + 1;
+    const float tm = nout > 0 ? fmaf((float)(nout - 1), ts, dtm0) : -TVAM_INF;
+    const float tf = (sv >= lo && sv < hi) ? TVAM_INF : -TVAM_INF;  // an axis that never steps
+    return dtm0 < TVAM_INF ? tm : tf;
+}
+
 // Bricks a segment's DDA visits, in time order: each axis' brick windows
 // partition time exactly (tvam_axis_window on brick bounds), so stepping the
 // axis whose window closes first walks the same sequence the brick kernel
 // resumes from.  F(brick id, relative time the segment enters / leaves the
-// brick) per brick; returns the count.
+// brick) per brick; returns the count.  Branch-free steps (selects; only the
+// stepped axis can leave the grid): the per-axis if / else chain compiled to ~50
+// scalar exec-mask instructions per step on top of ~70 VALU, and the fill kernel
+// and the record writer spend most of their time in this loop.
 template <typename F>
 __device__ __forceinline__ int sc_walk_bricks(const TvamConsts& k, const SegDda& q, F&& f) {
     const int nb0 = sc_nbr(k, 0), nb1 = sc_nbr(k, 1), nb2 = sc_nbr(k, 2);
@@ -180,30 +191,22 @@ __device__ __forceinline__ int sc_walk_bricks(const TvamConsts& k, const SegDda&
     for (int guard = 0; guard < 4096; ++guard) {
         const int bid = (b2 * nb1 + b1) * nb0 + b0;
         ++cnt;
-        float tin, t0, t1, t2;
-        int nin, nout;
-        tvam_axis_window(q.sv[0], q.step[0], q.dtm0[0], q.ts[0], b0 * TVAM_BX, min(b0 * TVAM_BX + TVAM_BX, k.res[0]),
-                         tin, t0, nin, nout);
-        tvam_axis_window(q.sv[1], q.step[1], q.dtm0[1], q.ts[1], b1 * TVAM_BY, min(b1 * TVAM_BY + TVAM_BY, k.res[1]),
-                         tin, t1, nin, nout);
-        tvam_axis_window(q.sv[2], q.step[2], q.dtm0[2], q.ts[2], b2 * TVAM_BZ, min(b2 * TVAM_BZ + TVAM_BZ, k.res[2]),
-                         tin, t2, nin, nout);
+        const float t0 = sc_axis_tout(q.sv[0], q.step[0], q.dtm0[0], q.ts[0], b0 * TVAM_BX,
+                                      min(b0 * TVAM_BX + TVAM_BX, k.res[0]));
+        const float t1 = sc_axis_tout(q.sv[1], q.step[1], q.dtm0[1], q.ts[1], b1 * TVAM_BY,
+                                      min(b1 * TVAM_BY + TVAM_BY, k.res[1]));
+        const float t2 = sc_axis_tout(q.sv[2], q.step[2], q.dtm0[2], q.ts[2], b2 * TVAM_BZ,
+                                      min(b2 * TVAM_BZ + TVAM_BZ, k.res[2]));
         const bool m0 = t0 <= t1 && t0 <= t2;
         const bool m1 = !m0 && t1 <= t2;
         const float tm = m0 ? t0 : (m1 ? t1 : t2);
         f(bid, tprev, fminf(tm, q.tau_end));
         tprev = tm;
         if (!(tm < q.tau_end)) break;
-        if (m0) {
-            b0 += q.step[0];
-            if (b0 < 0 || b0 >= nb0) break;
-        } else if (m1) {
-            b1 += q.step[1];
-            if (b1 < 0 || b1 >= nb1) break;
-        } else {
-            b2 += q.step[2];
-            if (b2 < 0 || b2 >= nb2) break;
-        }
+        b0 += m0 ? q.step[0] : 0;
+        b1 += m1 ? q.step[1] : 0;
+        b2 += (m0 || m1) ? 0 : q.step[2];
+        if ((unsigned)b0 >= (unsigned)nb0 || (unsigned)b1 >= (unsigned)nb1 || (unsigned)b2 >= (unsigned)nb2) break;
     }
     return cnt;
 }
