@@ -73,6 +73,8 @@ struct tvam_plan {
         bool valid = false;
         uint32_t spp = 0, seed = 0;
         bool sparse = false;  // records built for a sparse active set (streams by active position)
+        const void* pix = nullptr;  // ... that set (active_pixels pointer and count: the records'
+        uint64_t npix = 0;          // key; tvam_plan_set_active drops them after in-place changes)
         hipEvent_t ready = nullptr;
         uint64_t used = 0;
     };
@@ -1508,7 +1510,8 @@ static int ensure_dense(tvam_plan* p) {
 #define TVAM_FROZEN_CAP (1 << 20)
 #define TVAM_STRAY_CAP (1 << 22)  // stray rays per record set (more: the tile kernels use the full row lists)
 
-static int ensure_rays(tvam_plan* p, const TvamConsts& k, TvamTiles& t, const int32_t* idxmap, hipStream_t stream) {
+static int ensure_rays(tvam_plan* p, const TvamConsts& k, TvamTiles& t, const int32_t* idxmap, hipStream_t stream,
+                       const uint32_t* active_pixels = nullptr, uint64_t n_active = 0) {
     const uint64_t n = (uint64_t)(k.a1 - k.a0) * k.crop_y * k.crop_x * t.spp;
     hipError_t e;
     auto bind = [&](tvam_plan::RaySlot& r) {
@@ -1529,9 +1532,13 @@ static int ensure_rays(tvam_plan* p, const TvamConsts& k, TvamTiles& t, const in
         r.used = ++p->ray_tick;
     };
     // jittered records of a sparse active set depend on the set (sampler streams by active
-    // position): recomputed every call, like every call with a new seed
+    // position): reused for the same set (pointer and count; the slice ranges of one forward,
+    // the line-search forward of the same seed), like a dense set's for the same seed and spp
+    auto same_set = [&](const tvam_plan::RaySlot& r) {
+        return idxmap ? (r.sparse && r.pix == (const void*)active_pixels && r.npix == n_active) : !r.sparse;
+    };
     for (auto& r : p->rs)
-        if (r.valid && r.spp == t.spp && (k.regular || (r.seed == t.seed && !r.sparse && !idxmap))) {
+        if (r.valid && r.spp == t.spp && (k.regular || (r.seed == t.seed && same_set(r)))) {
             bind(r);
             e = hipStreamWaitEvent(stream, r.ready, 0);
             return e == hipSuccess ? 0 : hip_fail(e, "hipStreamWaitEvent");
@@ -1596,6 +1603,8 @@ static int ensure_rays(tvam_plan* p, const TvamConsts& k, TvamTiles& t, const in
     r->spp = t.spp;
     r->seed = t.seed;
     r->sparse = idxmap != nullptr;
+    r->pix = idxmap ? (const void*)active_pixels : nullptr;
+    r->npix = idxmap ? n_active : 0;
     return 0;
 }
 
@@ -1709,7 +1718,7 @@ static int forward_impl(tvam_plan* p, const float* active_data, const uint32_t* 
             t.kz0 = zb;
             t.kz1 = ze;
         }
-        if ((rc = ensure_rays(p, kc, t, idxmap, stream))) return rc;
+        if ((rc = ensure_rays(p, kc, t, idxmap, stream, active_pixels, n_active))) return rc;
         unsigned long long* stats = nullptr;
         if (p->desc.flags & TVAM_FLAG_FWD_STATS) {
             if ((e = hipMemsetAsync(p->d_counter, 0, sizeof(unsigned long long), stream)) != hipSuccess)
@@ -1783,7 +1792,7 @@ extern "C" int tvam_adjoint(tvam_plan* p, const float* grad_dose, const uint32_t
         TvamTiles t = p->tiles;
         t.spp = spp;
         t.seed = seed;
-        if ((rc = ensure_rays(p, k, t, idxmap, stream))) return rc;
+        if ((rc = ensure_rays(p, k, t, idxmap, stream, active_pixels, n_active))) return rc;
         e = tvam_launch_tiles(TVAM_MODE_ADJ, k, t, p->lds_bytes, nullptr, idxmap, grad_dose, grad_active, nullptr,
                               stream);
         if (e == hipSuccess)

@@ -68,11 +68,23 @@ class Projection:
         if t.device != self.device or t.dtype != dtype or not t.is_contiguous():
             raise ValueError(f"{name} must be a contiguous {dtype} tensor on {self.device}")
 
+    def _check_pixels(self, active_pixels: torch.Tensor):
+        """The plan keeps a sparse set's ray records keyed on the active_pixels pointer and count;
+        a tensor changed in place since the last call (same storage, new torch version) drops
+        them (tvam_plan_set_active)."""
+        self._check_tensor(active_pixels, torch.int32, "active_pixels")
+        key = (active_pixels.data_ptr(), active_pixels.numel())
+        ver = active_pixels._version
+        last = getattr(self, "_pix_key", None)
+        if last is not None and last[0] == key and last[1] != ver:
+            self.set_active(self.desc.active_base, self.desc.active_total)
+        self._pix_key = (key, ver)
+
     def forward(self, active_data: torch.Tensor, active_pixels: Optional[torch.Tensor] = None, spp: int = 1,
                 seed: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:
         self._check_tensor(active_data, torch.float32, "active_data")
         if active_pixels is not None:
-            self._check_tensor(active_pixels, torch.int32, "active_pixels")
+            self._check_pixels(active_pixels)
         if out is None:
             out = torch.empty(self.film_shape, dtype=torch.float32, device=self.device)
         self._check_tensor(out, torch.float32, "dose")
@@ -87,7 +99,7 @@ class Projection:
         """The forward of film slices [z_begin, z_end) into out (the other slices untouched)."""
         self._check_tensor(active_data, torch.float32, "active_data")
         if active_pixels is not None:
-            self._check_tensor(active_pixels, torch.int32, "active_pixels")
+            self._check_pixels(active_pixels)
         self._check_tensor(out, torch.float32, "dose")
         with torch.cuda.device(self.device):
             _abi.check(self.lib.tvam_forward_slices(
@@ -108,7 +120,7 @@ class Projection:
         if grad_dose.numel() != self.film_shape[0] * self.film_shape[1] * self.film_shape[2] * self.film_shape[3]:
             raise ValueError("grad_dose has the wrong number of elements")
         if active_pixels is not None:
-            self._check_tensor(active_pixels, torch.int32, "active_pixels")
+            self._check_pixels(active_pixels)
         if out is None:
             out = torch.empty(n_active, dtype=torch.float32, device=self.device)
         self._check_tensor(out, torch.float32, "grad_active")

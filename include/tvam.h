@@ -181,6 +181,10 @@ void tvam_plan_destroy(tvam_plan* plan);
  *                   (projector.active_pixels); NULL means the dense crop order
  *                   produced by TVAMProjector.__init__ (projector.py:90-98),
  *                   in which case n_active must equal A*crop_y*crop_x.
+ *                   Jittered sampling: the plan keeps the per-ray records of a sparse set
+ *                   keyed on (active_pixels pointer, n_active, seed, spp) and reuses them
+ *                   (slice ranges, the line-search forward of one seed); after changing the
+ *                   array's contents in place, call tvam_plan_set_active, which drops them.
  * spp / seed follow TVAMIntegrator.prepare (common.py:41-68).
  */
 int tvam_forward(tvam_plan* plan, const float* active_data,

@@ -60,6 +60,48 @@ def test_sparse_jittered_vs_oracle(oracle, spp):
     assert rel_l2(g, gref) < RTOL_L2
 
 
+def test_sparse_records_reused_and_dropped():
+    """A sparse jittered set's ray records are kept per (active_pixels, count, seed, spp): a second
+    forward of the same seed with new values, an adjoint of the same seed and slice-range
+    forwards reuse them; an in-place change of active_pixels drops them (the engine calls
+    tvam_plan_set_active).  Every result equals a fresh plan's."""
+    N, A, spp = 24, 12, 2
+    d = _desc(N, A, regular_sampling=False, spp=spp)
+    n = A * N * N
+    keep, pat = _set(n, 8)
+    pat2 = np.random.default_rng(9).uniform(0.01, 0.1, keep.size).astype(np.float32)
+    G = _t(np.random.default_rng(10).uniform(-1, 1, (N, N, N)).astype(np.float32))
+    pix = _t(keep, np.int32)
+    proj = Projection(d, "cuda:0")
+
+    def fresh_forward(p, px, seed):
+        q = Projection(d, "cuda:0")
+        out = q.forward(_t(p), px, spp, seed)
+        q.close()
+        return out
+
+    a = proj.forward(_t(pat), pix, spp, 7)
+    b = proj.forward(_t(pat2), pix, spp, 7)  # reused records, new values
+    assert torch.equal(b, fresh_forward(pat2, pix, 7))
+    g = proj.adjoint(G, keep.size, pix, spp, 7)
+    q = Projection(d, "cuda:0")
+    assert torch.equal(g, q.adjoint(G, keep.size, pix, spp, 7))
+    q.close()
+    zc = proj.fwd_chunk
+    if zc > 0:  # slice ranges of one forward assemble the whole forward
+        out = torch.zeros_like(a)
+        for z0 in range(0, N, zc):
+            proj.forward_slices(_t(pat), pix, spp, 7, z0, min(N, z0 + zc), out)
+        assert torch.equal(out, a)
+    # in-place change of the set: same pointer and count, other pixels
+    keep2 = np.sort(np.random.default_rng(11).choice(n, keep.size, replace=False)).astype(np.int32)
+    pix.copy_(_t(keep2))
+    c = proj.forward(_t(pat), pix, spp, 7)
+    assert torch.equal(c, fresh_forward(pat, pix, 7))
+    assert not torch.equal(c, a)
+    proj.close()
+
+
 @pytest.mark.parametrize("planar_regular", [False, True])
 def test_sparse_set_split_over_angle_shards(planar_regular):
     """Two angle-shard plans over halves of one sparse set draw the unsharded set's samples."""
