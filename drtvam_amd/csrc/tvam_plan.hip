@@ -541,14 +541,16 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
         // CUs, and even the full film (10K at 400^3) ends with a ragged last round
         // (measured 5.30 -> 5.20 ms at split 2 on config 2).  1024-thread workgroups each
         // reload a 71 KB gradient tile, so they aim at half as many: >= ~8K (config 2:
-        // split 3 instead of 5, adjoint 3.98 -> 3.72 ms; split 8: 4.29 ms)
+        // split 3 instead of 5, adjoint 3.98 -> 3.72 ms; split 8: 4.29 ms).  At most 4: the thin
+        // slabs of 4 / 8 z-slab ranks (split 8 by the rule) measured adjoint 1.15 / 0.63 ms at
+        // split 8, 1.01 / 0.57 ms at 4, 1.00 / 0.59 ms at 2 (profiles/r03/s2/slab_split_ab.jsonl)
         // 1024 threads at Z = 8: the 71 KB tile admits 2 workgroups per CU = 8 waves per SIMD
         const int ant = env_int("TVAM_ADJ_NT", p->planar_az >= 8 ? 1024 : 512);
         p->pl.adj_nt = ant == 256 || ant == 1024 ? ant : 512;
         const int64_t want = p->pl.adj_nt >= 1024 ? 8192 : 16384;
         const int64_t nwg = (int64_t)p->tiles.ntx * p->tiles.nty * ((k.nz + p->planar_az - 1) / p->planar_az) *
                             (p->pl.adj_quad ? 4 : 1);  // quadrant lists: one workgroup per quadrant
-        int split = (int)std::min<int64_t>(8, std::max<int64_t>(1, (want + nwg - 1) / std::max<int64_t>(nwg, 1)));
+        int split = (int)std::min<int64_t>(4, std::max<int64_t>(1, (want + nwg - 1) / std::max<int64_t>(nwg, 1)));
         const int es = env_int("TVAM_ADJ_SPLIT", 0);
         if (es >= 1 && es <= 64) split = es;
         p->pl.adj_split = split;
