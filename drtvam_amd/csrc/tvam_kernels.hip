@@ -176,8 +176,8 @@ struct TvamTileRay {
 // Appends this wave's stray rays (s: the lane's ray lies outside its row's main slice zl) to the
 // stray list with one atomic per wave, and adds the per-slice counts with one atomic per distinct
 // slice among them (a wave's lanes are neighbouring pixels of one row, so its strays share one or
-// two slices).  One atomic per stray on the single list counter serialised: config 5's ray setup
-// spent most of its time there.  List order is the atomics' (the tile kernels' sums ignore it).
+// two slices) instead of one per stray on the single list counter (no measurable change on
+// config 5, whose strays are few).  List order is the atomics' (the tile kernels' sums ignore it).
 __device__ __forceinline__ void tvam_append_strays(const TvamTiles& tp, bool s, int zl, uint32_t idx) {
     const unsigned long long m = __ballot(s);
     if (m == 0) return;
