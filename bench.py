@@ -15,12 +15,19 @@ configs[3]: that vial around a scattering resin, 16 jittered rays per pixel;
 
 Multi-GPU: one process per GPU (torch.distributed.run), angles sharded in
 contiguous blocks, dose all-reduced over RCCL twice per iteration, L-BFGS
-dots all-reduced.  Rank 0 prints one JSON line.
+dots all-reduced.  Rank 0 prints one JSON line.  `python bench.py --gpus N`
+without a torch.distributed environment starts those N ranks itself (a child
+torch.distributed.run, before this process touches the GPU) and passes rank
+0's line through.
 """
 import argparse
 import gc
+import glob
+import hashlib
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -114,7 +121,23 @@ def cpu_baseline(config, N, seconds, threads):
 # the launch duration of the counter run itself, against the 2.4 GHz spec peak (LDS 157.3 TB/s,
 # HBM 8 TB/s; MI355X_MICROARCH.md).  Every field can be recomputed from that one file; the bench's
 # own HIP-event time of the projection call that contains the kernel is reported beside it.
-ROOFLINE_DIR = os.path.join(ROOT, "profiles", "r03")
+ROOFLINE_DIR = os.path.join(ROOT, "profiles", "r04")
+
+
+def csrc_digest():
+    """sha256 (first 16 hex digits) of the kernel sources and the ABI header: the build a counter
+    summary was collected on (tools/pmc_bench.sh writes it beside the counters).  A summary whose
+    digest differs from the tree's describes other kernels and is reported as stale."""
+    h = hashlib.sha256()
+    files = sorted(glob.glob(os.path.join(ROOT, "drtvam_amd", "csrc", "*.hip"))
+                   + glob.glob(os.path.join(ROOT, "drtvam_amd", "csrc", "*.h"))
+                   + [os.path.join(ROOT, "drtvam_amd", "csrc", "build.sh"), os.path.join(ROOT, "include", "tvam.h")])
+    for f in files:
+        h.update(os.path.relpath(f, ROOT).encode())
+        h.update(b"\0")
+        with open(f, "rb") as fh:
+            h.update(fh.read())
+    return h.hexdigest()[:16]
 DOMINANT = {2: "forward: voxel-driven planar forward (two per iteration)",
             3: "forward: voxel-driven planar forward over refracted chords (two per iteration)",
             4: "forward brick march of the scattered segments (23 launches per forward, two forwards per iteration)",
@@ -134,6 +157,14 @@ def make_roofline(args, N, A, world, prob, visits, rays, fwd_s, adj_s):
                 "note": "counter summaries are committed for the BASELINE sizes on one GPU", **info}
     summ = json.load(open(path))
     r = summ["roofline"]
+    here = csrc_digest()
+    if summ.get("csrc_sha16") != here:
+        # counters of other kernel sources: no fraction is claimed for the kernels this run timed
+        return {"bound": r["bound"], "achieved": None, "peak": r["peak"], "unit": r["unit"], "frac": None,
+                "traffic": None, "stale": True, "kernel": summ["kernel"], "role": DOMINANT[args.config],
+                "counters": os.path.relpath(path, ROOT), "counters_build": summ["build"],
+                "counters_csrc_sha16": summ.get("csrc_sha16"), "csrc_sha16": here,
+                "stale_frac": r["frac"], **info}
     return {"bound": r["bound"], "achieved": r["achieved"], "peak": r["peak"], "unit": r["unit"], "frac": r["frac"],
             "traffic": r["traffic"], "traffic_over_min": r["traffic_over_min"], "min_bytes": r["min_bytes"],
             "kernel": summ["kernel"], "role": DOMINANT[args.config], "launch_ns_counter_run": summ["avg_ns"],
@@ -141,12 +172,29 @@ def make_roofline(args, N, A, world, prob, visits, rays, fwd_s, adj_s):
             "secondary": {"valu_issue_frac": r["valu_issue_frac"], "hbm_frac": r["hbm_frac"], "lds_frac": r["lds_frac"],
                           "lds_bank_conflict_frac": r["lds_bank_conflict_frac"],
                           "frac_at_measured_clock": r["frac_at_measured_clock"]},
-            "counters": os.path.relpath(path, ROOT), "counters_build": summ["build"], **info}
+            "counters": os.path.relpath(path, ROOT), "counters_build": summ["build"], "stale": False,
+            "counters_csrc_sha16": summ["csrc_sha16"], "csrc_sha16": here, **info}
+
+
+def launch_ranks(n):
+    """`bench.py --gpus N` outside torch.distributed: run this same command as N ranks of a child
+    torch.distributed.run (one process per GPU, 127.0.0.1 rendezvous on a free port) and exit with
+    its status.  Nothing here touches the GPU; rank 0's JSON line reaches stdout unchanged."""
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, MASTER_ADDR="127.0.0.1")
+    log(f"bench.py --gpus {n}: launching {n} ranks: {' '.join(cmd[1:])}")
+    return subprocess.run(cmd, env=env).returncode
 
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="ranks (one per GPU); > 1 without WORLD_SIZE in the environment starts them itself; "
+                         "under torch.distributed.run it must equal WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--prewarm", type=float, default=1.0,
@@ -178,7 +226,13 @@ def main():
                     help="compact the active set to the pixels whose rays cross the target (optimize.py:143-163)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="torch.distributed backend for WORLD_SIZE > 1 (nccl = RCCL over xGMI; gloo: tests)")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="start the ranks, form the process group, all-reduce one value and print the world "
+                         "line without touching a GPU (tests of the launcher; use with --backend gloo)")
     args = ap.parse_args()
+
+    if args.gpus is not None and args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args.gpus))
 
     import torch
     from drtvam_amd import _abi
@@ -187,6 +241,21 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.gpus is not None and args.gpus != world:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}")
+    if args.launch_check:
+        import torch.distributed as dist
+        if world > 1:
+            dist.init_process_group(args.backend)
+        ones = torch.ones(1, dtype=torch.float64)
+        if world > 1:
+            dist.all_reduce(ones)
+        if rank == 0:
+            print(json.dumps({"launch_check": True, "n_gpus": world, "backend": args.backend if world > 1 else None,
+                              "allreduce_ranks": int(ones.item())}), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
     ndev = torch.cuda.device_count()
     gpu = local % max(ndev, 1)  # one GPU per rank; ranks share a GPU only when there are fewer (tests)
     torch.cuda.set_device(gpu)
@@ -355,6 +424,8 @@ def main():
         "value": args.steps / elapsed,
         "unit": "it/s",
         "n_gpus": world,
+        "world_size": dist.get_world_size() if dist else 1,
+        "backend": (args.backend if dist else None),
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,

@@ -121,6 +121,18 @@ BOX_HOLE_SCATTERING = {
     "n_steps": 30,
 }
 
+# tests/files/box_hole_square_different_thresholds.json: the square vial of box_hole_scattering.json
+# (w_int 7 / w_ext 8, ior 1.24, extinction 0.09) with a non-scattering resin and thresholds 0.35 / 0.55
+BOX_HOLE_SQUARE_DIFFERENT_THRESHOLDS = {
+    "vial": {"type": "square", "w_int": 7.0, "w_ext": 8.0, "ior": 1.24,
+             "medium": {"ior": 1.347, "phase": {"type": "rayleigh"}, "extinction": 0.09, "albedo": 0.0}},
+    "projector": BOX_HOLE_SQUARE["projector"],
+    "sensor": BOX_HOLE_SQUARE["sensor"],
+    "target": {"filename": "tests/files/box_hole.ply", "size": 4.0},
+    "loss": {"type": "threshold", "tl": 0.35, "tu": 0.55},
+    "progressive": True,
+    "n_steps": 30,
+}
 
 # tests/files/box_hole_index_matched.json of the reference (data, restated)
 BOX_HOLE_INDEX_MATCHED = {

@@ -60,13 +60,15 @@ struct TvamPlanar {
     const int32_t* slice_off;  // [res_z + 1] CSR: DMD rows whose rays lie in each slice
     const int32_t* slice_rows;
     int32_t ns;
-    int32_t ncmax;             // forward: DMD columns staged per (16x16 tile, angle)
+    int32_t ncmax;             // forward: DMD columns staged per (16 fwd_px x 16 tile, angle)
+    int32_t fwd_px;            // forward: voxel columns per thread along x (1, or 2: a pair sharing its
+                               // candidate columns' staged slabs; tiles 32 x 16)
     float marg_u;              // forward: candidate-column margin (spawn offset of o2 + rounding), in columns
     float u0;                  // forward: crop column of lateral coordinate 0 (0.5 W - 0.5 - crop_off_x)
     int32_t fwd_nc;            // forward: candidate columns per (voxel, angle)
     int32_t fwd_multi;         // forward: some slice collects several DMD rows
     const float4* fwd_ang;     // forward: [ns][2] {s du, -c du, 1/d.x, 1/d.y}, {half width + margin, axis flags}
-    const int32_t* fwd_cb;     // forward: [16x16 tiles][ns] first column of the staged window
+    const int32_t* fwd_cb;     // forward: [16 fwd_px x 16 tiles][ns] first column of the staged window
     int32_t xcd_remap;         // forward: XCD-aware workgroup order
     int32_t fwd_pf;            // forward: staged values per thread and angle (2 or 4)
     int32_t max_rows_chunk;    // adjoint: most DMD rows in one chunk of Z slices

@@ -635,7 +635,8 @@ static int fwd_buffers(tvam_plan* p) {
     // every angle: at 3 resident workgroups per CU, 1250 of them (400^2 film,
     // 50 slices) fill 1.6 rounds of the 768 slots.  Split the angles into parts
     // until >= 4 rounds; the partial doses are summed in fixed order.
-    const int64_t nwg = (int64_t)((k.res[0] + 15) / 16) * ((k.res[1] + 15) / 16) *
+    const int tw = p->pl.fwd_px == 2 ? 32 : 16;
+    const int64_t nwg = (int64_t)((k.res[0] + tw - 1) / tw) * ((k.res[1] + 15) / 16) *
                         ((k.nz + p->planar_fz - 1) / p->planar_fz);
     int parts = (int)std::min<int64_t>(4, std::max<int64_t>(1, (4 * 768 + nwg - 1) / std::max<int64_t>(nwg, 1)));
     const int ep = env_int("TVAM_FWD_PARTS", 0);
@@ -788,6 +789,7 @@ static int refr_fwd_setup(tvam_plan* p, const std::vector<int32_t>& off) {
     }
     TvamPlanar save = p->pl;
     p->pl.fwd_refr = 1;
+    p->pl.fwd_px = 1;
     p->pl.ncmax = ncm;
     p->pl.fwd_nc = ncmax_c;
     p->pl.fwd_ab = 2;
@@ -864,29 +866,38 @@ static bool planar_fwd_setup(tvam_plan* p, const std::vector<float2>& cs, const 
         wmax = std::max(wmax, (double)w);
     }
     const int nc = (int)std::floor(2.0 * wmax + 1e-3) + 1;
-    const int ntx16 = (k.res[0] + 15) / 16, nty16 = (k.res[1] + 15) / 16;
-    std::vector<int32_t> fcb((size_t)ntx16 * nty16 * std::max(ns, 1));
-    int need = 0;
-    for (int t = 0; t < ntx16 * nty16; ++t) {
-        const int bx = t % ntx16, by = t / ntx16;
-        const double xc0 = (double)k.bmin[0] + (bx * 16 + 0.5) * k.h[0], xc1 = xc0 + 15.0 * k.h[0];
-        const double yc0 = (double)k.bmin[1] + (by * 16 + 0.5) * k.h[1], yc1 = yc0 + 15.0 * k.h[1];
-        for (int i = 0; i < ns; ++i) {
-            const double A = fang[2 * (size_t)i].x, B = fang[2 * (size_t)i].y, w = fang[2 * (size_t)i + 1].x;
-            const double uc[4] = {xc0 * A + yc0 * B, xc1 * A + yc0 * B, xc0 * A + yc1 * B, xc1 * A + yc1 * B};
-            const double umin = *std::min_element(uc, uc + 4) + u0, umax = *std::max_element(uc, uc + 4) + u0;
-            const int cb = (int)std::floor(umin - w) - 1;  // 1 column of slack for fp32 rounding in the kernel
-            fcb[(size_t)t * ns + i] = cb;
-            need = std::max(need, (int)std::ceil(umax - w) + 1 + nc - cb);
+    // per (16 px x 16 tile, angle): the first staged column and the window width that holds every
+    // voxel's candidates (px = 2: 32 x 16 tiles of voxel pairs)
+    auto windows = [&](int px, std::vector<int32_t>& fcb) {
+        const int tw = 16 * px;
+        const int ntx = (k.res[0] + tw - 1) / tw, nty = (k.res[1] + 15) / 16;
+        fcb.assign((size_t)ntx * nty * std::max(ns, 1), 0);
+        int need = 0;
+        for (int t = 0; t < ntx * nty; ++t) {
+            const int bx = t % ntx, by = t / ntx;
+            const double xc0 = (double)k.bmin[0] + (bx * tw + 0.5) * k.h[0], xc1 = xc0 + (tw - 1.0) * k.h[0];
+            const double yc0 = (double)k.bmin[1] + (by * 16 + 0.5) * k.h[1], yc1 = yc0 + 15.0 * k.h[1];
+            for (int i = 0; i < ns; ++i) {
+                const double A = fang[2 * (size_t)i].x, B = fang[2 * (size_t)i].y, w = fang[2 * (size_t)i + 1].x;
+                const double uc[4] = {xc0 * A + yc0 * B, xc1 * A + yc0 * B, xc0 * A + yc1 * B, xc1 * A + yc1 * B};
+                const double umin = *std::min_element(uc, uc + 4) + u0, umax = *std::max_element(uc, uc + 4) + u0;
+                const int cb = (int)std::floor(umin - w) - 1;  // 1 column of slack for fp32 rounding in the kernel
+                fcb[(size_t)t * ns + i] = cb;
+                need = std::max(need, (int)std::ceil(umax - w) + 1 + nc - cb);
+            }
         }
-    }
-    // a window wholly outside the crop stages only zero columns: clamp it into the
-    // slice-binned patterns' zero pads (ncmax columns either side)
-    for (auto& cb : fcb) cb = std::min(std::max(cb, -need), (int)d.crop_x);
+        // a window wholly outside the crop stages only zero columns: clamp it into the
+        // slice-binned patterns' zero pads (ncmax columns either side)
+        for (auto& cb : fcb) cb = std::min(std::max(cb, -need), (int)d.crop_x);
+        return need;
+    };
+    std::vector<int32_t> fcb;
+    const int need = windows(1, fcb);
     p->pl.marg_u = (float)marg_u;
     p->pl.u0 = u0;
     p->pl.fwd_nc = nc;
     p->pl.ncmax = need;
+    p->pl.fwd_px = 1;
     {
         bool multi = false;
         for (int z = 0; z < k.nz; ++z) multi |= off[z + 1] - off[z] > 1;
@@ -897,6 +908,24 @@ static bool planar_fwd_setup(tvam_plan* p, const std::vector<float2>& cs, const 
         p->pl.fwd_ab = (ab >= 1 && ab <= 4) ? ab : 2;
     }
     if (!choose_fwd_z(p)) return false;
+    // voxel pairs (TVAM_FWD_PX, default 2) where the depth has a pair variant (Z <= 32, binned
+    // staging of <= 2 float4 per thread, 2 angles per barrier) and the pair's union of candidates
+    // fits the kernel's NC + 2 (lateral centres <= 1 column apart)
+    if (env_int("TVAM_FWD_PX", 2) == 2 && p->planar_fz <= 32 && env_int("TVAM_FWD_BIN", 1) && p->pl.fwd_ab == 2) {
+        double dmax = 0.0;
+        for (int i = 0; i < ns; ++i) dmax = std::max(dmax, std::fabs((double)fang[2 * (size_t)i].x) * k.h[0]);
+        std::vector<int32_t> fcb2;
+        const int need2 = windows(2, fcb2);
+        const int need1 = p->pl.ncmax;
+        p->pl.ncmax = need2;
+        if (dmax <= 1.0 + 1e-6 && tvam_planar_fwd_fits(p->pl, p->planar_fz) &&
+            (need2 * (p->planar_fz / 4) + 255) / 256 <= 2) {  // fwd_buffers' binned staging (<= 2 float4 per thread)
+            p->pl.fwd_px = 2;
+            fcb = std::move(fcb2);
+        } else {
+            p->pl.ncmax = need1;
+        }
+    }
     p->pl.fwd_pf = (p->pl.ncmax * p->planar_fz + 255) / 256 <= 2 ? 2 : 4;
     p->fwd_ang_h = std::move(fang);
     p->fwd_cb_h = std::move(fcb);
@@ -1515,6 +1544,10 @@ static int ensure_dense(tvam_plan* p) {
 static int ensure_rays(tvam_plan* p, const TvamConsts& k, TvamTiles& t, const int32_t* idxmap, hipStream_t stream,
                        const uint32_t* active_pixels = nullptr, uint64_t n_active = 0) {
     const uint64_t n = (uint64_t)(k.a1 - k.a0) * k.crop_y * k.crop_x * t.spp;
+    if (n > 0xFFFFFFFFull) {  // stray lists hold 32-bit record indices: every slice walks its full row list
+        t.slice_moff = nullptr;
+        t.row_main = nullptr;
+    }
     hipError_t e;
     auto bind = [&](tvam_plan::RaySlot& r) {
         t.ray_f = r.f;
@@ -1737,7 +1770,9 @@ static int forward_impl(tvam_plan* p, const float* active_data, const uint32_t* 
         t.seed = seed;
         e = hipErrorNotSupported;
         p->bins.acc_float = env_int("TVAM_BIN_FLOAT", 0);
-        if (!(p->desc.flags & TVAM_FLAG_SCATTER_ATOMIC))
+        if (p->desc.flags & TVAM_FLAG_SCATTER_ATOMIC)
+            for (auto& v : p->bins.st) v = 0;  // nothing binned
+        else
             e = tvam_scatter_binned(TVAM_MODE_FWD, kc, t, pat, idxmap, nullptr, dose, p->bins, stream);
         if (e == hipErrorNotSupported)
             e = tvam_launch_scatter_paths(TVAM_MODE_FWD, kc, t, pat, idxmap, nullptr, dose, nullptr, stream);
@@ -1806,7 +1841,9 @@ extern "C" int tvam_adjoint(tvam_plan* p, const float* grad_dose, const uint32_t
         t.spp = spp;
         t.seed = seed;
         e = hipErrorNotSupported;
-        if (!(p->desc.flags & TVAM_FLAG_SCATTER_ATOMIC))
+        if (p->desc.flags & TVAM_FLAG_SCATTER_ATOMIC)
+            for (auto& v : p->bins.st) v = 0;  // nothing binned
+        else
             e = tvam_scatter_binned(TVAM_MODE_ADJ, k, t, nullptr, idxmap, grad_dose, grad_active, p->bins, stream);
         if (e == hipErrorNotSupported)
             e = tvam_launch_scatter_paths(TVAM_MODE_ADJ, k, t, nullptr, idxmap, grad_dose, grad_active, nullptr, stream);

@@ -136,10 +136,18 @@ __host__ __device__ constexpr int tvam_fwd_zs(int Z) { return ((Z + 4) / 4) % 2 
 // per-angle constants are the (tile, angle) model of the chord index u (tvam_refr_model_kernel),
 // and each voxel visits a per-(tile, angle) number of candidates (the same for the whole
 // workgroup) from ceil(u - w).
-template <int Z, int NC, bool MULTI, int PF, int AB, bool BIN = false, bool REFR = false>
+//
+// PX = 2: a thread owns two neighbouring voxel columns (ix, ix + 1) of a 32 x 16 tile.  Their
+// candidate columns overlap (their lateral centres are |s du| h <= 1 column apart), so each staged
+// slab a candidate needs is read from LDS once for both voxels: per angle a wave reads the union
+// of its pairs' candidates (NC + 1, at most NC + 2) for 128 voxel columns instead of NC for 64.
+// Each voxel's sum runs over the same candidates in the same order as PX = 1 (the union's extra
+// columns miss the voxel: weight exactly 0), so the dose is bit-identical.
+template <int Z, int NC, bool MULTI, int PF, int AB, bool BIN = false, bool REFR = false, int PX = 1>
 __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, TvamPlanar pl,
                                                                   const float* __restrict__ pat,
                                                                   float* __restrict__ dose) {
+    static_assert(PX == 1 || (PX == 2 && !REFR), "voxel pairs: straight rays only");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int ncm = pl.ncmax;
     constexpr int RW = REFR ? 2 : 1;  // records (float4) per staged column
@@ -156,7 +164,7 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
     int* s_cb = reinterpret_cast<int*>(s_ang + 2 * (TVAM_ACH + 4)); // [TVAM_ACH + 4]
     int* s_row = s_cb + (TVAM_ACH + 4);                            // [Z]: the slice's row, -1 none, -2 several
 
-    const int ntx = (k.res[0] + 15) >> 4, nty = (k.res[1] + 15) >> 4;
+    const int ntx = (k.res[0] + 16 * PX - 1) / (16 * PX), nty = (k.res[1] + 15) >> 4;
     // slice chunks of this launch: [fwd_zc0, fwd_zc0 + fwd_nzc) (tvam_forward_slices), else all
     const int nzc = pl.fwd_nzc > 0 ? pl.fwd_nzc : (k.nz + Z - 1) / Z;
     const int ntiles = ntx * nty, nwg1 = ntiles * nzc;
@@ -177,13 +185,15 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
     const int ab = (int)(((int64_t)pl.ns * part) / parts), ae = (int)(((int64_t)pl.ns * (part + 1)) / parts);
     const int tile = L % ntiles;
     const int bx = tile % ntx, by = tile / ntx;
-    const int ix = bx * 16 + (threadIdx.x & 15), iy = by * 16 + (threadIdx.x >> 4);
+    const int ix = bx * 16 * PX + PX * (threadIdx.x & 15), iy = by * 16 + (threadIdx.x >> 4);
     const int z0 = ((pl.fwd_nzc > 0 ? pl.fwd_zc0 : 0) + L / ntiles) * Z;
     const float hx = k.h[0], hy = k.h[1];
     // voxel edges exactly as the DDA places them (bmin + i * h, sensor.py:357)
     const float X0 = k.bmin[0] + (float)ix * hx, X1 = k.bmin[0] + (float)(ix + 1) * hx;
     const float Y0 = k.bmin[1] + (float)iy * hy, Y1 = k.bmin[1] + (float)(iy + 1) * hy;
     const float Xc = k.bmin[0] + ((float)ix + 0.5f) * hx, Yc = k.bmin[1] + ((float)iy + 0.5f) * hy;
+    // the pair's second voxel (PX = 2): x edges X1, X2, centre Xc1
+    const float X2 = k.bmin[0] + (float)(ix + 2) * hx, Xc1 = k.bmin[0] + ((float)(ix + 1) + 0.5f) * hx;
     const float u0 = pl.u0;
     const int32_t* cbt = pl.fwd_cb + (size_t)tile * pl.ns;  // first window column per angle
 
@@ -309,9 +319,11 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
         if ((int)threadIdx.x < ncm * RW) reinterpret_cast<pl_f4*>(s_r)[buf * ncm * RW + threadIdx.x] = rv;
     };
 
-    float acc[Z];
+    float acc[Z], acc1[PX == 2 ? Z : 1];
 #pragma unroll
     for (int z = 0; z < Z; ++z) acc[z] = 0.0f;
+#pragma unroll
+    for (int z = 0; z < (PX == 2 ? Z : 1); ++z) acc1[z] = 0.0f;
 
     auto compute_refr = [&](int al, int buf) {
         const int cb = s_cb[al - tbase];
@@ -361,9 +373,67 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
         for (int c = 2; c < nc; ++c) accumulate(jj0 + c, weight(jj0 + c));
     };
 
-    auto compute = [&](int al, int buf) {
+    auto compute_pair = [&](int al, int buf) __attribute__((always_inline)) {
+        const int cb = s_cb[al - tbase];
+        const float* sp = s_p + buf * bstride;
+        const float4* sr = s_r + buf * ncm;
+        const float4 g0 = s_ang[2 * (al - tbase)], g1 = s_ang[2 * (al - tbase) + 1];
+        const int fl = __float_as_int(g1.y);
+        // each voxel's candidates exactly as PX = 1 forms them, then their union [lo, hi]
+        const float ua = fmaf(Xc, g0.x, fmaf(Yc, g0.y, u0)), ub = fmaf(Xc1, g0.x, fmaf(Yc, g0.y, u0));
+        const int ja = (int)ceilf(ua - g1.x) - cb, jb = (int)ceilf(ub - g1.x) - cb;
+        const int lo = max(min(ja, jb), 0), hi = min(max(ja, jb) + NC - 1, ncm - 1);
+        const float xa = X0 * g0.z, xb = X1 * g0.z, xc = X2 * g0.z, ya = Y0 * g0.w, yb = Y1 * g0.w;
+        const float xn0 = fminf(xa, xb), xf0 = fmaxf(xa, xb), xn1 = fminf(xb, xc), xf1 = fmaxf(xb, xc);
+        const float yn = fminf(ya, yb), yf = fmaxf(ya, yb);
+        auto visit = [&](int j) __attribute__((always_inline)) {
+            const int jc = min(lo + j, ncm - 1);
+            float4 q = sr[jc];
+            asm volatile("" : "+v"(q.w));  // keep the 16-byte LDS read (ds_read_b128, not b96)
+            float tnx0 = xn0 + q.x, tfx0 = xf0 + q.x, tnx1 = xn1 + q.x, tfx1 = xf1 + q.x;
+            float tny = yn + q.y, tfy = yf + q.y;
+            if (!(fl & 1)) {  // |d.x| <= 1e-8: the DDA never steps x (q.x = its voxel index)
+                tnx0 = (float)ix == q.x ? -TVAM_INF : TVAM_INF;
+                tnx1 = (float)(ix + 1) == q.x ? -TVAM_INF : TVAM_INF;
+                tfx0 = tfx1 = TVAM_INF;
+            }
+            if (!(fl & 2)) {
+                tny = (float)iy == q.y ? -TVAM_INF : TVAM_INF;
+                tfy = TVAM_INF;
+            }
+            const float tin0 = fmaxf(fmaxf(tnx0, tny), 0.0f), tout0 = fminf(fminf(tfx0, tfy), q.z);
+            const float tin1 = fmaxf(fmaxf(tnx1, tny), 0.0f), tout1 = fminf(fminf(tfx1, tfy), q.z);
+            const float e0 = pl_exp2(k.nsig2 * tin0) - pl_exp2(k.nsig2 * tout0);
+            const float e1 = pl_exp2(k.nsig2 * tin1) - pl_exp2(k.nsig2 * tout1);
+            const bool in = lo + j <= hi;
+            const float w0 = (in && tout0 > tin0) ? e0 : 0.0f, w1 = (in && tout1 > tin1) ? e1 : 0.0f;
+            if (w0 != 0.0f || w1 != 0.0f) {
+#pragma unroll
+                for (int z4 = 0; z4 < Z / 4; ++z4) {
+                    const float4 p4 = reinterpret_cast<const float4*>(sp + jc * ZS)[z4];
+                    acc[4 * z4 + 0] = fmaf(w0, p4.x, acc[4 * z4 + 0]);
+                    acc[4 * z4 + 1] = fmaf(w0, p4.y, acc[4 * z4 + 1]);
+                    acc[4 * z4 + 2] = fmaf(w0, p4.z, acc[4 * z4 + 2]);
+                    acc[4 * z4 + 3] = fmaf(w0, p4.w, acc[4 * z4 + 3]);
+                    acc1[4 * z4 + 0] = fmaf(w1, p4.x, acc1[4 * z4 + 0]);
+                    acc1[4 * z4 + 1] = fmaf(w1, p4.y, acc1[4 * z4 + 1]);
+                    acc1[4 * z4 + 2] = fmaf(w1, p4.z, acc1[4 * z4 + 2]);
+                    acc1[4 * z4 + 3] = fmaf(w1, p4.w, acc1[4 * z4 + 3]);
+                }
+            }
+        };
+#pragma unroll
+        for (int j = 0; j <= NC; ++j) visit(j);
+        if (__ballot(hi - lo > NC)) visit(NC + 1);  // a union of NC + 2 (|u_b - u_a| rounded past 1)
+    };
+
+    auto compute = [&](int al, int buf) __attribute__((always_inline)) {
         if constexpr (REFR) {
             compute_refr(al, buf);
+            return;
+        }
+        if constexpr (PX == 2) {
+            compute_pair(al, buf);
             return;
         }
         const int cb = s_cb[al - tbase];
@@ -497,6 +567,11 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
 #pragma unroll
         for (int z = 0; z < Z; ++z)
             if (z0 + z < k.nz) out[(size_t)(z0 + z) * plane + (size_t)iy * k.res[0] + ix] = acc[z] * scale;
+        if (PX == 2 && ix + 1 < k.res[0]) {
+#pragma unroll
+            for (int z = 0; z < (PX == 2 ? Z : 0); ++z)
+                if (z0 + z < k.nz) out[(size_t)(z0 + z) * plane + (size_t)iy * k.res[0] + ix + 1] = acc1[z] * scale;
+        }
     }
 }
 
@@ -714,6 +789,16 @@ static void launch_fwd(dim3 grid, size_t lds, hipStream_t stream, const TvamCons
                                pat, dose);
         return;
     }
+    if (Z <= 32 && pl.fwd_px == 2) {  // voxel pairs: binned staging, 2 angles per barrier
+        if (!pl.fwd_bin || pl.fwd_ab != 2) return;  // the plan only selects the instantiated variants
+        if (pl.fwd_pf == 1)
+            hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 1, 2, true, false, (Z <= 32 ? 2 : 1)>), grid,
+                               dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
+        else
+            hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 2, 2, true, false, (Z <= 32 ? 2 : 1)>), grid,
+                               dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
+        return;
+    }
     if (pl.fwd_bin && pl.fwd_pf == 1 && pl.fwd_ab == 1)
         hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 1, 1, true>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
     else if (pl.fwd_bin && pl.fwd_pf == 1)
@@ -756,7 +841,9 @@ static hipError_t tvam_launch_fwd_planar_z(dim3 grid, size_t lds, hipStream_t st
 
 hipError_t tvam_launch_fwd_planar(const TvamConsts& k, const TvamPlanar& pl, int Z, const float* pat, float* dose,
                                   hipStream_t stream) {
-    const int ntx = (k.res[0] + 15) / 16, nty = (k.res[1] + 15) / 16;
+    const int tw = pl.fwd_px == 2 ? 32 : 16;
+    if (pl.fwd_px == 2 && (!pl.fwd_bin || pl.fwd_ab != 2 || Z > 32 || pl.fwd_refr)) return hipErrorInvalidValue;
+    const int ntx = (k.res[0] + tw - 1) / tw, nty = (k.res[1] + 15) / 16;
     const int parts = pl.fwd_parts > 1 ? pl.fwd_parts : 1;
     if (parts > 1 && !pl.fwd_part) return hipErrorInvalidValue;
     const int nzc = pl.fwd_nzc > 0 ? pl.fwd_nzc : (k.nz + Z - 1) / Z;

@@ -1576,6 +1576,7 @@ void tvam_bin_scratch_free(TvamBinScratch& s) {
 hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t, const float* pat,
                                const int32_t* idxmap, const float* gin, float* out, TvamBinScratch& s,
                                hipStream_t stream) {
+    for (int i = 0; i < 5; ++i) s.st[i] = 0;  // stats of this call, also when it bins nothing
     const int nsurf = k.vial_type == 0 ? 1 : 2;
     const int slots = k.max_depth - nsurf - 1;  // later medium segments per path
     if (slots <= 0) return hipSuccess;
@@ -1664,7 +1665,6 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
             hipLaunchKernelGGL((tvam_bin_march_kernel<0, 512>), grid, blk, 0, stream, k, sb, vals, bstart, out,
                                nullptr, 0u, nullptr, nullptr);
     };
-    for (int i = 0; i < 5; ++i) s.st[i] = 0;
     s.st[4] = chunk;
     for (int64_t p0 = 0; p0 < npaths; p0 += chunk) {
         const int64_t p1 = std::min(npaths, p0 + chunk);

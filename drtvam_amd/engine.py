@@ -69,16 +69,17 @@ class Projection:
             raise ValueError(f"{name} must be a contiguous {dtype} tensor on {self.device}")
 
     def _check_pixels(self, active_pixels: torch.Tensor):
-        """The plan keeps a sparse set's ray records keyed on the active_pixels pointer and count;
-        a tensor changed in place since the last call (same storage, new torch version) drops
-        them (tvam_plan_set_active)."""
+        """The plan keeps a sparse set's ray records keyed on the active_pixels pointer and count.
+        A pointer alone does not name a set: a freed tensor's address can be handed to a new one.
+        So the projection holds the last tensor it was given (its storage cannot be reused while
+        held) and drops the records (tvam_plan_set_active) whenever a call brings another tensor
+        object, or the same tensor changed in place (new torch version)."""
         self._check_tensor(active_pixels, torch.int32, "active_pixels")
-        key = (active_pixels.data_ptr(), active_pixels.numel())
         ver = active_pixels._version
-        last = getattr(self, "_pix_key", None)
-        if last is not None and last[0] == key and last[1] != ver:
+        last = getattr(self, "_pix_last", None)
+        if last is not None and (last[0] is not active_pixels or last[1] != ver):
             self.set_active(self.desc.active_base, self.desc.active_total)
-        self._pix_key = (key, ver)
+        self._pix_last = (active_pixels, ver)
 
     def forward(self, active_data: torch.Tensor, active_pixels: Optional[torch.Tensor] = None, spp: int = 1,
                 seed: int = 0, out: Optional[torch.Tensor] = None) -> torch.Tensor:

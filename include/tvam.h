@@ -184,7 +184,9 @@ void tvam_plan_destroy(tvam_plan* plan);
  *                   Jittered sampling: the plan keeps the per-ray records of a sparse set
  *                   keyed on (active_pixels pointer, n_active, seed, spp) and reuses them
  *                   (slice ranges, the line-search forward of one seed); after changing the
- *                   array's contents in place, call tvam_plan_set_active, which drops them.
+ *                   array's contents in place, or before passing a different array (a new
+ *                   allocation can land on a freed one's address), call
+ *                   tvam_plan_set_active, which drops them.
  * spp / seed follow TVAMIntegrator.prepare (common.py:41-68).
  */
 int tvam_forward(tvam_plan* plan, const float* active_data,

@@ -102,6 +102,33 @@ def test_sparse_records_reused_and_dropped():
     proj.close()
 
 
+def test_sparse_records_dropped_for_a_new_set_at_a_freed_address():
+    """set A is used, then set B, then A is freed and set C (same count, other pixels)
+    is allocated at A's old address.  A call on C with A's seed must not reuse A's ray records."""
+    N, A, spp = 24, 12, 2
+    d = _desc(N, A, regular_sampling=False, spp=spp)
+    n = A * N * N
+    keep_a, pat = _set(n, 8)
+    keep_b = np.sort(np.random.default_rng(12).choice(n, keep_a.size, replace=False)).astype(np.int32)
+    keep_c = np.sort(np.random.default_rng(13).choice(n, keep_a.size, replace=False)).astype(np.int32)
+    proj = Projection(d, "cuda:0")
+    pix_a = _t(keep_a, np.int32)
+    addr = pix_a.data_ptr()
+    proj.forward(_t(pat), pix_a, spp, 7)
+    pix_b = _t(keep_b)
+    proj.forward(_t(pat), pix_b, spp, 7)
+    del pix_a
+    torch.cuda.synchronize()
+    pix_c = torch.empty(keep_c.size, dtype=torch.int32, device="cuda:0")  # the caching allocator's freed block
+    pix_c.copy_(_t(keep_c))
+    assert pix_c.data_ptr() == addr, "the allocator did not reuse the freed block (test premise)"
+    got = proj.forward(_t(pat), pix_c, spp, 7)
+    q = Projection(d, "cuda:0")
+    assert torch.equal(got, q.forward(_t(pat), pix_c, spp, 7))
+    q.close()
+    proj.close()
+
+
 @pytest.mark.parametrize("planar_regular", [False, True])
 def test_sparse_set_split_over_angle_shards(planar_regular):
     """Two angle-shard plans over halves of one sparse set draw the unsharded set's samples."""

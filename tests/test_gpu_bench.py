@@ -41,3 +41,12 @@ def test_two_rank_line(shard, port):
     r = run(["--res", "64", "--steps", "3", "--warmup", "1", "--shard", shard], nproc=2, port=port)
     assert r["n_gpus"] == 2 and r["value"] > 0 and r["cpu_baseline"] is None
     assert ("z-slab" if shard == "slab" else "angle-shard") in r["config"]["parallelism"]
+
+
+def test_gpus_flag_launches_ranks():
+    """`bench.py --gpus 2` with no torch.distributed environment starts both ranks itself (both on
+    this box's one GPU over gloo) and prints rank 0's line with the world it measured."""
+    r = run(["--gpus", "2", "--backend", "gloo", "--res", "64", "--steps", "2", "--warmup", "1",
+             "--shard", "angle"])
+    assert r["n_gpus"] == 2 and r["world_size"] == 2 and r["backend"] == "gloo" and r["value"] > 0
+    assert "angle-shard x2" in r["config"]["parallelism"]

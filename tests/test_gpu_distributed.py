@@ -4,7 +4,10 @@ path) and the fused L-BFGS (one all-reduce of the dot vector per step) must
 reproduce the single-rank run.  Each rank owns a contiguous angle block and
 renders a partial dose that is all-reduced; under jittered
 sampling (per-ray tile kernels) the forward runs in 4 slice ranges whose async
-all-reduces overlap the next range's forward."""
+all-reduces overlap the next range's forward.  A scattering resin (config 4's path loop,
+volume.py:179-272) runs its later segments through the brick bins in several chunks per rank
+(TVAM_BIN_CHUNK_SLOTS), each rank with its own bin cache, sampler streams by active-set position
+(active_base / active_total) and the derived adjoint seed (optimize.py:294-315)."""
 import os
 import socket
 
@@ -19,9 +22,27 @@ pytestmark = pytest.mark.gpu
 CFG = dict(N=24, angles=12)
 
 
+SCATTER_CHUNK_SLOTS = 12000  # ~7 chunks for the whole set, ~4 per rank of two
+
+
 def _run(rank, world, steps, shard):
-    from drtvam_amd.configs import benchy_index_matched
+    from drtvam_amd.configs import benchy_index_matched, cylindrical_scattering
     from drtvam_amd.optimize import TvamProblem
+
+    if shard == "angle_scatter":
+        cfg = cylindrical_scattering(**CFG, spp=4)
+        cfg["shard"] = "angle"
+        prob = TvamProblem(cfg, device=torch.device("cuda", 0), rank=rank, world_size=world)
+        assert prob.shard == "angle" and prob.proj.desc.albedo == 0.5
+        g = torch.Generator().manual_seed(0)
+        prob.x0 = prob.local_from_global(torch.rand(prob.n_global, generator=g) * 0.1)
+        for i in range(steps):
+            prob.iteration(i)
+        st = prob.proj.bin_stats()  # the last (line-search) forward's chunks: >= 2, served from this rank's cache
+        assert st["chunks"] >= 2 and st["cached"] == st["chunks"], st
+        x = prob.gather_patterns(prob.patterns_local().float())
+        dose = prob.forward(prob.patterns_local().float().contiguous(), 5)  # all-reduced forward of a new seed
+        return np.asarray(prob.loss_hist), x.cpu().numpy(), dose.cpu().numpy()
 
     jitter = shard == "angle_jitter"  # the per-ray tile path: the dose all-reduce in 4 overlapped slice ranges
     cfg = benchy_index_matched(**CFG, regular_sampling=not jitter, spp=2 if jitter else 1)
@@ -42,6 +63,8 @@ def _run(rank, world, steps, shard):
 
 
 def _worker(rank, world, port, steps, shard, q):
+    if shard == "angle_scatter":
+        os.environ["TVAM_BIN_CHUNK_SLOTS"] = str(SCATTER_CHUNK_SLOTS)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -63,7 +86,7 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("shard", ["slab", "angle", "angle_jitter"])
+@pytest.mark.parametrize("shard", ["slab", "angle", "angle_jitter", "angle_scatter"])
 def test_two_rank_gpu_loop_matches_single_rank(shard):
     steps = 4
     ctx = mp.get_context("spawn")

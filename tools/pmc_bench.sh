@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # Counters of one BASELINE config's bench iteration for the committed roofline summaries
-# (tools/roofline_summary.py -> profiles/r03/roofline_config<K>.json, read by bench.py):
+# (tools/roofline_summary.py -> profiles/r04/roofline_config<K>.json, read by bench.py):
 # one rocprofv3 --pmc pass per counter set (never combined with tracing, each within the
 # per-block limits), then a --kernel-trace --stats pass of the same command.
 # usage (GPU box, repo root): tools/pmc_bench.sh OUT CONFIG [N]
@@ -10,6 +10,7 @@ export TMPDIR=/tmp
 mkdir -p "$out"
 cmd=(python3 bench.py --config "$c" --n "$n" --steps 1 --warmup 0 --prewarm 0 --cpu-baseline off)
 echo "${cmd[*]}" > "$out/command.txt"
+python3 -c "import bench; print(bench.csrc_digest())" > "$out/csrc_sha16.txt"
 sets=(
   "SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_LDS SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_ACTIVE_INST_VALU SQ_THREAD_CYCLES_VALU"
   "SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE"

@@ -65,6 +65,8 @@ def main():
         "config": int(config),
         "command": open(os.path.join(src, "command.txt")).read().strip(),
         "build": subprocess.run(["git", "rev-parse", "--short=12", "HEAD"], capture_output=True, text=True).stdout.strip(),
+        # digest of the kernel sources the counters ran on (bench.csrc_digest, written on the GPU box)
+        "csrc_sha16": open(os.path.join(src, "csrc_sha16.txt")).read().strip(),
         "kernel": kname,
         "launches_per_pass": len(counters.get("SQ_WAVES", counters.get("FETCH_SIZE", []))),
         "avg_ns": avg_ns,
