@@ -160,6 +160,10 @@ struct TvamSegBuf {
     float4* r;                    // [slots][3] segment records (48 B, one cache-line span per gather)
     uint32_t* m;
     uint32_t* wmax;               // forward: max |record weight| of the chunk (float bits, atomicMax)
+    // counting-sort bins (tvam_scatter_binned without TVAM_BIN_SORT): the record writer's per
+    // (brick, workgroup) entry counts, [nbricks][gridDim.x]; nullptr: the radix-sort path
+    uint32_t* hist;
+    int32_t nbricks;
 };
 
 // One chunk of forward bins kept in HBM for the next forward of the same (seed, spp): an
@@ -170,12 +174,13 @@ struct TvamSegBuf {
 struct TvamBinChunk {
     float4* r = nullptr;          // [3 * cap_slots] records
     int64_t cap_slots = 0;
-    uint32_t* vals = nullptr;     // [cap_vals] sorted segment slots
+    uint32_t* vals = nullptr;     // [cap_vals] sorted segment slots, or counting-sort entries (ws)
     int64_t cap_vals = 0;
     uint32_t* bstart = nullptr;   // [nbricks + 1]
     int64_t cap_bricks = 0;
     uint32_t total = 0;
     bool valid = false;
+    bool ws = false;              // vals are tvam_bin_fill2_kernel entries (slot | class << 28)
 };
 
 // Scratch of the binned forward (owned by the plan, grown on demand).
@@ -185,13 +190,16 @@ struct TvamBinScratch {
     uint32_t* off = nullptr;      // [cap_slots + 1] exclusive scan of m
     uint32_t* keys[2] = {nullptr, nullptr};
     uint32_t* vals[2] = {nullptr, nullptr};
-    int64_t cap_entries = 0;
+    int64_t cap_entries = 0, cap_entries2 = 0;
     uint32_t* bstart = nullptr;   // [nbricks + 1]
     int32_t cap_bricks = 0;
     void* temp = nullptr;
     size_t temp_bytes = 0;
     int acc_float = 0;            // 1: float LDS adds instead of int64 fixed point (TVAM_BIN_FLOAT)
     float* part = nullptr;        // [cap_entries] adjoint partial of each entry
+    uint32_t* hist = nullptr;     // [nbricks * G + 1] writer counts per (brick, workgroup), then their scan
+    uint32_t* hbase = nullptr;
+    int64_t cap_hist = 0;
     // forward bin cache (TvamBinChunk), keyed on the call's constants, seed, spp and chunking
     std::vector<TvamBinChunk> fc;
     bool fc_key = false;

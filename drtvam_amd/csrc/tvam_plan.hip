@@ -916,13 +916,15 @@ static bool planar_fwd_setup(tvam_plan* p, const std::vector<float2>& cs, const 
         for (int i = 0; i < ns; ++i) dmax = std::max(dmax, std::fabs((double)fang[2 * (size_t)i].x) * k.h[0]);
         std::vector<int32_t> fcb2;
         const int need2 = windows(2, fcb2);
+        // the pair variant stages binned slabs only: <= 2 float4 per thread (fwd_buffers), one record
+        // loader per window column, 1..4 candidates per voxel
         const int need1 = p->pl.ncmax;
+        p->pl.fwd_px = 2;
         p->pl.ncmax = need2;
-        if (dmax <= 1.0 + 1e-6 && tvam_planar_fwd_fits(p->pl, p->planar_fz) &&
-            (need2 * (p->planar_fz / 4) + 255) / 256 <= 2) {  // fwd_buffers' binned staging (<= 2 float4 per thread)
-            p->pl.fwd_px = 2;
+        if (dmax <= 1.0 + 1e-6 && tvam_planar_fwd_fits(p->pl, p->planar_fz)) {
             fcb = std::move(fcb2);
         } else {
+            p->pl.fwd_px = 1;
             p->pl.ncmax = need1;
         }
     }

@@ -641,7 +641,7 @@ bool tvam_planar_fwd_fits(const TvamPlanar& pl, int Z) {
     if (pl.fwd_refr)  // two record loaders per window column; the binned staging only
         return 2 * pl.ncmax <= TVAM_PB && pl.ncmax * (Z / 4) <= 2 * TVAM_PB && pl.fwd_nc >= 1 &&
                pl.fwd_nc <= pl.ncmax && tvam_planar_fwd_lds(pl, Z) <= 64 * 1024;
-    if (Z > 32)  // deep slabs: the binned staging only (at most 2 float4 per thread and angle)
+    if (Z > 32 || pl.fwd_px == 2)  // deep slabs, voxel pairs: the binned staging only (<= 2 float4 per thread and angle)
         return pl.ncmax <= TVAM_PB && pl.ncmax * (Z / 4) <= 2 * TVAM_PB && pl.fwd_nc >= 1 && pl.fwd_nc <= 4 &&
                pl.fwd_nc <= pl.ncmax;
     return pl.ncmax <= TVAM_PB && pl.ncmax * Z <= TVAM_PF * TVAM_PB && pl.fwd_nc >= 1 && pl.fwd_nc <= 4 &&

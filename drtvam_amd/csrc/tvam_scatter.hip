@@ -397,6 +397,15 @@ __global__ __launch_bounds__(256) void tvam_scatter_kernel(TvamConsts k, TvamTil
     const int nsurf = k.vial_type == 0 ? 1 : 2;  // glass vials: two surfaces before the medium
     uint64_t nvis = 0;
     float wmax = 0.0f;  // EMIT (forward): largest |record weight| of this thread's paths
+    // EMIT with sb.hist: this workgroup's entries per brick (LDS), written to hist[brick][block]:
+    // the counting sort of tvam_scatter_binned places the workgroup's entries of a brick after
+    // those of the lower-numbered workgroups (tvam_bin_fill2_kernel walks the same paths)
+    extern __shared__ uint32_t s_hist[];
+    const bool hist = MODE == TVAM_MODE_EMIT && sb.hist != nullptr;
+    if (hist) {
+        for (int b = threadIdx.x; b < sb.nbricks; b += blockDim.x) s_hist[b] = 0u;
+        __syncthreads();
+    }
     for (int64_t i = i0 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         if (MODE == TVAM_MODE_EMIT && !sb.adj)  // slots without a segment: attenuation 0 (the cache's rescale)
             for (int q = 0; q < sb.slots; ++q) reinterpret_cast<float*>(&sb.r[TVAM_REC_F4 * ((i - sb.p0) * sb.slots + q) + 2])[2] = 0.0f;
@@ -476,7 +485,9 @@ __global__ __launch_bounds__(256) void tvam_scatter_kernel(TvamConsts k, TvamTil
                                              q.ts[2] * (float)q.step[2]);
                     // .z: the attenuation alone, for the cached forward's rescale (tvam_bin_reweight_kernel)
                     sb.r[TVAM_REC_F4 * slot + 2] = make_float4(__int_as_float(q.sv[0] | (q.sv[1] << 11) | (q.sv[2] << 22)), em * att, att, 0.0f);
-                    sb.m[slot] = (uint32_t)sc_walk_bricks(k, q, [](int, float, float) {});
+                    sb.m[slot] = (uint32_t)sc_walk_bricks(k, q, [&](int bid, float, float) {
+                        if (hist) atomicAdd(&s_hist[bid], 1u);
+                    });
                     wmax = fmaxf(wmax, fabsf(em * att));
                 }
             } else if (seg > 0) {
@@ -510,6 +521,11 @@ __global__ __launch_bounds__(256) void tvam_scatter_kernel(TvamConsts k, TvamTil
         if ((threadIdx.x & 63) == 0 && nvis) atomicAdd(counter, (unsigned long long)nvis);
     }
     if (MODE == TVAM_MODE_EMIT && !sb.adj) sc_block_max(wmax, sb.wmax);
+    if (hist) {
+        __syncthreads();
+        for (int b = threadIdx.x; b < sb.nbricks; b += blockDim.x)
+            sb.hist[(size_t)b * gridDim.x + blockIdx.x] = s_hist[b];
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -1344,6 +1360,128 @@ __global__ __launch_bounds__(256) void tvam_bin_fill_kernel(TvamConsts k, TvamSe
     }
 }
 
+// Counting-sort fill (no radix sort): workgroup b of the record writer's grid walks the same
+// paths' segments again (its 256-path groups g = b, b + G, ...; in rounds of TVAM_FILL_T slots
+// ordered by brick count, as tvam_bin_fill_kernel) and writes each (segment, brick) entry at its
+// brick's next position among this workgroup's (base: the scan of the writer's per-(brick,
+// workgroup) counts, cursors in LDS).  An entry is its slot | class << 28 (the class of its
+// predicted in-brick visit count, 16 classes: the brick kernel orders each wave's entries by it).
+// The order of one workgroup's entries within a brick follows its LDS atomics: the forward sums
+// them exactly (int64 fixed point) and the adjoint reduces each pixel's partials in (slot, brick)
+// order through inv (inv[off[slot] + j] = position of the slot's j-th entry), so results do
+// not depend on it.
+#define TVAM_ENT_SLOT_BITS 28
+__global__ __launch_bounds__(256) void tvam_bin_fill2_kernel(TvamConsts k, TvamSegBuf sb, int64_t nslots,
+                                                             const uint32_t* __restrict__ base,
+                                                             uint32_t* __restrict__ ent,
+                                                             const uint32_t* __restrict__ off,
+                                                             uint32_t* __restrict__ inv) {
+    constexpr int U = TVAM_FILL_T / 256;
+    extern __shared__ uint32_t s_cur[];  // [nbricks]
+    __shared__ uint32_t s_cnt[256];
+    __shared__ uint32_t s_ord[TVAM_FILL_T];
+    const int G = (int)gridDim.x, beta = (int)blockIdx.x;
+    for (int b = threadIdx.x; b < sb.nbricks; b += 256) s_cur[b] = base[(size_t)b * G + beta];
+    const int64_t gslots = (int64_t)256 * sb.slots;  // one writer group: 256 paths
+    for (int64_t s0 = (int64_t)beta * gslots; s0 < nslots; s0 += (int64_t)G * gslots) {
+        const int64_t s1 = min(nslots, s0 + gslots);
+        for (int64_t t0 = s0; t0 < s1; t0 += TVAM_FILL_T) {
+            __syncthreads();  // s_cur ready; the previous round's s_ord consumed
+            s_cnt[threadIdx.x] = 0;
+            __syncthreads();
+            uint32_t bin[U], rk[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t si = t0 + threadIdx.x + u * 256;
+                const uint32_t m = si < s1 ? sb.m[si] : 0u;
+                bin[u] = m == 0 ? 255u : 254u - min(m - 1u, 254u);  // longest first, empty slots last
+                rk[u] = atomicAdd(&s_cnt[bin[u]], 1u);
+            }
+            __syncthreads();
+            if (threadIdx.x < 64) {  // exclusive scan of the 256 bin counts
+                const int l = threadIdx.x;
+                uint32_t c[4], tot = 0;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    c[j] = s_cnt[4 * l + j];
+                    tot += c[j];
+                }
+                uint32_t inc = tot;
+                for (int d = 1; d < 64; d <<= 1) {
+                    const uint32_t v = __shfl_up(inc, d, 64);
+                    if (l >= d) inc += v;
+                }
+                uint32_t run = inc - tot;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const uint32_t cj = c[j];
+                    s_cnt[4 * l + j] = run;
+                    run += cj;
+                }
+            }
+            __syncthreads();
+            const uint32_t nne = s_cnt[255];
+#pragma unroll
+            for (int u = 0; u < U; ++u) s_ord[s_cnt[bin[u]] + rk[u]] = threadIdx.x + u * 256;
+            __syncthreads();
+            for (uint32_t r = threadIdx.x; r < nne; r += 256) {
+                const int64_t si = t0 + s_ord[r];
+                SegDda q;
+                float w;
+                sc_unpack(sb.r[TVAM_REC_F4 * si], sb.r[TVAM_REC_F4 * si + 1], sb.r[TVAM_REC_F4 * si + 2], q, w);
+                uint32_t o = inv ? off[si] : 0u;
+                float rate = 0.0f;
+#pragma unroll
+                for (int a = 0; a < 3; ++a) rate += q.ts[a] < TVAM_INF ? 1.0f / q.ts[a] : 0.0f;
+                sc_walk_bricks(k, q, [&](int bid, float ta, float tb) {
+                    const int cls = (int)fminf(15.0f, fmaxf(tb - ta, 0.0f) * rate * 0.25f);  // classes of 4 visits
+                    const uint32_t pos = atomicAdd(&s_cur[bid], 1u);
+                    ent[pos] = (uint32_t)si | ((uint32_t)cls << TVAM_ENT_SLOT_BITS);
+                    if (inv) inv[o++] = pos;
+                });
+            }
+        }
+    }
+}
+
+// bstart[b] = the first entry of brick b (the scan of the per-(brick, workgroup) counts at
+// workgroup 0), bstart[nbricks] = the total
+__global__ void tvam_bin_bstart_kernel(const uint32_t* __restrict__ base, int G, int nbricks,
+                                       uint32_t* __restrict__ bstart) {
+    for (int b = blockIdx.x * blockDim.x + threadIdx.x; b <= nbricks; b += gridDim.x * blockDim.x)
+        bstart[b] = base[(size_t)b * G];
+}
+
+// Adjoint of the counting-sort bins: per DMD pixel of the chunk (one wave), the sum of its slots'
+// entry partials in (slot, brick) order -- inv lists each slot's entry positions contiguously
+// from off[slot], and a pixel's slots are contiguous -- added to the pattern gradient.
+__global__ __launch_bounds__(256) void tvam_bin_reduce2_kernel(TvamSegBuf sb, int spp, const uint32_t* __restrict__ off,
+                                                               const uint32_t* __restrict__ inv,
+                                                               const float* __restrict__ part,
+                                                               const int32_t* __restrict__ idxmap,
+                                                               float* __restrict__ grad) {
+    const int64_t l0 = sb.p0 / spp, l1 = sb.p1 / spp;
+    const int64_t pslots = (int64_t)spp * sb.slots;
+    const int lane = (int)(threadIdx.x & 63);
+    const int64_t w0 = ((int64_t)blockIdx.x * blockDim.x + threadIdx.x) >> 6, ws = ((int64_t)gridDim.x * blockDim.x) >> 6;
+    for (int64_t local = l0 + w0; local < l1; local += ws) {
+        const int64_t i = local - l0;
+        const uint32_t a = off[i * pslots], b = off[(i + 1) * pslots];
+        if (a == b) continue;  // (uniform over the wave)
+        float acc = 0.0f;
+        for (uint32_t e = a + (uint32_t)lane; e < b; e += 64) acc += part[inv[e]];
+        for (int o = 32; o > 0; o >>= 1) acc += __shfl_xor(acc, o, 64);
+        if (lane == 0) {
+            int64_t act = local;
+            if (idxmap) {
+                act = idxmap[local];
+                if (act < 0) continue;
+            }
+            grad[act] += acc;
+        }
+    }
+}
+
 __global__ void tvam_bin_start_kernel(const uint32_t* __restrict__ keys, int64_t n, int nbricks, uint32_t kmask,
                                       int cbits, uint32_t* __restrict__ bstart) {
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i <= n; i += (int64_t)gridDim.x * blockDim.x) {
@@ -1364,7 +1502,12 @@ __global__ void tvam_bin_start_kernel(const uint32_t* __restrict__ keys, int64_t
 // (pixel, partial) pairs by pixel and sums each pixel's run (a partial stored at the
 // segment's own entry index instead -- one random 4-byte store per entry -- took 57 % of
 // this kernel's time on config 4).
-template <int ACC, int NT>
+//
+// WS (counting-sort bins): vals are tvam_bin_fill2_kernel's entries (slot | class << 28, a brick's
+// entries in fill order).  Each wave takes batches of 256 of its brick's entries, orders a batch
+// by class in LDS (ballot counting sort, longest first; no workgroup barrier) and marches its lanes'
+// four entries in that order, so the lanes of a step march similar lengths.
+template <int ACC, int NT, bool WS = false>
 __global__ __launch_bounds__(NT) void tvam_bin_march_kernel(TvamConsts k, TvamSegBuf sb,
                                                              const uint32_t* __restrict__ vals,
                                                              const uint32_t* __restrict__ bstart,
@@ -1373,6 +1516,9 @@ __global__ __launch_bounds__(NT) void tvam_bin_march_kernel(TvamConsts k, TvamSe
                                                              float* __restrict__ part) {
     constexpr int NV = TVAM_BX * TVAM_BY * TVAM_BZ;
     __shared__ __attribute__((aligned(16))) unsigned char smem[NV * (ACC == 0 ? 8 : 4)];
+    constexpr int WSB = 256;  // entries per wave batch (WS): the batch order in LDS as byte offsets (4 KB;
+                              // the adjoint's two 64 KB tiles per CU stay resident)
+    __shared__ uint8_t s_wo[WS ? (NT / 64) * WSB : 1];
     long long* ltile = reinterpret_cast<long long*>(smem);
     float* ftile = reinterpret_cast<float*>(smem);
     const int nbx = sc_nbr(k, 0), nby = sc_nbr(k, 1);
@@ -1459,10 +1605,60 @@ __global__ __launch_bounds__(NT) void tvam_bin_march_kernel(TvamConsts k, TvamSe
             sc_brick_march<false>(k, q, lo, hi, visit);
         if (ACC == 2) {
             part[e] = w * fmaf(pc, pv, acc);
-            ppix[e] = r.slot / pslots;
+            if (!WS) ppix[e] = r.slot / pslots;
         }
     };
-    if (et < e1) {
+    if constexpr (WS) {
+        constexpr int U = WSB / 64, NW = NT / 64;
+        constexpr uint32_t SMASK = (1u << TVAM_ENT_SLOT_BITS) - 1u;
+        const int lane = (int)(threadIdx.x & 63), wv = (int)(threadIdx.x >> 6);
+        uint8_t* so = s_wo + wv * WSB;
+        const uint64_t lt = lane == 0 ? 0ull : (~0ull >> (64 - lane));  // the lanes below this one
+        for (uint32_t b0 = e0 + (uint32_t)wv * WSB; b0 < e1; b0 += (uint32_t)NW * WSB) {
+            uint32_t v[U];
+            int key[U], pos[U];
+#pragma unroll
+            for (int j = 0; j < U; ++j) {
+                const uint32_t idx = b0 + (uint32_t)(j * 64 + lane);
+                const bool ok = idx < e1;
+                v[j] = ok ? vals[idx] : 0u;
+                key[j] = ok ? 15 - (int)(v[j] >> TVAM_ENT_SLOT_BITS) : 16;  // longest class first, past e1 last
+                pos[j] = 0;
+            }
+            int run_ = 0;
+            for (int c = 0; c <= 16; ++c) {
+#pragma unroll
+                for (int j = 0; j < U; ++j) {
+                    const uint64_t m = __ballot(key[j] == c);
+                    if (key[j] == c) pos[j] = run_ + (int)__popcll(m & lt);
+                    run_ += (int)__popcll(m);
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < U; ++j) so[pos[j]] = (uint8_t)(j * 64 + lane);
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            const uint32_t nval = min(e1 - b0, (uint32_t)WSB);
+            uint32_t sl[U], eo[U];
+#pragma unroll
+            for (int j = 0; j < U; ++j) {  // the batch's entry at sorted position j * 64 + lane (re-read: L1)
+                eo[j] = b0 + (uint32_t)so[j * 64 + lane];
+                sl[j] = (uint32_t)(j * 64 + lane) < nval ? vals[eo[j]] & SMASK : 0u;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();  // every lane has read the batch before the next one is written
+            Ent rA, rB;
+            load(sl[0], 0u, rA);
+            load(sl[1], 0u, rB);
+            if ((uint32_t)lane < nval) run(rA, eo[0]);
+            load(sl[2], 0u, rA);
+            if ((uint32_t)(64 + lane) < nval) run(rB, eo[1]);
+            load(sl[3], 0u, rB);
+            if ((uint32_t)(128 + lane) < nval) run(rA, eo[2]);
+            if ((uint32_t)(192 + lane) < nval) run(rB, eo[3]);
+        }
+    } else if (et < e1) {
         uint32_t sB = vals[min(et + S, el)];
         Ent rA, rB;
         load(vals[et], et, rA);
@@ -1565,6 +1761,8 @@ void tvam_bin_scratch_free(TvamBinScratch& s) {
     (void)hipFree(s.bstart);
     (void)hipFree(s.temp);
     (void)hipFree(s.part);
+    (void)hipFree(s.hist);
+    (void)hipFree(s.hbase);
     for (auto& c : s.fc) {
         (void)hipFree(c.r);
         (void)hipFree(c.vals);
@@ -1609,6 +1807,17 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
     chunk = std::min(npaths, chunk);
     const int64_t nsl = chunk * slots;
     if (nsl >= ((int64_t)1 << 31)) return hipErrorNotSupported;  // 32-bit slot indices (reweight)
+    // counting-sort bins (default): the record writer counts each workgroup's entries per brick, a
+    // scan of those counts places every entry, and each brick wave orders its entries by class
+    // itself -- no radix sort of (brick, class) keys and, in the adjoint, none of (pixel, partial)
+    // pairs.  The radix-sort path stays for TVAM_BIN_SORT=1, float tiles, 512-thread bricks and
+    // grids whose brick counts exceed the writer's LDS histogram.
+    static const bool bin_sort = [] {
+        const char* v = getenv("TVAM_BIN_SORT");
+        return v && atoi(v) != 0;
+    }();
+    const bool csort = !bin_sort && !s.acc_float && bin_nt == 1024 && nbricks <= 16384 &&
+                       nsl <= ((int64_t)1 << TVAM_ENT_SLOT_BITS);
     hipError_t e;
     if (nsl > s.cap_slots) {
         const int keep_float = s.acc_float;
@@ -1650,9 +1859,12 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
         return hipMemGetInfo(&fr, &tot) == hipSuccess && fr > bytes + tot / 8 + ((size_t)1 << 30);
     };
     // forward brick march: int64 fixed point (default) or float LDS adds (TVAM_BIN_FLOAT)
-    auto march_fwd = [&](const TvamSegBuf& sb, const uint32_t* vals, const uint32_t* bstart) {
+    auto march_fwd = [&](const TvamSegBuf& sb, const uint32_t* vals, const uint32_t* bstart, bool ws) {
         const dim3 grid((unsigned)nbricks), blk(bin_nt);
-        if (s.acc_float && bin_nt == 1024)
+        if (ws)  // counting-sort entries (csort: int64 tiles, 1024 threads)
+            hipLaunchKernelGGL((tvam_bin_march_kernel<0, 1024, true>), grid, dim3(1024), 0, stream, k, sb, vals,
+                               bstart, out, nullptr, 0u, nullptr, nullptr);
+        else if (s.acc_float && bin_nt == 1024)
             hipLaunchKernelGGL((tvam_bin_march_kernel<1, 1024>), grid, blk, 0, stream, k, sb, vals, bstart, out,
                                nullptr, 0u, nullptr, nullptr);
         else if (s.acc_float)
@@ -1684,7 +1896,7 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
             sb.r = cc->r;
             int64_t g = std::min<int64_t>((ns + 255) / 256, 8192);
             hipLaunchKernelGGL(tvam_bin_reweight_kernel, dim3((unsigned)g), dim3(256), 0, stream, k, sb, spp, pat);
-            march_fwd(sb, cc->vals, cc->bstart);
+            march_fwd(sb, cc->vals, cc->bstart, cc->ws);
             if ((e = hipGetLastError()) != hipSuccess) return e;
             continue;
         }
@@ -1702,23 +1914,63 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
         if (cc) sb.r = cc->r;
         if ((e = hipMemsetAsync(sb.m, 0, (ns + 1) * sizeof(uint32_t), stream)) != hipSuccess) return e;
         int64_t g = std::min<int64_t>((p1 - p0 + 255) / 256, 262144);
-        hipLaunchKernelGGL(tvam_scatter_kernel<TVAM_MODE_EMIT>, dim3((unsigned)g), dim3(256), 0, stream, k, t, pat,
-                           idxmap, nullptr, nullptr, nullptr, sb);
-        // exclusive scan of the brick counts (ns + 1 entries: the last gives the total)
-        size_t tb = 0;
-        if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, sb.m, s.off, (int)(ns + 1), stream)) != hipSuccess)
-            return e;
-        if (tb > s.temp_bytes) {
-            (void)hipFree(s.temp);
-            s.temp = nullptr;
-            s.temp_bytes = 0;
-            if ((e = hipMalloc(&s.temp, tb)) != hipSuccess) return e;
-            s.temp_bytes = tb;
+        const int G = csort ? (int)std::min<int64_t>((p1 - p0 + 255) / 256, 2048) : 0;
+        const int64_t nh = (int64_t)nbricks * G + 1;  // per-(brick, workgroup) counts + the total
+        if (csort) {
+            if (nh > s.cap_hist) {
+                (void)hipFree(s.hist);
+                (void)hipFree(s.hbase);
+                s.hist = s.hbase = nullptr;
+                s.cap_hist = 0;
+                if ((e = hipMalloc((void**)&s.hist, nh * sizeof(uint32_t))) != hipSuccess ||
+                    (e = hipMalloc((void**)&s.hbase, nh * sizeof(uint32_t))) != hipSuccess)
+                    return e;
+                s.cap_hist = nh;
+            }
+            if ((e = hipMemsetAsync(s.hist + (nh - 1), 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
+            sb.hist = s.hist;
+            sb.nbricks = nbricks;
+            g = G;
+        } else {
+            sb.hist = nullptr;
         }
-        if ((e = hipcub::DeviceScan::ExclusiveSum(s.temp, tb, sb.m, s.off, (int)(ns + 1), stream)) != hipSuccess)
-            return e;
+        hipLaunchKernelGGL(tvam_scatter_kernel<TVAM_MODE_EMIT>, dim3((unsigned)g), dim3(256),
+                           csort ? (size_t)nbricks * sizeof(uint32_t) : 0, stream, k, t, pat, idxmap, nullptr, nullptr,
+                           nullptr, sb);
+        sb.hist = nullptr;  // the march kernels read none of it
+        if (csort) {
+            size_t tbh = 0;
+            if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tbh, s.hist, s.hbase, (int)nh, stream)) != hipSuccess)
+                return e;
+            if (tbh > s.temp_bytes) {
+                (void)hipFree(s.temp);
+                s.temp = nullptr;
+                s.temp_bytes = 0;
+                if ((e = hipMalloc(&s.temp, tbh)) != hipSuccess) return e;
+                s.temp_bytes = tbh;
+            }
+            if ((e = hipcub::DeviceScan::ExclusiveSum(s.temp, tbh, s.hist, s.hbase, (int)nh, stream)) != hipSuccess)
+                return e;
+        }
+        // exclusive scan of the brick counts (ns + 1 entries: the last gives the total); the
+        // counting-sort forward needs none (its positions come from the histogram scan)
+        size_t tb = 0;
+        if (!csort || adj) {
+            if ((e = hipcub::DeviceScan::ExclusiveSum(nullptr, tb, sb.m, s.off, (int)(ns + 1), stream)) != hipSuccess)
+                return e;
+            if (tb > s.temp_bytes) {
+                (void)hipFree(s.temp);
+                s.temp = nullptr;
+                s.temp_bytes = 0;
+                if ((e = hipMalloc(&s.temp, tb)) != hipSuccess) return e;
+                s.temp_bytes = tb;
+            }
+            if ((e = hipcub::DeviceScan::ExclusiveSum(s.temp, tb, sb.m, s.off, (int)(ns + 1), stream)) != hipSuccess)
+                return e;
+        }
         uint32_t total = 0;
-        if ((e = hipMemcpyAsync(&total, s.off + ns, sizeof(uint32_t), hipMemcpyDeviceToHost, stream)) != hipSuccess)
+        if ((e = hipMemcpyAsync(&total, csort ? s.hbase + (nh - 1) : s.off + ns, sizeof(uint32_t),
+                                hipMemcpyDeviceToHost, stream)) != hipSuccess)
             return e;
         if ((e = hipStreamSynchronize(stream)) != hipSuccess) return e;
         if (cc && (int64_t)total > cc->cap_vals) {
@@ -1744,28 +1996,62 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
         // a chunk whose sorted slots find no room runs from the scratch arrays, uncached
         const bool keep = cc && (total == 0 || (cc->vals && cc->bstart));
         if (keep) cc->total = total;
+        if (keep) cc->ws = csort;
         if (keep) ++s.st[2];
         s.st[3] += total;
         if (total == 0) {
             if (keep) cc->valid = true;
             continue;
         }
+        // entry arrays: keys[0] (sort keys / the counting-sort adjoint's inv), vals[1] (sorted slots /
+        // entries), part (adjoint partials); the radix sort's second buffers keys[1] / vals[0] only
+        // on that path (cap_entries2)
         if ((int64_t)total > s.cap_entries) {
-            for (int i = 0; i < 2; ++i) {
-                (void)hipFree(s.keys[i]);
-                (void)hipFree(s.vals[i]);
-                s.keys[i] = s.vals[i] = nullptr;
-            }
+            (void)hipFree(s.keys[0]);
+            (void)hipFree(s.vals[1]);
             (void)hipFree(s.part);
+            s.keys[0] = s.vals[1] = nullptr;
             s.part = nullptr;
             s.cap_entries = 0;
             const int64_t cap = (int64_t)total + total / 4;
-            for (int i = 0; i < 2; ++i)
-                if ((e = hipMalloc((void**)&s.keys[i], cap * sizeof(uint32_t))) != hipSuccess ||
-                    (e = hipMalloc((void**)&s.vals[i], cap * sizeof(uint32_t))) != hipSuccess)
-                    return e;
-            if ((e = hipMalloc((void**)&s.part, cap * sizeof(float))) != hipSuccess) return e;
+            if ((e = hipMalloc((void**)&s.keys[0], cap * sizeof(uint32_t))) != hipSuccess ||
+                (e = hipMalloc((void**)&s.vals[1], cap * sizeof(uint32_t))) != hipSuccess ||
+                (e = hipMalloc((void**)&s.part, cap * sizeof(float))) != hipSuccess)
+                return e;
             s.cap_entries = cap;
+        }
+        if (!csort && (int64_t)total > s.cap_entries2) {
+            (void)hipFree(s.keys[1]);
+            (void)hipFree(s.vals[0]);
+            s.keys[1] = s.vals[0] = nullptr;
+            s.cap_entries2 = 0;
+            const int64_t cap = (int64_t)total + total / 4;
+            if ((e = hipMalloc((void**)&s.keys[1], cap * sizeof(uint32_t))) != hipSuccess ||
+                (e = hipMalloc((void**)&s.vals[0], cap * sizeof(uint32_t))) != hipSuccess)
+                return e;
+            s.cap_entries2 = cap;
+        }
+        if (csort) {
+            uint32_t* ent = keep ? cc->vals : s.vals[1];
+            uint32_t* bstart = keep ? cc->bstart : s.bstart;
+            uint32_t* inv = adj ? s.keys[0] : nullptr;
+            hipLaunchKernelGGL(tvam_bin_bstart_kernel, dim3((unsigned)((nbricks + 256) / 256)), dim3(256), 0, stream,
+                               s.hbase, G, nbricks, bstart);
+            hipLaunchKernelGGL(tvam_bin_fill2_kernel, dim3((unsigned)G), dim3(256), (size_t)nbricks * sizeof(uint32_t),
+                               stream, k, sb, ns, s.hbase, ent, adj ? s.off : nullptr, inv);
+            if (adj) {
+                hipLaunchKernelGGL((tvam_bin_march_kernel<2, 1024, true>), dim3((unsigned)nbricks), dim3(1024), 0,
+                                   stream, k, sb, ent, bstart, nullptr, gin, 0u, nullptr, s.part);
+                const int64_t npix = (p1 - p0) / spp;
+                g = std::min<int64_t>((npix + 3) / 4, 65536);  // a wave per pixel
+                hipLaunchKernelGGL(tvam_bin_reduce2_kernel, dim3((unsigned)g), dim3(256), 0, stream, sb, spp, s.off,
+                                   inv, s.part, idxmap, out);
+            } else {
+                march_fwd(sb, ent, bstart, true);
+            }
+            if ((e = hipGetLastError()) != hipSuccess) return e;
+            if (keep) cc->valid = true;
+            continue;
         }
         size_t tb2 = 0;
         if ((e = hipcub::DeviceRadixSort::SortPairs(nullptr, tb2, s.keys[0], s.keys[1], s.vals[0], s.vals[1],
@@ -1826,7 +2112,7 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
             hipLaunchKernelGGL(tvam_bin_reduce_kernel, dim3((unsigned)g), dim3(256), 0, stream, sb, spp, s.off, psort,
                                idxmap, out);
         } else {
-            march_fwd(sb, vals_out, bstart);
+            march_fwd(sb, vals_out, bstart, false);
         }
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (keep) cc->valid = true;
