@@ -88,6 +88,12 @@ struct TvamPlanar {
     const uint32_t* adj_qslots;
     const int64_t* adj_qoff;   // [ntiles * 4 + 1]
     int32_t adj_quad;
+    // adjoint: per-tile ray pairs (adj_pair = 1, tvam_plan.hip adj_pair_lists): the tile's crossing
+    // rays of each angle in column order, ray j paired with ray j + ceil(n / 2) (complementary
+    // chord lengths through a square tile), stored as consecutive entries; 0xffffffff pads
+    const uint32_t* adj_pslots;
+    const int64_t* adj_poff;   // [ntiles + 1], even lengths
+    int32_t adj_pair;
     int32_t adj_pitch2;        // row pitch of quadrants 1, 2 (opposite step signs); adj_pitch: 0, 3
     int32_t rayfwd_pitch;      // ray-driven forward: LDS row pitch of its dose tile (>= tile + 2)
     int32_t rayfwd_nt;         // ray-driven forward: threads per workgroup (256 or 512)

@@ -94,6 +94,8 @@ struct tvam_plan {
     int32_t* d_pl_rec_i = nullptr;
     float4* d_pl_rec_g = nullptr;
     uint32_t* d_adjq_slots = nullptr;  // planar adjoint: per (tile, quadrant) ray lists
+    uint32_t* d_adjp_slots = nullptr;  // planar adjoint: per-tile ray pairs
+    int64_t* d_adjp_off = nullptr;
     int64_t* d_adjq_off = nullptr;
     float* d_pl_part = nullptr;  // voxel-driven forward: partial doses of the angle parts
     float* d_pl_bin = nullptr;   // voxel-driven forward: slice-binned patterns
@@ -181,6 +183,8 @@ static void plan_free(tvam_plan* p) {
     (void)hipFree(p->d_pl_rec_i);
     (void)hipFree(p->d_pl_rec_g);
     (void)hipFree(p->d_adjq_slots);
+    (void)hipFree(p->d_adjp_slots);
+    (void)hipFree(p->d_adjp_off);
     (void)hipFree(p->d_adjq_off);
     (void)hipFree(p->d_pl_part);
     (void)hipFree(p->d_pl_bin);
@@ -475,6 +479,88 @@ static int adj_quadrant_lists(tvam_plan* p) {
     return 0;
 }
 
+// Planar adjoint ray pairs per tile (TvamPlanar::adj_pair).  A lane marches two rays of one
+// angle: its in-tile chords through a square tile are a trapezoid in column order (0.68 of the
+// lanes busy with one ray per lane on config 2), and ray j plus ray j + ceil(n / 2) of the angle's n
+// crossing rays have complementary lengths, while neighbouring lanes keep neighbouring columns in
+// both halves (the march's LDS reads stay coherent).  Rays that miss the tile (the kernel would
+// skip them) are left out; the exact crossing test is the kernel's closed-form resume.
+static int adj_pair_lists(tvam_plan* p) {
+    const TvamConsts& k = p->k;
+    const TvamTiles& t = p->tiles;
+    const int ns = p->pl.ns, ntiles = t.ntx * t.nty;
+    const size_t nrec = (size_t)ns * k.crop_x;
+    std::vector<float4> rf(nrec), rg, ang((size_t)std::max(ns, 1));
+    std::vector<int32_t> ri(nrec);
+    std::vector<int64_t> off((size_t)ntiles + 1);
+    hipError_t e;
+    if ((e = hipMemcpy(rf.data(), p->d_pl_rec_f, nrec * sizeof(float4), hipMemcpyDeviceToHost)) != hipSuccess ||
+        (e = hipMemcpy(ri.data(), p->d_pl_rec_i, nrec * sizeof(int32_t), hipMemcpyDeviceToHost)) != hipSuccess ||
+        (e = hipMemcpy(off.data(), p->d_slot_off, off.size() * sizeof(int64_t), hipMemcpyDeviceToHost)) != hipSuccess ||
+        (ns > 0 && (e = hipMemcpy(ang.data(), p->d_ang, (size_t)ns * sizeof(float4), hipMemcpyDeviceToHost)) != hipSuccess))
+        return hip_fail(e, "hipMemcpy (adjoint pairs)");
+    if (p->d_pl_rec_g) {
+        rg.resize(nrec);
+        if ((e = hipMemcpy(rg.data(), p->d_pl_rec_g, nrec * sizeof(float4), hipMemcpyDeviceToHost)) != hipSuccess)
+            return hip_fail(e, "hipMemcpy (adjoint pairs)");
+    }
+    std::vector<uint32_t> slots((size_t)off[ntiles]);
+    if (!slots.empty() && (e = hipMemcpy(slots.data(), p->d_slots, slots.size() * sizeof(uint32_t),
+                                         hipMemcpyDeviceToHost)) != hipSuccess)
+        return hip_fail(e, "hipMemcpy (adjoint pairs)");
+    constexpr uint32_t PAD = 0xffffffffu;
+    std::vector<uint32_t> out;
+    std::vector<int64_t> poff((size_t)ntiles + 1, 0);
+    std::vector<uint32_t> run;
+    for (int tile = 0; tile < ntiles; ++tile) {
+        const int x0 = (tile % t.ntx) * t.tsx, y0 = (tile / t.ntx) * t.tsy;
+        const int x1 = std::min(x0 + t.tsx, k.res[0]), y1 = std::min(y0 + t.tsy, k.res[1]);
+        auto flush = [&]() {
+            const size_t n = run.size(), h = (n + 1) / 2;
+            for (size_t j = 0; j < h; ++j) {
+                out.push_back(run[j]);
+                out.push_back(j + h < n ? run[j + h] : PAD);
+            }
+            run.clear();
+        };
+        int cur = -1;
+        for (int64_t j = off[tile]; j < off[tile + 1]; ++j) {
+            const uint32_t ev = slots[(size_t)j];
+            const int al = (int)(ev >> 16), colc = (int)(ev & 0xffffu);
+            if (al != cur) {
+                flush();
+                cur = al;
+            }
+            const size_t r = (size_t)al * k.crop_x + colc;
+            const int rv = ri[r];
+            if (rv < 0) continue;  // misses the vial / grid
+            const float4 ff = rf[r];
+            float4 an = ang[(size_t)al];
+            if (!rg.empty()) {
+                const float4 gg = rg[r];
+                an = make_float4(std::fabs(gg.x), std::fabs(gg.y), gg.x < 0.0f ? -1.0f : 1.0f, gg.y < 0.0f ? -1.0f : 1.0f);
+            }
+            const int svx = rv & 0xffff, svy = rv >> 16, stx = (int)an.z, sty = (int)an.w;
+            float tin0, tout0, tin1, tout1;
+            int nin0, nout0, nin1, nout1;
+            tvam_axis_window(svx, stx, ff.z, an.x, x0, x1, tin0, tout0, nin0, nout0);
+            tvam_axis_window(svy, sty, ff.w, an.y, y0, y1, tin1, tout1, nin1, nout1);
+            const float tau_e = std::max(std::max(tin0, tin1), 0.0f);
+            const float tau_x = std::min(std::min(tout0, tout1), ff.y);
+            if (!(tau_e < tau_x)) continue;  // does not cross this tile
+            run.push_back(ev);
+        }
+        flush();
+        poff[(size_t)tile + 1] = (int64_t)out.size();
+    }
+    int rc;
+    if ((rc = upload(&p->d_adjp_slots, out)) || (rc = upload(&p->d_adjp_off, poff))) return rc;
+    p->pl.adj_pslots = p->d_adjp_slots;
+    p->pl.adj_poff = p->d_adjp_off;
+    p->pl.adj_pair = 1;
+    return 0;
+}
+
 static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     const tvam_desc& d = p->desc;
     const TvamConsts& k = p->k;
@@ -619,6 +705,8 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
         if (rc) return rc;
     }
     if (p->pl.adj_quad && (rc = adj_quadrant_lists(p))) return rc;
+    // ray pairs (TVAM_ADJ_PAIR, default 1): balanced lanes in the planar adjoint
+    if (!p->pl.adj_quad && env_int("TVAM_ADJ_PAIR", 1) && (rc = adj_pair_lists(p))) return rc;
     p->planar = true;
     return 0;
 }

@@ -924,6 +924,11 @@ __global__ __launch_bounds__(NT) void tvam_adj_planar_kernel(TvamConsts k, TvamP
         const int nwv = (int)((q1 - q0) >> 6);
         gb = (int)(((int64_t)nwv * part) / nparts) * 64;
         nrt = (int)(((int64_t)nwv * (part + 1)) / nparts) * 64;
+    } else if (pl.adj_pair) {  // ray pairs (adj_pair_lists): parts of whole pairs
+        slots = pl.adj_pslots + pl.adj_poff[tile_id];
+        const int npair = (int)((pl.adj_poff[tile_id + 1] - pl.adj_poff[tile_id]) >> 1);
+        gb = (int)(((int64_t)npair * blockIdx.z) / gridDim.z) * 2;
+        nrt = (int)(((int64_t)npair * (blockIdx.z + 1)) / gridDim.z) * 2;
     } else {
         slots = tp.slots + tp.slot_off[tile_id];
         const int nall = (int)(tp.slot_off[tile_id + 1] - tp.slot_off[tile_id]);
@@ -967,8 +972,13 @@ __global__ __launch_bounds__(NT) void tvam_adj_planar_kernel(TvamConsts k, TvamP
     if (s_roff[Z] == 0) return;  // no DMD row lies in these slices
 
     // PF: a two-stage software pipeline over this lane's rays -- the slot of ray
-    // k + 2 and the records of ray k + 1 are loaded while ray k marches
-    int g = gb + (int)threadIdx.x;
+    // k + 2 and the records of ray k + 1 are loaded while ray k marches.  A lane's rays are list
+    // entries gb + lane + q NT, or with ray pairs (pl.adj_pair) the pairs gb + 2 lane + 2 q NT
+    // and + 1 (a long chord and a short one of the same angle: balanced lanes)
+    const bool pair = pl.adj_pair != 0 && !pl.adj_quad;
+    auto at = [&](int q) { return pair ? gb + 2 * (int)threadIdx.x + (q >> 1) * 2 * NT + (q & 1) : gb + (int)threadIdx.x + q * NT; };
+    int qi = 0;
+    int g = at(0);
     uint32_t e_n = 0, e_nn = 0;
     int ri_n = -1;
     float4 ff_n = make_float4(0.0f, 0.0f, 0.0f, 0.0f), an_n = ff_n;
@@ -997,9 +1007,9 @@ __global__ __launch_bounds__(NT) void tvam_adj_planar_kernel(TvamConsts k, TvamP
             e_n = slots[g];
             records(e_n, ri_n, ff_n, an_n, w_n);
         }
-        if (g + NT < nrt) e_nn = slots[g + NT];
+        if (at(1) < nrt) e_nn = slots[at(1)];
     }
-    for (; g < nrt; g += NT) {
+    for (; g < nrt; g = at(++qi)) {
         uint32_t e;
         int ri;
         float4 ff, an;
@@ -1010,11 +1020,11 @@ __global__ __launch_bounds__(NT) void tvam_adj_planar_kernel(TvamConsts k, TvamP
             ff = ff_n;
             an = an_n;
             wray = w_n;
-            if (g + NT < nrt) {
+            if (at(qi + 1) < nrt) {
                 e_n = e_nn;
                 records(e_n, ri_n, ff_n, an_n, w_n);
             }
-            if (g + 2 * NT < nrt) e_nn = slots[g + 2 * NT];
+            if (at(qi + 2) < nrt) e_nn = slots[at(qi + 2)];
         } else {
             e = slots[g];
             records(e, ri, ff, an, wray);

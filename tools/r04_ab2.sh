@@ -1,16 +1,18 @@
 #!/usr/bin/env bash
 # Round 4 A/B benches: projection variants of config 2 (tools/proj_ab.py), configs 2/4/5 bench lines
-# with the current defaults, and the previous paths (TVAM_BIN_SORT=1, the no-prefetch tile build).
-# usage: tools/r04_ab2.sh OUT
+# with the current defaults and with the previous paths (TVAM_BIN_SORT=1 and the no-prefetch tile
+# build), then the parity tests of the changed kernels.  usage: tools/r04_ab2.sh OUT
 set -euo pipefail
 o="$1"; mkdir -p "$o"
 export TMPDIR=/tmp
-timeout -k 10 300 python tools/proj_ab.py 400 "TVAM_FWD_PX=1" "TVAM_FWD_PX=2" "TVAM_FWD_PX=2 TVAM_PLANAR_FWD_Z=24" \
-  "TVAM_FWD_PX=2 TVAM_PLANAR_FWD_Z=16" "TVAM_PLANAR_ADJ_Z=16" "TVAM_PLANAR_ADJ_Z=16 tile=32" > "$o/proj_ab.jsonl" 2> "$o/proj_ab.err"
-timeout -k 10 300 python bench.py --cpu-baseline off > "$o/c2.json" 2> "$o/c2.err"
-timeout -k 10 400 python bench.py --config 4 --steps 3 --warmup 1 --cpu-baseline off > "$o/c4.json" 2> "$o/c4.err"
-TVAM_BIN_SORT=1 TVAM_LIB=$PWD/_variants/libtvam_nopf.so timeout -k 10 400 python bench.py --config 4 --steps 3 --warmup 1 \
-  --cpu-baseline off > "$o/c4_old.json" 2> "$o/c4_old.err"
-timeout -k 10 400 python bench.py --config 5 --n 800 --steps 3 --warmup 1 --cpu-baseline off > "$o/c5.json" 2> "$o/c5.err"
-TVAM_LIB=$PWD/_variants/libtvam_nopf.so timeout -k 10 400 python bench.py --config 5 --n 800 --steps 3 --warmup 1 \
-  --cpu-baseline off > "$o/c5_nopf.json" 2> "$o/c5_nopf.err"
+timeout -k 10 240 python tools/proj_ab.py 400 "TVAM_FWD_PX=1 TVAM_ADJ_PAIR=0" "" "TVAM_PLANAR_FWD_Z=24" \
+  "TVAM_ADJ_PAIR=0" "TVAM_PLANAR_ADJ_Z=16" "TVAM_PLANAR_ADJ_Z=16 tile=32" > "$o/proj_ab.jsonl" 2> "$o/proj_ab.err"
+timeout -k 10 200 python bench.py --cpu-baseline off > "$o/c2.json" 2> "$o/c2.err"
+timeout -k 10 200 python bench.py --config 4 --steps 2 --warmup 1 --prewarm 0 --cpu-baseline off > "$o/c4.json" 2> "$o/c4.err"
+TVAM_BIN_SORT=1 TVAM_LIB=$PWD/_variants/libtvam_nopf.so timeout -k 10 200 python bench.py --config 4 --steps 2 --warmup 1 \
+  --prewarm 0 --cpu-baseline off > "$o/c4_old.json" 2> "$o/c4_old.err"
+timeout -k 10 200 python bench.py --config 5 --n 800 --steps 2 --warmup 1 --prewarm 0 --cpu-baseline off > "$o/c5.json" 2> "$o/c5.err"
+TVAM_LIB=$PWD/_variants/libtvam_nopf.so timeout -k 10 200 python bench.py --config 5 --n 800 --steps 2 --warmup 1 \
+  --prewarm 0 --cpu-baseline off > "$o/c5_nopf.json" 2> "$o/c5_nopf.err"
+timeout -k 10 450 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_scattering.py \
+  tests/test_gpu_parity.py tests/test_gpu_square.py tests/test_gpu_active_set.py > "$o/tests.log" 2>&1
