@@ -188,25 +188,37 @@ __device__ __forceinline__ int sc_walk_bricks(const TvamConsts& k, const SegDda&
     int b0 = q.sv[0] / TVAM_BX, b1 = q.sv[1] / TVAM_BY, b2 = q.sv[2] / TVAM_BZ;
     int cnt = 0;
     float tprev = 0.0f;
+    // each axis' exit time from the current brick; a step changes one axis' brick, so only that
+    // axis' exit is formed again (the same sc_axis_tout values as forming all three every step)
+    float t0 = sc_axis_tout(q.sv[0], q.step[0], q.dtm0[0], q.ts[0], b0 * TVAM_BX, min(b0 * TVAM_BX + TVAM_BX, k.res[0]));
+    float t1 = sc_axis_tout(q.sv[1], q.step[1], q.dtm0[1], q.ts[1], b1 * TVAM_BY, min(b1 * TVAM_BY + TVAM_BY, k.res[1]));
+    float t2 = sc_axis_tout(q.sv[2], q.step[2], q.dtm0[2], q.ts[2], b2 * TVAM_BZ, min(b2 * TVAM_BZ + TVAM_BZ, k.res[2]));
     for (int guard = 0; guard < 4096; ++guard) {
         const int bid = (b2 * nb1 + b1) * nb0 + b0;
         ++cnt;
-        const float t0 = sc_axis_tout(q.sv[0], q.step[0], q.dtm0[0], q.ts[0], b0 * TVAM_BX,
-                                      min(b0 * TVAM_BX + TVAM_BX, k.res[0]));
-        const float t1 = sc_axis_tout(q.sv[1], q.step[1], q.dtm0[1], q.ts[1], b1 * TVAM_BY,
-                                      min(b1 * TVAM_BY + TVAM_BY, k.res[1]));
-        const float t2 = sc_axis_tout(q.sv[2], q.step[2], q.dtm0[2], q.ts[2], b2 * TVAM_BZ,
-                                      min(b2 * TVAM_BZ + TVAM_BZ, k.res[2]));
         const bool m0 = t0 <= t1 && t0 <= t2;
         const bool m1 = !m0 && t1 <= t2;
         const float tm = m0 ? t0 : (m1 ? t1 : t2);
         f(bid, tprev, fminf(tm, q.tau_end));
         tprev = tm;
         if (!(tm < q.tau_end)) break;
-        b0 += m0 ? q.step[0] : 0;
-        b1 += m1 ? q.step[1] : 0;
-        b2 += (m0 || m1) ? 0 : q.step[2];
-        if ((unsigned)b0 >= (unsigned)nb0 || (unsigned)b1 >= (unsigned)nb1 || (unsigned)b2 >= (unsigned)nb2) break;
+        // the stepped axis: its next brick and exit (selects: one exit formed per step)
+        const int B = m0 ? TVAM_BX : (m1 ? TVAM_BY : TVAM_BZ);
+        const int st = m0 ? q.step[0] : (m1 ? q.step[1] : q.step[2]);
+        const int bn = (m0 ? b0 : (m1 ? b1 : b2)) + st;
+        const int nb = m0 ? nb0 : (m1 ? nb1 : nb2);
+        if ((unsigned)bn >= (unsigned)nb) break;
+        const int sv = m0 ? q.sv[0] : (m1 ? q.sv[1] : q.sv[2]);
+        const float dtm = m0 ? q.dtm0[0] : (m1 ? q.dtm0[1] : q.dtm0[2]);
+        const float ts = m0 ? q.ts[0] : (m1 ? q.ts[1] : q.ts[2]);
+        const int res = m0 ? k.res[0] : (m1 ? k.res[1] : k.res[2]);
+        const float tn = sc_axis_tout(sv, st, dtm, ts, bn * B, min(bn * B + B, res));
+        b0 = m0 ? bn : b0;
+        b1 = m1 ? bn : b1;
+        b2 = (m0 || m1) ? b2 : bn;
+        t0 = m0 ? tn : t0;
+        t1 = m1 ? tn : t1;
+        t2 = (m0 || m1) ? t2 : tn;
     }
     return cnt;
 }
