@@ -705,8 +705,9 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
         if (rc) return rc;
     }
     if (p->pl.adj_quad && (rc = adj_quadrant_lists(p))) return rc;
-    // ray pairs (TVAM_ADJ_PAIR, default 1): balanced lanes in the planar adjoint
-    if (!p->pl.adj_quad && env_int("TVAM_ADJ_PAIR", 1) && (rc = adj_pair_lists(p))) return rc;
+    // ray pairs (TVAM_ADJ_PAIR=1; off by default: config 2 adjoint 3.65 -> 3.90 ms, the two halves'
+    // lanes drift apart and the march's LDS reads lose their coherence, profiles/r04/ab2/proj_ab.jsonl)
+    if (!p->pl.adj_quad && env_int("TVAM_ADJ_PAIR", 0) && (rc = adj_pair_lists(p))) return rc;
     p->planar = true;
     return 0;
 }
@@ -996,10 +997,11 @@ static bool planar_fwd_setup(tvam_plan* p, const std::vector<float2>& cs, const 
         p->pl.fwd_ab = (ab >= 1 && ab <= 4) ? ab : 2;
     }
     if (!choose_fwd_z(p)) return false;
-    // voxel pairs (TVAM_FWD_PX, default 2) where the depth has a pair variant (Z <= 32, binned
-    // staging of <= 2 float4 per thread, 2 angles per barrier) and the pair's union of candidates
-    // fits the kernel's NC + 2 (lateral centres <= 1 column apart)
-    if (env_int("TVAM_FWD_PX", 2) == 2 && p->planar_fz <= 32 && env_int("TVAM_FWD_BIN", 1) && p->pl.fwd_ab == 2) {
+    // voxel pairs (TVAM_FWD_PX=2; off by default: config 2 forward 3.07 -> 3.92 ms, the pair's 64
+    // accumulators leave 3 waves per SIMD instead of 5, profiles/r04/ab2/proj_ab.jsonl) where the
+    // depth has a pair variant (Z <= 32, binned staging of <= 2 float4 per thread, 2 angles per
+    // barrier) and the pair's union of candidates fits the kernel's NC + 2
+    if (env_int("TVAM_FWD_PX", 1) == 2 && p->planar_fz <= 32 && env_int("TVAM_FWD_BIN", 1) && p->pl.fwd_ab == 2) {
         double dmax = 0.0;
         for (int i = 0; i < ns; ++i) dmax = std::max(dmax, std::fabs((double)fang[2 * (size_t)i].x) * k.h[0]);
         std::vector<int32_t> fcb2;

@@ -9,6 +9,9 @@ from __future__ import annotations
 import ctypes
 import os
 import subprocess
+import sys
+import threading
+import time
 
 import numpy as np
 
@@ -72,6 +75,22 @@ def _ptr(a):
     return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
 
 
+def _call(name, fn, *args):
+    """fn(*args) (a ctypes call: it releases the GIL) on a worker thread; while it runs longer than
+    50 s, one progress line per 50 s on the process's real stderr (a full-size scattering oracle
+    pass takes minutes of silent CPU work, which a hang watchdog would otherwise take for a hang)."""
+    out = {}
+    th = threading.Thread(target=lambda: out.__setitem__("rc", fn(*args)), daemon=True)
+    t0 = time.perf_counter()
+    th.start()
+    while True:
+        th.join(50.0)
+        if not th.is_alive():
+            break
+        print(f"[oracle] {name}: running for {time.perf_counter() - t0:.0f} s", file=sys.__stderr__, flush=True)
+    return out["rc"]
+
+
 def film_shape(desc):
     rx, ry, rz = desc.film_res
     return (rz, ry, rx)
@@ -89,12 +108,12 @@ def forward(desc, active_data, active_pixels=None, spp=1, seed=0, nthreads=1, pa
     if streams is not None:
         st = np.ascontiguousarray(streams, dtype=np.uint64)
         assert pix is not None and st.size == data.size == pix.size and part == -1
-        rc = lib().oracle_forward_streams(ctypes.byref(desc), _ptr(data), _ptr(pix), _ptr(st), data.size, spp, seed,
+        rc = _call("forward", lib().oracle_forward_streams, ctypes.byref(desc), _ptr(data), _ptr(pix), _ptr(st), data.size, spp, seed,
                                           _ptr(dose), ctypes.cast(ctypes.byref(visits), ctypes.c_void_p), nthreads)
         if rc:
             raise ValueError(f"oracle_forward_streams failed ({rc})")
         return dose, visits.value
-    rc = lib().oracle_forward_part(ctypes.byref(desc), _ptr(data), _ptr(pix), data.size, spp, seed, _ptr(dose),
+    rc = _call("forward", lib().oracle_forward_part, ctypes.byref(desc), _ptr(data), _ptr(pix), data.size, spp, seed, _ptr(dose),
                                    ctypes.cast(ctypes.byref(visits), ctypes.c_void_p), nthreads, part)
     if rc:
         raise ValueError(f"oracle_forward failed ({rc})")
@@ -112,12 +131,12 @@ def adjoint(desc, grad_dose, active_pixels=None, n_active=None, spp=1, seed=0, n
     if streams is not None:
         st = np.ascontiguousarray(streams, dtype=np.uint64)
         assert pix is not None and st.size == pix.size == n_active
-        rc = lib().oracle_adjoint_streams(ctypes.byref(desc), _ptr(g), _ptr(pix), _ptr(st), n_active, spp, seed,
+        rc = _call("adjoint", lib().oracle_adjoint_streams, ctypes.byref(desc), _ptr(g), _ptr(pix), _ptr(st), n_active, spp, seed,
                                           _ptr(out), ctypes.cast(ctypes.byref(visits), ctypes.c_void_p), nthreads)
         if rc:
             raise ValueError(f"oracle_adjoint_streams failed ({rc})")
         return out, visits.value
-    rc = lib().oracle_adjoint(ctypes.byref(desc), _ptr(g), _ptr(pix), n_active, spp, seed, _ptr(out),
+    rc = _call("adjoint", lib().oracle_adjoint, ctypes.byref(desc), _ptr(g), _ptr(pix), n_active, spp, seed, _ptr(out),
                               ctypes.cast(ctypes.byref(visits), ctypes.c_void_p), nthreads)
     if rc:
         raise ValueError(f"oracle_adjoint failed ({rc})")

@@ -35,7 +35,7 @@ def test_quadrant_lists_match(oracle, monkeypatch, mk, block):
 @pytest.mark.parametrize("mk", [benchy_index_matched, cylindrical_refraction], ids=["index_matched", "cylindrical"])
 @pytest.mark.parametrize("split", ["1", "3"])
 def test_ray_pairs_match(oracle, monkeypatch, mk, split):
-    """The default ray pairs (tvam_plan.hip adj_pair_lists: ray j with ray j + ceil(n / 2) of each
+    """The opt-in ray pairs (TVAM_ADJ_PAIR=1, tvam_plan.hip adj_pair_lists: ray j with ray j + ceil(n / 2) of each
     angle's crossing rays, one lane) against the plain (angle, column) lists and the oracle, with
     the tile's list split over 1 and 3 workgroups (parts of whole pairs)."""
     N, A = 60, 36

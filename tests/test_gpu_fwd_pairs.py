@@ -1,4 +1,4 @@
-"""The voxel-driven planar forward with voxel pairs (TVAM_FWD_PX=2, the default: a thread owns two
+"""The voxel-driven planar forward with voxel pairs (TVAM_FWD_PX=2, opt-in: a thread owns two
 neighbouring voxel columns of a 32 x 16 tile and reads each candidate slab once for both) against
 the one-voxel variant (TVAM_FWD_PX=1) and the oracle.  Every voxel sums the same candidates in the
 same order (the pair's extra union column misses the voxel: weight 0), so the doses are identical."""

@@ -14,6 +14,4 @@ TVAM_BIN_SORT=1 TVAM_LIB=$PWD/_variants/libtvam_nopf.so timeout -k 10 200 python
 timeout -k 10 200 python bench.py --config 5 --n 800 --steps 2 --warmup 1 --prewarm 0 --cpu-baseline off > "$o/c5.json" 2> "$o/c5.err"
 TVAM_LIB=$PWD/_variants/libtvam_nopf.so timeout -k 10 200 python bench.py --config 5 --n 800 --steps 2 --warmup 1 \
   --prewarm 0 --cpu-baseline off > "$o/c5_nopf.json" 2> "$o/c5_nopf.err"
-timeout -k 10 450 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gpu_scattering.py \
-  tests/test_gpu_parity.py tests/test_gpu_square.py tests/test_gpu_active_set.py tests/test_gpu_fwd_pairs.py \
-  tests/test_gpu_adj_quadrants.py > "$o/tests.log" 2>&1
+timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout-method thread > "$o/tests.log" 2>&1
