@@ -23,9 +23,6 @@
 #define TVAM_WAVES (TVAM_BLOCK / 64)
 #ifndef TVAM_FWD_ACC64
 #define TVAM_FWD_ACC64 0  // 1: forward accumulates 64-bit fixed point (8 B per voxel of LDS)
-#ifndef TVAM_TILE_PF
-#define TVAM_TILE_PF 1  // software-pipelined slot / record loads in the tile kernels' main slot loop
-#endif
 #endif
 #ifndef TVAM_TILE_DIAG
 #define TVAM_TILE_DIAG 0  // 1 (diagnostic builds only): per-wave slot / visit / cycle counters
@@ -637,88 +634,6 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
     };
 #endif
 
-#if TVAM_TILE_PF && !TVAM_TILE_DIAG
-    // Software pipeline over this lane's slots f, f + B, f + 2B (B = the block size): while slot f
-    // marches, the records of slot f + B (ray_f, ray_g, pattern; only when its ray_i says it lies in
-    // this slice) and the ray_i of slot f + 2B (from its slot / row entries) are in flight, so the
-    // chain slot -> row -> ray_i -> records no longer stalls every slot (config 5's jittered
-    // forward spent 45 % of its wave time waiting).
-    {
-        struct Rec {
-            int al, colc;
-            int64_t local, ri, act;
-            int2 ii;
-            float4 ff, gg;
-            float p;
-            bool ok, hit;
-        };
-        const int64_t nloc = (int64_t)tp.n_shard * k.crop_y * k.crop_x;
-        const int slice = kz + k.z0;
-        TvamSlot sl;
-        tvam_slot_init(sl, threadIdx.x, max(per_row, 1));
-        int fa = threadIdx.x;  // the slot of the leading stage
-        // stage A: slot -> ray (slot and row lists), then its ray_i (and idxmap entry)
-        auto stage_a = [&](Rec& R) __attribute__((always_inline)) {
-            R.ok = fa < total;
-            const int smp = spp == 1 ? 0 : sl.ri / nrows;
-            const uint32_t e = R.ok ? slots[sl.rrem] : 0u;
-            const int rowc = R.ok ? rows[rbeg + sl.ri - smp * nrows] : 0;
-            R.al = (int)(e >> 16);
-            R.colc = (int)(e & 0xffffu);
-            R.local = ((int64_t)(k.a0 + R.al) * k.crop_y + rowc) * k.crop_x + R.colc - k.shard_base;
-            R.ri = (int64_t)smp * nloc + R.local;
-            R.ii = R.ok ? tp.ray_i[R.ri] : make_int2(0, -1);
-            R.act = R.local;
-            if (idxmap && R.ok) R.act = idxmap[R.local];
-            fa += TVAM_BLOCK;
-            tvam_slot_next(sl, per_row);
-        };
-        // stage B: the records of a ray in this slice
-        auto stage_b = [&](Rec& R) __attribute__((always_inline)) {
-            R.hit = R.ok && R.ii.y == slice && R.act >= 0;
-            R.ff = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            R.gg = R.ff;
-            R.p = 0.0f;
-            if (R.hit) {
-                R.ff = tp.ray_f[R.ri];
-                if (tp.ray_g) R.gg = tp.ray_g[R.ri];
-                if (MODE == TVAM_MODE_FWD) R.p = pat[R.local];
-            }
-        };
-        Rec P0, P1, P2;
-        stage_a(P0);
-        stage_a(P1);
-        stage_b(P0);
-        for (int f = threadIdx.x; f < total; f += TVAM_BLOCK) {
-            stage_a(P2);
-            stage_b(P1);
-            // slot f (P0)
-            bool go = P0.hit && !(MODE == TVAM_MODE_FWD && k.skip_zero && P0.p == 0.0f);
-            TvamTileRay r;
-            if (go) go = tvam_tile_resume(k, tp, x0, x1, y0, y1, P0.al, P0.ii, P0.ff, P0.gg, r);
-            if (go) {
-                float em = 1.0f;
-                if (MODE == TVAM_MODE_FWD) {
-                    em = P0.p * k.wscale;  // Le * weight (common.py:108-111, volume.py:49)
-                    if (acc_mode != ACC_FLOAT) em *= fscale;
-                    em *= r.weight;  // attenuation of the vial's interfaces (sensor.py:404)
-                }
-                TvamMarchRay m;
-                m.pv = reinterpret_cast<char*>(tile) + r.lidx * ESZ;
-                m.Tx = r.dtx;
-                m.Ty = r.dty;
-                m.rem = r.rem;
-                m.stop = r.rem - 1e-6f;
-                m.e0 = (W2 ? em * k.sig_t : em) * tvam_exp2(k.nsig2 * r.t);
-                const float acc = march(m, r.tsx, r.tsy, r.sx * ESZ, r.sy * ESZ);
-                if (MODE == TVAM_MODE_ADJ)
-                    atomicAdd(&out[P0.act], acc * (k.wscale * r.weight));  // backward_from(Le * em_grad), volume.py:274-276
-            }
-            P0 = P1;
-            P1 = P2;
-        }
-    }
-#else
     TvamSlot sl;
     tvam_slot_init(sl, threadIdx.x, max(per_row, 1));
     for (int f = threadIdx.x; f < total; f += TVAM_BLOCK, tvam_slot_next(sl, per_row)) {
@@ -751,7 +666,6 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
         dg[6] += why == 3;
         dg[7] += why == 0;
         diag_round();
-#endif
     }
 #endif
     for (int f = sbeg + (int)threadIdx.x; f < send; f += TVAM_BLOCK) {  // the slice's stray rays

@@ -1819,14 +1819,16 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
     chunk = std::min(npaths, chunk);
     const int64_t nsl = chunk * slots;
     if (nsl >= ((int64_t)1 << 31)) return hipErrorNotSupported;  // 32-bit slot indices (reweight)
-    // counting-sort bins (default): the record writer counts each workgroup's entries per brick, a
-    // scan of those counts places every entry, and each brick wave orders its entries by class
-    // itself -- no radix sort of (brick, class) keys and, in the adjoint, none of (pixel, partial)
-    // pairs.  The radix-sort path stays for TVAM_BIN_SORT=1, float tiles, 512-thread bricks and
-    // grids whose brick counts exceed the writer's LDS histogram.
+    // counting-sort bins (TVAM_BIN_SORT=0; the radix sort stays the default): the record writer
+    // counts each workgroup's entries per brick, a scan of those counts places every entry, and each
+    // brick wave orders its entries by class itself -- no radix sort of (brick, class) keys and, in
+    // the adjoint, none of (pixel, partial) pairs.  Measured on config 4 (profiles/r04/ab3): the
+    // sorts' 8.4 ms per chunk go, but the fill's scattered 4-byte entry stores take 10.0 ms instead
+    // of 5.6, and the brick marches lose the record-line sharing of the class-sorted fill order
+    // (forward 18.8 -> 23.7 ms, adjoint 16.2 -> 20.1 ms per chunk): 0.2856 -> 0.2853 it/s.
     static const bool bin_sort = [] {
         const char* v = getenv("TVAM_BIN_SORT");
-        return v && atoi(v) != 0;
+        return !(v && atoi(v) == 0);
     }();
     const bool csort = !bin_sort && !s.acc_float && bin_nt == 1024 && nbricks <= 16384 &&
                        nsl <= ((int64_t)1 << TVAM_ENT_SLOT_BITS);
