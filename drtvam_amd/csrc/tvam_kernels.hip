@@ -328,10 +328,6 @@ hipError_t tvam_launch_stray_lists(const TvamConsts& k, const TvamTiles& t, hipS
     return hipGetLastError();
 }
 
-__device__ __forceinline__ bool tvam_tile_resume(const TvamConsts& k, const TvamTiles& tp, int x0, int x1, int y0,
-                                                 int y1, int al, const int2 ii, const float4 ff, const float4 gg,
-                                                 TvamTileRay& r);
-
 // Resume one ray (pre-computed record) at the tile entry, in closed form of
 // the reference march.  Returns false when the ray does not reach the tile.
 __device__ __forceinline__ bool tvam_tile_ray(const TvamConsts& k, const TvamTiles& tp, int kz, int x0, int x1, int y0,
@@ -349,19 +345,10 @@ __device__ __forceinline__ bool tvam_tile_ray(const TvamConsts& k, const TvamTil
     r.why = 2;
     if (ii.y != kz + k.z0) return false;  // misses the grid / vial, or lies in another z-slice
     const float4 ff = tp.ray_f[ri];
-    const float4 gg = tp.ray_g ? tp.ray_g[ri] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-    r.why = 3;
-    return tvam_tile_resume(k, tp, x0, x1, y0, y1, al, ii, ff, gg, r);
-}
-
-// The resumed march state of a ray at the tile entry from its loaded records (ray_i, ray_f and,
-// behind a refracting vial, ray_g); false when the ray does not reach the tile.
-__device__ __forceinline__ bool tvam_tile_resume(const TvamConsts& k, const TvamTiles& tp, int x0, int x1, int y0,
-                                                 int y1, int al, const int2 ii, const float4 ff, const float4 gg,
-                                                 TvamTileRay& r) {
     float4 an;
     r.weight = 1.0f;
     if (tp.ray_g) {  // refracted ray: its own direction (signed step times) and weight
+        const float4 gg = tp.ray_g[ri];
         an = make_float4(fabsf(gg.x), fabsf(gg.y), gg.x < 0.0f ? -1.0f : 1.0f, gg.y < 0.0f ? -1.0f : 1.0f);
         r.weight = gg.z;
     } else {
@@ -375,6 +362,7 @@ __device__ __forceinline__ bool tvam_tile_resume(const TvamConsts& k, const Tvam
     tvam_axis_window(svy, sty, ff.w, an.y, y0, y1, tin1, tout1, nin1, nout1);
     const float tau_e = fmaxf(fmaxf(tin0, tin1), 0.0f);
     const float tau_x = fminf(fminf(tout0, tout1), ff.y);
+    r.why = 3;
     if (!(tau_e < tau_x)) return false;
     const int n0 = tvam_axis_steps(tau_e, ff.z, an.x, nin0, nout0);
     const int n1 = tvam_axis_steps(tau_e, ff.w, an.y, nin1, nout1);
@@ -666,8 +654,8 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
         dg[6] += why == 3;
         dg[7] += why == 0;
         diag_round();
-    }
 #endif
+    }
     for (int f = sbeg + (int)threadIdx.x; f < send; f += TVAM_BLOCK) {  // the slice's stray rays
         int al, rowc, colc, smp;
         tvam_ray_of(k, tp, tp.stray_list[f], al, rowc, colc, smp);
