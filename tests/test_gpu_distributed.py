@@ -30,8 +30,10 @@ def _run(rank, world, steps, shard):
     from drtvam_amd.optimize import TvamProblem
 
     if shard == "angle_scatter":
+        from drtvam_amd import _abi
         cfg = cylindrical_scattering(**CFG, spp=4)
         cfg["shard"] = "angle"
+        cfg["flags"] = _abi.FLAG_NO_ZERO_SKIP  # every path marched: the forward bin cache serves the line search
         prob = TvamProblem(cfg, device=torch.device("cuda", 0), rank=rank, world_size=world)
         assert prob.shard == "angle" and prob.proj.desc.albedo == 0.5
         g = torch.Generator().manual_seed(0)
