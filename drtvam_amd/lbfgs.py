@@ -200,6 +200,10 @@ class FusedLinearLBFGS(LinearLBFGS):
                   'work': torch.empty(_abi_work_doubles(), dtype=torch.float64, device=dev),
                   'dots': torch.empty(5 * (self.m + 1) + 1, dtype=torch.float64, device=dev),
                   'SY': {}, 'YY': {}}
+            # device addresses of the ring's rows (plain integers: a tensor view per row and call
+            # cost microseconds of host time between the dot read and the direction launch)
+            st['S_ptr'] = [st['S'].data_ptr() + j * npad * 4 for j in range(self.m)]
+            st['Y_ptr'] = [st['Y'].data_ptr() + j * npad * 4 for j in range(self.m)]
             self.state[k] = st
         return st
 
@@ -230,13 +234,13 @@ class FusedLinearLBFGS(LinearLBFGS):
                     del st['YY'][key]
             kept = list(st['slots'])
             h = len(kept)
-            S_ptrs = (ctypes.c_void_p * max(h, 1))(*[st['S'][j].data_ptr() for j in kept])
-            Y_ptrs = (ctypes.c_void_p * max(h, 1))(*[st['Y'][j].data_ptr() for j in kept])
+            S_ptrs = (ctypes.c_void_p * max(h, 1))(*[st['S_ptr'][j] for j in kept])
+            Y_ptrs = (ctypes.c_void_p * max(h, 1))(*[st['Y_ptr'][j] for j in kept])
             slot = st['free'][0] if new else None
             _abi.check(lib.tvam_lbfgs_history(
                 n, pf.data_ptr() if new else None, st['p_old'].data_ptr() if new else None, g.data_ptr(),
                 st['g_old'].data_ptr() if new else None, h, S_ptrs, Y_ptrs,
-                st['S'][slot].data_ptr() if new else None, st['Y'][slot].data_ptr() if new else None,
+                st['S_ptr'][slot] if new else None, st['Y_ptr'][slot] if new else None,
                 st['work'].data_ptr(), st['dots'].data_ptr(), stream))
             nd = 5 * (h + 1) + 1 if new else 2 * h + 1
             dots = st['dots'][:nd]
@@ -290,8 +294,8 @@ class FusedLinearLBFGS(LinearLBFGS):
             d = torch.empty_like(g)
             cs_c = (ctypes.c_float * max(H, 1))(*[float(v) for v in cs])
             cy_c = (ctypes.c_float * max(H, 1))(*[float(v) for v in cy])
-            S2 = (ctypes.c_void_p * max(H, 1))(*[st['S'][j].data_ptr() for j in order])
-            Y2 = (ctypes.c_void_p * max(H, 1))(*[st['Y'][j].data_ptr() for j in order])
+            S2 = (ctypes.c_void_p * max(H, 1))(*[st['S_ptr'][j] for j in order])
+            Y2 = (ctypes.c_void_p * max(H, 1))(*[st['Y_ptr'][j] for j in order])
             _abi.check(lib.tvam_lbfgs_direction(n, g.data_ptr(), H, S2, Y2, float(cg), cs_c, cy_c, d.data_ptr(),
                                                 stream))
             search[k] = d
