@@ -138,6 +138,8 @@ EXPORTS = {
                                           _P]),
     "tvam_lbfgs_direction": (ctypes.c_int, [ctypes.c_uint64, _P, ctypes.c_int32, _P, _P, ctypes.c_float, _P, _P, _P,
                                             _P]),
+    "tvam_lbfgs_coef": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P, _P, _P, _P, _P]),
+    "tvam_lbfgs_direction_dev": (ctypes.c_int, [ctypes.c_uint64, _P, ctypes.c_int32, _P, _P, _P, _P, _P]),
     "tvam_axpy_clamp": (ctypes.c_int, [ctypes.c_uint64, _P, ctypes.c_float, _P, ctypes.c_float, _P, _P]),
     "tvam_row_slices": (ctypes.c_int, [ctypes.POINTER(TvamDesc), _P]),
     "tvam_plan_path": (ctypes.c_int, [_P]),

@@ -170,7 +170,11 @@ struct TvamSegBuf {
     // (brick, workgroup) entry counts, [nbricks][gridDim.x]; nullptr: the radix-sort path
     uint32_t* hist;
     int32_t nbricks;
+    uint32_t* bad;                // bin fill: slots whose walk disagreed with the writer's count
 };
+// a radix-path bin entry (segment slot) that marches nothing: padding of a slot whose walk fell
+// short of its count (slots stay below 2^31)
+#define TVAM_ENT_NULL 0x80000000u
 
 // One chunk of forward bins kept in HBM for the next forward of the same (seed, spp): an
 // optimiser iteration renders seed i twice (the forward and the line-search forward, the
@@ -287,5 +291,9 @@ hipError_t tvam_launch_lbfgs_history(uint64_t n, const float* p, const float* p_
 hipError_t tvam_launch_lbfgs_direction(uint64_t n, const float* g, int h, const float* const* S,
                                        const float* const* Y, float cg, const float* cs, const float* cy, float* d,
                                        hipStream_t stream);
+hipError_t tvam_launch_lbfgs_coef(int h, int is_new, int first, const int* order, const double* dots, double* gram,
+                                  float* coef, double* gdz, hipStream_t stream);
+hipError_t tvam_launch_lbfgs_direction_dev(uint64_t n, const float* g, int h, const float* const* S,
+                                           const float* const* Y, const float* coef, float* d, hipStream_t stream);
 hipError_t tvam_launch_axpy_clamp(uint64_t n, const float* p, float alpha, const float* d, float lo, float* out,
                                   hipStream_t stream);

@@ -2095,7 +2095,15 @@ extern "C" int tvam_plan_bin_stats(tvam_plan* p, int64_t* stats) {
     // the chunk scratch: records, brick counts and offsets, sort keys / values, adjoint partials
     stats[6] = b.cap_slots * (TVAM_REC_F4 * (int64_t)sizeof(float4) + 2 * (int64_t)sizeof(uint32_t)) +
                b.cap_entries * (int64_t)(4 * sizeof(uint32_t) + sizeof(float)) + b.cap_bricks * 4 + b.temp_cap();
+    // slots of the last call whose bin-fill walk disagreed with the record writer's closed-form
+    // brick count (sc_brick_count; 0 by construction, checked by the tests)
     stats[7] = 0;
+    if (b.sb.bad && b.st[0] > 0) {
+        uint32_t bad = 0;
+        if (hipMemcpy(&bad, b.sb.bad, sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
+            return fail(TVAM_ERR_HIP, "tvam_plan_bin_stats: reading the count check");
+        stats[7] = bad;
+    }
     return 0;
 }
 
@@ -2147,6 +2155,29 @@ extern "C" int tvam_lbfgs_direction(uint64_t n, const float* g, int32_t h, const
     for (int j = 0; j < h; ++j) ok = ok && S[j] && Y[j] && aligned16(S[j]) && aligned16(Y[j]);
     if (!ok) return fail(TVAM_ERR_INVALID, "tvam_lbfgs_direction: vectors must be 16-byte aligned");
     hipError_t e = tvam_launch_lbfgs_direction(n, g, h, S, Y, cg, cs, cy, d, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "lbfgs direction launch");
+}
+
+extern "C" int tvam_lbfgs_coef(int32_t h, int32_t is_new, int32_t first, const int32_t* order, const double* dots,
+                               double* gram, float* coef, double* gdz, void* stream) {
+    if (h < 0 || h > 8) return fail(TVAM_ERR_INVALID, "tvam_lbfgs_coef: 0 <= h <= 8 pairs");
+    if (!dots || !gram || !coef || !gdz || (h > 0 && !order)) return fail(TVAM_ERR_INVALID, "null argument");
+    if (is_new && h == 0) return fail(TVAM_ERR_INVALID, "tvam_lbfgs_coef: a new pair needs h >= 1");
+    for (int j = 0; j < h; ++j)
+        if (order[j] < 0 || order[j] >= 8) return fail(TVAM_ERR_INVALID, "tvam_lbfgs_coef: ring slots are 0..7");
+    hipError_t e = tvam_launch_lbfgs_coef(h, is_new ? 1 : 0, first ? 1 : 0, order, dots, gram, coef, gdz,
+                                          (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "lbfgs coefficient launch");
+}
+
+extern "C" int tvam_lbfgs_direction_dev(uint64_t n, const float* g, int32_t h, const float* const* S,
+                                        const float* const* Y, const float* coef, float* d, void* stream) {
+    if (!g || !d || !coef || (h > 0 && (!S || !Y))) return fail(TVAM_ERR_INVALID, "null argument");
+    if (h < 0 || h > 8) return fail(TVAM_ERR_INVALID, "tvam_lbfgs_direction_dev: 0 <= h <= 8 pairs");
+    bool ok = aligned16(g) && aligned16(d);
+    for (int j = 0; j < h; ++j) ok = ok && S[j] && Y[j] && aligned16(S[j]) && aligned16(Y[j]);
+    if (!ok) return fail(TVAM_ERR_INVALID, "tvam_lbfgs_direction_dev: vectors must be 16-byte aligned");
+    hipError_t e = tvam_launch_lbfgs_direction_dev(n, g, h, S, Y, coef, d, (hipStream_t)stream);
     return e == hipSuccess ? 0 : hip_fail(e, "lbfgs direction launch");
 }
 

@@ -25,6 +25,8 @@
 #include <algorithm>
 #include <vector>
 
+#include "tvam_bricks.h"
+
 namespace {
 
 __device__ __forceinline__ float sc_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
@@ -122,106 +124,7 @@ __device__ __forceinline__ void sc_phase(const TvamConsts& k, float dx, float dy
 // workgroup marches only its part of every segment crossing it, adding into an
 // LDS tile, and writes the tile once.
 // ---------------------------------------------------------------------------
-struct SegDda {
-    float t_start, tau_end;
-    float dtm0[3], ts[3];  // ts > 0; step sign separate
-    int sv[3], step[3];
-};
-
-__device__ __forceinline__ bool sc_dda_init(const TvamConsts& k, const float o[3], const float d[3], float maxt,
-                                            SegDda& q) {
-    float lo[3], hi[3];
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const float tb0 = (k.bmin[a] - o[a]) / d[a];
-        const float tb1 = (k.bmax[a] - o[a]) / d[a];
-        lo[a] = fminf(tb0, tb1);
-        hi[a] = fmaxf(tb0, tb1);
-    }
-    const float t_start = fmaxf(fmaxf(fmaxf(fmaxf(lo[0], lo[1]), lo[2]), 0.0f), 0.0f);
-    const float t_end = fminf(fminf(fminf(hi[0], hi[1]), hi[2]), maxt);
-    if (!(isfinite(t_start) && isfinite(t_end) && t_start < t_end)) return false;
-    q.t_start = t_start;
-    q.tau_end = t_end - t_start;
-#pragma unroll
-    for (int a = 0; a < 3; ++a) {
-        const float gs = fmaf(d[a], t_start, o[a]);
-        q.step[a] = d[a] > 0.0f ? 1 : -1;
-        int sv = (int)((gs - k.bmin[a]) / k.h[a]);
-        sv = sv < 0 ? 0 : (sv > k.res[a] - 1 ? k.res[a] - 1 : sv);
-        q.sv[a] = sv;
-        float next = k.bmin[a] + (float)(sv + q.step[a]) * k.h[a];
-        if (d[a] < 0.0f) next = next + k.h[a];
-        const bool valid = fabsf(d[a]) > 1e-8f;
-        float dtm = valid ? (next - gs) / d[a] : TVAM_INF;
-        if (dtm < 0.0f) dtm = TVAM_INF;
-        q.dtm0[a] = dtm;
-        q.ts[a] = valid ? (k.h[a] / d[a]) * (float)q.step[a] : TVAM_INF;
-    }
-    return true;
-}
-
-__device__ __forceinline__ int sc_nbr(const TvamConsts& k, int a) {
-    const int B = a == 0 ? TVAM_BX : (a == 1 ? TVAM_BY : TVAM_BZ);
-    return (k.res[a] + B - 1) / B;
-}
-
-// tvam_axis_window's exit time of one axis' window [lo, hi), without branches (the same values)
-__device__ __forceinline__ float sc_axis_tout(int sv, int step, float dtm0, float ts, int lo, int hi) {
-    const int nout = step > 0 ? hi - sv : sv - lo + 1;
-    const float tm = nout > 0 ? fmaf((float)(nout - 1), ts, dtm0) : -TVAM_INF;
-    const float tf = (sv >= lo && sv < hi) ? TVAM_INF : -TVAM_INF;  // an axis that never steps
-    return dtm0 < TVAM_INF ? tm : tf;
-}
-
-// Bricks a segment's DDA visits, in time order: each axis' brick windows
-// partition time exactly (tvam_axis_window on brick bounds), so stepping the
-// axis whose window closes first walks the same sequence the brick kernel
-// resumes from.  F(brick id, relative time the segment enters / leaves the
-// brick) per brick; returns the count.  Branch-free steps (selects; only the
-// stepped axis can leave the grid): the per-axis if / else chain compiled to ~50
-// scalar exec-mask instructions per step on top of ~70 VALU, and the fill kernel
-// and the record writer spend most of their time in this loop.
-template <typename F>
-__device__ __forceinline__ int sc_walk_bricks(const TvamConsts& k, const SegDda& q, F&& f) {
-    const int nb0 = sc_nbr(k, 0), nb1 = sc_nbr(k, 1), nb2 = sc_nbr(k, 2);
-    int b0 = q.sv[0] / TVAM_BX, b1 = q.sv[1] / TVAM_BY, b2 = q.sv[2] / TVAM_BZ;
-    int cnt = 0;
-    float tprev = 0.0f;
-    // each axis' exit time from the current brick; a step changes one axis' brick, so only that
-    // axis' exit is formed again (the same sc_axis_tout values as forming all three every step)
-    float t0 = sc_axis_tout(q.sv[0], q.step[0], q.dtm0[0], q.ts[0], b0 * TVAM_BX, min(b0 * TVAM_BX + TVAM_BX, k.res[0]));
-    float t1 = sc_axis_tout(q.sv[1], q.step[1], q.dtm0[1], q.ts[1], b1 * TVAM_BY, min(b1 * TVAM_BY + TVAM_BY, k.res[1]));
-    float t2 = sc_axis_tout(q.sv[2], q.step[2], q.dtm0[2], q.ts[2], b2 * TVAM_BZ, min(b2 * TVAM_BZ + TVAM_BZ, k.res[2]));
-    for (int guard = 0; guard < 4096; ++guard) {
-        const int bid = (b2 * nb1 + b1) * nb0 + b0;
-        ++cnt;
-        const bool m0 = t0 <= t1 && t0 <= t2;
-        const bool m1 = !m0 && t1 <= t2;
-        const float tm = m0 ? t0 : (m1 ? t1 : t2);
-        f(bid, tprev, fminf(tm, q.tau_end));
-        tprev = tm;
-        if (!(tm < q.tau_end)) break;
-        // the stepped axis: its next brick and exit (selects: one exit formed per step)
-        const int B = m0 ? TVAM_BX : (m1 ? TVAM_BY : TVAM_BZ);
-        const int st = m0 ? q.step[0] : (m1 ? q.step[1] : q.step[2]);
-        const int bn = (m0 ? b0 : (m1 ? b1 : b2)) + st;
-        const int nb = m0 ? nb0 : (m1 ? nb1 : nb2);
-        if ((unsigned)bn >= (unsigned)nb) break;
-        const int sv = m0 ? q.sv[0] : (m1 ? q.sv[1] : q.sv[2]);
-        const float dtm = m0 ? q.dtm0[0] : (m1 ? q.dtm0[1] : q.dtm0[2]);
-        const float ts = m0 ? q.ts[0] : (m1 ? q.ts[1] : q.ts[2]);
-        const int res = m0 ? k.res[0] : (m1 ? k.res[1] : k.res[2]);
-        const float tn = sc_axis_tout(sv, st, dtm, ts, bn * B, min(bn * B + B, res));
-        b0 = m0 ? bn : b0;
-        b1 = m1 ? bn : b1;
-        b2 = (m0 || m1) ? b2 : bn;
-        t0 = m0 ? tn : t0;
-        t1 = m1 ? tn : t1;
-        t2 = (m0 || m1) ? t2 : tn;
-    }
-    return cnt;
-}
+// SegDda, sc_dda_init, sc_walk_bricks, sc_brick_count: tvam_bricks.h
 
 // The visits of a segment inside the voxel box [lo, hi) (a brick), resumed in
 // closed form at the box entry: per axis the step count n at the entry time,
@@ -497,9 +400,12 @@ __global__ __launch_bounds__(256) void tvam_scatter_kernel(TvamConsts k, TvamTil
                                              q.ts[2] * (float)q.step[2]);
                     // .z: the attenuation alone, for the cached forward's rescale (tvam_bin_reweight_kernel)
                     sb.r[TVAM_REC_F4 * slot + 2] = make_float4(__int_as_float(q.sv[0] | (q.sv[1] << 11) | (q.sv[2] << 22)), em * att, att, 0.0f);
-                    sb.m[slot] = (uint32_t)sc_walk_bricks(k, q, [&](int bid, float, float) {
-                        if (hist) atomicAdd(&s_hist[bid], 1u);
-                    });
+                    // the bricks it crosses: counted in closed form (the bin fill does the only walk),
+                    // or walked when the counting sort needs each brick's count
+                    sb.m[slot] = hist ? (uint32_t)sc_walk_bricks(k, q, [&](int bid, float, float) {
+                        atomicAdd(&s_hist[bid], 1u);
+                    })
+                                      : (uint32_t)sc_brick_count(k, q);
                     wmax = fmaxf(wmax, fabsf(em * att));
                 }
             } else if (seg > 0) {
@@ -1353,20 +1259,33 @@ __global__ __launch_bounds__(256) void tvam_bin_fill_kernel(TvamConsts k, TvamSe
             float w;
             sc_unpack(sb.r[TVAM_REC_F4 * s], sb.r[TVAM_REC_F4 * s + 1], sb.r[TVAM_REC_F4 * s + 2], q, w);
             uint32_t o = off[s];
+            const uint32_t oe = o + sb.m[s];  // the record writer's closed-form count (sc_brick_count)
             // visits per unit length: one per voxel-face crossing of each moving axis
             float rate = 0.0f;
 #pragma unroll
             for (int a = 0; a < 3; ++a) rate += q.ts[a] < TVAM_INF ? 1.0f / q.ts[a] : 0.0f;
+            uint32_t klast = 0u;
             sc_walk_bricks(k, q, [&](int bid, float ta, float tb) {
                 // low key bits: a class of the predicted in-brick visit count, so that the lanes of a
                 // wave of the brick kernel march entries of similar length
                 // classes of 4 visits (16 classes) or 8 (8 classes)
                 const int cls = (int)fminf((float)((1 << cbits) - 1),
                                            fmaxf(tb - ta, 0.0f) * rate * (0.015625f * (float)(1 << cbits)));
-                keys[o] = ((uint32_t)bid << cbits) | (uint32_t)cls;
-                vals[o] = (uint32_t)s;
+                klast = ((uint32_t)bid << cbits) | (uint32_t)cls;
+                if (o < oe) {
+                    keys[o] = klast;
+                    vals[o] = (uint32_t)s;
+                }
                 ++o;
             });
+            // the walk and the count disagree (never, by construction: counted for the tests,
+            // tvam_plan_bin_stats): the slot keeps its own range, short ranges padded with null
+            // entries (TVAM_ENT_NULL: marched with weight 0)
+            if (o != oe) atomicAdd(sb.bad, 1u);
+            for (; o < oe; ++o) {
+                keys[o] = klast;
+                vals[o] = (uint32_t)s | TVAM_ENT_NULL;
+            }
         }
         __syncthreads();
     }
@@ -1582,17 +1501,19 @@ __global__ __launch_bounds__(NT) void tvam_bin_march_kernel(TvamConsts k, TvamSe
         float4 a, b, c;
         uint32_t slot;
     };
-    auto load = [&](uint32_t slot, uint32_t e, Ent& r) {
+    auto load = [&](uint32_t v, uint32_t e, Ent& r) {
         (void)e;
+        const uint32_t slot = v & ~TVAM_ENT_NULL;
         r.a = sb.r[TVAM_REC_F4 * slot];
         r.b = sb.r[TVAM_REC_F4 * slot + 1];
         r.c = sb.r[TVAM_REC_F4 * slot + 2];
-        r.slot = slot;
+        r.slot = v;
     };
     auto run = [&](const Ent& r, uint32_t e) {
         SegDda q;
         float w;
         sc_unpack(r.a, r.b, r.c, q, w);
+        if (r.slot & TVAM_ENT_NULL) w = 0.0f;  // a null entry (tvam_bin_fill_kernel's padding)
         const float ws = w * scale;
         float acc = 0.0f;
         // adjoint: each visit's LDS value is consumed one visit later, so its read latency overlaps
@@ -1617,7 +1538,7 @@ __global__ __launch_bounds__(NT) void tvam_bin_march_kernel(TvamConsts k, TvamSe
             sc_brick_march<false>(k, q, lo, hi, visit);
         if (ACC == 2) {
             part[e] = w * fmaf(pc, pv, acc);
-            if (!WS) ppix[e] = r.slot / pslots;
+            if (!WS) ppix[e] = (r.slot & ~TVAM_ENT_NULL) / pslots;
         }
     };
     if constexpr (WS) {
@@ -1765,6 +1686,7 @@ void tvam_bin_scratch_free(TvamBinScratch& s) {
     (void)hipFree(s.sb.r);
     (void)hipFree(s.sb.m);
     (void)hipFree(s.sb.wmax);
+    (void)hipFree(s.sb.bad);
     (void)hipFree(s.off);
     for (int i = 0; i < 2; ++i) {
         (void)hipFree(s.keys[i]);
@@ -1840,10 +1762,13 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
         if ((e = hipMalloc((void**)&s.sb.r, TVAM_REC_F4 * nsl * sizeof(float4))) != hipSuccess ||
             (e = hipMalloc((void**)&s.sb.m, (nsl + 1) * sizeof(uint32_t))) != hipSuccess ||
             (e = hipMalloc((void**)&s.off, (nsl + 1) * sizeof(uint32_t))) != hipSuccess ||
-            (e = hipMalloc((void**)&s.sb.wmax, sizeof(uint32_t))) != hipSuccess)
+            (e = hipMalloc((void**)&s.sb.wmax, sizeof(uint32_t))) != hipSuccess ||
+            (e = hipMalloc((void**)&s.sb.bad, sizeof(uint32_t))) != hipSuccess)
             return e;
         s.cap_slots = nsl;
     }
+    // this call's fill walks that disagreed with the record writer's brick counts (bin stats)
+    if ((e = hipMemsetAsync(s.sb.bad, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
     int64_t capb = s.cap_bricks;
     if ((e = grow(&s.bstart, capb, (int64_t)nbricks + 1)) != hipSuccess) return e;
     s.cap_bricks = (int32_t)capb;

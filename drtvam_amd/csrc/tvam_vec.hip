@@ -219,9 +219,19 @@ struct DirCoef {
     float cs[TVAM_HMAX], cy[TVAM_HMAX];
 };
 
-template <int H>
+// DEV: the coefficients come from device memory (tvam_lbfgs_coef_kernel's output: cg, cs[8], cy[8])
+template <int H, bool DEV = false>
 __global__ __launch_bounds__(TVAM_VB) void tvam_lbfgs_dir_kernel(uint64_t n, const float* __restrict__ g, VecPtrs hv,
-                                                                  DirCoef c, float* __restrict__ d) {
+                                                                  DirCoef c, const float* __restrict__ cdev,
+                                                                  float* __restrict__ d) {
+    if (DEV) {
+        c.cg = cdev[0];
+#pragma unroll
+        for (int j = 0; j < H; ++j) {
+            c.cs[j] = cdev[1 + j];
+            c.cy[j] = cdev[1 + TVAM_HMAX + j];
+        }
+    }
     const uint64_t n4 = n / 4, stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (uint64_t i = tid; i < n4; i += stride) {
@@ -261,7 +271,99 @@ hipError_t tvam_launch_lbfgs_direction(uint64_t n, const float* g, int h, const 
     const dim3 grid(dir_grid()), block(TVAM_VB);
     switch (h) {
 #define TVAM_H(H) \
-    case H: hipLaunchKernelGGL(tvam_lbfgs_dir_kernel<H>, grid, block, 0, stream, n, g, hv, c, d); break;
+    case H: hipLaunchKernelGGL(tvam_lbfgs_dir_kernel<H>, grid, block, 0, stream, n, g, hv, c, nullptr, d); break;
+        TVAM_H(0) TVAM_H(1) TVAM_H(2) TVAM_H(3) TVAM_H(4) TVAM_H(5) TVAM_H(6) TVAM_H(7) TVAM_H(8)
+#undef TVAM_H
+        default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// The two-loop recursion on the device (lbfgs.py:221-243 in Gram form, as the host recursion of
+// drtvam_amd/lbfgs.py evaluated it before): one lane, so the direction pass follows the history
+// pass and its all-reduce on the stream without a host round trip.  gram[] keeps the retained
+// pairs' entries between steps, indexed by ring slot: s_a.y_b at [a][b], y_a.y_b at 64 + [a][b];
+// a new pair's entries come from the history pass's dots.  The same fp64 operations in the same
+// order as that host code (no contraction), so the f32-rounded coefficients -- and the
+// direction -- are bit-identical to it.  coef: cg | cs[8] | cy[8]; gdz: g.d (the Armijo slope).
+struct LbfgsOrder {
+    int slot[TVAM_HMAX];
+};
+
+__global__ void tvam_lbfgs_coef_kernel(int H, int is_new, int first, LbfgsOrder o, const double* __restrict__ dots,
+                                       double* __restrict__ gram, float* __restrict__ coef,
+                                       double* __restrict__ gdz) {
+#pragma clang fp contract(off)
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    double* SY = gram;
+    double* YY = gram + TVAM_HMAX * TVAM_HMAX;
+    const double* Sg = dots;
+    const double* Yg = dots + H;
+    const double gg = dots[(is_new ? 5 * H : 2 * H)];
+    if (is_new) {
+        const int sl = o.slot[H - 1];
+        for (int j = 0; j < H; ++j) {
+            const int sj = o.slot[j];
+            SY[sl * TVAM_HMAX + sj] = dots[2 * H + j];  // s_new . y_j
+            SY[sj * TVAM_HMAX + sl] = dots[3 * H + j];  // s_j . y_new
+            YY[sl * TVAM_HMAX + sj] = dots[4 * H + j];
+            YY[sj * TVAM_HMAX + sl] = dots[4 * H + j];
+        }
+    }
+    double a[TVAM_HMAX], b[TVAM_HMAX];
+    for (int i = H - 1; i >= 0; --i) {
+        const int si = o.slot[i];
+        double s = 0.0;
+        for (int j = i + 1; j < H; ++j) s = s + a[j] * SY[si * TVAM_HMAX + o.slot[j]];
+        a[i] = (Sg[i] - s) / SY[si * TVAM_HMAX + si];
+    }
+    const int last = H > 0 ? o.slot[H - 1] : 0;
+    const double gamma = (first || H == 0) ? 1.0 : SY[last * TVAM_HMAX + last] / YY[last * TVAM_HMAX + last];
+    for (int i = 0; i < H; ++i) {
+        const int yi = o.slot[i];
+        double s1 = 0.0;
+        for (int j = 0; j < H; ++j) s1 = s1 + a[j] * YY[yi * TVAM_HMAX + o.slot[j]];
+        double yz = gamma * (Yg[i] - s1);
+        double s2 = 0.0;
+        for (int j = 0; j < i; ++j) s2 = s2 + (a[j] - b[j]) * SY[o.slot[j] * TVAM_HMAX + yi];
+        yz = yz + s2;
+        b[i] = yz / SY[yi * TVAM_HMAX + yi];
+    }
+    // d = -z, z = gamma (g - sum a_j y_j) + sum (a_j - b_j) s_j
+    const double cg = -gamma;
+    double r = cg * gg, rs = 0.0, ry = 0.0;
+    coef[0] = (float)cg;
+    for (int j = 0; j < H; ++j) {
+        const double cs = -(a[j] - b[j]), cy = gamma * a[j];
+        coef[1 + j] = (float)cs;
+        coef[1 + TVAM_HMAX + j] = (float)cy;
+        rs = rs + cs * Sg[j];
+        ry = ry + cy * Yg[j];
+    }
+    gdz[0] = r + rs + ry;
+}
+
+hipError_t tvam_launch_lbfgs_coef(int h, int is_new, int first, const int* order, const double* dots, double* gram,
+                                  float* coef, double* gdz, hipStream_t stream) {
+    LbfgsOrder o{};
+    for (int j = 0; j < h; ++j) o.slot[j] = order[j];
+    hipLaunchKernelGGL(tvam_lbfgs_coef_kernel, dim3(1), dim3(64), 0, stream, h, is_new, first, o, dots, gram, coef, gdz);
+    return hipGetLastError();
+}
+
+hipError_t tvam_launch_lbfgs_direction_dev(uint64_t n, const float* g, int h, const float* const* S,
+                                           const float* const* Y, const float* coef, float* d, hipStream_t stream) {
+    VecPtrs hv{};
+    for (int j = 0; j < h; ++j) {
+        hv.s[j] = S[j];
+        hv.y[j] = Y[j];
+    }
+    const DirCoef c{};
+    const dim3 grid(dir_grid()), block(TVAM_VB);
+    switch (h) {
+#define TVAM_H(H) \
+    case H: hipLaunchKernelGGL((tvam_lbfgs_dir_kernel<H, true>), grid, block, 0, stream, n, g, hv, c, coef, d); break;
         TVAM_H(0) TVAM_H(1) TVAM_H(2) TVAM_H(3) TVAM_H(4) TVAM_H(5) TVAM_H(6) TVAM_H(7) TVAM_H(8)
 #undef TVAM_H
         default: return hipErrorInvalidValue;

@@ -200,14 +200,15 @@ class Projection:
     def bin_stats(self):
         """Chunking of the last brick-binned call (scattering media): a dict with the chunks of
         paths, those served from / stored into the forward bin cache, the brick entries marched,
-        the paths per chunk and the device bytes of the bin cache and scratch (tvam_plan_bin_stats)."""
+        the paths per chunk, the device bytes of the bin cache and scratch, and the slots whose bin-fill
+        walk disagreed with the record writer's closed-form brick count (0; tvam_plan_bin_stats)."""
         import numpy as np
         v = np.zeros(8, dtype=np.int64)
         with torch.cuda.device(self.device):
             torch.cuda.synchronize(self.device)
             _abi.check(self.lib.tvam_plan_bin_stats(self._plan, v.ctypes.data))
-        return dict(zip(("chunks", "cached", "stored", "entries", "chunk_paths", "cache_bytes", "scratch_bytes"),
-                        (int(x) for x in v)))
+        return dict(zip(("chunks", "cached", "stored", "entries", "chunk_paths", "cache_bytes", "scratch_bytes",
+                         "count_mismatch"), (int(x) for x in v)))
 
     def count_visits(self, spp: int = 1, seed: int = 0) -> int:
         v = ctypes.c_uint64(0)

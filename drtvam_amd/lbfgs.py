@@ -150,11 +150,13 @@ class FusedLinearLBFGS(LinearLBFGS):
     recursion with m pairs and gamma = s.y / y.y, one render of the search
     direction, backtracking Armijo on loss(vol + alpha dvol).  The recursion is
     evaluated on fp64 scalars from the dot products of one fused pass
-    (tvam_lbfgs_history), the direction is one linear combination of g, s_i,
-    y_i (tvam_lbfgs_direction), and the update p + alpha d is fused with the
-    clamp of optimize.py:316-318 when ``clamp_min`` is set (tvam_axpy_clamp).
-    History pairs live in a preallocated ring of m slots.  ``allreduce`` sums
-    the dot vector over angle shards (one collective per step).
+    (tvam_lbfgs_history) by one device lane (tvam_lbfgs_coef, the Gram entries
+    kept on the device by ring slot), the direction is one linear combination
+    of g, s_i, y_i (tvam_lbfgs_direction_dev, coefficients read from the
+    device), and the update p + alpha d is fused with the clamp of
+    optimize.py:316-318 when ``clamp_min`` is set (tvam_axpy_clamp).  History
+    pairs live in a preallocated ring of m slots.  ``allreduce`` sums the dot
+    vector over angle shards (one collective per step).
     """
 
     probe_batch = 4  # Armijo step sizes per loss_steps pass
@@ -199,7 +201,10 @@ class FusedLinearLBFGS(LinearLBFGS):
                   'Y': torch.empty((self.m, npad), dtype=torch.float32, device=dev)[:, :n],
                   'work': torch.empty(_abi_work_doubles(), dtype=torch.float64, device=dev),
                   'dots': torch.empty(5 * (self.m + 1) + 1, dtype=torch.float64, device=dev),
-                  'SY': {}, 'YY': {}}
+                  # Gram entries by ring slot (s_a.y_b, then y_a.y_b; tvam_lbfgs_coef) and the direction's
+                  # coefficients (cg | cs[8] | cy[8])
+                  'gram': torch.zeros(2 * 64, dtype=torch.float64, device=dev),
+                  'coef': torch.zeros(17, dtype=torch.float32, device=dev)}
             # device addresses of the ring's rows (plain integers: a tensor view per row and call
             # cost microseconds of host time between the dot read and the direction launch)
             st['S_ptr'] = [st['S'].data_ptr() + j * npad * 4 for j in range(self.m)]
@@ -209,15 +214,17 @@ class FusedLinearLBFGS(LinearLBFGS):
 
     @torch.no_grad()
     def step(self, vol, loss, loss_dev=None, loss_summed=False):
-        """One L-BFGS step.  loss: the host value, or None with loss_dev (f64 device scalar)
-        read together with the dot vector -- one all-reduce (loss_summed: the ranks' values
-        add up, else every rank holds the same value) and one host sync; returns the loss
-        value (and skips the update when it is exactly 0, the converged case)."""
-        import numpy as np
+        """One L-BFGS step.  loss: the host value, or None with loss_dev (f64 device scalar),
+        all-reduced with the dot vector (loss_summed: the ranks' values add up, else every rank
+        holds the same value) and read with the first Armijo probes; returns the loss value (and
+        skips the update when it is exactly 0, the converged case).  The recursion runs on the
+        device (tvam_lbfgs_coef), so the history pass, the direction and its render follow each
+        other on the stream: one host read per step (the probes), none before the render."""
         from . import _abi
         lib = self._lib()
         search = {}
-        gdz_total = 0.0
+        gdz_dev = []
+        loss_cell = None
         for k, p in self.variables.items():
             st = self._st(k, p)
             pf = _aligned(p.detach().reshape(-1))
@@ -226,12 +233,7 @@ class FusedLinearLBFGS(LinearLBFGS):
             stream = self._stream(pf.device)
             new = st['t'] > 0
             if new and len(st['slots']) == self.m:  # evict the oldest pair (lbfgs.py:214-217)
-                old = st['slots'].pop(0)
-                st['free'].append(old)
-                for key in [kk for kk in st['SY'] if old in kk]:
-                    del st['SY'][key]
-                for key in [kk for kk in st['YY'] if old in kk]:
-                    del st['YY'][key]
+                st['free'].append(st['slots'].pop(0))
             kept = list(st['slots'])
             h = len(kept)
             S_ptrs = (ctypes.c_void_p * max(h, 1))(*[st['S_ptr'][j] for j in kept])
@@ -244,78 +246,71 @@ class FusedLinearLBFGS(LinearLBFGS):
                 st['work'].data_ptr(), st['dots'].data_ptr(), stream))
             nd = 5 * (h + 1) + 1 if new else 2 * h + 1
             dots = st['dots'][:nd]
-            if loss_dev is not None and loss is None:
+            with_loss = loss_dev is not None and loss is None and loss_cell is None
+            if with_loss:
                 dots = torch.cat([dots, loss_dev.reshape(1).to(torch.float64)])
             if self.allreduce is not None:
                 dots = self.allreduce(dots.clone())
-            dv = dots.cpu().numpy().astype(np.float64)
-            if loss_dev is not None and loss is None:
-                lv = float(dv[-1])
-                if self.allreduce is not None and not loss_summed:
-                    import torch.distributed as _d
-                    lv = lv / _d.get_world_size()
-                loss = lv
-                dv = dv[:-1]
-                if loss == 0.0:  # converged (optimize.py:305-307): no update
-                    return loss
+            if with_loss:
+                loss_cell = dots[nd:nd + 1]
             if new:
                 st['free'].pop(0)
                 st['slots'].append(slot)
             order = st['slots']
             H = len(order)
-            Sg, Yg = dv[:H], dv[H:2 * H]
-            if new:
-                sny, sjyn, yny = dv[2 * H:3 * H], dv[3 * H:4 * H], dv[4 * H:5 * H]
-                for j, sj in enumerate(order):
-                    st['SY'][(slot, sj)] = sny[j]   # s_new . y_j
-                    st['SY'][(sj, slot)] = sjyn[j]  # s_j . y_new
-                    st['YY'][(slot, sj)] = st['YY'][(sj, slot)] = yny[j]
-            gg = dv[-1]
             st['p_old'], st['g_old'] = pf, g
             st['t'] += 1
-            # two-loop recursion on the Gram entries (lbfgs.py:221-243)
-            SY, YY = st['SY'], st['YY']
-            a = np.zeros(H)
-            for i in range(H - 1, -1, -1):
-                si = order[i]
-                sq = Sg[i] - sum(a[j] * SY[(si, order[j])] for j in range(i + 1, H))
-                a[i] = sq / SY[(si, si)]
-            gamma = 1.0 if st['t'] == 1 else SY[(order[-1], order[-1])] / YY[(order[-1], order[-1])]
-            b = np.zeros(H)
-            for i in range(H):
-                yi = order[i]
-                yz = gamma * (Yg[i] - sum(a[j] * YY[(yi, order[j])] for j in range(H)))
-                yz += sum((a[j] - b[j]) * SY[(order[j], yi)] for j in range(i))
-                b[i] = yz / SY[(yi, yi)]
-            # d = -z, z = gamma (g - sum a_j y_j) + sum (a_j - b_j) s_j
-            cg = -gamma
-            cy = gamma * a
-            cs = -(a - b)
+            # two-loop recursion on the Gram entries (lbfgs.py:221-243), on the device
+            gdz = torch.empty(1, dtype=torch.float64, device=pf.device)
+            order_c = (ctypes.c_int32 * max(H, 1))(*order)
+            _abi.check(lib.tvam_lbfgs_coef(H, int(new), int(st['t'] == 1), order_c, dots.data_ptr(),
+                                           st['gram'].data_ptr(), st['coef'].data_ptr(), gdz.data_ptr(), stream))
             d = torch.empty_like(g)
-            cs_c = (ctypes.c_float * max(H, 1))(*[float(v) for v in cs])
-            cy_c = (ctypes.c_float * max(H, 1))(*[float(v) for v in cy])
             S2 = (ctypes.c_void_p * max(H, 1))(*[st['S_ptr'][j] for j in order])
             Y2 = (ctypes.c_void_p * max(H, 1))(*[st['Y_ptr'][j] for j in order])
-            _abi.check(lib.tvam_lbfgs_direction(n, g.data_ptr(), H, S2, Y2, float(cg), cs_c, cy_c, d.data_ptr(),
-                                                stream))
+            _abi.check(lib.tvam_lbfgs_direction_dev(n, g.data_ptr(), H, S2, Y2, st['coef'].data_ptr(), d.data_ptr(),
+                                                    stream))
             search[k] = d
-            gdz_total += cg * gg + float(np.dot(cs, Sg)) + float(np.dot(cy, Yg))  # g . d
+            gdz_dev.append(gdz)
+
+        def host_scalars(extra=None):
+            """(loss, g.d summed over the variables[, extra values]) in one host read."""
+            parts = ([loss_cell] if loss_cell is not None else []) + gdz_dev + ([extra] if extra is not None else [])
+            v = torch.cat([t.reshape(-1).to(torch.float64) for t in parts]).cpu().tolist()
+            lv = loss
+            if loss_cell is not None:
+                lv = v.pop(0)
+                if self.allreduce is not None and not loss_summed:
+                    import torch.distributed as _d
+                    lv = lv / _d.get_world_size()
+            gdz_total = 0.0
+            for _ in gdz_dev:
+                gdz_total += v.pop(0)
+            return float(lv), gdz_total, v
 
         c1 = 1e-4
         params = {k: search[k].reshape(self.variables[k].shape) for k in self.variables}
         dvol = self.render_fn(params)
-        loss_v = float(loss)
         key = 'projector.active_data' if 'projector.active_data' in params else next(iter(params))
         alpha = 1.0
         steps = 0
         if self.loss_steps is not None:
             # the same backtracking sequence (alpha = 1, 1/2, ...; first Armijo pass wins), its
             # probes evaluated probe_batch at a time: one loss pass and one host read per batch
+            # (the first read also carries the loss and g.d)
             done = False
+            first = True
             while steps < self.search_it and not done:
                 nb = min(self.probe_batch, self.search_it - steps)
                 alphas = [alpha * 0.5 ** j for j in range(nb)]
-                fv = self.loss_steps(vol, dvol, alphas, params[key]).cpu().tolist()
+                fd = self.loss_steps(vol, dvol, alphas, params[key])
+                if first:
+                    loss_v, gdz_total, fv = host_scalars(fd)
+                    first = False
+                    if loss_cell is not None and loss_v == 0.0:  # converged (optimize.py:305-307): no update
+                        return loss_v
+                else:
+                    fv = fd.cpu().tolist()
                 for a, f_new in zip(alphas, fv):
                     steps += 1
                     alpha = a
@@ -325,6 +320,9 @@ class FusedLinearLBFGS(LinearLBFGS):
                 if not done:
                     alpha *= 0.5
         else:
+            loss_v, gdz_total, _ = host_scalars()
+            if loss_cell is not None and loss_v == 0.0:
+                return loss_v
             for _ in range(self.search_it):
                 steps += 1
                 if self.loss_step is not None:
@@ -344,4 +342,4 @@ class FusedLinearLBFGS(LinearLBFGS):
             _abi.check(lib.tvam_axpy_clamp(pf.numel(), pf.data_ptr(), float(alpha), search[k].data_ptr(), lo,
                                            out.data_ptr(), self._stream(pf.device)))
             self.variables[k] = out.reshape(p.shape).requires_grad_(True)
-        return float(loss)
+        return loss_v

@@ -265,8 +265,9 @@ int tvam_plan_fwd_scale(tvam_plan* plan, float* scale);
    chunks of paths, [1] = chunks served from the forward bin cache (weights rescaled to the
    new pattern, no replay / sort), [2] = chunks stored into the cache, [3] = brick entries
    marched, [4] = paths per chunk (all 0 when the plan's last call binned nothing), [5] = device
-   bytes the forward bin cache holds, [6] = device bytes of the chunk scratch, [7] = 0
-   (reserved).  stats has 8 entries.  (ABI v10) */
+   bytes the forward bin cache holds, [6] = device bytes of the chunk scratch, [7] = slots of the
+   last call whose bin-fill walk disagreed with the record writer's closed-form brick count (0 by
+   construction; host-synchronous read).  stats has 8 entries.  (ABI v10) */
 int tvam_plan_bin_stats(tvam_plan* plan, int64_t* stats);
 
 /* Surface-aware plans: the per-channel voxel volumes the forward divides by and the
@@ -293,6 +294,15 @@ int tvam_plan_path(const tvam_plan* plan);
  *   (h entries each).  work: >= TVAM_LBFGS_WORK_DOUBLES f64 of scratch.
  * tvam_lbfgs_direction: d = cg g + sum_j (cs[j] S[j] + cy[j] Y[j]), h <= 8.
  * tvam_axpy_clamp: out = max(p + alpha d, lo) (out may alias p).
+ * tvam_lbfgs_coef: the two-loop recursion (lbfgs.py:221-243) on the device, in
+ *   Gram form, one lane: order[h] = the ring slots (0..7) of the pairs, oldest
+ *   first, the new pair last when is_new; dots = tvam_lbfgs_history's output
+ *   for those pairs (device, after any all-reduce); gram (device, 128 f64) keeps
+ *   s_a.y_b / y_a.y_b by slot across steps (the new pair's entries are stored
+ *   into it).  Writes coef (device, 17 f32: cg | cs[8] | cy[8]) and gdz (device
+ *   f64: g.d).  first: the first step (gamma = 1).  No host synchronisation.
+ * tvam_lbfgs_direction_dev: tvam_lbfgs_direction with coef read from device
+ *   memory (tvam_lbfgs_coef's output).
  */
 #define TVAM_LBFGS_WORK_DOUBLES (2048 * 64)
 int tvam_lbfgs_history(uint64_t n, const float* p, const float* p_old, const float* g, const float* g_old,
@@ -300,6 +310,10 @@ int tvam_lbfgs_history(uint64_t n, const float* p, const float* p_old, const flo
                        double* work, double* dots, void* hip_stream);
 int tvam_lbfgs_direction(uint64_t n, const float* g, int32_t h, const float* const* S, const float* const* Y,
                          float cg, const float* cs, const float* cy, float* d, void* hip_stream);
+int tvam_lbfgs_coef(int32_t h, int32_t is_new, int32_t first, const int32_t* order, const double* dots,
+                    double* gram, float* coef, double* gdz, void* hip_stream);
+int tvam_lbfgs_direction_dev(uint64_t n, const float* g, int32_t h, const float* const* S, const float* const* Y,
+                             const float* coef, float* d, void* hip_stream);
 int tvam_axpy_clamp(uint64_t n, const float* p, float alpha, const float* d, float lo, float* out,
                     void* hip_stream);
 

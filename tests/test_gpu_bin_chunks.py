@@ -106,7 +106,7 @@ def _check_adjoint(s, g):
 def _default_chunks(s, min_chunks):
     proj = s["proj"]
     st = proj.bin_stats()  # of the fixture's adjoint
-    assert st["chunks"] >= min_chunks, st
+    assert st["chunks"] >= min_chunks and st["count_mismatch"] == 0, st
     _check_adjoint(s, s["g_default"])
     (p1, ref1), (p2, ref2) = s["pats"]
     got = proj.forward(_dense(s, p1), None, SPP4, SEED4).cpu().numpy()[..., 0]
@@ -115,6 +115,7 @@ def _default_chunks(s, min_chunks):
     # chunks are cached while an eighth of the device memory stays free: the rest (if any) run
     # uncached again in the second forward, next to the cached ones
     assert st["chunks"] >= min_chunks and st["cached"] == 0 and st["stored"] >= 1, st
+    assert st["count_mismatch"] == 0, st  # the fill's walks agree with the writer's closed-form counts
     stored = st["stored"]
     e1 = rel_l2(got, ref1)
     got = proj.forward(_dense(s, p2), None, SPP4, SEED4).cpu().numpy()[..., 0]
@@ -145,7 +146,7 @@ def test_config4_shard_many_chunks(shard4, monkeypatch):
     (p1, ref1), (p2, ref2) = s["pats"]
     got = proj.forward(_dense(s, p1), None, SPP4, SEED4).cpu().numpy()[..., 0]
     st = proj.bin_stats()
-    assert st["chunks"] >= 8 and st["cached"] == 0 and st["stored"] >= 1, st
+    assert st["chunks"] >= 8 and st["cached"] == 0 and st["stored"] >= 1 and st["count_mismatch"] == 0, st
     stored = st["stored"]
     e1 = rel_l2(got, ref1)
     got = proj.forward(_dense(s, p2), None, SPP4, SEED4).cpu().numpy()[..., 0]
@@ -155,7 +156,8 @@ def test_config4_shard_many_chunks(shard4, monkeypatch):
     print(f"config 4 shard, {st['chunks']} chunks: forward rel-L2 {e1:.3e}, cached forward {e2:.3e}")
     assert e1 < RTOL and e2 < RTOL
     g = proj.adjoint(torch.as_tensor(s["G"], device=DEV), s["n"], None, SPP4, SEED4).cpu().numpy()[s["sub"]]
-    assert proj.bin_stats()["chunks"] >= 8
+    st = proj.bin_stats()
+    assert st["chunks"] >= 8 and st["count_mismatch"] == 0, st
     _check_adjoint(s, g)
 
 

@@ -111,3 +111,68 @@ def test_batched_probes_same_search():
     assert [t[:2] for t in runs['batched']] == [t[:2] for t in runs['one']]
     np.testing.assert_allclose([t[2] for t in runs['batched']], [t[2] for t in runs['one']], rtol=1e-6)
     assert max(t[1] for t in runs['one']) > FusedLinearLBFGS.probe_batch  # a search spanning batches
+
+
+@pytest.mark.parametrize("is_new", [False, True])
+def test_device_recursion_matches_host(is_new):
+    """tvam_lbfgs_coef (the two-loop recursion on one device lane) against its host restatement
+    (tests/test_lbfgs_fused.py NumpyVecLib.tvam_lbfgs_coef) on the dots of a real history pass over
+    ring slots out of order; the coefficients bit-identical, then tvam_lbfgs_direction_dev against
+    tvam_lbfgs_direction with those coefficients by value (bit-identical directions)."""
+    import ctypes
+    from drtvam_amd import _abi
+    from test_lbfgs_fused import NumpyVecLib
+    lib = _abi.load_library()
+    n, m = 1 << 15, 7
+    gen = torch.Generator().manual_seed(11)
+    P = torch.randn(2, n, generator=gen).cuda()
+    G = torch.randn(2, n, generator=gen).cuda()
+    S = torch.randn(m, n, generator=gen).cuda() * 0.1
+    Y = S * 0.5 + torch.randn(m, n, generator=gen).cuda() * 0.05  # s.y > 0
+    slots = [3, 0, 5, 1]  # retained pairs, oldest first
+    new_slot = 6
+    h = len(slots)
+    ptr = lambda t: ctypes.c_void_p(t.data_ptr())
+    Sp = (ctypes.c_void_p * m)(*[S[j].data_ptr() for j in slots])
+    Yp = (ctypes.c_void_p * m)(*[Y[j].data_ptr() for j in slots])
+    work = torch.empty(_abi.LBFGS_WORK_DOUBLES, dtype=torch.float64, device='cuda')
+    dots = torch.empty(5 * (m + 1) + 1, dtype=torch.float64, device='cuda')
+    gram = torch.zeros(128, dtype=torch.float64)
+    for a in range(m):  # the retained pairs' entries, as earlier steps stored them
+        for b in range(m):
+            gram[a * 8 + b] = float(torch.dot(S[a].double(), Y[b].double()))
+            gram[64 + a * 8 + b] = float(torch.dot(Y[a].double(), Y[b].double()))
+    stream = torch.cuda.current_stream().cuda_stream
+    _abi.check(lib.tvam_lbfgs_history(n, ptr(P[1]) if is_new else None, ptr(P[0]) if is_new else None, ptr(G[1]),
+                                      ptr(G[0]) if is_new else None, h, Sp, Yp,
+                                      ptr(S[new_slot]) if is_new else None, ptr(Y[new_slot]) if is_new else None,
+                                      ptr(work), ptr(dots), stream))
+    order = slots + ([new_slot] if is_new else [])
+    H = len(order)
+    order_c = (ctypes.c_int32 * 8)(*order)
+    gram_d = gram.cuda()
+    coef = torch.zeros(17, dtype=torch.float32, device='cuda')
+    gdz = torch.zeros(1, dtype=torch.float64, device='cuda')
+    _abi.check(lib.tvam_lbfgs_coef(H, int(is_new), 0, order_c, ptr(dots), ptr(gram_d), ptr(coef), ptr(gdz), stream))
+    # host restatement on the same dots and Gram entries
+    dots_h, gram_h = dots.cpu(), gram.clone()
+    coef_h = torch.zeros(17, dtype=torch.float32)
+    gdz_h = torch.zeros(1, dtype=torch.float64)
+    NumpyVecLib().tvam_lbfgs_coef(H, int(is_new), 0, order_c, dots_h.data_ptr(), gram_h.data_ptr(),
+                                  coef_h.data_ptr(), gdz_h.data_ptr(), None)
+    assert torch.equal(coef.cpu(), coef_h)
+    assert torch.equal(gram_d.cpu(), gram_h)
+    np.testing.assert_allclose(gdz.item(), gdz_h.item(), rtol=1e-12)
+    # the direction from device coefficients == the direction from the same values by value
+    S2 = (ctypes.c_void_p * 8)(*[S[j].data_ptr() for j in order])
+    Y2 = (ctypes.c_void_p * 8)(*[Y[j].data_ptr() for j in order])
+    d_dev = torch.empty(n, device='cuda')
+    d_val = torch.empty(n, device='cuda')
+    _abi.check(lib.tvam_lbfgs_direction_dev(n, ptr(G[1]), H, S2, Y2, ptr(coef), ptr(d_dev), stream))
+    c = coef_h.numpy()
+    cs = (ctypes.c_float * 8)(*[float(v) for v in c[1:1 + H]])
+    cy = (ctypes.c_float * 8)(*[float(v) for v in c[9:9 + H]])
+    _abi.check(lib.tvam_lbfgs_direction(n, ptr(G[1]), H, S2, Y2, float(c[0]), cs, cy, ptr(d_val), stream))
+    assert torch.equal(d_dev, d_val)
+    # and g.d of the direction itself
+    np.testing.assert_allclose(gdz.item(), float(torch.dot(G[1].double(), d_dev.double())), rtol=1e-4)

@@ -17,7 +17,7 @@ def _view(ptr, n, ctype=ctypes.c_float):
 
 
 class NumpyVecLib:
-    """Host restatement of tvam_lbfgs_history / _direction / tvam_axpy_clamp (include/tvam.h)."""
+    """Host restatement of tvam_lbfgs_history / _coef / _direction(_dev) / tvam_axpy_clamp (include/tvam.h)."""
 
     def tvam_lbfgs_history(self, n, p, p_old, g, g_old, h, S, Y, s_new, y_new, work, dots, stream):
         gv = _view(g, n).astype(np.float64)
@@ -45,6 +45,41 @@ class NumpyVecLib:
             r += cs[j] * _view(S[j], n) + cy[j] * _view(Y[j], n)
         _view(d, n)[:] = r.astype(np.float32)
         return 0
+
+    def tvam_lbfgs_coef(self, h, is_new, first, order, dots, gram, coef, gdz, stream):
+        """The device recursion (tvam_vec.hip tvam_lbfgs_coef_kernel): Gram entries by ring slot."""
+        o = [order[j] for j in range(h)]
+        nd = 5 * h + 1 if is_new else 2 * h + 1
+        dv = _view(dots, nd, ctypes.c_double).copy()
+        gr = _view(gram, 128, ctypes.c_double)
+        SY, YY = gr[:64].reshape(8, 8), gr[64:].reshape(8, 8)
+        Sg, Yg, gg = dv[:h], dv[h:2 * h], dv[nd - 1]
+        if is_new:
+            sl = o[-1]
+            for j, sj in enumerate(o):
+                SY[sl, sj] = dv[2 * h + j]
+                SY[sj, sl] = dv[3 * h + j]
+                YY[sl, sj] = YY[sj, sl] = dv[4 * h + j]
+        a = np.zeros(h)
+        for i in range(h - 1, -1, -1):
+            a[i] = (Sg[i] - sum(a[j] * SY[o[i], o[j]] for j in range(i + 1, h))) / SY[o[i], o[i]]
+        gamma = 1.0 if (first or h == 0) else SY[o[-1], o[-1]] / YY[o[-1], o[-1]]
+        b = np.zeros(h)
+        for i in range(h):
+            yz = gamma * (Yg[i] - sum(a[j] * YY[o[i], o[j]] for j in range(h)))
+            yz += sum((a[j] - b[j]) * SY[o[j], o[i]] for j in range(i))
+            b[i] = yz / SY[o[i], o[i]]
+        cs, cy = -(a - b), gamma * a
+        c = _view(coef, 17)
+        c[0] = -gamma
+        c[1:1 + h] = cs
+        c[9:9 + h] = cy
+        _view(gdz, 1, ctypes.c_double)[0] = -gamma * gg + float(np.dot(cs, Sg)) + float(np.dot(cy, Yg))
+        return 0
+
+    def tvam_lbfgs_direction_dev(self, n, g, h, S, Y, coef, d, stream):
+        c = _view(coef, 17)
+        return self.tvam_lbfgs_direction(n, g, h, S, Y, float(c[0]), c[1:1 + h], c[9:9 + h], d, stream)
 
     def tvam_axpy_clamp(self, n, p, alpha, d, lo, out, stream):
         _view(out, n)[:] = np.maximum(_view(p, n) + np.float32(alpha) * _view(d, n), np.float32(lo))
