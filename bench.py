@@ -226,6 +226,9 @@ def main():
                     help="compact the active set to the pixels whose rays cross the target (optimize.py:143-163)")
     ap.add_argument("--backend", choices=["nccl", "gloo"], default="nccl",
                     help="torch.distributed backend for WORLD_SIZE > 1 (nccl = RCCL over xGMI; gloo: tests)")
+    ap.add_argument("--slab-bands", type=int, default=None,
+                    help="slab bands of a pipelined planar iteration (TvamProblem.direction_parts; 1: unbanded, the "
+                         "full-film launches the committed counters describe)")
     ap.add_argument("--launch-check", action="store_true",
                     help="start the ranks, form the process group, all-reduce one value and print the world "
                          "line without touching a GPU (tests of the launcher; use with --backend gloo)")
@@ -276,6 +279,8 @@ def main():
     cfg["flags"] = (0 if args.zero_skip else _abi.FLAG_NO_ZERO_SKIP) | (_abi.FLAG_FWD_STATS if args.stats else 0)
     if args.filter_radon:
         cfg["filter_radon"] = True
+    if args.slab_bands is not None:
+        cfg["direction_parts"] = args.slab_bands
     t_setup = time.perf_counter()
     if args.emulate:
         er, ew = (int(v) for v in args.emulate.split("/"))
@@ -449,6 +454,8 @@ def main():
                             if prob.shard == "slab" else
                             f"angle-shard x{world} + {'RCCL' if args.backend == 'nccl' else 'gloo'} dose all-reduce"),
             "zero_skip": bool(args.zero_skip), "prewarm_forwards": n_pre, "tile": prob.proj.desc.tile,
+            # slab bands of the pipelined iteration (TvamProblem._iteration_pipelined; 1: unbanded)
+            "slab_bands": (len(prob.opt.pipeline.parts) if getattr(prob.opt, "pipeline", None) is not None else 1),
             "filter_radon": ({"active": prob.n_filtered, "of": prob.n_global} if prob.active_pixels is not None
                              else None),
             "fwd_ms": fwd_avg * 1e3, "adj_ms": adj_avg * 1e3, "visits_per_pass": visits, "rays_per_pass": rays,

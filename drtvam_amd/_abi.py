@@ -140,9 +140,16 @@ EXPORTS = {
                                             _P]),
     "tvam_lbfgs_coef": (ctypes.c_int, [ctypes.c_int32, ctypes.c_int32, ctypes.c_int32, _P, _P, _P, _P, _P, _P]),
     "tvam_lbfgs_direction_dev": (ctypes.c_int, [ctypes.c_uint64, _P, ctypes.c_int32, _P, _P, _P, _P, _P]),
+    "tvam_lbfgs_history_rows": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _P,
+                                               _P, _P, _P, ctypes.c_int32, _P, _P, _P, _P, _P, _P, _P]),
+    "tvam_lbfgs_direction_rows": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _P,
+                                                 ctypes.c_int32, _P, _P, _P, _P, _P]),
     "tvam_axpy_clamp": (ctypes.c_int, [ctypes.c_uint64, _P, ctypes.c_float, _P, ctypes.c_float, _P, _P]),
     "tvam_row_slices": (ctypes.c_int, [ctypes.POINTER(TvamDesc), _P]),
     "tvam_plan_path": (ctypes.c_int, [_P]),
+    "tvam_adjoint_slices": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
+                                           ctypes.c_int32, _P, _P]),
+    "tvam_plan_adj_chunk": (ctypes.c_int, [_P]),
     "tvam_plan_set_active": (ctypes.c_int, [_P, ctypes.c_int64, ctypes.c_int64]),
     "tvam_compute_volume": (ctypes.c_int, [_P, ctypes.c_uint32, _P, _P]),
     "tvam_plan_set_volumes": (ctypes.c_int, [_P, _P]),

@@ -108,6 +108,7 @@ struct TvamPlanar {
     // own direction, and the candidate columns of a voxel come from a per-(16x16 tile, angle)
     // bilinear model of the chord index u(x, y) (tvam_refr_model_kernel)
     int32_t fwd_zc0, fwd_nzc;  // voxel-driven forward launch: slice chunks [zc0, zc0 + nzc) of Z slices (0, 0: all)
+    int32_t adj_zc0, adj_nzc;  // planar adjoint launch: slice chunks [zc0, zc0 + nzc) of Z slices (0, 0: all)
     int32_t fwd_refr;
     float4* vox2;              // [ns][crop_x] {1/d.x, 1/d.y, axis flags (int bits), interface weight}
     float4* chord;             // plan creation only: [ns][crop_x] {o2.x, o2.y, d2.x, d2.y} of the medium chord
@@ -287,13 +288,17 @@ hipError_t tvam_launch_loss_threshold(const float* dose, const float* ddose, flo
 // Fused L-BFGS vector kernels (tvam_vec.hip).
 hipError_t tvam_launch_lbfgs_history(uint64_t n, const float* p, const float* p_old, const float* g,
                                      const float* g_old, int h, const float* const* S, const float* const* Y,
-                                     float* s_new, float* y_new, double* work, double* dots, hipStream_t stream);
+                                     float* s_new, float* y_new, double* work, double* dots, hipStream_t stream,
+                                     uint64_t nseg = 0, uint64_t seg_len = 0, uint64_t seg_stride = 0,
+                                     uint64_t seg_off = 0);
 hipError_t tvam_launch_lbfgs_direction(uint64_t n, const float* g, int h, const float* const* S,
                                        const float* const* Y, float cg, const float* cs, const float* cy, float* d,
                                        hipStream_t stream);
 hipError_t tvam_launch_lbfgs_coef(int h, int is_new, int first, const int* order, const double* dots, double* gram,
                                   float* coef, double* gdz, hipStream_t stream);
 hipError_t tvam_launch_lbfgs_direction_dev(uint64_t n, const float* g, int h, const float* const* S,
-                                           const float* const* Y, const float* coef, float* d, hipStream_t stream);
+                                           const float* const* Y, const float* coef, float* d, hipStream_t stream,
+                                           uint64_t nseg = 0, uint64_t seg_len = 0, uint64_t seg_stride = 0,
+                                           uint64_t seg_off = 0);
 hipError_t tvam_launch_axpy_clamp(uint64_t n, const float* p, float alpha, const float* d, float lo, float* out,
                                   hipStream_t stream);

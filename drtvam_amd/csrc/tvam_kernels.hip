@@ -156,8 +156,8 @@ __device__ __forceinline__ void tvam_slot_init(TvamSlot& sl, int f, int per_row)
     sl.rrem = f - sl.ri * per_row;
 }
 
-__device__ __forceinline__ void tvam_slot_next(TvamSlot& sl, int per_row) {
-    sl.rrem += TVAM_BLOCK;
+__device__ __forceinline__ void tvam_slot_next(TvamSlot& sl, int per_row, int step = TVAM_BLOCK) {
+    sl.rrem += step;
     while (sl.rrem >= per_row) {
         sl.rrem -= per_row;
         ++sl.ri;
@@ -622,16 +622,25 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
     };
 #endif
 
+    // Adjoint with spp a power of two <= 64: the sample FASTEST instead (lanes of a group of spp march
+    // one pixel's jittered rays), so the group sums its partials with shuffles and adds them to the
+    // pixel's gradient with one global atomic per tile instead of spp (config 4: 16 atomics on one
+    // address per workgroup).  The gather reads the same LDS words on the group's near-identical
+    // paths: broadcasts, not conflicts (the forward's LDS atomics are why it keeps the sample slowest).
+    const bool sfast = MODE == TVAM_MODE_ADJ && spp > 1 && spp <= 64 && (spp & (spp - 1)) == 0;
+    const int sshift = sfast ? __ffs(spp) - 1 : 0;
     TvamSlot sl;
-    tvam_slot_init(sl, threadIdx.x, max(per_row, 1));
-    for (int f = threadIdx.x; f < total; f += TVAM_BLOCK, tvam_slot_next(sl, per_row)) {
-        const int smp = spp == 1 ? 0 : sl.ri / nrows;
+    tvam_slot_init(sl, (int)threadIdx.x >> sshift, max(per_row, 1));
+    for (int f = threadIdx.x; f < total; f += TVAM_BLOCK, tvam_slot_next(sl, per_row, TVAM_BLOCK >> sshift)) {
+        const int smp = sfast ? (f & (spp - 1)) : (spp == 1 ? 0 : sl.ri / nrows);
+        const int rowi = sfast ? sl.ri : sl.ri - smp * nrows;
         const uint32_t e = slots[sl.rrem];
         TvamTileRay r;
         float e0;
         int why = 5;
+        float part = 0.0f;  // sfast: this lane's weighted partial
         if (tvam_tile_slot<MODE, W2>(k, tp, pat, idxmap, kz, x0, x1, y0, y1, (int)(e >> 16), (int)(e & 0xffffu),
-                                     rows[rbeg + sl.ri - smp * nrows], smp, acc_mode, fscale, r, e0, why)) {
+                                     rows[rbeg + rowi], smp, acc_mode, fscale, r, e0, why)) {
             TvamMarchRay m;
             m.pv = reinterpret_cast<char*>(tile) + r.lidx * ESZ;
             m.Tx = r.dtx;
@@ -640,8 +649,22 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
             m.stop = r.rem - 1e-6f;
             m.e0 = e0;
             const float acc = march(m, r.tsx, r.tsy, r.sx * ESZ, r.sy * ESZ);
-            if (MODE == TVAM_MODE_ADJ)
-                atomicAdd(&out[r.act], acc * (k.wscale * r.weight));  // backward_from(Le * em_grad), volume.py:274-276
+            if (MODE == TVAM_MODE_ADJ) {
+                const float v = acc * (k.wscale * r.weight);  // backward_from(Le * em_grad), volume.py:274-276
+                if (sfast)
+                    part = v;
+                else
+                    atomicAdd(&out[r.act], v);
+            }
+        }
+        if (MODE == TVAM_MODE_ADJ && sfast) {  // the pixel's spp partials (groups are whole: total = first * spp)
+            for (int o = 1; o < spp; o <<= 1) part += __shfl_xor(part, o, 64);
+            if (smp == 0 && part != 0.0f) {
+                const int64_t local = ((int64_t)(k.a0 + (int)(e >> 16)) * k.crop_y + rows[rbeg + rowi]) * k.crop_x +
+                                      (int)(e & 0xffffu) - k.shard_base;
+                const int64_t act = idxmap ? (int64_t)idxmap[local] : local;
+                if (act >= 0) atomicAdd(&out[act], part);
+            }
         }
 #if TVAM_TILE_DIAG
         if ((int)blockIdx.x == tvam_tile_dsel[0] && (int)blockIdx.y == tvam_tile_dsel[1] && f < (1 << 21))

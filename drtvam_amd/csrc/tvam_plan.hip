@@ -1873,6 +1873,42 @@ static int forward_impl(tvam_plan* p, const float* active_data, const uint32_t* 
     return 0;
 }
 
+// The planar adjoint of film slices [z_begin, z_end) alone, into the DMD rows [row_begin, row_end) of every
+// angle of grad_active (dense crop order; those rows zeroed first, the others untouched): the caller's rows
+// are exactly the rows whose rays lie in those slices (tvam_row_slices), so the rows hold their whole
+// gradient.  Regular-sampling planar plans of a dense set; slices on the adjoint's Z-slice chunks.
+extern "C" int tvam_adjoint_slices(tvam_plan* p, const float* grad_dose, uint64_t n_active, int32_t z_begin,
+                                   int32_t z_end, int32_t row_begin, int32_t row_end, float* grad_active,
+                                   void* stream_) {
+    if (!p || !grad_dose || !grad_active) return fail(TVAM_ERR_INVALID, "null argument");
+    if (!p->planar || p->general || p->surface || p->desc.albedo != 0.0f || p->empty)
+        return fail(TVAM_ERR_UNSUPPORTED, "tvam_adjoint_slices: planar plans only");
+    hipStream_t stream = (hipStream_t)stream_;
+    TvamConsts k;
+    uint32_t spp = 1;
+    int rc = call_setup(p, n_active, nullptr, spp, k);
+    if (rc) return rc;
+    const int Z = p->planar_az, nz = k.nz;
+    const int64_t R = k.crop_y, C = k.crop_x, A = (int64_t)p->tiles.n_shard;
+    if (z_begin < 0 || z_end > nz || z_begin >= z_end || z_begin % Z != 0 || (z_end % Z != 0 && z_end != nz) ||
+        row_begin < 0 || row_end > R || row_begin > row_end || (int64_t)n_active != A * R * C)
+        return fail(TVAM_ERR_INVALID, "tvam_adjoint_slices: slices on the adjoint's chunks, rows in the crop, dense set");
+    hipError_t e = hipSuccess;
+    if (row_end > row_begin)
+        e = hipMemset2DAsync(grad_active + (size_t)row_begin * C, (size_t)(R * C) * sizeof(float), 0,
+                             (size_t)(row_end - row_begin) * C * sizeof(float), (size_t)A, stream);
+    if (e != hipSuccess) return hip_fail(e, "hipMemset2DAsync");
+    TvamPlanar pl = p->pl;
+    pl.adj_zc0 = z_begin / Z;
+    pl.adj_nzc = (z_end - z_begin + Z - 1) / Z;
+    e = tvam_launch_adj_planar(k, pl, p->tiles, Z, nullptr, grad_dose, grad_active, stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "planar adjoint launch");
+}
+
+extern "C" int tvam_plan_adj_chunk(const tvam_plan* p) {
+    return p && p->planar && !p->general && !p->surface && p->desc.albedo == 0.0f ? p->planar_az : 0;
+}
+
 extern "C" int tvam_adjoint(tvam_plan* p, const float* grad_dose, const uint32_t* active_pixels, uint64_t n_active,
                             uint32_t spp, uint32_t seed, float* grad_active, void* stream_) {
     if (!p || !grad_dose || (!grad_active && n_active)) return fail(TVAM_ERR_INVALID, "null argument");
@@ -2146,6 +2182,25 @@ extern "C" int tvam_lbfgs_history(uint64_t n, const float* p, const float* p_old
     return e == hipSuccess ? 0 : hip_fail(e, "lbfgs history launch");
 }
 
+extern "C" int tvam_lbfgs_history_rows(uint64_t nseg, uint64_t seg_len, uint64_t seg_stride, uint64_t seg_off,
+                                       const float* p, const float* p_old, const float* g, const float* g_old,
+                                       int32_t h, const float* const* S, const float* const* Y, float* s_new,
+                                       float* y_new, double* work, double* dots, void* stream) {
+    if (!g || !work || !dots || (h > 0 && (!S || !Y))) return fail(TVAM_ERR_INVALID, "null argument");
+    if (h < 0 || h > 7) return fail(TVAM_ERR_INVALID, "tvam_lbfgs_history_rows: 0 <= h <= 7 retained pairs");
+    if (p_old && (!p || !g_old || !s_new || !y_new)) return fail(TVAM_ERR_INVALID, "null argument");
+    if (nseg == 0 || seg_len == 0 || seg_len % 4 || seg_stride % 4 || seg_off % 4 || seg_len > seg_stride ||
+        seg_len / 4 > 0xffffffffull)
+        return fail(TVAM_ERR_INVALID, "tvam_lbfgs_history_rows: segments of a multiple of 4 entries, 4-aligned");
+    bool ok = aligned16(g) && (!p_old || (aligned16(p) && aligned16(p_old) && aligned16(g_old) &&
+                                          aligned16(s_new) && aligned16(y_new)));
+    for (int j = 0; j < h; ++j) ok = ok && S[j] && Y[j] && aligned16(S[j]) && aligned16(Y[j]);
+    if (!ok) return fail(TVAM_ERR_INVALID, "tvam_lbfgs_history_rows: vectors must be 16-byte aligned");
+    hipError_t e = tvam_launch_lbfgs_history(0, p, p_old, g, g_old, h, S, Y, s_new, y_new, work, dots,
+                                             (hipStream_t)stream, nseg, seg_len, seg_stride, seg_off);
+    return e == hipSuccess ? 0 : hip_fail(e, "lbfgs history launch");
+}
+
 extern "C" int tvam_lbfgs_direction(uint64_t n, const float* g, int32_t h, const float* const* S,
                                     const float* const* Y, float cg, const float* cs, const float* cy, float* d,
                                     void* stream) {
@@ -2178,6 +2233,22 @@ extern "C" int tvam_lbfgs_direction_dev(uint64_t n, const float* g, int32_t h, c
     for (int j = 0; j < h; ++j) ok = ok && S[j] && Y[j] && aligned16(S[j]) && aligned16(Y[j]);
     if (!ok) return fail(TVAM_ERR_INVALID, "tvam_lbfgs_direction_dev: vectors must be 16-byte aligned");
     hipError_t e = tvam_launch_lbfgs_direction_dev(n, g, h, S, Y, coef, d, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "lbfgs direction launch");
+}
+
+extern "C" int tvam_lbfgs_direction_rows(uint64_t nseg, uint64_t seg_len, uint64_t seg_stride, uint64_t seg_off,
+                                         const float* g, int32_t h, const float* const* S, const float* const* Y,
+                                         const float* coef, float* d, void* stream) {
+    if (!g || !d || !coef || (h > 0 && (!S || !Y))) return fail(TVAM_ERR_INVALID, "null argument");
+    if (h < 0 || h > 8) return fail(TVAM_ERR_INVALID, "tvam_lbfgs_direction_rows: 0 <= h <= 8 pairs");
+    if (nseg == 0 || seg_len == 0 || seg_len % 4 || seg_stride % 4 || seg_off % 4 || seg_len > seg_stride ||
+        seg_len / 4 > 0xffffffffull)
+        return fail(TVAM_ERR_INVALID, "tvam_lbfgs_direction_rows: segments of a multiple of 4 entries, 4-aligned");
+    bool ok = aligned16(g) && aligned16(d);
+    for (int j = 0; j < h; ++j) ok = ok && S[j] && Y[j] && aligned16(S[j]) && aligned16(Y[j]);
+    if (!ok) return fail(TVAM_ERR_INVALID, "tvam_lbfgs_direction_rows: vectors must be 16-byte aligned");
+    hipError_t e = tvam_launch_lbfgs_direction_dev(0, g, h, S, Y, coef, d, (hipStream_t)stream, nseg, seg_len,
+                                                   seg_stride, seg_off);
     return e == hipSuccess ? 0 : hip_fail(e, "lbfgs direction launch");
 }
 

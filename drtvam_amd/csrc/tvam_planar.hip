@@ -908,7 +908,7 @@ __global__ __launch_bounds__(NT) void tvam_adj_planar_kernel(TvamConsts k, TvamP
                                                                   float* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tsx = tp.tsx, tsy = tp.tsy;
-    const int tile_id = blockIdx.x, z0 = blockIdx.y * Z;
+    const int tile_id = blockIdx.x, z0 = ((int)blockIdx.y + pl.adj_zc0) * Z;
     // this workgroup's part of the tile's ray list: with quadrant lists (pl.adj_quad) blockIdx.z =
     // split part * 4 + step quadrant, parts of whole waves, and the row pitch of the quadrant;
     // else a part of the one (angle, column)-ordered list (a thin slab has few slice chunks:
@@ -1106,8 +1106,9 @@ size_t tvam_planar_adj_lds(const TvamPlanar& pl, const TvamTiles& t, int Z) {
 
 hipError_t tvam_launch_adj_planar(const TvamConsts& k, const TvamPlanar& pl, const TvamTiles& t, int Z,
                                   const int32_t* idxmap, const float* gin, float* out, hipStream_t stream) {
-    dim3 grid((unsigned)(t.ntx * t.nty), (unsigned)((k.nz + Z - 1) / Z),
-              (unsigned)std::max(pl.adj_split, 1) * (pl.adj_quad ? 4u : 1u));
+    // slice chunks of this launch: [adj_zc0, adj_zc0 + adj_nzc) (tvam_adjoint_slices), else all
+    const int nzc = pl.adj_nzc > 0 ? pl.adj_nzc : (k.nz + Z - 1) / Z;
+    dim3 grid((unsigned)(t.ntx * t.nty), (unsigned)nzc, (unsigned)std::max(pl.adj_split, 1) * (pl.adj_quad ? 4u : 1u));
     const size_t lds = tvam_planar_adj_lds(pl, t, Z);
     const bool pf = pl.adj_prefetch != 0;
     // 512-thread workgroups (adj_nt): the LDS tile (28 KB at 40 x 40 x 4) admits 5

@@ -20,6 +20,7 @@
 #define TVAM_VGRID_MAX 2048  // most blocks of the reduction kernels (work[] holds grid * ndots doubles)
 #define TVAM_HMAX 8
 
+#include <algorithm>
 #include <cstdlib>
 
 // launch geometry knobs (read once): blocks of the history pass and of the direction pass
@@ -41,6 +42,19 @@ struct VecPtrs {
     const float* s[TVAM_HMAX];
     const float* y[TVAM_HMAX];
 };
+
+// Segments of the vectors (tvam_lbfgs_history_rows / tvam_lbfgs_direction_rows): float4 index t
+// of the part -> segment t / len4, float4 off4 + segment * stride4 + t % len4 (a band of DMD rows
+// of every angle)
+struct VecSeg {
+    uint32_t len4;
+    uint64_t stride4, off4;
+};
+
+__device__ __forceinline__ uint64_t vec_seg_index(const VecSeg& sg, uint64_t t) {
+    const uint64_t a = t / sg.len4;
+    return sg.off4 + a * sg.stride4 + (t - a * sg.len4);
+}
 
 __device__ __forceinline__ double warp_sum(double v) {
     for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
@@ -79,14 +93,14 @@ struct HistLayout {
     static constexpr int ND = (NEW ? 5 * HT : 2 * HT) + 1;
 };
 
-template <int H, bool NEW>
+template <int H, bool NEW, bool SEG = false>
 __global__ __launch_bounds__(TVAM_VB) void tvam_lbfgs_hist_kernel(uint64_t n, const float* __restrict__ p,
                                                                    const float* __restrict__ p_old,
                                                                    const float* __restrict__ g,
                                                                    const float* __restrict__ g_old, VecPtrs hv,
                                                                    float* __restrict__ s_new,
                                                                    float* __restrict__ y_new,
-                                                                   double* __restrict__ work) {
+                                                                   double* __restrict__ work, VecSeg sg) {
     using L = HistLayout<H, NEW>;
     constexpr int HT = L::HT, ND = L::ND;
     double acc[ND];
@@ -113,7 +127,8 @@ __global__ __launch_bounds__(TVAM_VB) void tvam_lbfgs_hist_kernel(uint64_t n, co
 
     const uint64_t n4 = n / 4, stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (uint64_t i = tid; i < n4; i += stride) {
+    for (uint64_t t = tid; t < n4; t += stride) {
+        const uint64_t i = SEG ? vec_seg_index(sg, t) : t;
         const float4 g4 = reinterpret_cast<const float4*>(g)[i];
         float4 p4 = make_float4(0, 0, 0, 0), po4 = p4, go4 = p4;
         if (NEW) {
@@ -142,7 +157,7 @@ __global__ __launch_bounds__(TVAM_VB) void tvam_lbfgs_hist_kernel(uint64_t n, co
             reinterpret_cast<float4*>(y_new)[i] = yn4;
         }
     }
-    for (uint64_t i = 4 * n4 + tid; i < n; i += stride) {  // tail
+    for (uint64_t i = 4 * n4 + tid; !SEG && i < n; i += stride) {  // tail
         float sv[TVAM_HMAX], yv[TVAM_HMAX];
 #pragma unroll
         for (int j = 0; j < H; ++j) {
@@ -179,10 +194,16 @@ __global__ __launch_bounds__(TVAM_VB) void tvam_partials_kernel(int nd, int nblo
 template <int H, bool NEW>
 static hipError_t launch_hist(uint64_t n, const float* p, const float* p_old, const float* g, const float* g_old,
                               const VecPtrs& hv, float* s_new, float* y_new, double* work, double* dots,
-                              hipStream_t stream) {
-    const int nb = hist_grid();
-    hipLaunchKernelGGL((tvam_lbfgs_hist_kernel<H, NEW>), dim3(nb), dim3(TVAM_VB), 0, stream, n, p, p_old, g,
-                       g_old, hv, s_new, y_new, work);
+                              hipStream_t stream, const VecSeg& sg) {
+    // a band of rows (sg.len4 > 0): fewer blocks, the rest of the GPU keeps the neighbouring band's adjoint
+    const int nb = sg.len4 ? std::max(64, (int)std::min<uint64_t>(hist_grid(), (n / 4 + TVAM_VB - 1) / TVAM_VB))
+                           : hist_grid();
+    if (sg.len4)
+        hipLaunchKernelGGL((tvam_lbfgs_hist_kernel<H, NEW, true>), dim3(nb), dim3(TVAM_VB), 0, stream, n, p, p_old, g,
+                           g_old, hv, s_new, y_new, work, sg);
+    else
+        hipLaunchKernelGGL((tvam_lbfgs_hist_kernel<H, NEW>), dim3(nb), dim3(TVAM_VB), 0, stream, n, p, p_old, g,
+                           g_old, hv, s_new, y_new, work, sg);
     hipLaunchKernelGGL(tvam_partials_kernel, dim3(HistLayout<H, NEW>::ND), dim3(TVAM_VB), 0, stream,
                        HistLayout<H, NEW>::ND, nb, work, dots);
     return hipGetLastError();
@@ -191,10 +212,10 @@ static hipError_t launch_hist(uint64_t n, const float* p, const float* p_old, co
 template <bool NEW>
 static hipError_t dispatch_hist(int h, uint64_t n, const float* p, const float* p_old, const float* g,
                                 const float* g_old, const VecPtrs& hv, float* s_new, float* y_new, double* work,
-                                double* dots, hipStream_t stream) {
+                                double* dots, hipStream_t stream, const VecSeg& sg) {
     switch (h) {
 #define TVAM_H(H) \
-    case H: return launch_hist<H, NEW>(n, p, p_old, g, g_old, hv, s_new, y_new, work, dots, stream);
+    case H: return launch_hist<H, NEW>(n, p, p_old, g, g_old, hv, s_new, y_new, work, dots, stream, sg);
         TVAM_H(0) TVAM_H(1) TVAM_H(2) TVAM_H(3) TVAM_H(4) TVAM_H(5) TVAM_H(6) TVAM_H(7)
 #undef TVAM_H
         default: return hipErrorInvalidValue;
@@ -203,14 +224,22 @@ static hipError_t dispatch_hist(int h, uint64_t n, const float* p, const float* 
 
 hipError_t tvam_launch_lbfgs_history(uint64_t n, const float* p, const float* p_old, const float* g,
                                      const float* g_old, int h, const float* const* S, const float* const* Y,
-                                     float* s_new, float* y_new, double* work, double* dots, hipStream_t stream) {
+                                     float* s_new, float* y_new, double* work, double* dots, hipStream_t stream,
+                                     uint64_t nseg, uint64_t seg_len, uint64_t seg_stride, uint64_t seg_off) {
     VecPtrs hv{};
     for (int j = 0; j < h; ++j) {
         hv.s[j] = S[j];
         hv.y[j] = Y[j];
     }
-    if (p_old) return dispatch_hist<true>(h, n, p, p_old, g, g_old, hv, s_new, y_new, work, dots, stream);
-    return dispatch_hist<false>(h, n, p, p_old, g, g_old, hv, s_new, y_new, work, dots, stream);
+    VecSeg sg{};
+    if (nseg > 0) {
+        n = nseg * seg_len;
+        sg.len4 = (uint32_t)(seg_len / 4);
+        sg.stride4 = seg_stride / 4;
+        sg.off4 = seg_off / 4;
+    }
+    if (p_old) return dispatch_hist<true>(h, n, p, p_old, g, g_old, hv, s_new, y_new, work, dots, stream, sg);
+    return dispatch_hist<false>(h, n, p, p_old, g, g_old, hv, s_new, y_new, work, dots, stream, sg);
 }
 
 // ---------------------------------------------------------------------------
@@ -219,11 +248,12 @@ struct DirCoef {
     float cs[TVAM_HMAX], cy[TVAM_HMAX];
 };
 
-// DEV: the coefficients come from device memory (tvam_lbfgs_coef_kernel's output: cg, cs[8], cy[8])
-template <int H, bool DEV = false>
+// DEV: the coefficients come from device memory (tvam_lbfgs_coef_kernel's output: cg, cs[8], cy[8]).
+// SEG: n = the part's elements (segments x length), indices through VecSeg.
+template <int H, bool DEV = false, bool SEG = false>
 __global__ __launch_bounds__(TVAM_VB) void tvam_lbfgs_dir_kernel(uint64_t n, const float* __restrict__ g, VecPtrs hv,
                                                                   DirCoef c, const float* __restrict__ cdev,
-                                                                  float* __restrict__ d) {
+                                                                  float* __restrict__ d, VecSeg sg = VecSeg{}) {
     if (DEV) {
         c.cg = cdev[0];
 #pragma unroll
@@ -234,7 +264,8 @@ __global__ __launch_bounds__(TVAM_VB) void tvam_lbfgs_dir_kernel(uint64_t n, con
     }
     const uint64_t n4 = n / 4, stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (uint64_t i = tid; i < n4; i += stride) {
+    for (uint64_t t = tid; t < n4; t += stride) {
+        const uint64_t i = SEG ? vec_seg_index(sg, t) : t;
         const float4 g4 = reinterpret_cast<const float4*>(g)[i];
         float4 r = make_float4(c.cg * g4.x, c.cg * g4.y, c.cg * g4.z, c.cg * g4.w);
 #pragma unroll
@@ -248,7 +279,7 @@ __global__ __launch_bounds__(TVAM_VB) void tvam_lbfgs_dir_kernel(uint64_t n, con
         }
         reinterpret_cast<float4*>(d)[i] = r;
     }
-    for (uint64_t i = 4 * n4 + tid; i < n; i += stride) {
+    for (uint64_t i = 4 * n4 + tid; !SEG && i < n; i += stride) {
         float r = c.cg * g[i];
 #pragma unroll
         for (int j = 0; j < H; ++j) r = fmaf(c.cs[j], hv.s[j][i], fmaf(c.cy[j], hv.y[j][i], r));
@@ -271,7 +302,7 @@ hipError_t tvam_launch_lbfgs_direction(uint64_t n, const float* g, int h, const 
     const dim3 grid(dir_grid()), block(TVAM_VB);
     switch (h) {
 #define TVAM_H(H) \
-    case H: hipLaunchKernelGGL(tvam_lbfgs_dir_kernel<H>, grid, block, 0, stream, n, g, hv, c, nullptr, d); break;
+    case H: hipLaunchKernelGGL(tvam_lbfgs_dir_kernel<H>, grid, block, 0, stream, n, g, hv, c, nullptr, d, VecSeg{}); break;
         TVAM_H(0) TVAM_H(1) TVAM_H(2) TVAM_H(3) TVAM_H(4) TVAM_H(5) TVAM_H(6) TVAM_H(7) TVAM_H(8)
 #undef TVAM_H
         default: return hipErrorInvalidValue;
@@ -353,17 +384,36 @@ hipError_t tvam_launch_lbfgs_coef(int h, int is_new, int first, const int* order
 }
 
 hipError_t tvam_launch_lbfgs_direction_dev(uint64_t n, const float* g, int h, const float* const* S,
-                                           const float* const* Y, const float* coef, float* d, hipStream_t stream) {
+                                           const float* const* Y, const float* coef, float* d, hipStream_t stream,
+                                           uint64_t nseg, uint64_t seg_len, uint64_t seg_stride, uint64_t seg_off) {
     VecPtrs hv{};
     for (int j = 0; j < h; ++j) {
         hv.s[j] = S[j];
         hv.y[j] = Y[j];
     }
     const DirCoef c{};
-    const dim3 grid(dir_grid()), block(TVAM_VB);
+    VecSeg sg{};
+    const bool seg = nseg > 0;
+    if (seg) {
+        n = nseg * seg_len;
+        sg.len4 = (uint32_t)(seg_len / 4);
+        sg.stride4 = seg_stride / 4;
+        sg.off4 = seg_off / 4;
+    }
+    // a part of the vector: fewer blocks, so that the rest of the GPU keeps the forward of the
+    // previous part (tvam_lbfgs_direction_rows)
+    const int nb = seg ? std::max(64, (int)std::min<uint64_t>(dir_grid(), (n / 4 + TVAM_VB - 1) / TVAM_VB)) : dir_grid();
+    const dim3 grid(nb), block(TVAM_VB);
     switch (h) {
-#define TVAM_H(H) \
-    case H: hipLaunchKernelGGL((tvam_lbfgs_dir_kernel<H, true>), grid, block, 0, stream, n, g, hv, c, coef, d); break;
+#define TVAM_H(H)                                                                                                 \
+    case H:                                                                                                       \
+        if (seg)                                                                                                  \
+            hipLaunchKernelGGL((tvam_lbfgs_dir_kernel<H, true, true>), grid, block, 0, stream, n, g, hv, c, coef, \
+                               d, sg);                                                                            \
+        else                                                                                                      \
+            hipLaunchKernelGGL((tvam_lbfgs_dir_kernel<H, true>), grid, block, 0, stream, n, g, hv, c, coef, d,    \
+                               sg);                                                                               \
+        break;
         TVAM_H(0) TVAM_H(1) TVAM_H(2) TVAM_H(3) TVAM_H(4) TVAM_H(5) TVAM_H(6) TVAM_H(7) TVAM_H(8)
 #undef TVAM_H
         default: return hipErrorInvalidValue;

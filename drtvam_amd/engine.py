@@ -131,6 +131,25 @@ class Projection:
                 n_active, spp, seed & 0xFFFFFFFF, out.data_ptr(), _stream_ptr(self.device)))
         return out
 
+    def adjoint_slices(self, grad_dose: torch.Tensor, n_active: int, z_begin: int, z_end: int, row_begin: int,
+                       row_end: int, out: torch.Tensor) -> torch.Tensor:
+        """The planar adjoint of film slices [z_begin, z_end) into DMD rows [row_begin, row_end) of every
+        angle of out (dense set; those rows zeroed first, the rest untouched; tvam_adjoint_slices)."""
+        self._check_tensor(grad_dose, torch.float32, "grad_dose")
+        self._check_tensor(out, torch.float32, "grad_active")
+        if out.numel() != n_active:
+            raise ValueError("adjoint_slices: out must hold n_active entries")
+        with torch.cuda.device(self.device):
+            _abi.check(self.lib.tvam_adjoint_slices(self._plan, grad_dose.data_ptr(), n_active, int(z_begin),
+                                                    int(z_end), int(row_begin), int(row_end), out.data_ptr(),
+                                                    _stream_ptr(self.device)))
+        return out
+
+    @property
+    def adj_chunk(self) -> int:
+        """Slice granularity of adjoint_slices (0: not available)."""
+        return int(self.lib.tvam_plan_adj_chunk(self._plan))
+
     def set_active(self, active_base: int, active_total: int) -> None:
         """Position of this plan's first active entry in the whole active set and that set's
         size (desc.active_base / active_total): sampler streams and the ray weight of later

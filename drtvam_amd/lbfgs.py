@@ -138,6 +138,31 @@ class LinearLBFGS:
             self.variables[k] = newp.requires_grad_(True)
 
 
+class DirectionPipeline:
+    """Slab bands of one optimiser iteration for FusedLinearLBFGS.step_pipelined (one variable,
+    dense patterns [nseg][rows][cols], CUDA): parts = [(row0, row1, z0, z1), ...] tile the rows and
+    the film, and film slices [z0, z1) depend only on pattern rows [row0, row1) (planar rays: a
+    row's rays stay in its slice).  The projections of a band run on the current stream, the
+    HBM-bound vector passes of the neighbouring band on ``side``, so each hides under the other.
+    Callbacks: render_part(x, z0, z1, out) (forward of slices [z0, z1) into out), probe_part(vol,
+    dvol, alphas, z0, z1) (f64 device losses of that slab, no all-reduce), reduce(t) (sum over
+    slab ranks, or identity), new_dose()."""
+
+    def __init__(self, nseg, rows, cols, parts, render_part, probe_part, reduce, new_dose):
+        self.nseg, self.rows, self.cols = nseg, rows, cols
+        self.parts = parts
+        self.render_part = render_part
+        self.probe_part = probe_part
+        self.reduce = reduce
+        self.new_dose = new_dose
+        self._side = None
+
+    def side(self, dev):
+        if self._side is None:
+            self._side = torch.cuda.Stream(dev)
+        return self._side
+
+
 def _aligned(v):
     """v itself when 16-byte aligned and contiguous (the fused kernels read float4), else an aligned copy."""
     return v if v.is_contiguous() and v.data_ptr() % 16 == 0 else v.clone(memory_format=torch.contiguous_format)
@@ -162,12 +187,15 @@ class FusedLinearLBFGS(LinearLBFGS):
     probe_batch = 4  # Armijo step sizes per loss_steps pass
 
     def __init__(self, lr=1.0, m=5, params=None, render_fn=None, loss_fn=None, search_it=20, loss_step=None,
-                 allreduce=None, clamp_min=None, loss_steps=None):
+                 allreduce=None, clamp_min=None, loss_steps=None, pipeline=None):
         if m > 7:
             raise ValueError("FusedLinearLBFGS keeps at most 7 history pairs")
         self.allreduce = allreduce
         self.clamp_min = clamp_min
         self.loss_steps = loss_steps  # (vol, dvol, alphas, patterns) -> losses: the probes batched
+        # DirectionPipeline (one variable, CUDA): the direction formed in row bands, each band's
+        # forward (its film slices) rendered on a second stream while the next band is formed
+        self.pipeline = pipeline
         self.state = {}
         super().__init__(lr=lr, m=m, params=params, render_fn=render_fn, loss_fn=loss_fn, search_it=search_it,
                          loss_step=loss_step)
@@ -185,6 +213,140 @@ class FusedLinearLBFGS(LinearLBFGS):
     def _lib(self):
         from . import _abi
         return _abi.load_library()
+
+    @torch.no_grad()
+    def step_pipelined(self, vol, loss_parts, loss_summed, grad_ready):
+        """step() for one variable under self.pipeline, the gradient arriving in row bands: grad_ready
+        = [(event, row0, row1), ...], band k of p.grad final once event k (recorded on the current
+        stream) has fired; loss_parts = the slab bands' loss values (f64 device scalars, on the side
+        stream).  The same algorithm and kernels as step(), banded: the history pass of band k
+        (tvam_lbfgs_history_rows, its dots summed over the bands in band order) runs on the side
+        stream while band k + 1's adjoint runs; after the recursion, direction band k
+        (tvam_lbfgs_direction_rows) precedes band k's render on the current stream, and band k's
+        first four Armijo probes follow it on the side stream.  One host read (loss, g.d, probes)."""
+        from . import _abi
+        lib = self._lib()
+        pipe = self.pipeline
+        (k, p), = self.variables.items()
+        st = self._st(k, p)
+        pf = _aligned(p.detach().reshape(-1))
+        g = p.grad.detach().reshape(-1)
+        if not (g.is_contiguous() and g.data_ptr() % 16 == 0):
+            raise ValueError("step_pipelined: the gradient must be a 16-byte aligned contiguous tensor")
+        dev = pf.device
+        main = torch.cuda.current_stream(dev)
+        side = pipe.side(dev)
+        ss = side.cuda_stream
+        R, C = pipe.rows, pipe.cols
+        new = st['t'] > 0
+        if new and len(st['slots']) == self.m:  # evict the oldest pair (lbfgs.py:214-217)
+            st['free'].append(st['slots'].pop(0))
+        kept = list(st['slots'])
+        h = len(kept)
+        S_ptrs = (ctypes.c_void_p * max(h, 1))(*[st['S_ptr'][j] for j in kept])
+        Y_ptrs = (ctypes.c_void_p * max(h, 1))(*[st['Y_ptr'][j] for j in kept])
+        slot = st['free'][0] if new else None
+        nd = 5 * (h + 1) + 1 if new else 2 * h + 1
+        K = len(pipe.parts)
+        if st.get('dots_b') is None or st['dots_b'].shape[0] != K:
+            st['dots_b'] = torch.zeros((K, 64), dtype=torch.float64, device=dev)
+        dots_b = st['dots_b']
+        with torch.cuda.stream(side):
+            dots_b.zero_()
+            for ev, r0, r1 in grad_ready:
+                side.wait_event(ev)
+                b = [i for i, q in enumerate(pipe.parts) if q[0] == r0][0]
+                if r1 > r0:
+                    _abi.check(lib.tvam_lbfgs_history_rows(
+                        pipe.nseg, (r1 - r0) * C, R * C, r0 * C, pf.data_ptr() if new else None,
+                        st['p_old'].data_ptr() if new else None, g.data_ptr(), st['g_old'].data_ptr() if new else None,
+                        h, S_ptrs, Y_ptrs, st['S_ptr'][slot] if new else None, st['Y_ptr'][slot] if new else None,
+                        st['work'].data_ptr(), dots_b[b].data_ptr(), ss))
+            dots = dots_b[:, :nd].sum(0)
+            with_loss = loss_parts is not None
+            if with_loss:
+                lsum = loss_parts[0]
+                for v in loss_parts[1:]:
+                    lsum = lsum + v
+                dots = torch.cat([dots, lsum.reshape(1).to(torch.float64)])
+            if self.allreduce is not None:
+                dots = self.allreduce(dots.clone())
+            loss_cell = dots[nd:nd + 1] if with_loss else None
+            if new:
+                st['free'].pop(0)
+                st['slots'].append(slot)
+            order = st['slots']
+            H = len(order)
+            st['p_old'], st['g_old'] = pf, g
+            st['t'] += 1
+            gdz = torch.empty(1, dtype=torch.float64, device=dev)
+            order_c = (ctypes.c_int32 * max(H, 1))(*order)
+            _abi.check(lib.tvam_lbfgs_coef(H, int(new), int(st['t'] == 1), order_c, dots.data_ptr(),
+                                           st['gram'].data_ptr(), st['coef'].data_ptr(), gdz.data_ptr(), ss))
+            d = torch.empty_like(g)
+            d.record_stream(main)  # rendered and stepped along on the current stream
+            S2 = (ctypes.c_void_p * max(H, 1))(*[st['S_ptr'][j] for j in order])
+            Y2 = (ctypes.c_void_p * max(H, 1))(*[st['Y_ptr'][j] for j in order])
+        dvol = pipe.new_dose()
+        alphas = [0.5 ** j for j in range(min(self.probe_batch, self.search_it))]
+        probes = []
+        for r0, r1, z0, z1 in pipe.parts:
+            with torch.cuda.stream(side):
+                if r1 > r0:
+                    _abi.check(lib.tvam_lbfgs_direction_rows(pipe.nseg, (r1 - r0) * C, R * C, r0 * C, g.data_ptr(), H,
+                                                             S2, Y2, st['coef'].data_ptr(), d.data_ptr(), ss))
+                ev = torch.cuda.Event()
+                ev.record(side)
+            main.wait_event(ev)
+            if z1 > z0:
+                pipe.render_part(d, z0, z1, dvol)
+                evf = torch.cuda.Event()
+                evf.record(main)
+                side.wait_event(evf)
+                with torch.cuda.stream(side):
+                    probes.append(pipe.probe_part(vol, dvol, alphas, z0, z1))
+        with torch.cuda.stream(side):
+            pv = probes[0]
+            for v in probes[1:]:
+                pv = pv + v
+            pv = pipe.reduce(pv)
+            parts = ([loss_cell] if loss_cell is not None else []) + [gdz, pv]
+            hv = torch.cat([t.reshape(-1).to(torch.float64) for t in parts]).cpu().tolist()
+        main.wait_stream(side)
+        loss_v = hv.pop(0) if loss_cell is not None else None
+        if loss_cell is not None and self.allreduce is not None and not loss_summed:
+            import torch.distributed as _d
+            loss_v = loss_v / _d.get_world_size()
+        gdz_v = hv.pop(0)
+        if loss_cell is not None and loss_v == 0.0:  # converged (optimize.py:305-307): no update
+            return loss_v
+        # the backtracking sequence of step(): the first batch came with the read
+        c1 = 1e-4
+        params = {k: d.reshape(p.shape)}
+        alpha, steps, done, fv = 1.0, 0, False, hv
+        while True:
+            for a, f_new in zip(alphas, fv):
+                steps += 1
+                alpha = a
+                if f_new <= loss_v + c1 * a * gdz_v:
+                    done = True
+                    break
+            if done:
+                break
+            alpha *= 0.5
+            if steps >= self.search_it:
+                break
+            nb = min(self.probe_batch, self.search_it - steps)
+            alphas = [alpha * 0.5 ** j for j in range(nb)]
+            fv = self.loss_steps(vol, dvol, alphas, params[k]).cpu().tolist()
+        self.last_alpha = alpha
+        self.last_search_steps = steps
+        lo = -float('inf') if self.clamp_min is None else float(self.clamp_min)
+        out = torch.empty_like(pf)
+        _abi.check(lib.tvam_axpy_clamp(pf.numel(), pf.data_ptr(), float(alpha), d.data_ptr(), lo, out.data_ptr(),
+                                       self._stream(dev)))
+        self.variables[k] = out.reshape(p.shape).requires_grad_(True)
+        return loss_v
 
     @staticmethod
     def _stream(dev):

@@ -20,6 +20,7 @@ from __future__ import annotations
 
 import argparse
 import ctypes
+import math
 import gc
 import json
 import os
@@ -32,7 +33,7 @@ import torch
 from .engine import derive_seed_grad
 from .geometry import geometries
 from .integrators import VolumeIntegrator
-from .lbfgs import FusedLinearLBFGS, LinearLBFGS
+from .lbfgs import DirectionPipeline, FusedLinearLBFGS, LinearLBFGS
 from .loss import losses, ThresholdedLoss
 from .scene import load_dict
 from .utils import discretize, analytic_target, mesh_bbox, target_transform, save_vol, save_img
@@ -157,6 +158,11 @@ class ShardedLoop:
     def dose_buffer(self):
         raise NotImplementedError
 
+    def direction_pipeline(self):
+        """A DirectionPipeline (the iteration in slab bands, projections of one band overlapping the
+        vector passes of the next), or None."""
+        return None
+
     def forward(self, x, seed):
         """This rank's partial dose, all-reduced over the angle shards.  When the
         projection can render slice ranges, range k's all-reduce (async: RCCL runs it on its own
@@ -232,7 +238,8 @@ class ShardedLoop:
             # three fused HIP passes per step and one all-reduce of the dot vector
             opt = FusedLinearLBFGS(render_fn=render_fn, loss_fn=None, loss_step=self.loss_step,
                                    allreduce=self.allreduce_ if self.dist is not None else None, clamp_min=0.0,
-                                   loss_steps=self.loss_steps if self.fused else None)
+                                   loss_steps=self.loss_steps if self.fused else None,
+                                   pipeline=self.direction_pipeline())
         else:
             opt = LinearLBFGS(render_fn=render_fn, loss_fn=None, dot=self.dot, loss_step=self.loss_step)
         opt[key] = self.x0
@@ -248,6 +255,10 @@ class ShardedLoop:
         key = 'projector.active_data'
         self._seed = i
         x = self.opt[key]
+        if isinstance(self.opt, FusedLinearLBFGS) and self.fused and self.opt.pipeline is not None:
+            loss_v = self._iteration_pipelined(x, i)
+            self.loss_hist.append(loss_v)
+            return loss_v
         vol = self.forward(x, i)
         if isinstance(self.opt, FusedLinearLBFGS) and self.fused:
             # The loss value is read with the L-BFGS dot vector: the adjoint and the history
@@ -277,6 +288,42 @@ class ShardedLoop:
             with torch.no_grad():
                 self.opt[key] = torch.clamp_min(self.opt[key].detach(), 0.0)
         return loss_v
+
+    def _iteration_pipelined(self, x, i):
+        """iteration() in slab bands (DirectionPipeline): the forward of band k on the current
+        stream, its loss + dL/dvol on the side stream (hidden under band k + 1's forward), then band
+        k's adjoint (tvam_adjoint_slices, its pattern rows) on the current stream while the side
+        stream runs band k - 1's history pass; FusedLinearLBFGS.step_pipelined continues the same
+        way through the direction, its render and the probes.  The same kernels per element as the
+        unbanded iteration; the loss, the dots and the probes are summed over the bands."""
+        pipe = self.opt.pipeline
+        dev = self.device
+        main = torch.cuda.current_stream(dev)
+        side = pipe.side(dev)
+        xd = x.detach().contiguous()
+        vol = self.dose_buffer()
+        loss_evs, loss_parts = [], []
+        for r0, r1, z0, z1 in pipe.parts:
+            pipe.render_part(xd, z0, z1, vol)
+            ev = torch.cuda.Event()
+            ev.record(main)
+            side.wait_event(ev)
+            with torch.cuda.stream(side):
+                loss_parts.append(self.loss_fn.fused_value_grad(vol[z0:z1], self.target[z0:z1], None,
+                                                                self.grad_vol[z0:z1], count=self.n_vox))
+                evl = torch.cuda.Event()
+                evl.record(side)
+            loss_evs.append(evl)
+        g = torch.empty(self.n_local, dtype=torch.float32, device=dev)
+        grad_ready = []
+        for (r0, r1, z0, z1), evl in zip(pipe.parts, loss_evs):
+            main.wait_event(evl)
+            self.proj.adjoint_slices(self.grad_vol, self.n_local, z0, z1, r0, r1, g)
+            ev = torch.cuda.Event()
+            ev.record(main)
+            grad_ready.append((ev, r0, r1))
+        x.grad = g
+        return self.opt.step_pipelined(vol, loss_parts, self.dose_sharded, grad_ready)
 
     def patterns_local(self):
         return self.opt['projector.active_data'].detach() if self.opt is not None else self.x0
@@ -531,6 +578,77 @@ class TvamProblem(ShardedLoop):
 
     def dose_buffer(self):
         return torch.empty(self.proj.film_shape, dtype=torch.float32, device=self.device)
+
+    # slab bands of a pipelined iteration (config 'direction_parts'; <= 1: off).  Off by default:
+    # measured slower on config 2 (3 bands: 83.1 / 83.7 -> 75.8 / 75.9 it/s, profiles/r04/ab12/), the
+    # banded launches' tails and the concurrent vector passes cost the LDS-bound projections more
+    # than the passes they hide
+    direction_parts = 1
+
+    def direction_pipeline(self):
+        """Row bands of the dense local patterns whose film slices tile the plan's film in ranges
+        of whole 64-slice blocks (the slice-binned forward bins per 64 slices): band k's render
+        needs only band k's rows.  Planar voxel-driven forwards of a dense set on one rank or one
+        z-slab (the angle-sharded forward all-reduces its ranges instead)."""
+        from . import _abi
+        n = int(self.config.get('direction_parts', self.direction_parts))
+        zc, za = self.proj.fwd_chunk, self.proj.adj_chunk
+        nz = self.proj.film_shape[0]
+        if (n <= 1 or zc <= 1 or za <= 0 or self.active_pixels is not None or not self.fused or
+                getattr(self.loss_fn, 'weight_sparsity', 0) or (self.dist is not None and not self.dose_sharded)
+                or self.device.type != 'cuda' or self.proj.film_shape[-1] != 1):
+            return None
+        desc = self.proj.desc
+        m = np.empty(desc.crop_y, dtype=np.int32)
+        _abi.check(_abi.load_library().tvam_row_slices(ctypes.byref(desc), m.ctypes.data_as(ctypes.c_void_p)))
+        m = np.where(m >= 0, m - int(desc.slab_begin), -1)  # this plan's film slices
+        blk = 64 * zc // math.gcd(64, zc)  # slice ranges: whole forward / adjoint chunks and 64-slice bin blocks
+        blk = blk * za // math.gcd(blk, za)
+        # n ranges of about nz / n slices, boundaries on whole blocks
+        cuts = sorted({min(nz, max(0, int(round(j * nz / n / blk)) * blk)) for j in range(1, n)} - {0, nz})
+        edges = [0] + cuts + [nz]
+        ranges = list(zip(edges[:-1], edges[1:]))
+        if len(ranges) <= 1:
+            return None
+        R, C = int(desc.crop_y), int(desc.crop_x)
+        if C % 4:
+            return None
+        # each range's rows: one contiguous band (DMD rows run top-down or bottom-up through the
+        # slices); the bands, extended over rows whose rays miss the grid, tile the rows
+        mapped = m >= 0
+        bands = []
+        for z0, z1 in ranges:
+            rows = np.nonzero(mapped & (m >= z0) & (m < z1))[0]
+            if not rows.size:
+                return None
+            lo, hi = int(rows.min()), int(rows.max()) + 1
+            if not np.all(((m[lo:hi] >= z0) & (m[lo:hi] < z1)) | ~mapped[lo:hi]):
+                return None
+            bands.append((lo, hi))
+        order = sorted(range(len(ranges)), key=lambda q: bands[q][0])
+        ext = {}
+        for j, q in enumerate(order):
+            lo = 0 if j == 0 else bands[q][0]
+            hi = R if j == len(order) - 1 else bands[order[j + 1]][0]
+            if hi < bands[q][1]:
+                return None  # overlapping bands
+            ext[q] = (lo, hi)
+        parts = [(ext[q][0], ext[q][1], z0, z1) for q, (z0, z1) in enumerate(ranges)]
+        nseg = self.n_local // (R * C)
+        if nseg * R * C != self.n_local:
+            return None
+
+        def render_part(d, z0, z1, out):
+            self.proj.forward_slices(d, None, self.spp, self._seed, z0, z1, out)
+
+        def probe_part(vol, dvol, alphas, z0, z1):
+            return self.loss_fn.fused_values(vol[z0:z1], self.target[z0:z1], None, dvol[z0:z1], alphas,
+                                             count=self.n_vox)
+
+        def reduce(t):
+            return self.allreduce_(t) if self.dose_sharded else t
+
+        return DirectionPipeline(nseg, R, C, parts, render_part, probe_part, reduce, self.dose_buffer)
 
     def adjoint_local(self, grad_vol, seed):
         return self.proj.adjoint(grad_vol, self.n_local, self.active_pixels, self.spp_grad, derive_seed_grad(seed))

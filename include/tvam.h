@@ -303,17 +303,32 @@ int tvam_plan_path(const tvam_plan* plan);
  *   f64: g.d).  first: the first step (gamma = 1).  No host synchronisation.
  * tvam_lbfgs_direction_dev: tvam_lbfgs_direction with coef read from device
  *   memory (tvam_lbfgs_coef's output).
+ * tvam_lbfgs_history_rows: tvam_lbfgs_history over the entries seg_off +
+ *   a * seg_stride + [0, seg_len) of every a < nseg only (a band of DMD rows):
+ *   s_new / y_new of those entries and the band's dots (summed over the bands by
+ *   the caller, in band order, before tvam_lbfgs_coef).
+ * tvam_lbfgs_direction_rows: the same for the entries seg_off + a * seg_stride +
+ *   [0, seg_len) of every a < nseg only (a band of DMD rows of every angle:
+ *   seg_stride = rows * columns), so that the forward of one band's slices can
+ *   start while the next band's direction is formed (all multiples of 4).
  */
 #define TVAM_LBFGS_WORK_DOUBLES (2048 * 64)
 int tvam_lbfgs_history(uint64_t n, const float* p, const float* p_old, const float* g, const float* g_old,
                        int32_t h, const float* const* S, const float* const* Y, float* s_new, float* y_new,
                        double* work, double* dots, void* hip_stream);
+int tvam_lbfgs_history_rows(uint64_t nseg, uint64_t seg_len, uint64_t seg_stride, uint64_t seg_off, const float* p,
+                            const float* p_old, const float* g, const float* g_old, int32_t h, const float* const* S,
+                            const float* const* Y, float* s_new, float* y_new, double* work, double* dots,
+                            void* hip_stream);
 int tvam_lbfgs_direction(uint64_t n, const float* g, int32_t h, const float* const* S, const float* const* Y,
                          float cg, const float* cs, const float* cy, float* d, void* hip_stream);
 int tvam_lbfgs_coef(int32_t h, int32_t is_new, int32_t first, const int32_t* order, const double* dots,
                     double* gram, float* coef, double* gdz, void* hip_stream);
 int tvam_lbfgs_direction_dev(uint64_t n, const float* g, int32_t h, const float* const* S, const float* const* Y,
                              const float* coef, float* d, void* hip_stream);
+int tvam_lbfgs_direction_rows(uint64_t nseg, uint64_t seg_len, uint64_t seg_stride, uint64_t seg_off,
+                              const float* g, int32_t h, const float* const* S, const float* const* Y,
+                              const float* coef, float* d, void* hip_stream);
 int tvam_axpy_clamp(uint64_t n, const float* p, float alpha, const float* d, float lo, float* out,
                     void* hip_stream);
 
@@ -322,6 +337,17 @@ int tvam_axpy_clamp(uint64_t n, const float* p, float alpha, const float* d, flo
    computed with the plan's own fp32 ray generation: the row <-> slice map
    that z-slab sharding of planar scenes partitions. */
 int tvam_row_slices(const tvam_desc* desc, int32_t* slice_of_row);
+
+/* The planar adjoint of film slices [z_begin, z_end) alone (tvam_adjoint of a dense set restricted
+   to them), into DMD rows [row_begin, row_end) of every angle of grad_active (n_active = the dense
+   crop count; those rows zeroed first, the others untouched).  The rows must be exactly the rows
+   whose rays lie in those slices (tvam_row_slices); slices on tvam_plan_adj_chunk's chunks.  With
+   tvam_forward_slices it lets a caller pipeline a slab's forward, loss and adjoint with the vector
+   passes of the neighbouring slabs.  TVAM_ERR_UNSUPPORTED off the planar path. */
+int tvam_adjoint_slices(tvam_plan* plan, const float* grad_dose, uint64_t n_active, int32_t z_begin, int32_t z_end,
+                        int32_t row_begin, int32_t row_end, float* grad_active, void* hip_stream);
+/* Slice granularity of tvam_adjoint_slices (0: not available). */
+int tvam_plan_adj_chunk(const tvam_plan* plan);
 
 /* Exact number of DDA voxel visits of one pass (host-synchronous). */
 int tvam_count_visits(tvam_plan* plan, uint32_t spp, uint32_t seed,

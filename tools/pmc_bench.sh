@@ -8,7 +8,8 @@ set -euo pipefail
 out="$1"; c="$2"; n="${3:-400}"
 export TMPDIR=/tmp
 mkdir -p "$out"
-cmd=(python3 bench.py --config "$c" --n "$n" --steps 1 --warmup 0 --prewarm 0 --cpu-baseline off)
+# --slab-bands 1: the planar configs' kernels as full-film launches (the summaries' per-launch bytes)
+cmd=(python3 bench.py --config "$c" --n "$n" --steps 1 --warmup 0 --prewarm 0 --cpu-baseline off --slab-bands 1)
 echo "${cmd[*]}" > "$out/command.txt"
 python3 -c "import bench; print(bench.csrc_digest())" > "$out/csrc_sha16.txt"
 sets=(
