@@ -329,6 +329,41 @@ class ShardedLoop:
         return self.opt['projector.active_data'].detach() if self.opt is not None else self.x0
 
 
+
+def slab_bands(m, nz, n, zc, za, R):
+    """[(row0, row1, z0, z1), ...] of a banded planar iteration, or None: about n film slice ranges
+    with boundaries on whole forward (zc) / adjoint (za) slice chunks and 64-slice bin blocks, each
+    with the one contiguous band of DMD rows whose rays lie in it (m = each crop row's film slice,
+    -1: misses the grid; rows may run top-down or bottom-up); the bands, extended over the unmapped
+    rows between them, tile [0, R)."""
+    blk = 64 * zc // math.gcd(64, zc)
+    blk = blk * za // math.gcd(blk, za)
+    cuts = sorted({min(nz, max(0, int(round(j * nz / n / blk)) * blk)) for j in range(1, n)} - {0, nz})
+    edges = [0] + cuts + [nz]
+    ranges = list(zip(edges[:-1], edges[1:]))
+    if len(ranges) <= 1:
+        return None
+    m = np.asarray(m)
+    mapped = m >= 0
+    bands = []
+    for z0, z1 in ranges:
+        rows = np.nonzero(mapped & (m >= z0) & (m < z1))[0]
+        if not rows.size:
+            return None
+        lo, hi = int(rows.min()), int(rows.max()) + 1
+        if not np.all(((m[lo:hi] >= z0) & (m[lo:hi] < z1)) | ~mapped[lo:hi]):
+            return None
+        bands.append((lo, hi))
+    order = sorted(range(len(ranges)), key=lambda q: bands[q][0])
+    ext = {}
+    for j, q in enumerate(order):
+        lo = 0 if j == 0 else bands[q][0]
+        hi = R if j == len(order) - 1 else bands[order[j + 1]][0]
+        if hi < bands[q][1]:
+            return None  # overlapping bands
+        ext[q] = (lo, hi)
+    return [(ext[q][0], ext[q][1], z0, z1) for q, (z0, z1) in enumerate(ranges)]
+
 class TvamProblem(ShardedLoop):
     """Scene + target + loss + optimizer state of one optimisation run (one rank's angle shard)."""
 
@@ -602,38 +637,10 @@ class TvamProblem(ShardedLoop):
         m = np.empty(desc.crop_y, dtype=np.int32)
         _abi.check(_abi.load_library().tvam_row_slices(ctypes.byref(desc), m.ctypes.data_as(ctypes.c_void_p)))
         m = np.where(m >= 0, m - int(desc.slab_begin), -1)  # this plan's film slices
-        blk = 64 * zc // math.gcd(64, zc)  # slice ranges: whole forward / adjoint chunks and 64-slice bin blocks
-        blk = blk * za // math.gcd(blk, za)
-        # n ranges of about nz / n slices, boundaries on whole blocks
-        cuts = sorted({min(nz, max(0, int(round(j * nz / n / blk)) * blk)) for j in range(1, n)} - {0, nz})
-        edges = [0] + cuts + [nz]
-        ranges = list(zip(edges[:-1], edges[1:]))
-        if len(ranges) <= 1:
-            return None
         R, C = int(desc.crop_y), int(desc.crop_x)
-        if C % 4:
+        parts = slab_bands(m, nz, n, zc, za, R) if C % 4 == 0 else None
+        if parts is None:
             return None
-        # each range's rows: one contiguous band (DMD rows run top-down or bottom-up through the
-        # slices); the bands, extended over rows whose rays miss the grid, tile the rows
-        mapped = m >= 0
-        bands = []
-        for z0, z1 in ranges:
-            rows = np.nonzero(mapped & (m >= z0) & (m < z1))[0]
-            if not rows.size:
-                return None
-            lo, hi = int(rows.min()), int(rows.max()) + 1
-            if not np.all(((m[lo:hi] >= z0) & (m[lo:hi] < z1)) | ~mapped[lo:hi]):
-                return None
-            bands.append((lo, hi))
-        order = sorted(range(len(ranges)), key=lambda q: bands[q][0])
-        ext = {}
-        for j, q in enumerate(order):
-            lo = 0 if j == 0 else bands[q][0]
-            hi = R if j == len(order) - 1 else bands[order[j + 1]][0]
-            if hi < bands[q][1]:
-                return None  # overlapping bands
-            ext[q] = (lo, hi)
-        parts = [(ext[q][0], ext[q][1], z0, z1) for q, (z0, z1) in enumerate(ranges)]
         nseg = self.n_local // (R * C)
         if nseg * R * C != self.n_local:
             return None
