@@ -5,7 +5,7 @@
 #   b: counters of configs 4 and 5;
 #   c: bench lines of configs 3 / 4 / 5 (+ filter_radon), the 8-rank angle-shard emulation of
 #      config 4 and the z-slab emulation of config 2;
-#   d: the whole -m gpu suite and smoke().
+#   d: the whole -m gpu suite, smoke() and the default bench line again (with every summary current).
 # usage: tools/r04_record.sh PART OUT
 set -euo pipefail
 part="$1"; o="$(realpath -m "$2")"; mkdir -p "$o"
@@ -37,5 +37,6 @@ case "$part" in
     timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 400 --timeout-method thread -p no:cacheprovider \
       > "$o/gpu_tests.log" 2>&1
     timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$o/smoke.log" 2>&1
+    timeout -k 10 300 python bench.py > "$o/bench.json" 2> "$o/bench.err"
     ;;
 esac
