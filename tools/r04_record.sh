@@ -38,5 +38,8 @@ case "$part" in
       > "$o/gpu_tests.log" 2>&1
     timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$o/smoke.log" 2>&1
     timeout -k 10 300 python bench.py > "$o/bench.json" 2> "$o/bench.err"
+    for b in 2 3 4; do  # the opt-in banded iteration at 2 / 3 / 4 slab bands, same box
+      timeout -k 10 150 python bench.py --slab-bands $b --cpu-baseline off > "$o/bench_bands$b.json" 2> "$o/bench_bands$b.err"
+    done
     ;;
 esac
