@@ -77,3 +77,31 @@ def test_plan_create_rejects_invalid_desc(field, value, msg):
     assert msg in lib.tvam_last_error().decode()
     with pytest.raises(ValueError, match=msg):
         _abi.check(rc)
+
+
+def test_round4_vector_entry_points_validate_before_hip():
+    """tvam_lbfgs_coef / _direction_rows / _history_rows and tvam_adjoint_slices reject bad
+    arguments with TVAM_ERR_INVALID (or UNSUPPORTED) before any HIP call, with a message."""
+    lib = _abi.load_library()
+    buf = (ctypes.c_double * 256)()
+    f32 = (ctypes.c_float * 64)()
+    order = (ctypes.c_int32 * 8)(0, 1, 2, 3, 4, 5, 6, 7)
+    bad_order = (ctypes.c_int32 * 8)(0, 9, 0, 0, 0, 0, 0, 0)
+    ptrs = (ctypes.c_void_p * 8)(*([ctypes.addressof(f32)] * 8))
+    p = ctypes.addressof(buf)
+    q = ctypes.addressof(f32)
+    cases = [
+        lib.tvam_lbfgs_coef(9, 0, 0, order, p, p, q, p, None),             # h > 8
+        lib.tvam_lbfgs_coef(2, 0, 0, bad_order, p, p, q, p, None),         # slot out of the ring
+        lib.tvam_lbfgs_coef(0, 1, 0, order, p, p, q, p, None),             # a new pair needs h >= 1
+        lib.tvam_lbfgs_coef(2, 0, 0, order, None, p, q, p, None),          # null dots
+        lib.tvam_lbfgs_direction_rows(0, 4, 8, 0, q, 1, ptrs, ptrs, q, q, None),     # no segments
+        lib.tvam_lbfgs_direction_rows(2, 6, 8, 0, q, 1, ptrs, ptrs, q, q, None),     # length not a multiple of 4
+        lib.tvam_lbfgs_direction_rows(2, 12, 8, 0, q, 1, ptrs, ptrs, q, q, None),    # segment longer than stride
+        lib.tvam_lbfgs_history_rows(2, 4, 8, 2, q, q, q, q, 1, ptrs, ptrs, q, q, p, p, None),  # offset misaligned
+        lib.tvam_lbfgs_history_rows(1, 4, 8, 0, q, q, q, q, 8, ptrs, ptrs, q, q, p, p, None),  # h > 7
+        lib.tvam_adjoint_slices(None, q, 16, 0, 8, 0, 4, q, None),                    # null plan
+    ]
+    for i, rc in enumerate(cases):
+        assert rc in (_abi.TVAM_ERR_INVALID, _abi.TVAM_ERR_UNSUPPORTED), (i, rc)
+    assert lib.tvam_last_error()
