@@ -314,11 +314,14 @@ class ShardedLoop:
                 evl = torch.cuda.Event()
                 evl.record(side)
             loss_evs.append(evl)
-        g = torch.empty(self.n_local, dtype=torch.float32, device=dev)
+        # the gradient zeroed once (one contiguous fill: tvam_adjoint_slices' own zeroing of a row
+        # band is a strided 2-D fill over every angle, 6x slower), then every band adds into it
+        # (an empty row range: no zeroing)
+        g = torch.zeros(self.n_local, dtype=torch.float32, device=dev)
         grad_ready = []
         for (r0, r1, z0, z1), evl in zip(pipe.parts, loss_evs):
             main.wait_event(evl)
-            self.proj.adjoint_slices(self.grad_vol, self.n_local, z0, z1, r0, r1, g)
+            self.proj.adjoint_slices(self.grad_vol, self.n_local, z0, z1, r0, r0, g)
             ev = torch.cuda.Event()
             ev.record(main)
             grad_ready.append((ev, r0, r1))
