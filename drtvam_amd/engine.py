@@ -134,7 +134,9 @@ class Projection:
     def adjoint_slices(self, grad_dose: torch.Tensor, n_active: int, z_begin: int, z_end: int, row_begin: int,
                        row_end: int, out: torch.Tensor) -> torch.Tensor:
         """The planar adjoint of film slices [z_begin, z_end) into DMD rows [row_begin, row_end) of every
-        angle of out (dense set; those rows zeroed first, the rest untouched; tvam_adjoint_slices)."""
+        angle of out (dense set; those rows zeroed first, the rest untouched; tvam_adjoint_slices).
+        An empty row range (row_begin == row_end) zeroes nothing: the slices' contributions are added
+        to out as it stands (a caller that zeroed the whole vector once)."""
         self._check_tensor(grad_dose, torch.float32, "grad_dose")
         self._check_tensor(out, torch.float32, "grad_active")
         if out.numel() != n_active:
