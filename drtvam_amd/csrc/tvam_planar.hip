@@ -630,6 +630,61 @@ __global__ __launch_bounds__(256) void tvam_slice_bin_kernel(TvamConsts k, TvamP
         if (c0 + cc < k.crop_x) out[(size_t)(c0 + cc) * pl.bin_nz + z] = s_t[cc][lc];
 }
 
+// tvam_slice_bin_kernel with 16-byte accesses (crop_x a multiple of 4, the patterns 16-byte
+// aligned, bin_nz a multiple of 4): a thread loads four columns of a slice's row and stores four
+// slices of a column; slices in [nz, bin_nz) are written as the zeros they hold.  The same sums in
+// the same order (bit-identical bins); 136 -> 100 us at config 2's size as a standalone transpose
+// (tools/proto_slice_bin.hip, profiles/r04/proto_bin/).
+__global__ __launch_bounds__(256) void tvam_slice_bin4_kernel(TvamConsts k, TvamPlanar pl,
+                                                             const float* __restrict__ pat, int zblock0) {
+    __shared__ float s_t[64][65];
+    __shared__ int s_row[64];
+    const int c0 = blockIdx.x * 64, z0 = ((int)blockIdx.y + zblock0) * 64, al = blockIdx.z;
+    if (threadIdx.x < 64) {
+        const int z = z0 + (int)threadIdx.x;
+        int r = -1;
+        if (z < k.nz) {
+            const int b = pl.slice_off[z], e = pl.slice_off[z + 1];
+            r = e - b == 1 ? pl.slice_rows[b] * k.crop_x : (e == b ? -1 : -2);
+        }
+        s_row[threadIdx.x] = r;
+    }
+    __syncthreads();
+    const float* pa = pat + (size_t)al * k.crop_y * k.crop_x;
+    const int q = threadIdx.x & 15, lz = threadIdx.x >> 4;
+    const int c = c0 + 4 * q;
+    const bool cin = c < k.crop_x;  // crop_x % 4 == 0: a thread's four columns are all in or all out
+#pragma unroll
+    for (int zz = lz; zz < 64; zz += 16) {
+        const int r = s_row[zz];
+        float4 v = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        if (cin && r >= 0) {
+            v = *reinterpret_cast<const float4*>(pa + (size_t)r + c);
+        } else if (cin && r == -2) {
+            for (int t = pl.slice_off[z0 + zz]; t < pl.slice_off[z0 + zz + 1]; ++t) {
+                const float4 w = *reinterpret_cast<const float4*>(pa + (size_t)pl.slice_rows[t] * k.crop_x + c);
+                v.x += w.x;
+                v.y += w.y;
+                v.z += w.z;
+                v.w += w.w;
+            }
+        }
+        s_t[4 * q + 0][zz] = v.x;
+        s_t[4 * q + 1][zz] = v.y;
+        s_t[4 * q + 2][zz] = v.z;
+        s_t[4 * q + 3][zz] = v.w;
+    }
+    __syncthreads();
+    float* out = pl.fwd_bin + ((size_t)al * (k.crop_x + 2 * pl.bin_pad) + pl.bin_pad) * pl.bin_nz;
+    const int z = z0 + 4 * q;
+    if (z >= pl.bin_nz) return;
+#pragma unroll
+    for (int cc = lz; cc < 64; cc += 16)
+        if (c0 + cc < k.crop_x)
+            *reinterpret_cast<float4*>(out + (size_t)(c0 + cc) * pl.bin_nz + z) =
+                make_float4(s_t[cc][4 * q], s_t[cc][4 * q + 1], s_t[cc][4 * q + 2], s_t[cc][4 * q + 3]);
+}
+
 size_t tvam_planar_fwd_lds(const TvamPlanar& pl, int Z) {
     const int ab = pl.fwd_ab > 1 ? pl.fwd_ab : 1;
     const size_t rw = pl.fwd_refr ? 2 : 1;
@@ -857,7 +912,14 @@ hipError_t tvam_launch_fwd_planar(const TvamConsts& k, const TvamPlanar& pl, int
         const int zhi = pl.fwd_nzc > 0 ? std::min(k.nz, (pl.fwd_zc0 + pl.fwd_nzc) * Z) : k.nz;
         const int b0 = zlo / 64, b1 = (zhi + 63) / 64;
         const dim3 bg((unsigned)((k.crop_x + 63) / 64), (unsigned)std::max(b1 - b0, 1), (unsigned)pl.ns);
-        hipLaunchKernelGGL(tvam_slice_bin_kernel, bg, dim3(256), 0, stream, k, pl, pat, b0);
+        static const bool bin1 = [] {  // TVAM_SLICE_BIN1=1: the one-float-per-thread binning (A/B, tests)
+            const char* v = getenv("TVAM_SLICE_BIN1");
+            return v && atoi(v) == 1;
+        }();
+        if (!bin1 && k.crop_x % 4 == 0 && pl.bin_nz % 4 == 0 && ((uintptr_t)pat & 15u) == 0)
+            hipLaunchKernelGGL(tvam_slice_bin4_kernel, bg, dim3(256), 0, stream, k, pl, pat, b0);
+        else
+            hipLaunchKernelGGL(tvam_slice_bin_kernel, bg, dim3(256), 0, stream, k, pl, pat, b0);
     }
     hipError_t e = tvam_launch_fwd_planar_z(grid, lds, stream, k, pl, Z, pat, dose);
     if (e != hipSuccess || parts == 1) return e;

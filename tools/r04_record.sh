@@ -5,7 +5,9 @@
 #   b: counters of configs 4 and 5;
 #   c: bench lines of configs 3 / 4 / 5 (+ filter_radon), the 8-rank angle-shard emulation of
 #      config 4 and the z-slab emulation of config 2;
-#   d: the whole -m gpu suite, smoke() and the default bench line again (with every summary current).
+#   d: the whole -m gpu suite, smoke() and the default bench line again (with every summary current);
+#   f: bench lines of configs 3 / 4 / 5 (+ filter_radon) and the z-slab emulation of config 2
+#      (run after the summaries of a and b are committed, so the lines carry live rooflines).
 # usage: tools/r04_record.sh PART OUT
 set -euo pipefail
 part="$1"; o="$(realpath -m "$2")"; mkdir -p "$o"
@@ -31,6 +33,16 @@ case "$part" in
     timeout -k 10 300 python bench.py --config 5 --n 800 --steps 5 --warmup 1 --filter-radon --cpu-baseline off \
       > "$o/bench_config5_filter_radon.json" 2> "$o/bench_config5_filter_radon.err"
     tools/emulate_angle8.sh "$o/emulate_c4" 4
+    tools/scale_emulate.sh "$o/emulate_slab"
+    ;;
+  f)
+    timeout -k 10 300 python bench.py --config 3 --cpu-baseline off > "$o/bench_config3.json" 2> "$o/bench_config3.err"
+    timeout -k 10 300 python bench.py --config 4 --steps 5 --warmup 1 --cpu-baseline off > "$o/bench_config4.json" \
+      2> "$o/bench_config4.err"
+    timeout -k 10 300 python bench.py --config 5 --n 800 --steps 5 --warmup 1 --cpu-baseline off \
+      > "$o/bench_config5.json" 2> "$o/bench_config5.err"
+    timeout -k 10 300 python bench.py --config 5 --n 800 --steps 5 --warmup 1 --filter-radon --cpu-baseline off \
+      > "$o/bench_config5_filter_radon.json" 2> "$o/bench_config5_filter_radon.err"
     tools/scale_emulate.sh "$o/emulate_slab"
     ;;
   d)
