@@ -14,7 +14,7 @@ flags=(--offload-arch=gfx950 -O3 -std=c++17 -fPIC
        -Wall -Wno-unused-function -I"$here/../../include")
 pids=()
 objs=()
-for src in tvam_plan tvam_kernels tvam_planar tvam_vec tvam_scatter tvam_radon; do
+for src in tvam_plan tvam_kernels tvam_planar tvam_adjlist tvam_vec tvam_scatter tvam_radon; do
   "$HIPCC" "${flags[@]}" ${TVAM_CXXFLAGS:-} -c "$here/$src.hip" -o "$objdir/$src.o" &
   pids+=($!)
   objs+=("$objdir/$src.o")

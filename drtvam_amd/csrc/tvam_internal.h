@@ -114,7 +114,30 @@ struct TvamPlanar {
     float4* chord;             // plan creation only: [ns][crop_x] {o2.x, o2.y, d2.x, d2.y} of the medium chord
     const float4* fwd_model;   // [16x16 tiles][ns][2] {u00, du/dlx, du/dly, d2u/dlx dly},
                                //   {half width + model error, candidates (int bits), first window column (int bits), 0}
+    // adjoint over slice-invariant visit lists (tvam_adjlist.hip; adjl_ngroups = 0: the tile adjoint)
+    const int32_t* adjl_gchunk;  // [ngroups + 1] first chunk of each (tile, part) group
+    const int64_t* adjl_coff;    // [nchunks + 1] first float4 row of each chunk's weights
+    const int4* adjl_hdr;        // [nchunks][64] {entry LDS offset, slot, interface weight bits, x | y step << 16}
+    const float4* adjl_w;        // [rows][64] weights, 4 visits per float4, LSB = y step after the visit
+    int32_t adjl_ngroups, adjl_parts;  // groups = (tile, step quadrant, part)
+    int32_t adjl_tw0, adjl_tw1;        // row pitch (voxels) for equal / opposite step signs: 1 / 15 (mod 16)
+    int32_t adjl_slack;                // zeroed bytes around each plane (padding visits walk there)
 };
+
+// Device buffers of the visit lists (owned by the plan).
+struct TvamAdjListBufs {
+    int32_t* gchunk = nullptr;
+    int64_t* coff = nullptr;
+    int4* hdr = nullptr;
+    float4* w = nullptr;
+    size_t bytes = 0;
+    int64_t visits_padded = 0;
+};
+size_t tvam_adjl_lds(const TvamPlanar& pl, const TvamTiles& t, int Z);
+hipError_t tvam_build_adj_lists(const TvamConsts& k, TvamPlanar& pl, const TvamTiles& t, int parts, int order,
+                                size_t max_bytes, TvamAdjListBufs& bufs, hipStream_t stream);
+hipError_t tvam_launch_adj_lists(const TvamConsts& k, const TvamPlanar& pl, const TvamTiles& t, int Z,
+                                 const int32_t* idxmap, const float* gin, float* out, hipStream_t stream);
 
 hipError_t tvam_launch_planar_rays(const TvamConsts& k, const TvamPlanar& pl, hipStream_t stream);
 // Refracted voxel-driven forward: per (16x16 tile, angle) model of the chord index (needs pl.chord);

@@ -104,6 +104,7 @@ struct tvam_plan {
     unsigned* d_amax = nullptr;  // ray-driven forward: per-angle max |pattern|, fixed-point scale
     float* d_fscale = nullptr;
     int32_t planar_rz = 4;
+    TvamAdjListBufs adjl;  // planar adjoint: slice-invariant visit lists (tvam_adjlist.hip)
     TvamBinScratch bins;  // scattering media: brick-binned forward scratch
     std::vector<float4> fwd_ang_h;  // host staging of the forward tables (plan creation only)
     std::vector<int32_t> fwd_cb_h;
@@ -149,6 +150,14 @@ extern "C" void tvam_desc_init(tvam_desc* d) {
 extern "C" const char* tvam_last_error(void) { return g_err.c_str(); }
 extern "C" int tvam_abi_version(void) { return TVAM_ABI_VERSION; }
 
+static void adjl_free(TvamAdjListBufs& b) {
+    (void)hipFree(b.gchunk);
+    (void)hipFree(b.coff);
+    (void)hipFree(b.hdr);
+    (void)hipFree(b.w);
+    b = TvamAdjListBufs{};
+}
+
 static void plan_free(tvam_plan* p) {
     if (!p) return;
     (void)hipFree(p->d_cs);
@@ -188,6 +197,7 @@ static void plan_free(tvam_plan* p) {
     (void)hipFree(p->d_adjq_off);
     (void)hipFree(p->d_pl_part);
     (void)hipFree(p->d_pl_bin);
+    adjl_free(p->adjl);
     (void)hipFree(p->d_pl_vox2);
     (void)hipFree(p->d_pl_fwd_model);
     (void)hipFree(p->d_amax);
@@ -708,6 +718,24 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     // ray pairs (TVAM_ADJ_PAIR=1; off by default: config 2 adjoint 3.65 -> 3.90 ms, the two halves'
     // lanes drift apart and the march's LDS reads lose their coherence, profiles/r04/ab2/proj_ab.jsonl)
     if (!p->pl.adj_quad && env_int("TVAM_ADJ_PAIR", 0) && (rc = adj_pair_lists(p))) return rc;
+    // the adjoint over slice-invariant visit lists (tvam_adjlist.hip), when they fit in a quarter of
+    // the free device memory (config 2: ~0.5 GB); else the tile adjoint re-derives the visits.
+    // Groups = (tile, step quadrant, part), parts until the grid holds >= 8K workgroups.
+    p->pl.adjl_ngroups = 0;
+    if (p->planar_az == 8 && ns > 0 && !p->pl.adj_quad && !p->pl.adj_pair && env_int("TVAM_ADJ_LISTS", 1)) {
+        size_t fr = 0, tot = 0;
+        if ((e = hipMemGetInfo(&fr, &tot)) != hipSuccess) return hip_fail(e, "hipMemGetInfo");
+        const int64_t nwg4 = (int64_t)p->tiles.ntx * p->tiles.nty * 4 * ((k.nz + 7) / 8);
+        const int parts = (int)std::min<int64_t>(4, std::max<int64_t>(1, (8192 + nwg4 - 1) / std::max<int64_t>(nwg4, 1)));
+        e = tvam_build_adj_lists(k, p->pl, p->tiles, parts, 0, fr / 4, p->adjl, nullptr);
+        if (e == hipSuccess && tvam_adjl_lds(p->pl, p->tiles, 8) > 160 * 1024) e = hipErrorOutOfMemory;
+        if (e != hipSuccess) {
+            adjl_free(p->adjl);
+            p->pl.adjl_ngroups = 0;
+            if (e != hipErrorOutOfMemory) return hip_fail(e, "adjoint visit lists");
+            (void)hipGetLastError();
+        }
+    }
     p->planar = true;
     return 0;
 }
@@ -1588,6 +1616,15 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
     return 0;
 }
 
+// tvam_scatter_binned found brick walks that disagree with the record writer's counts
+static int bin_mismatch_fail(tvam_plan* p) {
+    uint32_t bad = 0;
+    if (p->bins.sb.bad) (void)hipMemcpy(&bad, p->bins.sb.bad, sizeof(uint32_t), hipMemcpyDeviceToHost);
+    return fail(TVAM_ERR_HIP, "brick bins: " + std::to_string(bad) +
+                                  " scattered segments' brick walks disagree with their closed-form brick counts "
+                                  "(entries would be lost); rerun with TVAM_FLAG_SCATTER_ATOMIC");
+}
+
 // per-call constants: spp forced to 1 under regular sampling (common.py:49-51),
 // weight = inv_pdf / n_samples * print_time (projector.py:164-165, :187; common.py:111)
 static int call_setup(tvam_plan* p, uint64_t n_active, const uint32_t* active_pixels, uint32_t& spp, TvamConsts& k) {
@@ -1868,6 +1905,7 @@ static int forward_impl(tvam_plan* p, const float* active_data, const uint32_t* 
             e = tvam_scatter_binned(TVAM_MODE_FWD, kc, t, pat, idxmap, nullptr, dose, p->bins, stream);
         if (e == hipErrorNotSupported)
             e = tvam_launch_scatter_paths(TVAM_MODE_FWD, kc, t, pat, idxmap, nullptr, dose, nullptr, stream);
+        if (e == hipErrorIllegalState) return bin_mismatch_fail(p);
         if (e != hipSuccess) return hip_fail(e, "scatter forward launch");
     }
     return 0;
@@ -1975,6 +2013,7 @@ extern "C" int tvam_adjoint(tvam_plan* p, const float* grad_dose, const uint32_t
             e = tvam_scatter_binned(TVAM_MODE_ADJ, k, t, nullptr, idxmap, grad_dose, grad_active, p->bins, stream);
         if (e == hipErrorNotSupported)
             e = tvam_launch_scatter_paths(TVAM_MODE_ADJ, k, t, nullptr, idxmap, grad_dose, grad_active, nullptr, stream);
+        if (e == hipErrorIllegalState) return bin_mismatch_fail(p);
         if (e != hipSuccess) return hip_fail(e, "scatter adjoint launch");
     }
     return 0;

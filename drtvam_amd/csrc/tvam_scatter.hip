@@ -2056,5 +2056,14 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (keep) cc->valid = true;
     }
+    // a slot whose brick walk disagreed with the writer's closed-form count (never, by
+    // construction) may have dropped entries: fail loudly rather than return a short dose
+    if (s.sb.bad && s.st[0] > 0) {
+        uint32_t bad = 0;
+        if ((e = hipMemcpyAsync(&bad, s.sb.bad, sizeof(uint32_t), hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+            (e = hipStreamSynchronize(stream)) != hipSuccess)
+            return e;
+        if (bad) return hipErrorIllegalState;
+    }
     return hipSuccess;
 }

@@ -228,14 +228,21 @@ class FusedLinearLBFGS(LinearLBFGS):
         lib = self._lib()
         pipe = self.pipeline
         (k, p), = self.variables.items()
-        st = self._st(k, p)
+        dev0 = p.device
+        side = pipe.side(dev0)
+        K = len(pipe.parts)
+        # state created here is zero-filled on the side stream, which writes it next (the fills
+        # must not race the side stream's history / coefficient kernels)
+        with torch.cuda.stream(side):
+            st = self._st(k, p)
+            if st.get('dots_b') is None or st['dots_b'].shape[0] != K:
+                st['dots_b'] = torch.zeros((K, 64), dtype=torch.float64, device=dev0)
         pf = _aligned(p.detach().reshape(-1))
         g = p.grad.detach().reshape(-1)
         if not (g.is_contiguous() and g.data_ptr() % 16 == 0):
             raise ValueError("step_pipelined: the gradient must be a 16-byte aligned contiguous tensor")
         dev = pf.device
         main = torch.cuda.current_stream(dev)
-        side = pipe.side(dev)
         ss = side.cuda_stream
         R, C = pipe.rows, pipe.cols
         new = st['t'] > 0
@@ -247,9 +254,6 @@ class FusedLinearLBFGS(LinearLBFGS):
         Y_ptrs = (ctypes.c_void_p * max(h, 1))(*[st['Y_ptr'][j] for j in kept])
         slot = st['free'][0] if new else None
         nd = 5 * (h + 1) + 1 if new else 2 * h + 1
-        K = len(pipe.parts)
-        if st.get('dots_b') is None or st['dots_b'].shape[0] != K:
-            st['dots_b'] = torch.zeros((K, 64), dtype=torch.float64, device=dev)
         dots_b = st['dots_b']
         with torch.cuda.stream(side):
             dots_b.zero_()
@@ -379,7 +383,8 @@ class FusedLinearLBFGS(LinearLBFGS):
         """One L-BFGS step.  loss: the host value, or None with loss_dev (f64 device scalar),
         all-reduced with the dot vector (loss_summed: the ranks' values add up, else every rank
         holds the same value) and read with the first Armijo probes; returns the loss value (and
-        skips the update when it is exactly 0, the converged case).  The recursion runs on the
+        skips the update when it is exactly 0, the converged case: the history, ring and Gram have
+        then already taken this step's pair, so the caller stops iterating, optimize.py:305-307).  The recursion runs on the
         device (tvam_lbfgs_coef), so the history pass, the direction and its render follow each
         other on the stream: one host read per step (the probes), none before the render."""
         from . import _abi
@@ -456,7 +461,7 @@ class FusedLinearLBFGS(LinearLBFGS):
         key = 'projector.active_data' if 'projector.active_data' in params else next(iter(params))
         alpha = 1.0
         steps = 0
-        if self.loss_steps is not None:
+        if self.loss_steps is not None and self.search_it > 0:
             # the same backtracking sequence (alpha = 1, 1/2, ...; first Armijo pass wins), its
             # probes evaluated probe_batch at a time: one loss pass and one host read per batch
             # (the first read also carries the loss and g.d)

@@ -671,6 +671,10 @@ class TvamProblem(ShardedLoop):
     def on_progressive(self):
         self.integrator.max_depth = self.max_depth
         self.proj = self._active_projection(self.integrator, self.sensor)
+        if getattr(self.opt, 'pipeline', None) is not None:
+            # the new plan may chunk its slices differently: re-derive the slab bands (or run the
+            # unbanded iteration when they no longer tile its film)
+            self.opt.pipeline = self.direction_pipeline()
 
     def final_render(self, spp=None):
         proj = self._active_projection(self.final_integrator, self.final_sensor)
