@@ -170,8 +170,8 @@ __global__ __launch_bounds__(256) void tvam_adjl_fill_kernel(TvamConsts k, TvamP
 // the same +-1 and the lanes of a ds_read_b128 lane group keep the distinct chunks (mod 16) they
 // entered with: no bank conflicts.  Padding visits keep stepping in x through zeroed slack
 // (adjl_slack bytes) before, between and after the two planes.
-template <int Z, int NT>
-__global__ __launch_bounds__(NT) void tvam_adjl_kernel(TvamConsts k, TvamPlanar pl, TvamTiles tp, int nzc,
+template <int Z, int NT, int MINW = 1>
+__global__ __launch_bounds__(NT, MINW) void tvam_adjl_kernel(TvamConsts k, TvamPlanar pl, TvamTiles tp, int nzc,
                                                        const int32_t* __restrict__ idxmap,
                                                        const float* __restrict__ gin, float* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -231,13 +231,38 @@ __global__ __launch_bounds__(NT) void tvam_adjl_kernel(TvamConsts k, TvamPlanar 
 
     const int lane = (int)threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform chunk loop
-    for (int c = c0 + wv; c < c1; c += NT / 64) {
-        const int4 h = pl.adjl_hdr[(size_t)c * 64 + lane];
-        const int64_t r0 = pl.adjl_coff[c];
-        const int n4 = (int)(pl.adjl_coff[c + 1] - r0);
-        const float4* wp = pl.adjl_w + r0 * 64 + lane;
+    // Pipelined over the wave's chunks: a chunk's header and its first four weight rows are loaded
+    // before the previous chunk's gradient atomics are issued.  A load's data waits for every older
+    // vector-memory operation of the wave (atomics included, ~3000 cycles each under load), so the
+    // march of the next chunk starts on rows that do not queue behind the atomics, and by the time
+    // it needs row 4 (16 visits later) they have drained.
+    int c = c0 + wv;
+    if (c >= c1) return;
+    int4 h;
+    int n4;
+    const float4* wp;
+    float4 w0, w1, w2, w3;
+    auto load_chunk = [&](int cc) {
+        h = pl.adjl_hdr[(size_t)cc * 64 + lane];
+        const int64_t r0 = pl.adjl_coff[cc];
+        n4 = (int)(pl.adjl_coff[cc + 1] - r0);  // >= 1: chunks hold crossing rays only
+#if defined(TVAM_ADJL_PROBE) && TVAM_ADJL_PROBE == 1  // timing probe (wrong results): weights of chunk 0's rows only
+        wp = pl.adjl_w + lane;
+#else
+        wp = pl.adjl_w + r0 * 64 + lane;
+#endif
+        const int last = n4 - 1;
+        w0 = wp[0];
+        w1 = wp[(size_t)min(1, last) * 64];
+        w2 = wp[(size_t)min(2, last) * 64];
+        w3 = wp[(size_t)min(3, last) * 64];
+    };
+    load_chunk(c);
+    for (;;) {
         int pv = h.x;
         const int dx = (int)(short)(h.w & 0xffff), ddy = (h.w >> 16) - dx;
+        const uint32_t e = (uint32_t)h.y;
+        const float wsc = k.wscale * __int_as_float(h.z);
         float acc[Z];
 #pragma unroll
         for (int z = 0; z < Z; ++z) acc[z] = 0.0f;
@@ -257,57 +282,94 @@ __global__ __launch_bounds__(NT) void tvam_adjl_kernel(TvamConsts k, TvamPlanar 
                 pv += dx + ((__float_as_int(cw) & 1) ? ddy : 0);
             }
         };
-        // weights two rows ahead (ping-pong registers: a row is consumed one step after the
-        // next row's load is issued)
-        const int last = n4 - 1;  // (n4 >= 1: chunks hold crossing rays only)
-        float4 wa = wp[0], wb = wp[(size_t)min(1, last) * 64];
+        // weight rows four ahead, in a ring of four registers
+        const int last = n4 - 1;
         int q = 0;
 #pragma unroll 1
-        for (; q + 1 < n4; q += 2) {
-            const float4 ca = wa;
-            wa = wp[(size_t)min(q + 2, last) * 64];
-            visits(ca);
-            const float4 cb = wb;
-            wb = wp[(size_t)min(q + 3, last) * 64];
-            visits(cb);
+        for (; q + 3 < n4; q += 4) {
+            float4 t = w0;
+            w0 = wp[(size_t)min(q + 4, last) * 64];
+            visits(t);
+            t = w1;
+            w1 = wp[(size_t)min(q + 5, last) * 64];
+            visits(t);
+            t = w2;
+            w2 = wp[(size_t)min(q + 6, last) * 64];
+            visits(t);
+            t = w3;
+            w3 = wp[(size_t)min(q + 7, last) * 64];
+            visits(t);
         }
-        if (q < n4) visits(wa);
-        const uint32_t e = (uint32_t)h.y;
-        if (e == 0xffffffffu) continue;  // empty lane
-        const int al = (int)(e >> 16), colc = (int)(e & 0xffffu);
-        const float wray = __int_as_float(h.z);
-        const int64_t base = (int64_t)(k.a0 + al) * k.crop_y * k.crop_x + colc - k.shard_base;
+        if (q < n4) visits(w0);
+        if (q + 1 < n4) visits(w1);
+        if (q + 2 < n4) visits(w2);
 #pragma unroll
-        for (int z = 0; z < Z; ++z) {
-            const float v = acc[z] * (k.wscale * wray);
-            for (int q2 = s_roff[z]; q2 < s_roff[z + 1]; ++q2) {
-                int64_t act = base + (int64_t)s_rows[q2] * k.crop_x;
-                if (idxmap) {
-                    act = idxmap[act];
-                    if (act < 0) continue;
+        for (int z = 0; z < Z; ++z) acc[z] *= wsc;
+        const int cn = c + NT / 64;
+        if (cn < c1) load_chunk(cn);  // before this chunk's atomics
+#if defined(TVAM_ADJL_PROBE) && TVAM_ADJL_PROBE == 2  // timing probe (wrong results): no gradient atomics
+        if (acc[0] == 1.2345e-30f)
+#endif
+        if (e != 0xffffffffu) {  // (empty lanes add nothing)
+            const int al = (int)(e >> 16), colc = (int)(e & 0xffffu);
+            const int64_t base = (int64_t)(k.a0 + al) * k.crop_y * k.crop_x + colc - k.shard_base;
+#pragma unroll
+            for (int z = 0; z < Z; ++z) {
+                for (int q2 = s_roff[z]; q2 < s_roff[z + 1]; ++q2) {
+                    int64_t act = base + (int64_t)s_rows[q2] * k.crop_x;
+                    if (idxmap) {
+                        act = idxmap[act];
+                        if (act < 0) continue;
+                    }
+#if defined(TVAM_ADJL_PROBE) && TVAM_ADJL_PROBE == 3  // timing probe (wrong results): u32 atomics
+                    atomicAdd(reinterpret_cast<unsigned*>(out) + act, (unsigned)__float_as_int(acc[z]));
+#else
+                    atomicAdd(&out[act], acc[z]);  // backward_from(Le * em_grad), volume.py:274-276
+#endif
                 }
-                atomicAdd(&out[act], v);  // backward_from(Le * em_grad), volume.py:274-276
             }
         }
+        if (cn >= c1) break;
+        c = cn;
     }
 }
 
 size_t tvam_adjl_lds(const TvamPlanar& pl, const TvamTiles& t, int Z) {
     const int tw = std::max(pl.adjl_tw0, pl.adjl_tw1);
     return (size_t)(Z / 4) * ((size_t)tw * (t.tsy + 2) * 16 + pl.adjl_slack) + pl.adjl_slack +
-           (size_t)(Z + 1 + pl.max_rows_chunk) * sizeof(int);
+           (size_t)(Z + 1 + pl.max_rows_chunk * ((Z + 7) / 8)) * sizeof(int);
 }
 
 hipError_t tvam_launch_adj_lists(const TvamConsts& k, const TvamPlanar& pl, const TvamTiles& t, int Z,
                                  const int32_t* idxmap, const float* gin, float* out, hipStream_t stream) {
-    if (Z != 8) return hipErrorInvalidValue;
-    const int nzc = pl.adj_nzc > 0 ? pl.adj_nzc : (k.nz + Z - 1) / Z;
+    // slice chunks of this launch in units of the plan's adjoint chunk Z (tvam_adjoint_slices)
+    const int ZL = pl.adjl_z;
+    if (ZL != 8 && ZL != 16) return hipErrorInvalidValue;
+    TvamPlanar q = pl;
+    if (pl.adj_nzc > 0) {
+        const int z0 = pl.adj_zc0 * Z, z1 = std::min(k.nz, (pl.adj_zc0 + pl.adj_nzc) * Z);
+        if (z0 % ZL) return hipErrorInvalidValue;
+        q.adj_zc0 = z0 / ZL;
+        q.adj_nzc = (z1 - z0 + ZL - 1) / ZL;
+    }
+    const int nzc = q.adj_nzc > 0 ? q.adj_nzc : (k.nz + ZL - 1) / ZL;
     const int64_t gpad = ((int64_t)pl.adjl_ngroups + 7) / 8 * 8;
     const int64_t nb = gpad * nzc;
     if (nb <= 0) return hipSuccess;
     if (nb > 0x7fffffff) return hipErrorInvalidValue;
-    hipLaunchKernelGGL((tvam_adjl_kernel<8, 1024>), dim3((unsigned)nb), dim3(1024), tvam_adjl_lds(pl, t, Z), stream, k,
-                       pl, t, nzc, idxmap, gin, out);
+    const size_t lds = tvam_adjl_lds(pl, t, ZL);
+    if (ZL == 16)
+        hipLaunchKernelGGL((tvam_adjl_kernel<16, 1024>), dim3((unsigned)nb), dim3(1024), lds, stream, k, q, t, nzc, idxmap,
+                           gin, out);
+    else if (pl.adjl_nt == 896)  // 14 waves, 2 workgroups (7 waves per SIMD) per CU at <= 72 VGPRs
+        hipLaunchKernelGGL((tvam_adjl_kernel<8, 896, 7>), dim3((unsigned)nb), dim3(896), lds, stream, k, q, t, nzc, idxmap,
+                           gin, out);
+    else if (pl.adjl_nt == 768)
+        hipLaunchKernelGGL((tvam_adjl_kernel<8, 768, 6>), dim3((unsigned)nb), dim3(768), lds, stream, k, q, t, nzc, idxmap,
+                           gin, out);
+    else
+        hipLaunchKernelGGL((tvam_adjl_kernel<8, 1024>), dim3((unsigned)nb), dim3(1024), lds, stream, k, q, t, nzc, idxmap,
+                           gin, out);
     return hipGetLastError();
 }
 

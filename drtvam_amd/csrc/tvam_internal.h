@@ -122,6 +122,8 @@ struct TvamPlanar {
     int32_t adjl_ngroups, adjl_parts;  // groups = (tile, step quadrant, part)
     int32_t adjl_tw0, adjl_tw1;        // row pitch (voxels) for equal / opposite step signs: 1 / 15 (mod 16)
     int32_t adjl_slack;                // zeroed bytes around each plane (padding visits walk there)
+    int32_t adjl_z;                    // slices per workgroup (8 or 16)
+    int32_t adjl_nt;                   // threads per workgroup (1024, 896 or 768)
 };
 
 // Device buffers of the visit lists (owned by the plan).

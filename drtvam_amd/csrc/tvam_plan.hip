@@ -725,10 +725,14 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     if (p->planar_az == 8 && ns > 0 && !p->pl.adj_quad && !p->pl.adj_pair && env_int("TVAM_ADJ_LISTS", 1)) {
         size_t fr = 0, tot = 0;
         if ((e = hipMemGetInfo(&fr, &tot)) != hipSuccess) return hip_fail(e, "hipMemGetInfo");
-        const int64_t nwg4 = (int64_t)p->tiles.ntx * p->tiles.nty * 4 * ((k.nz + 7) / 8);
-        const int parts = (int)std::min<int64_t>(4, std::max<int64_t>(1, (8192 + nwg4 - 1) / std::max<int64_t>(nwg4, 1)));
+        p->pl.adjl_z = env_int("TVAM_ADJL_Z", 16) == 8 ? 8 : 16;
+        const int64_t nwg4 = (int64_t)p->tiles.ntx * p->tiles.nty * 4 * ((k.nz + p->pl.adjl_z - 1) / p->pl.adjl_z);
+        const int parts = (int)std::min<int64_t>(4, std::max<int64_t>(1, (4096 + nwg4 - 1) / std::max<int64_t>(nwg4, 1)));
+        p->pl.adjl_nt = env_int("TVAM_ADJL_NT", 768);
         e = tvam_build_adj_lists(k, p->pl, p->tiles, parts, 0, fr / 4, p->adjl, nullptr);
-        if (e == hipSuccess && tvam_adjl_lds(p->pl, p->tiles, 8) > 160 * 1024) e = hipErrorOutOfMemory;
+        // 16 slices per workgroup where the tile's 4 planes fit in LDS (the weights are the same)
+        if (e == hipSuccess && p->pl.adjl_z == 16 && tvam_adjl_lds(p->pl, p->tiles, 16) > 160 * 1024) p->pl.adjl_z = 8;
+        if (e == hipSuccess && tvam_adjl_lds(p->pl, p->tiles, p->pl.adjl_z) > 160 * 1024) e = hipErrorOutOfMemory;
         if (e != hipSuccess) {
             adjl_free(p->adjl);
             p->pl.adjl_ngroups = 0;
@@ -1926,7 +1930,7 @@ extern "C" int tvam_adjoint_slices(tvam_plan* p, const float* grad_dose, uint64_
     uint32_t spp = 1;
     int rc = call_setup(p, n_active, nullptr, spp, k);
     if (rc) return rc;
-    const int Z = p->planar_az, nz = k.nz;
+    const int Z = p->pl.adjl_ngroups > 0 ? std::max(p->planar_az, p->pl.adjl_z) : p->planar_az, nz = k.nz;
     const int64_t R = k.crop_y, C = k.crop_x, A = (int64_t)p->tiles.n_shard;
     if (z_begin < 0 || z_end > nz || z_begin >= z_end || z_begin % Z != 0 || (z_end % Z != 0 && z_end != nz) ||
         row_begin < 0 || row_end > R || row_begin > row_end || (int64_t)n_active != A * R * C)
@@ -1937,14 +1941,15 @@ extern "C" int tvam_adjoint_slices(tvam_plan* p, const float* grad_dose, uint64_
                              (size_t)(row_end - row_begin) * C * sizeof(float), (size_t)A, stream);
     if (e != hipSuccess) return hip_fail(e, "hipMemset2DAsync");
     TvamPlanar pl = p->pl;
-    pl.adj_zc0 = z_begin / Z;
-    pl.adj_nzc = (z_end - z_begin + Z - 1) / Z;
-    e = tvam_launch_adj_planar(k, pl, p->tiles, Z, nullptr, grad_dose, grad_active, stream);
+    pl.adj_zc0 = z_begin / p->planar_az;  // (in the tile adjoint's chunks; the list adjoint converts)
+    pl.adj_nzc = (z_end - z_begin + p->planar_az - 1) / p->planar_az;
+    e = tvam_launch_adj_planar(k, pl, p->tiles, p->planar_az, nullptr, grad_dose, grad_active, stream);
     return e == hipSuccess ? 0 : hip_fail(e, "planar adjoint launch");
 }
 
 extern "C" int tvam_plan_adj_chunk(const tvam_plan* p) {
-    return p && p->planar && !p->general && !p->surface && p->desc.albedo == 0.0f ? p->planar_az : 0;
+    if (!p || !p->planar || p->general || p->surface || p->desc.albedo != 0.0f) return 0;
+    return p->pl.adjl_ngroups > 0 ? std::max(p->planar_az, p->pl.adjl_z) : p->planar_az;
 }
 
 extern "C" int tvam_adjoint(tvam_plan* p, const float* grad_dose, const uint32_t* active_pixels, uint64_t n_active,

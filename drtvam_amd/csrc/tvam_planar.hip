@@ -1168,7 +1168,7 @@ size_t tvam_planar_adj_lds(const TvamPlanar& pl, const TvamTiles& t, int Z) {
 
 hipError_t tvam_launch_adj_planar(const TvamConsts& k, const TvamPlanar& pl, const TvamTiles& t, int Z,
                                   const int32_t* idxmap, const float* gin, float* out, hipStream_t stream) {
-    if (pl.adjl_ngroups > 0 && Z == 8) return tvam_launch_adj_lists(k, pl, t, Z, idxmap, gin, out, stream);
+    if (pl.adjl_ngroups > 0) return tvam_launch_adj_lists(k, pl, t, Z, idxmap, gin, out, stream);
     // slice chunks of this launch: [adj_zc0, adj_zc0 + adj_nzc) (tvam_adjoint_slices), else all
     const int nzc = pl.adj_nzc > 0 ? pl.adj_nzc : (k.nz + Z - 1) / Z;
     dim3 grid((unsigned)(t.ntx * t.nty), (unsigned)nzc, (unsigned)std::max(pl.adj_split, 1) * (pl.adj_quad ? 4u : 1u));
