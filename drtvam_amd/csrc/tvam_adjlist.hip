@@ -313,8 +313,11 @@ __global__ __launch_bounds__(NT, MINW) void tvam_adjl_kernel(TvamConsts k, TvamP
         if (e != 0xffffffffu) {  // (empty lanes add nothing)
             const int al = (int)(e >> 16), colc = (int)(e & 0xffffu);
             const int64_t base = (int64_t)(k.a0 + al) * k.crop_y * k.crop_x + colc - k.shard_base;
+            // a partial of exactly 0 (every visited gradient voxel 0: the thresholded loss is flat
+            // wherever the dose meets its bounds) adds nothing: no atomic for it
 #pragma unroll
             for (int z = 0; z < Z; ++z) {
+                if (acc[z] == 0.0f) continue;
                 for (int q2 = s_roff[z]; q2 < s_roff[z + 1]; ++q2) {
                     int64_t act = base + (int64_t)s_rows[q2] * k.crop_x;
                     if (idxmap) {
@@ -384,7 +387,7 @@ hipError_t tvam_build_adj_lists(const TvamConsts& k, TvamPlanar& pl, const TvamT
                                 size_t max_bytes, TvamAdjListBufs& bufs, hipStream_t stream) {
     (void)order;
     const int ntiles = t.ntx * t.nty;
-    const bool w2 = pl.adj_w2 && k.vox_chord < TVAM_W2_MAX;
+    const bool w2 = k.vox_chord < TVAM_W2_MAX;  // the tile adjoint's weight form (tvam_launch_adj_planar)
     const int w = t.tsx + 2;
     pl.adjl_tw0 = w + ((1 - w) % 16 + 16) % 16;   // = 1 (mod 16)
     pl.adjl_tw1 = w + ((15 - w) % 16 + 16) % 16;  // = 15 (mod 16)

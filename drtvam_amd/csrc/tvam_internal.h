@@ -13,6 +13,10 @@
 #include "tvam_common.h"
 #include "../../include/tvam.h"
 
+// A tuning knob: the environment variable `name` under TVAM_EXPERIMENTAL=1 (logged), else `def`
+// (tvam_plan.hip).
+int tvam_knob(const char* name, int def);
+
 // Device tables that drive one tile launch.
 struct TvamTiles {
     const float2* cs;          // [n_shard] (cos, sin) of each angle of the shard
@@ -60,41 +64,19 @@ struct TvamPlanar {
     const int32_t* slice_off;  // [res_z + 1] CSR: DMD rows whose rays lie in each slice
     const int32_t* slice_rows;
     int32_t ns;
-    int32_t ncmax;             // forward: DMD columns staged per (16 fwd_px x 16 tile, angle)
-    int32_t fwd_px;            // forward: voxel columns per thread along x (1, or 2: a pair sharing its
-                               // candidate columns' staged slabs; tiles 32 x 16)
+    int32_t ncmax;             // forward: DMD columns staged per (16 x 16 tile, angle)
     float marg_u;              // forward: candidate-column margin (spawn offset of o2 + rounding), in columns
     float u0;                  // forward: crop column of lateral coordinate 0 (0.5 W - 0.5 - crop_off_x)
     int32_t fwd_nc;            // forward: candidate columns per (voxel, angle)
     int32_t fwd_multi;         // forward: some slice collects several DMD rows
     const float4* fwd_ang;     // forward: [ns][2] {s du, -c du, 1/d.x, 1/d.y}, {half width + margin, axis flags}
-    const int32_t* fwd_cb;     // forward: [16 fwd_px x 16 tiles][ns] first column of the staged window
-    int32_t xcd_remap;         // forward: XCD-aware workgroup order
+    const int32_t* fwd_cb;     // forward: [16 x 16 tiles][ns] first column of the staged window
     int32_t fwd_pf;            // forward: staged values per thread and angle (2 or 4)
     int32_t max_rows_chunk;    // adjoint: most DMD rows in one chunk of Z slices
     int32_t adj_pitch;         // adjoint: LDS row pitch of the gradient tile in voxels (>= tile + 2)
     int32_t max_rows_slice;    // ray-driven forward: most DMD rows in one slice (fixed-point bound)
     int32_t adj_split;         // adjoint: workgroups sharing one (tile, slice chunk)'s ray list (thin slabs)
-    int32_t adj_prefetch;      // adjoint: software-pipelined record loads (slot k + 2, records k + 1)
     int32_t adj_nt;            // adjoint: threads per workgroup (256 or 512)
-    int32_t adj_planes;        // adjoint: gradient tile as Z/4 planes [z/4][voxel][4] (else interleaved [voxel][z])
-    int32_t adj_w2;            // adjoint: degree-2 visit weights where vox_chord < TVAM_W2_MAX
-    // adjoint: per (tile, step quadrant) ray lists (adj_quad = 1, tvam_plan.hip adj_quadrant_lists).
-    // With the gradient tile's row pitch = +1 (mod 16) for rays whose x and y steps have equal
-    // signs and -1 (mod 16) for opposite signs, every visit moves a lane's 16-byte LDS chunk by
-    // the same +-1, so the lanes of a wave keep their entry chunks' differences: each 16-lane group
-    // of a ds_read_b128 is dealt rays of distinct entry chunks mod 16 (conflict-free throughout)
-    // and similar in-tile lengths.  Lists padded to whole waves with 0xffffffff.
-    const uint32_t* adj_qslots;
-    const int64_t* adj_qoff;   // [ntiles * 4 + 1]
-    int32_t adj_quad;
-    // adjoint: per-tile ray pairs (adj_pair = 1, tvam_plan.hip adj_pair_lists): the tile's crossing
-    // rays of each angle in column order, ray j paired with ray j + ceil(n / 2) (complementary
-    // chord lengths through a square tile), stored as consecutive entries; 0xffffffff pads
-    const uint32_t* adj_pslots;
-    const int64_t* adj_poff;   // [ntiles + 1], even lengths
-    int32_t adj_pair;
-    int32_t adj_pitch2;        // row pitch of quadrants 1, 2 (opposite step signs); adj_pitch: 0, 3
     int32_t rayfwd_pitch;      // ray-driven forward: LDS row pitch of its dose tile (>= tile + 2)
     int32_t rayfwd_nt;         // ray-driven forward: threads per workgroup (256 or 512)
     int32_t fwd_parts;         // forward: angle parts per (tile, slice chunk) (thin slabs; 1 = none)

@@ -93,10 +93,6 @@ struct tvam_plan {
     float4* d_pl_rec_f = nullptr;
     int32_t* d_pl_rec_i = nullptr;
     float4* d_pl_rec_g = nullptr;
-    uint32_t* d_adjq_slots = nullptr;  // planar adjoint: per (tile, quadrant) ray lists
-    uint32_t* d_adjp_slots = nullptr;  // planar adjoint: per-tile ray pairs
-    int64_t* d_adjp_off = nullptr;
-    int64_t* d_adjq_off = nullptr;
     float* d_pl_part = nullptr;  // voxel-driven forward: partial doses of the angle parts
     float* d_pl_bin = nullptr;   // voxel-driven forward: slice-binned patterns
     float4* d_pl_vox2 = nullptr;      // refracted voxel-driven forward: per-column 1/d, flags, weight
@@ -191,10 +187,6 @@ static void plan_free(tvam_plan* p) {
     (void)hipFree(p->d_pl_rec_f);
     (void)hipFree(p->d_pl_rec_i);
     (void)hipFree(p->d_pl_rec_g);
-    (void)hipFree(p->d_adjq_slots);
-    (void)hipFree(p->d_adjp_slots);
-    (void)hipFree(p->d_adjp_off);
-    (void)hipFree(p->d_adjq_off);
     (void)hipFree(p->d_pl_part);
     (void)hipFree(p->d_pl_bin);
     adjl_free(p->adjl);
@@ -350,10 +342,22 @@ static int upload(T** dst, const std::vector<T>& v) {
     return 0;
 }
 
-static int env_int(const char* name, int def) {
+// Tuning knobs (TVAM_<NAME> environment variables) are honoured only under TVAM_EXPERIMENTAL=1 --
+// A/B runs and the tests that force a code path (work splits, slab depths, chunk sizes) -- and
+// each honoured one is logged; production plans take the defaults whatever the environment holds.
+int tvam_knob(const char* name, int def) {
+    static const bool on = [] {
+        const char* v = std::getenv("TVAM_EXPERIMENTAL");
+        return v && std::atoi(v) == 1;
+    }();
+    if (!on) return def;
     const char* v = std::getenv(name);
-    return v && *v ? std::atoi(v) : def;
+    if (!(v && *v)) return def;
+    const int r = std::atoi(v);
+    std::fprintf(stderr, "[tvam] TVAM_EXPERIMENTAL: %s=%d (default %d)\n", name, r, def);
+    return r;
 }
+#define env_int tvam_knob
 
 // Planar fast path: regular sampling and rows whose vial entry offset is
 // row-independent (|z| <= 0.7 r < r / sqrt(2) <= max(|p_x|, |p_y|) on the
@@ -363,213 +367,6 @@ static bool planar_fwd_setup(tvam_plan* p, const std::vector<float2>& cs, const 
 static int fwd_buffers(tvam_plan* p);
 static int choose_fwd_z(tvam_plan* p);
 static int refr_fwd_setup(tvam_plan* p, const std::vector<int32_t>& off);
-
-// Planar adjoint ray lists per (tile, step quadrant) (TvamPlanar::adj_quad).  The gradient tile
-// is [z/4][voxel][4] with voxel = (y + 1) * pitch + x + 1, one 16-byte chunk per voxel and read;
-// a ds_read_b128 is served in four 16-lane groups ({0-3, 12-15, 20-27}, {4-11, 16-19, 28-31},
-// + 32), each conflict-free when its lanes' chunks differ mod 16.  With pitch = +1 (mod 16) for
-// quadrants whose x and y steps have equal signs and -1 (mod 16) otherwise, every step moves a
-// lane's chunk by the same +-1 in one quadrant, so lanes that enter a tile at distinct chunks mod
-// 16 stay distinct for the whole march.  Per (tile, quadrant): the rays in (angle, column) order,
-// blocks of 256 sorted by predicted in-tile visits (lane balance), each block dealt into waves
-// whose 16-lane groups take rays of distinct entry chunks first.  The entry voxel and the visit
-// count come from the plan's own ray records with the kernel's closed-form resume
-// (tvam_axis_window / tvam_axis_steps), so the residues are exact.  Host model of the gain:
-// tools/lds_bank_model2.py (config 2: LDS cycles 2.65 -> 1.45 x the conflict-free full-wave cost).
-static int adj_quadrant_lists(tvam_plan* p) {
-    const TvamConsts& k = p->k;
-    const TvamTiles& t = p->tiles;
-    const int ns = p->pl.ns, ntiles = t.ntx * t.nty;
-    const size_t nrec = (size_t)ns * k.crop_x;
-    std::vector<float4> rf(nrec), rg, ang((size_t)std::max(ns, 1));
-    std::vector<int32_t> ri(nrec);
-    std::vector<int64_t> off((size_t)ntiles + 1);
-    hipError_t e;
-    if ((e = hipMemcpy(rf.data(), p->d_pl_rec_f, nrec * sizeof(float4), hipMemcpyDeviceToHost)) != hipSuccess ||
-        (e = hipMemcpy(ri.data(), p->d_pl_rec_i, nrec * sizeof(int32_t), hipMemcpyDeviceToHost)) != hipSuccess ||
-        (e = hipMemcpy(off.data(), p->d_slot_off, off.size() * sizeof(int64_t), hipMemcpyDeviceToHost)) != hipSuccess ||
-        (ns > 0 && (e = hipMemcpy(ang.data(), p->d_ang, (size_t)ns * sizeof(float4), hipMemcpyDeviceToHost)) != hipSuccess))
-        return hip_fail(e, "hipMemcpy (adjoint lists)");
-    if (p->d_pl_rec_g) {
-        rg.resize(nrec);
-        if ((e = hipMemcpy(rg.data(), p->d_pl_rec_g, nrec * sizeof(float4), hipMemcpyDeviceToHost)) != hipSuccess)
-            return hip_fail(e, "hipMemcpy (adjoint lists)");
-    }
-    std::vector<uint32_t> slots((size_t)off[ntiles]);
-    if (!slots.empty() &&
-        (e = hipMemcpy(slots.data(), p->d_slot_off ? p->d_slots : nullptr, slots.size() * sizeof(uint32_t),
-                       hipMemcpyDeviceToHost)) != hipSuccess)
-        return hip_fail(e, "hipMemcpy (adjoint lists)");
-    const int tw1 = p->pl.adj_pitch, tw2 = p->pl.adj_pitch2;
-    static const int G[4][16] = {{0, 1, 2, 3, 12, 13, 14, 15, 20, 21, 22, 23, 24, 25, 26, 27},
-                                 {4, 5, 6, 7, 8, 9, 10, 11, 16, 17, 18, 19, 28, 29, 30, 31},
-                                 {32, 33, 34, 35, 44, 45, 46, 47, 52, 53, 54, 55, 56, 57, 58, 59},
-                                 {36, 37, 38, 39, 40, 41, 42, 43, 48, 49, 50, 51, 60, 61, 62, 63}};
-    constexpr uint32_t PAD = 0xffffffffu;
-    const int W = std::max(64, env_int("TVAM_ADJ_QBLOCK", 256)) / 64 * 64;
-    const bool qsort = env_int("TVAM_ADJ_QSORT", 1) != 0, qdeal = env_int("TVAM_ADJ_QDEAL", 1) != 0;
-    struct Ray { uint32_t e; int len, res; };
-    std::vector<uint32_t> out;
-    std::vector<int64_t> qoff((size_t)ntiles * 4 + 1, 0);
-    std::vector<Ray> q[4];
-    for (int tile = 0; tile < ntiles; ++tile) {
-        const int x0 = (tile % t.ntx) * t.tsx, y0 = (tile / t.ntx) * t.tsy;
-        const int x1 = std::min(x0 + t.tsx, k.res[0]), y1 = std::min(y0 + t.tsy, k.res[1]);
-        for (auto& v : q) v.clear();
-        for (int64_t j = off[tile]; j < off[tile + 1]; ++j) {
-            const uint32_t ev = slots[(size_t)j];
-            const int al = (int)(ev >> 16), colc = (int)(ev & 0xffffu);
-            const size_t r = (size_t)al * k.crop_x + colc;
-            const int rv = ri[r];
-            if (rv < 0) continue;  // misses the vial / grid (the kernel skips it)
-            const float4 ff = rf[r];
-            float4 an = ang[(size_t)al];
-            if (!rg.empty()) {
-                const float4 gg = rg[r];
-                an = make_float4(std::fabs(gg.x), std::fabs(gg.y), gg.x < 0.0f ? -1.0f : 1.0f, gg.y < 0.0f ? -1.0f : 1.0f);
-            }
-            const int svx = rv & 0xffff, svy = rv >> 16, stx = (int)an.z, sty = (int)an.w;
-            float tin0, tout0, tin1, tout1;
-            int nin0, nout0, nin1, nout1;
-            tvam_axis_window(svx, stx, ff.z, an.x, x0, x1, tin0, tout0, nin0, nout0);
-            tvam_axis_window(svy, sty, ff.w, an.y, y0, y1, tin1, tout1, nin1, nout1);
-            const float tau_e = std::max(std::max(tin0, tin1), 0.0f);
-            const float tau_x = std::min(std::min(tout0, tout1), ff.y);
-            if (!(tau_e < tau_x)) continue;  // does not cross this tile (the kernel skips it)
-            const int n0 = tvam_axis_steps(tau_e, ff.z, an.x, nin0, nout0);
-            const int n1 = tvam_axis_steps(tau_e, ff.w, an.y, nin1, nout1);
-            const int m0 = tvam_axis_steps(tau_x, ff.z, an.x, nin0, nout0);
-            const int m1 = tvam_axis_steps(tau_x, ff.w, an.y, nin1, nout1);
-            const int vx = svx + stx * n0, vy = svy + sty * n1;
-            const int qd = (stx < 0 ? 2 : 0) + (sty < 0 ? 1 : 0);
-            const int tw = (qd == 0 || qd == 3) ? tw1 : tw2;
-            const int res = ((vy - y0 + 1) * tw + (vx - x0 + 1)) & 15;
-            q[qd].push_back({ev, std::abs(m0 - n0) + std::abs(m1 - n1) + 1, res});
-        }
-        for (int qd = 0; qd < 4; ++qd) {
-            std::vector<Ray>& v = q[qd];
-            for (size_t b0 = 0; b0 < v.size(); b0 += (size_t)W) {
-                std::vector<Ray> blk(v.begin() + (std::ptrdiff_t)b0, v.begin() + (std::ptrdiff_t)std::min(v.size(), b0 + (size_t)W));
-                if (qsort)
-                    std::stable_sort(blk.begin(), blk.end(), [](const Ray& a, const Ray& b) { return a.len > b.len; });
-                std::vector<char> used(blk.size(), 0);
-                size_t left = blk.size(), first = 0;
-                while (left > 0) {
-                    uint32_t wave[64];
-                    for (int l = 0; l < 64; ++l) wave[l] = PAD;
-                    for (int g = 0; g < 4 && left > 0; ++g) {
-                        int pick[16], np = 0;
-                        unsigned seen = 0;
-                        for (size_t i = first; i < blk.size() && np < 16; ++i)
-                            if (qdeal && !used[i] && !(seen >> blk[i].res & 1u)) {
-                                seen |= 1u << blk[i].res;
-                                pick[np++] = (int)i;
-                                used[i] = 1;
-                            }
-                        for (size_t i = first; i < blk.size() && np < 16; ++i)
-                            if (!used[i]) {
-                                pick[np++] = (int)i;
-                                used[i] = 1;
-                            }
-                        for (int j = 0; j < np; ++j) wave[G[g][j]] = blk[(size_t)pick[j]].e;
-                        left -= (size_t)np;
-                        while (first < blk.size() && used[first]) ++first;
-                    }
-                    out.insert(out.end(), wave, wave + 64);
-                }
-            }
-            qoff[(size_t)tile * 4 + qd + 1] = (int64_t)out.size();
-        }
-    }
-    int rc;
-    if ((rc = upload(&p->d_adjq_slots, out)) || (rc = upload(&p->d_adjq_off, qoff))) return rc;
-    p->pl.adj_qslots = p->d_adjq_slots;
-    p->pl.adj_qoff = p->d_adjq_off;
-    p->pl.adj_quad = 1;
-    return 0;
-}
-
-// Planar adjoint ray pairs per tile (TvamPlanar::adj_pair).  A lane marches two rays of one
-// angle: its in-tile chords through a square tile are a trapezoid in column order (0.68 of the
-// lanes busy with one ray per lane on config 2), and ray j plus ray j + ceil(n / 2) of the angle's n
-// crossing rays have complementary lengths, while neighbouring lanes keep neighbouring columns in
-// both halves (the march's LDS reads stay coherent).  Rays that miss the tile (the kernel would
-// skip them) are left out; the exact crossing test is the kernel's closed-form resume.
-static int adj_pair_lists(tvam_plan* p) {
-    const TvamConsts& k = p->k;
-    const TvamTiles& t = p->tiles;
-    const int ns = p->pl.ns, ntiles = t.ntx * t.nty;
-    const size_t nrec = (size_t)ns * k.crop_x;
-    std::vector<float4> rf(nrec), rg, ang((size_t)std::max(ns, 1));
-    std::vector<int32_t> ri(nrec);
-    std::vector<int64_t> off((size_t)ntiles + 1);
-    hipError_t e;
-    if ((e = hipMemcpy(rf.data(), p->d_pl_rec_f, nrec * sizeof(float4), hipMemcpyDeviceToHost)) != hipSuccess ||
-        (e = hipMemcpy(ri.data(), p->d_pl_rec_i, nrec * sizeof(int32_t), hipMemcpyDeviceToHost)) != hipSuccess ||
-        (e = hipMemcpy(off.data(), p->d_slot_off, off.size() * sizeof(int64_t), hipMemcpyDeviceToHost)) != hipSuccess ||
-        (ns > 0 && (e = hipMemcpy(ang.data(), p->d_ang, (size_t)ns * sizeof(float4), hipMemcpyDeviceToHost)) != hipSuccess))
-        return hip_fail(e, "hipMemcpy (adjoint pairs)");
-    if (p->d_pl_rec_g) {
-        rg.resize(nrec);
-        if ((e = hipMemcpy(rg.data(), p->d_pl_rec_g, nrec * sizeof(float4), hipMemcpyDeviceToHost)) != hipSuccess)
-            return hip_fail(e, "hipMemcpy (adjoint pairs)");
-    }
-    std::vector<uint32_t> slots((size_t)off[ntiles]);
-    if (!slots.empty() && (e = hipMemcpy(slots.data(), p->d_slots, slots.size() * sizeof(uint32_t),
-                                         hipMemcpyDeviceToHost)) != hipSuccess)
-        return hip_fail(e, "hipMemcpy (adjoint pairs)");
-    constexpr uint32_t PAD = 0xffffffffu;
-    std::vector<uint32_t> out;
-    std::vector<int64_t> poff((size_t)ntiles + 1, 0);
-    std::vector<uint32_t> run;
-    for (int tile = 0; tile < ntiles; ++tile) {
-        const int x0 = (tile % t.ntx) * t.tsx, y0 = (tile / t.ntx) * t.tsy;
-        const int x1 = std::min(x0 + t.tsx, k.res[0]), y1 = std::min(y0 + t.tsy, k.res[1]);
-        auto flush = [&]() {
-            const size_t n = run.size(), h = (n + 1) / 2;
-            for (size_t j = 0; j < h; ++j) {
-                out.push_back(run[j]);
-                out.push_back(j + h < n ? run[j + h] : PAD);
-            }
-            run.clear();
-        };
-        int cur = -1;
-        for (int64_t j = off[tile]; j < off[tile + 1]; ++j) {
-            const uint32_t ev = slots[(size_t)j];
-            const int al = (int)(ev >> 16), colc = (int)(ev & 0xffffu);
-            if (al != cur) {
-                flush();
-                cur = al;
-            }
-            const size_t r = (size_t)al * k.crop_x + colc;
-            const int rv = ri[r];
-            if (rv < 0) continue;  // misses the vial / grid
-            const float4 ff = rf[r];
-            float4 an = ang[(size_t)al];
-            if (!rg.empty()) {
-                const float4 gg = rg[r];
-                an = make_float4(std::fabs(gg.x), std::fabs(gg.y), gg.x < 0.0f ? -1.0f : 1.0f, gg.y < 0.0f ? -1.0f : 1.0f);
-            }
-            const int svx = rv & 0xffff, svy = rv >> 16, stx = (int)an.z, sty = (int)an.w;
-            float tin0, tout0, tin1, tout1;
-            int nin0, nout0, nin1, nout1;
-            tvam_axis_window(svx, stx, ff.z, an.x, x0, x1, tin0, tout0, nin0, nout0);
-            tvam_axis_window(svy, sty, ff.w, an.y, y0, y1, tin1, tout1, nin1, nout1);
-            const float tau_e = std::max(std::max(tin0, tin1), 0.0f);
-            const float tau_x = std::min(std::min(tout0, tout1), ff.y);
-            if (!(tau_e < tau_x)) continue;  // does not cross this tile
-            run.push_back(ev);
-        }
-        flush();
-        poff[(size_t)tile + 1] = (int64_t)out.size();
-    }
-    int rc;
-    if ((rc = upload(&p->d_adjp_slots, out)) || (rc = upload(&p->d_adjp_off, poff))) return rc;
-    p->pl.adj_pslots = p->d_adjp_slots;
-    p->pl.adj_poff = p->d_adjp_off;
-    p->pl.adj_pair = 1;
-    return 0;
-}
 
 static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     const tvam_desc& d = p->desc;
@@ -607,22 +404,9 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     p->pl.max_rows_chunk = mrc;
     p->pl.max_rows_slice = 0;
     for (int z = 0; z < k.nz; ++z) p->pl.max_rows_slice = std::max(p->pl.max_rows_slice, off[z + 1] - off[z]);
-    p->planar_rz = env_int("TVAM_RAY_FWD_Z", 4);
-    if (p->planar_rz != 4 && p->planar_rz != 8) p->planar_rz = 4;
-    p->pl.adj_pitch = p->tiles.tsx + 2 + std::max(0, env_int("TVAM_ADJ_PITCH_PAD", 0));
-    // quadrant lists (adj_quadrant_lists, TVAM_ADJ_QUAD=0: one list in (angle, column) order): row
-    // pitches = +1 / -1 (mod 16), at least the tile + guard band
-    p->pl.adj_quad = env_int("TVAM_ADJ_QUAD", 0) != 0 && env_int("TVAM_ADJ_PLANES", 1) != 0;
-    p->pl.adj_pitch2 = p->pl.adj_pitch;
+    p->planar_rz = 4;
+    p->pl.adj_pitch = p->tiles.tsx + 2;
     p->pl.rayfwd_pitch = p->pl.adj_pitch;
-    if (p->pl.adj_quad) {
-        const int w = p->tiles.tsx + 2;
-        p->pl.adj_pitch = w + ((1 - w) % 16 + 16) % 16;    // = 1 (mod 16)
-        p->pl.adj_pitch2 = w + ((15 - w) % 16 + 16) % 16;  // = 15 (mod 16)
-    }
-    p->pl.adj_planes = env_int("TVAM_ADJ_PLANES", 1);
-    p->pl.adj_w2 = env_int("TVAM_ADJ_W2", 1);
-    p->pl.xcd_remap = env_int("TVAM_XCD_REMAP", 1);
     // Refracted rays are not parallel, and a DMD much finer than the voxels
     // overflows the voxel-driven forward's column window: there the forward
     // is ray-driven like the adjoint (one record per (angle, column), shared
@@ -642,16 +426,14 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
         // split 8, 1.01 / 0.57 ms at 4, 1.00 / 0.59 ms at 2 (profiles/r03/s2/slab_split_ab.jsonl)
         // 1024 threads at Z = 8: the 71 KB tile admits 2 workgroups per CU = 8 waves per SIMD
         const int ant = env_int("TVAM_ADJ_NT", p->planar_az >= 8 ? 1024 : 512);
-        p->pl.adj_nt = ant == 256 || ant == 1024 ? ant : 512;
+        p->pl.adj_nt = ant == 1024 ? 1024 : 512;
         const int64_t want = p->pl.adj_nt >= 1024 ? 8192 : 16384;
-        const int64_t nwg = (int64_t)p->tiles.ntx * p->tiles.nty * ((k.nz + p->planar_az - 1) / p->planar_az) *
-                            (p->pl.adj_quad ? 4 : 1);  // quadrant lists: one workgroup per quadrant
+        const int64_t nwg = (int64_t)p->tiles.ntx * p->tiles.nty * ((k.nz + p->planar_az - 1) / p->planar_az);
         int split = (int)std::min<int64_t>(4, std::max<int64_t>(1, (want + nwg - 1) / std::max<int64_t>(nwg, 1)));
         const int es = env_int("TVAM_ADJ_SPLIT", 0);
         if (es >= 1 && es <= 64) split = es;
         p->pl.adj_split = split;
-        p->pl.adj_prefetch = env_int("TVAM_ADJ_PREFETCH", 1);
-        p->pl.rayfwd_nt = env_int("TVAM_RAYFWD_NT", 512) == 1024 ? 1024 : 512;
+        p->pl.rayfwd_nt = 512;
     }
     if (tvam_planar_rayfwd_lds(p->pl, p->tiles, p->planar_rz) > 160 * 1024) p->planar_rz = 4;
     if (tvam_planar_rayfwd_lds(p->pl, p->tiles, p->planar_rz) > 160 * 1024) return 0;
@@ -676,7 +458,7 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
         (e = hipMalloc((void**)&p->d_fscale, 2 * sizeof(float))) != hipSuccess)
         return hip_fail(e, "hipMalloc (planar tables)");
     // refracting vial: the voxel-driven forward over per-column chords (tvam_refr_model_kernel)
-    const bool try_refr = p->cyl && !(d.flags & TVAM_FLAG_RAY_FWD) && env_int("TVAM_REFR_FWD", 1) && ns > 0;
+    const bool try_refr = p->cyl && !(d.flags & TVAM_FLAG_RAY_FWD) && ns > 0;
     float4* d_chord = nullptr;
     if (try_refr && ((e = hipMalloc((void**)&p->d_pl_vox2, nrec * sizeof(float4))) != hipSuccess ||
                      (e = hipMalloc((void**)&d_chord, nrec * sizeof(float4))) != hipSuccess)) {
@@ -714,15 +496,11 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
         p->pl.chord = nullptr;
         if (rc) return rc;
     }
-    if (p->pl.adj_quad && (rc = adj_quadrant_lists(p))) return rc;
-    // ray pairs (TVAM_ADJ_PAIR=1; off by default: config 2 adjoint 3.65 -> 3.90 ms, the two halves'
-    // lanes drift apart and the march's LDS reads lose their coherence, profiles/r04/ab2/proj_ab.jsonl)
-    if (!p->pl.adj_quad && env_int("TVAM_ADJ_PAIR", 0) && (rc = adj_pair_lists(p))) return rc;
     // the adjoint over slice-invariant visit lists (tvam_adjlist.hip), when they fit in a quarter of
     // the free device memory (config 2: ~0.5 GB); else the tile adjoint re-derives the visits.
     // Groups = (tile, step quadrant, part), parts until the grid holds >= 8K workgroups.
     p->pl.adjl_ngroups = 0;
-    if (p->planar_az == 8 && ns > 0 && !p->pl.adj_quad && !p->pl.adj_pair && env_int("TVAM_ADJ_LISTS", 1)) {
+    if (p->planar_az == 8 && ns > 0 && env_int("TVAM_ADJ_LISTS", 1)) {
         size_t fr = 0, tot = 0;
         if ((e = hipMemGetInfo(&fr, &tot)) != hipSuccess) return hip_fail(e, "hipMemGetInfo");
         p->pl.adjl_z = env_int("TVAM_ADJL_Z", 16) == 8 ? 8 : 16;
@@ -756,7 +534,7 @@ static int fwd_buffers(tvam_plan* p) {
     // every angle: at 3 resident workgroups per CU, 1250 of them (400^2 film,
     // 50 slices) fill 1.6 rounds of the 768 slots.  Split the angles into parts
     // until >= 4 rounds; the partial doses are summed in fixed order.
-    const int tw = p->pl.fwd_px == 2 ? 32 : 16;
+    const int tw = 16;
     const int64_t nwg = (int64_t)((k.res[0] + tw - 1) / tw) * ((k.res[1] + 15) / 16) *
                         ((k.nz + p->planar_fz - 1) / p->planar_fz);
     int parts = (int)std::min<int64_t>(4, std::max<int64_t>(1, (4 * 768 + nwg - 1) / std::max<int64_t>(nwg, 1)));
@@ -797,7 +575,7 @@ static int choose_fwd_z(tvam_plan* p) {
     if (p->planar_fz == 0) {
         int best = 8;
         int64_t bcost = INT64_MAX;
-        const bool deep = env_int("TVAM_FWD_BIN", 1) != 0 && env_int("TVAM_FWD_DEEP", 1) != 0;
+        const bool deep = env_int("TVAM_FWD_BIN", 1) != 0;
         for (int Z : {52, 40, 32, 28, 24, 16, 8}) {
             if ((Z > 32 && !deep) || !tvam_planar_fwd_fits(p->pl, Z)) continue;
             // deep slabs (Z > 32: 4 instead of 5 waves per SIMD) measured ~4 % slower per slice at 400^3
@@ -891,26 +669,8 @@ static int refr_fwd_setup(tvam_plan* p, const std::vector<int32_t>& off) {
         std::memcpy(&cb, &mdl[2 * i + 1].z, sizeof(int));
         (void)cb;
     }
-    if (env_int("TVAM_DEBUG_REFR", 0)) {
-        std::vector<int64_t> hist(16, 0);
-        double wsum = 0.0, wave_nc = 0.0;
-        for (size_t i = 0; i < nm; ++i) {
-            int nc, ncw;
-            std::memcpy(&nc, &mdl[2 * i + 1].y, sizeof(int));
-            std::memcpy(&ncw, &mdl[2 * i + 1].w, sizeof(int));
-            hist[std::min(nc, 15)]++;
-            wsum += mdl[2 * i + 1].x;
-            for (int w = 0; w < 4; ++w) wave_nc += (double)((ncw >> (8 * w)) & 0xff);
-        }
-        std::fprintf(stderr, "refr forward: window %d columns, candidates max %d, mean half width %.3f, mean per-wave "
-                     "candidates %.3f; tile nc histogram:", ncm, ncmax_c, wsum / (double)nm, wave_nc / (4.0 * (double)nm));
-        for (int i = 0; i < 16; ++i)
-            if (hist[i]) std::fprintf(stderr, " %d:%lld", i, (long long)hist[i]);
-        std::fprintf(stderr, "\n");
-    }
     TvamPlanar save = p->pl;
     p->pl.fwd_refr = 1;
-    p->pl.fwd_px = 1;
     p->pl.ncmax = ncm;
     p->pl.fwd_nc = ncmax_c;
     p->pl.fwd_ab = 2;
@@ -922,15 +682,7 @@ static int refr_fwd_setup(tvam_plan* p, const std::vector<int32_t>& off) {
     }
     // clamp windows into the binned patterns' zero pads (bin_pad = ncmax on either side)
     bool changed = false;
-    const bool wave_nc = env_int("TVAM_REFR_WAVE_NC", 1) != 0;  // 0: every wave runs the tile's count (A/B)
     for (size_t i = 0; i < nm; ++i) {
-        if (!wave_nc) {
-            int nc;
-            std::memcpy(&nc, &mdl[2 * i + 1].y, sizeof(int));
-            const int ncw = nc | (nc << 8) | (nc << 16) | (nc << 24);
-            std::memcpy(&mdl[2 * i + 1].w, &ncw, sizeof(int));
-            changed = true;
-        }
         int cb;
         std::memcpy(&cb, &mdl[2 * i + 1].z, sizeof(int));
         const int cl = std::min(std::max(cb, -ncm), (int)d.crop_x);
@@ -989,8 +741,8 @@ static bool planar_fwd_setup(tvam_plan* p, const std::vector<float2>& cs, const 
     const int nc = (int)std::floor(2.0 * wmax + 1e-3) + 1;
     // per (16 px x 16 tile, angle): the first staged column and the window width that holds every
     // voxel's candidates (px = 2: 32 x 16 tiles of voxel pairs)
-    auto windows = [&](int px, std::vector<int32_t>& fcb) {
-        const int tw = 16 * px;
+    auto windows = [&](std::vector<int32_t>& fcb) {
+        const int tw = 16;
         const int ntx = (k.res[0] + tw - 1) / tw, nty = (k.res[1] + 15) / 16;
         fcb.assign((size_t)ntx * nty * std::max(ns, 1), 0);
         int need = 0;
@@ -1013,43 +765,18 @@ static bool planar_fwd_setup(tvam_plan* p, const std::vector<float2>& cs, const 
         return need;
     };
     std::vector<int32_t> fcb;
-    const int need = windows(1, fcb);
+    const int need = windows(fcb);
     p->pl.marg_u = (float)marg_u;
     p->pl.u0 = u0;
     p->pl.fwd_nc = nc;
     p->pl.ncmax = need;
-    p->pl.fwd_px = 1;
     {
         bool multi = false;
         for (int z = 0; z < k.nz; ++z) multi |= off[z + 1] - off[z] > 1;
         p->pl.fwd_multi = multi ? 1 : 0;
     }
-    {
-        const int ab = env_int("TVAM_FWD_AB", 2);
-        p->pl.fwd_ab = (ab >= 1 && ab <= 4) ? ab : 2;
-    }
+    p->pl.fwd_ab = 2;  // two angles per barrier (4.34 -> 3.80 ms on config 2)
     if (!choose_fwd_z(p)) return false;
-    // voxel pairs (TVAM_FWD_PX=2; off by default: config 2 forward 3.07 -> 3.92 ms, the pair's 64
-    // accumulators leave 3 waves per SIMD instead of 5, profiles/r04/ab2/proj_ab.jsonl) where the
-    // depth has a pair variant (Z <= 32, binned staging of <= 2 float4 per thread, 2 angles per
-    // barrier) and the pair's union of candidates fits the kernel's NC + 2
-    if (env_int("TVAM_FWD_PX", 1) == 2 && p->planar_fz <= 32 && env_int("TVAM_FWD_BIN", 1) && p->pl.fwd_ab == 2) {
-        double dmax = 0.0;
-        for (int i = 0; i < ns; ++i) dmax = std::max(dmax, std::fabs((double)fang[2 * (size_t)i].x) * k.h[0]);
-        std::vector<int32_t> fcb2;
-        const int need2 = windows(2, fcb2);
-        // the pair variant stages binned slabs only: <= 2 float4 per thread (fwd_buffers), one record
-        // loader per window column, 1..4 candidates per voxel
-        const int need1 = p->pl.ncmax;
-        p->pl.fwd_px = 2;
-        p->pl.ncmax = need2;
-        if (dmax <= 1.0 + 1e-6 && tvam_planar_fwd_fits(p->pl, p->planar_fz)) {
-            fcb = std::move(fcb2);
-        } else {
-            p->pl.fwd_px = 1;
-            p->pl.ncmax = need1;
-        }
-    }
     p->pl.fwd_pf = (p->pl.ncmax * p->planar_fz + 255) / 256 <= 2 ? 2 : 4;
     p->fwd_ang_h = std::move(fang);
     p->fwd_cb_h = std::move(fcb);
@@ -1496,8 +1223,6 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
             max_nrt = std::max<int64_t>(max_nrt, (int64_t)per_tile[t].size());
         }
     } else {
-    const bool adj_order = env_int("TVAM_ADJ_ORDER", 0) != 0 && d.regular_sampling;
-    const int adj_tw = tsx + 2 + std::max(0, env_int("TVAM_ADJ_PITCH_PAD", 0));  // = pl.adj_pitch
     for (int ty = 0; ty < nty; ++ty)
         for (int tx = 0; tx < ntx; ++tx) {
             int tile = ty * ntx + tx;
@@ -1518,50 +1243,6 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
                 int ch = std::min((int)std::ceil(c_hi) + 1 - d.crop_offset_x, d.crop_x - 1);
                 // (column order: ordering by in-tile chord length, as behind refracting vials, made the
                 // planar adjoint slower, 3.82 -> 3.96 ms on config 2)
-                if (adj_order && cl <= ch) {
-                    // TVAM_ADJ_ORDER=1: the columns dealt round-robin over the 16 LDS bank groups of
-                    // their tile-entry voxel (the planar adjoint's [z/4][voxel][4] tile: a 16-lane
-                    // group of a ds_read_b128 is conflict-free when its voxels differ mod 16), so
-                    // that 16 consecutive lanes start in 16 different groups
-                    std::vector<int> bucket[16];
-                    const double dxr = -c, dyr = -s;
-                    for (int col = cl; col <= ch; ++col) {
-                        const double lat = ex * (0.5 - ((double)(col + d.crop_offset_x) + 0.5) / W);
-                        const double px0 = lat * s, py0 = -lat * c;
-                        double tin = -1e300, tout = 1e300;
-                        auto slab = [&](double o, double dd, double a, double b) {
-                            if (std::fabs(dd) < 1e-12) {
-                                if (o < a || o > b) tout = -1e300;
-                                return;
-                            }
-                            const double t1 = (a - o) / dd, t2 = (b - o) / dd;
-                            tin = std::max(tin, std::min(t1, t2));
-                            tout = std::min(tout, std::max(t1, t2));
-                        };
-                        slab(px0, dxr, X0, X1);
-                        slab(py0, dyr, Y0, Y1);
-                        int grp = 0;
-                        if (tin < tout) {
-                            const double te = tin + 1e-6 * std::min(k.h[0], k.h[1]);
-                            const int x0v = tx * tsx, y0v = ty * tsy;
-                            int ix = (int)std::floor((px0 + te * dxr - (double)k.bmin[0]) / k.h[0]);
-                            int iy = (int)std::floor((py0 + te * dyr - (double)k.bmin[1]) / k.h[1]);
-                            ix = std::min(std::max(ix, x0v), std::min(x0v + tsx, k.res[0]) - 1);
-                            iy = std::min(std::max(iy, y0v), std::min(y0v + tsy, k.res[1]) - 1);
-                            grp = ((iy - y0v + 1) * adj_tw + (ix - x0v + 1)) & 15;
-                        }
-                        bucket[grp].push_back(col);
-                    }
-                    for (size_t r = 0;; ++r) {
-                        bool any = false;
-                        for (int b = 0; b < 16; ++b)
-                            if (r < bucket[b].size()) {
-                                slots.push_back(((uint32_t)i << 16) | (uint32_t)bucket[b][r]);
-                                any = true;
-                            }
-                        if (!any) break;
-                    }
-                } else
                 for (int col = cl; col <= ch; ++col) slots.push_back(((uint32_t)i << 16) | (uint32_t)col);
             }
             slot_off[(size_t)tile + 1] = (int64_t)slots.size();

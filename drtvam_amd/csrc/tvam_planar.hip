@@ -136,18 +136,10 @@ __host__ __device__ constexpr int tvam_fwd_zs(int Z) { return ((Z + 4) / 4) % 2 
 // per-angle constants are the (tile, angle) model of the chord index u (tvam_refr_model_kernel),
 // and each voxel visits a per-(tile, angle) number of candidates (the same for the whole
 // workgroup) from ceil(u - w).
-//
-// PX = 2: a thread owns two neighbouring voxel columns (ix, ix + 1) of a 32 x 16 tile.  Their
-// candidate columns overlap (their lateral centres are |s du| h <= 1 column apart), so each staged
-// slab a candidate needs is read from LDS once for both voxels: per angle a wave reads the union
-// of its pairs' candidates (NC + 1, at most NC + 2) for 128 voxel columns instead of NC for 64.
-// Each voxel's sum runs over the same candidates in the same order as PX = 1 (the union's extra
-// columns miss the voxel: weight exactly 0), so the dose is bit-identical.
-template <int Z, int NC, bool MULTI, int PF, int AB, bool BIN = false, bool REFR = false, int PX = 1>
+template <int Z, int NC, bool MULTI, int PF, int AB, bool BIN = false, bool REFR = false>
 __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, TvamPlanar pl,
                                                                   const float* __restrict__ pat,
                                                                   float* __restrict__ dose) {
-    static_assert(PX == 1 || (PX == 2 && !REFR), "voxel pairs: straight rays only");
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int ncm = pl.ncmax;
     constexpr int RW = REFR ? 2 : 1;  // records (float4) per staged column
@@ -164,7 +156,7 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
     int* s_cb = reinterpret_cast<int*>(s_ang + 2 * (TVAM_ACH + 4)); // [TVAM_ACH + 4]
     int* s_row = s_cb + (TVAM_ACH + 4);                            // [Z]: the slice's row, -1 none, -2 several
 
-    const int ntx = (k.res[0] + 16 * PX - 1) / (16 * PX), nty = (k.res[1] + 15) >> 4;
+    const int ntx = (k.res[0] + 15) >> 4, nty = (k.res[1] + 15) >> 4;
     // slice chunks of this launch: [fwd_zc0, fwd_zc0 + fwd_nzc) (tvam_forward_slices), else all
     const int nzc = pl.fwd_nzc > 0 ? pl.fwd_nzc : (k.nz + Z - 1) / Z;
     const int ntiles = ntx * nty, nwg1 = ntiles * nzc;
@@ -172,11 +164,8 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
     // XCD-aware order: workgroup b runs on XCD b % 8; give each XCD a contiguous
     // run of (z-chunk, tile) pairs so the tiles sharing a z-chunk's pattern rows
     // share that XCD's L2
-    int L = blockIdx.x;
-    if (pl.xcd_remap) {
-        const int per = (int)(gridDim.x >> 3);
-        L = (int)(blockIdx.x & 7) * per + (int)(blockIdx.x >> 3);
-    }
+    const int L0 = (int)(gridDim.x >> 3);
+    int L = (int)(blockIdx.x & 7) * L0 + (int)(blockIdx.x >> 3);
     if (L >= nwg) return;
     // angle part [ab, ae) of this workgroup (thin slabs: parts > 1 workgroups per
     // (tile, chunk), partial doses summed in fixed order by tvam_fwd_parts_kernel)
@@ -185,15 +174,13 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
     const int ab = (int)(((int64_t)pl.ns * part) / parts), ae = (int)(((int64_t)pl.ns * (part + 1)) / parts);
     const int tile = L % ntiles;
     const int bx = tile % ntx, by = tile / ntx;
-    const int ix = bx * 16 * PX + PX * (threadIdx.x & 15), iy = by * 16 + (threadIdx.x >> 4);
+    const int ix = bx * 16 + (threadIdx.x & 15), iy = by * 16 + (threadIdx.x >> 4);
     const int z0 = ((pl.fwd_nzc > 0 ? pl.fwd_zc0 : 0) + L / ntiles) * Z;
     const float hx = k.h[0], hy = k.h[1];
     // voxel edges exactly as the DDA places them (bmin + i * h, sensor.py:357)
     const float X0 = k.bmin[0] + (float)ix * hx, X1 = k.bmin[0] + (float)(ix + 1) * hx;
     const float Y0 = k.bmin[1] + (float)iy * hy, Y1 = k.bmin[1] + (float)(iy + 1) * hy;
     const float Xc = k.bmin[0] + ((float)ix + 0.5f) * hx, Yc = k.bmin[1] + ((float)iy + 0.5f) * hy;
-    // the pair's second voxel (PX = 2): x edges X1, X2, centre Xc1
-    const float X2 = k.bmin[0] + (float)(ix + 2) * hx, Xc1 = k.bmin[0] + ((float)(ix + 1) + 0.5f) * hx;
     const float u0 = pl.u0;
     const int32_t* cbt = pl.fwd_cb + (size_t)tile * pl.ns;  // first window column per angle
 
@@ -319,11 +306,9 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
         if ((int)threadIdx.x < ncm * RW) reinterpret_cast<pl_f4*>(s_r)[buf * ncm * RW + threadIdx.x] = rv;
     };
 
-    float acc[Z], acc1[PX == 2 ? Z : 1];
+    float acc[Z];
 #pragma unroll
     for (int z = 0; z < Z; ++z) acc[z] = 0.0f;
-#pragma unroll
-    for (int z = 0; z < (PX == 2 ? Z : 1); ++z) acc1[z] = 0.0f;
 
     auto compute_refr = [&](int al, int buf) {
         const int cb = s_cb[al - tbase];
@@ -373,67 +358,9 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
         for (int c = 2; c < nc; ++c) accumulate(jj0 + c, weight(jj0 + c));
     };
 
-    auto compute_pair = [&](int al, int buf) __attribute__((always_inline)) {
-        const int cb = s_cb[al - tbase];
-        const float* sp = s_p + buf * bstride;
-        const float4* sr = s_r + buf * ncm;
-        const float4 g0 = s_ang[2 * (al - tbase)], g1 = s_ang[2 * (al - tbase) + 1];
-        const int fl = __float_as_int(g1.y);
-        // each voxel's candidates exactly as PX = 1 forms them, then their union [lo, hi]
-        const float ua = fmaf(Xc, g0.x, fmaf(Yc, g0.y, u0)), ub = fmaf(Xc1, g0.x, fmaf(Yc, g0.y, u0));
-        const int ja = (int)ceilf(ua - g1.x) - cb, jb = (int)ceilf(ub - g1.x) - cb;
-        const int lo = max(min(ja, jb), 0), hi = min(max(ja, jb) + NC - 1, ncm - 1);
-        const float xa = X0 * g0.z, xb = X1 * g0.z, xc = X2 * g0.z, ya = Y0 * g0.w, yb = Y1 * g0.w;
-        const float xn0 = fminf(xa, xb), xf0 = fmaxf(xa, xb), xn1 = fminf(xb, xc), xf1 = fmaxf(xb, xc);
-        const float yn = fminf(ya, yb), yf = fmaxf(ya, yb);
-        auto visit = [&](int j) __attribute__((always_inline)) {
-            const int jc = min(lo + j, ncm - 1);
-            float4 q = sr[jc];
-            asm volatile("" : "+v"(q.w));  // keep the 16-byte LDS read (ds_read_b128, not b96)
-            float tnx0 = xn0 + q.x, tfx0 = xf0 + q.x, tnx1 = xn1 + q.x, tfx1 = xf1 + q.x;
-            float tny = yn + q.y, tfy = yf + q.y;
-            if (!(fl & 1)) {  // |d.x| <= 1e-8: the DDA never steps x (q.x = its voxel index)
-                tnx0 = (float)ix == q.x ? -TVAM_INF : TVAM_INF;
-                tnx1 = (float)(ix + 1) == q.x ? -TVAM_INF : TVAM_INF;
-                tfx0 = tfx1 = TVAM_INF;
-            }
-            if (!(fl & 2)) {
-                tny = (float)iy == q.y ? -TVAM_INF : TVAM_INF;
-                tfy = TVAM_INF;
-            }
-            const float tin0 = fmaxf(fmaxf(tnx0, tny), 0.0f), tout0 = fminf(fminf(tfx0, tfy), q.z);
-            const float tin1 = fmaxf(fmaxf(tnx1, tny), 0.0f), tout1 = fminf(fminf(tfx1, tfy), q.z);
-            const float e0 = pl_exp2(k.nsig2 * tin0) - pl_exp2(k.nsig2 * tout0);
-            const float e1 = pl_exp2(k.nsig2 * tin1) - pl_exp2(k.nsig2 * tout1);
-            const bool in = lo + j <= hi;
-            const float w0 = (in && tout0 > tin0) ? e0 : 0.0f, w1 = (in && tout1 > tin1) ? e1 : 0.0f;
-            if (w0 != 0.0f || w1 != 0.0f) {
-#pragma unroll
-                for (int z4 = 0; z4 < Z / 4; ++z4) {
-                    const float4 p4 = reinterpret_cast<const float4*>(sp + jc * ZS)[z4];
-                    acc[4 * z4 + 0] = fmaf(w0, p4.x, acc[4 * z4 + 0]);
-                    acc[4 * z4 + 1] = fmaf(w0, p4.y, acc[4 * z4 + 1]);
-                    acc[4 * z4 + 2] = fmaf(w0, p4.z, acc[4 * z4 + 2]);
-                    acc[4 * z4 + 3] = fmaf(w0, p4.w, acc[4 * z4 + 3]);
-                    acc1[4 * z4 + 0] = fmaf(w1, p4.x, acc1[4 * z4 + 0]);
-                    acc1[4 * z4 + 1] = fmaf(w1, p4.y, acc1[4 * z4 + 1]);
-                    acc1[4 * z4 + 2] = fmaf(w1, p4.z, acc1[4 * z4 + 2]);
-                    acc1[4 * z4 + 3] = fmaf(w1, p4.w, acc1[4 * z4 + 3]);
-                }
-            }
-        };
-#pragma unroll
-        for (int j = 0; j <= NC; ++j) visit(j);
-        if (__ballot(hi - lo > NC)) visit(NC + 1);  // a union of NC + 2 (|u_b - u_a| rounded past 1)
-    };
-
     auto compute = [&](int al, int buf) __attribute__((always_inline)) {
         if constexpr (REFR) {
             compute_refr(al, buf);
-            return;
-        }
-        if constexpr (PX == 2) {
-            compute_pair(al, buf);
             return;
         }
         const int cb = s_cb[al - tbase];
@@ -567,11 +494,6 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
 #pragma unroll
         for (int z = 0; z < Z; ++z)
             if (z0 + z < k.nz) out[(size_t)(z0 + z) * plane + (size_t)iy * k.res[0] + ix] = acc[z] * scale;
-        if (PX == 2 && ix + 1 < k.res[0]) {
-#pragma unroll
-            for (int z = 0; z < (PX == 2 ? Z : 0); ++z)
-                if (z0 + z < k.nz) out[(size_t)(z0 + z) * plane + (size_t)iy * k.res[0] + ix + 1] = acc1[z] * scale;
-        }
     }
 }
 
@@ -696,7 +618,7 @@ bool tvam_planar_fwd_fits(const TvamPlanar& pl, int Z) {
     if (pl.fwd_refr)  // two record loaders per window column; the binned staging only
         return 2 * pl.ncmax <= TVAM_PB && pl.ncmax * (Z / 4) <= 2 * TVAM_PB && pl.fwd_nc >= 1 &&
                pl.fwd_nc <= pl.ncmax && tvam_planar_fwd_lds(pl, Z) <= 64 * 1024;
-    if (Z > 32 || pl.fwd_px == 2)  // deep slabs, voxel pairs: the binned staging only (<= 2 float4 per thread and angle)
+    if (Z > 32)  // deep slabs: the binned staging only (<= 2 float4 per thread and angle)
         return pl.ncmax <= TVAM_PB && pl.ncmax * (Z / 4) <= 2 * TVAM_PB && pl.fwd_nc >= 1 && pl.fwd_nc <= 4 &&
                pl.fwd_nc <= pl.ncmax;
     return pl.ncmax <= TVAM_PB && pl.ncmax * Z <= TVAM_PF * TVAM_PB && pl.fwd_nc >= 1 && pl.fwd_nc <= 4 &&
@@ -844,16 +766,6 @@ static void launch_fwd(dim3 grid, size_t lds, hipStream_t stream, const TvamCons
                                pat, dose);
         return;
     }
-    if (Z <= 32 && pl.fwd_px == 2) {  // voxel pairs: binned staging, 2 angles per barrier
-        if (!pl.fwd_bin || pl.fwd_ab != 2) return;  // the plan only selects the instantiated variants
-        if (pl.fwd_pf == 1)
-            hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 1, 2, true, false, (Z <= 32 ? 2 : 1)>), grid,
-                               dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
-        else
-            hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 2, 2, true, false, (Z <= 32 ? 2 : 1)>), grid,
-                               dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
-        return;
-    }
     if (pl.fwd_bin && pl.fwd_pf == 1 && pl.fwd_ab == 1)
         hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 1, 1, true>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
     else if (pl.fwd_bin && pl.fwd_pf == 1)
@@ -896,14 +808,12 @@ static hipError_t tvam_launch_fwd_planar_z(dim3 grid, size_t lds, hipStream_t st
 
 hipError_t tvam_launch_fwd_planar(const TvamConsts& k, const TvamPlanar& pl, int Z, const float* pat, float* dose,
                                   hipStream_t stream) {
-    const int tw = pl.fwd_px == 2 ? 32 : 16;
-    if (pl.fwd_px == 2 && (!pl.fwd_bin || pl.fwd_ab != 2 || Z > 32 || pl.fwd_refr)) return hipErrorInvalidValue;
-    const int ntx = (k.res[0] + tw - 1) / tw, nty = (k.res[1] + 15) / 16;
+    const int ntx = (k.res[0] + 15) / 16, nty = (k.res[1] + 15) / 16;
     const int parts = pl.fwd_parts > 1 ? pl.fwd_parts : 1;
     if (parts > 1 && !pl.fwd_part) return hipErrorInvalidValue;
     const int nzc = pl.fwd_nzc > 0 ? pl.fwd_nzc : (k.nz + Z - 1) / Z;
     const unsigned nwg = (unsigned)(ntx * nty) * (unsigned)nzc * (unsigned)parts;
-    dim3 grid(pl.xcd_remap ? (nwg + 7) / 8 * 8 : nwg);
+    dim3 grid((nwg + 7) / 8 * 8);  // XCD-aware order (tvam_fwd_planar_kernel): a multiple of 8
     const size_t lds = tvam_planar_fwd_lds(pl, Z);
     if (pl.fwd_bin) {
         if (pl.bin_nz % Z != 0 || pl.bin_nz < k.nz) return hipErrorInvalidValue;
@@ -912,10 +822,7 @@ hipError_t tvam_launch_fwd_planar(const TvamConsts& k, const TvamPlanar& pl, int
         const int zhi = pl.fwd_nzc > 0 ? std::min(k.nz, (pl.fwd_zc0 + pl.fwd_nzc) * Z) : k.nz;
         const int b0 = zlo / 64, b1 = (zhi + 63) / 64;
         const dim3 bg((unsigned)((k.crop_x + 63) / 64), (unsigned)std::max(b1 - b0, 1), (unsigned)pl.ns);
-        static const bool bin1 = [] {  // TVAM_SLICE_BIN1=1: the one-float-per-thread binning (A/B, tests)
-            const char* v = getenv("TVAM_SLICE_BIN1");
-            return v && atoi(v) == 1;
-        }();
+        static const bool bin1 = tvam_knob("TVAM_SLICE_BIN1", 0) == 1;  // the one-float-per-thread binning (tests)
         if (!bin1 && k.crop_x % 4 == 0 && pl.bin_nz % 4 == 0 && ((uintptr_t)pat & 15u) == 0)
             hipLaunchKernelGGL(tvam_slice_bin4_kernel, bg, dim3(256), 0, stream, k, pl, pat, b0);
         else
@@ -971,36 +878,17 @@ __global__ __launch_bounds__(NT) void tvam_adj_planar_kernel(TvamConsts k, TvamP
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int tsx = tp.tsx, tsy = tp.tsy;
     const int tile_id = blockIdx.x, z0 = ((int)blockIdx.y + pl.adj_zc0) * Z;
-    // this workgroup's part of the tile's ray list: with quadrant lists (pl.adj_quad) blockIdx.z =
-    // split part * 4 + step quadrant, parts of whole waves, and the row pitch of the quadrant;
-    // else a part of the one (angle, column)-ordered list (a thin slab has few slice chunks:
-    // several workgroups then share one tile's rays, each ray once)
-    int tw = pl.adj_pitch;  // row pitch >= tsx + 2
-    const uint32_t* slots;
-    int gb, nrt;
-    if (pl.adj_quad) {
-        const int qd = (int)(blockIdx.z & 3u), part = (int)(blockIdx.z >> 2), nparts = (int)(gridDim.z >> 2);
-        if (qd == 1 || qd == 2) tw = pl.adj_pitch2;
-        const int64_t q0 = pl.adj_qoff[(size_t)tile_id * 4 + qd], q1 = pl.adj_qoff[(size_t)tile_id * 4 + qd + 1];
-        slots = pl.adj_qslots + q0;
-        const int nwv = (int)((q1 - q0) >> 6);
-        gb = (int)(((int64_t)nwv * part) / nparts) * 64;
-        nrt = (int)(((int64_t)nwv * (part + 1)) / nparts) * 64;
-    } else if (pl.adj_pair) {  // ray pairs (adj_pair_lists): parts of whole pairs
-        slots = pl.adj_pslots + pl.adj_poff[tile_id];
-        const int npair = (int)((pl.adj_poff[tile_id + 1] - pl.adj_poff[tile_id]) >> 1);
-        gb = (int)(((int64_t)npair * blockIdx.z) / gridDim.z) * 2;
-        nrt = (int)(((int64_t)npair * (blockIdx.z + 1)) / gridDim.z) * 2;
-    } else {
-        slots = tp.slots + tp.slot_off[tile_id];
-        const int nall = (int)(tp.slot_off[tile_id + 1] - tp.slot_off[tile_id]);
-        gb = (int)(((int64_t)nall * blockIdx.z) / gridDim.z);
-        nrt = (int)(((int64_t)nall * (blockIdx.z + 1)) / gridDim.z);
-    }
+    // this workgroup's part of the tile's ray list (a thin slab has few slice chunks: several
+    // workgroups then share one tile's rays, each ray once)
+    const int tw = pl.adj_pitch;  // row pitch >= tsx + 2
+    const uint32_t* slots = tp.slots + tp.slot_off[tile_id];
+    const int nall = (int)(tp.slot_off[tile_id + 1] - tp.slot_off[tile_id]);
+    const int gb = (int)(((int64_t)nall * blockIdx.z) / gridDim.z);
+    const int nrt = (int)(((int64_t)nall * (blockIdx.z + 1)) / gridDim.z);
     if (gb >= nrt) return;  // (uniform over the workgroup)
     const int th = tsy + 2;
     float* tile = reinterpret_cast<float*>(smem);
-    int* s_roff = reinterpret_cast<int*>(tile + (size_t)max(pl.adj_pitch, pl.adj_pitch2) * th * Z);  // [Z + 1] CSR
+    int* s_roff = reinterpret_cast<int*>(tile + (size_t)pl.adj_pitch * th * Z);  // [Z + 1] CSR
     int* s_rows = s_roff + Z + 1;                                       // [pl.max_rows_chunk]
 
     const int x0 = (tile_id % tp.ntx) * tsx, y0 = (tile_id / tp.ntx) * tsy;
@@ -1035,10 +923,8 @@ __global__ __launch_bounds__(NT) void tvam_adj_planar_kernel(TvamConsts k, TvamP
 
     // PF: a two-stage software pipeline over this lane's rays -- the slot of ray
     // k + 2 and the records of ray k + 1 are loaded while ray k marches.  A lane's rays are list
-    // entries gb + lane + q NT, or with ray pairs (pl.adj_pair) the pairs gb + 2 lane + 2 q NT
-    // and + 1 (a long chord and a short one of the same angle: balanced lanes)
-    const bool pair = pl.adj_pair != 0 && !pl.adj_quad;
-    auto at = [&](int q) { return pair ? gb + 2 * (int)threadIdx.x + (q >> 1) * 2 * NT + (q & 1) : gb + (int)threadIdx.x + q * NT; };
+    // entries gb + lane + q NT
+    auto at = [&](int q) { return gb + (int)threadIdx.x + q * NT; };
     int qi = 0;
     int g = at(0);
     uint32_t e_n = 0, e_nn = 0;
@@ -1046,12 +932,6 @@ __global__ __launch_bounds__(NT) void tvam_adj_planar_kernel(TvamConsts k, TvamP
     float4 ff_n = make_float4(0.0f, 0.0f, 0.0f, 0.0f), an_n = ff_n;
     float w_n = 1.0f;
     auto records = [&](uint32_t e, int& ri, float4& ff, float4& an, float& wray) {
-        if (e == 0xffffffffu) {  // padding slot of a quadrant list
-            ri = -1;
-            ff = an = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-            wray = 1.0f;
-            return;
-        }
         const int al = (int)(e >> 16), colc = (int)(e & 0xffffu);
         ri = pl.rec_i[(size_t)al * k.crop_x + colc];
         ff = pl.rec_f[(size_t)al * k.crop_x + colc];
@@ -1151,18 +1031,14 @@ __global__ __launch_bounds__(NT) void tvam_adj_planar_kernel(TvamConsts k, TvamP
                     act = idxmap[act];
                     if (act < 0) continue;
                 }
-#ifdef TVAM_ADJ_NOATOMIC_DEBUG  // timing experiment only (wrong results): no gradient atomics
-                if (v == 1.2345e-30f) out[act] = v;
-#else
                 atomicAdd(&out[act], v);  // backward_from(Le * em_grad), volume.py:274-276
-#endif
             }
         }
     }
 }
 
 size_t tvam_planar_adj_lds(const TvamPlanar& pl, const TvamTiles& t, int Z) {
-    return (size_t)std::max(pl.adj_pitch, pl.adj_pitch2) * (t.tsy + 2) * Z * sizeof(float) +
+    return (size_t)pl.adj_pitch * (t.tsy + 2) * Z * sizeof(float) +
            (size_t)(Z + 1 + pl.max_rows_chunk) * sizeof(int);
 }
 
@@ -1171,44 +1047,25 @@ hipError_t tvam_launch_adj_planar(const TvamConsts& k, const TvamPlanar& pl, con
     if (pl.adjl_ngroups > 0) return tvam_launch_adj_lists(k, pl, t, Z, idxmap, gin, out, stream);
     // slice chunks of this launch: [adj_zc0, adj_zc0 + adj_nzc) (tvam_adjoint_slices), else all
     const int nzc = pl.adj_nzc > 0 ? pl.adj_nzc : (k.nz + Z - 1) / Z;
-    dim3 grid((unsigned)(t.ntx * t.nty), (unsigned)nzc, (unsigned)std::max(pl.adj_split, 1) * (pl.adj_quad ? 4u : 1u));
+    dim3 grid((unsigned)(t.ntx * t.nty), (unsigned)nzc, (unsigned)std::max(pl.adj_split, 1));
     const size_t lds = tvam_planar_adj_lds(pl, t, Z);
-    const bool pf = pl.adj_prefetch != 0;
-    // 512-thread workgroups (adj_nt): the LDS tile (28 KB at 40 x 40 x 4) admits 5
-    // workgroups per CU, i.e. 5 waves per SIMD at 256 threads, 8 at 512
-#define TVAM_ADJ_LAUNCH_PL(ZZ, PLL)                                                                                \
-    if (pl.adj_nt == 1024)                                                                                         \
-        hipLaunchKernelGGL((tvam_adj_planar_kernel<ZZ, true, 1024, PLL>), grid, dim3(1024), lds, stream, k, pl, t,   \
-                           idxmap, gin, out);                                                                      \
-    else if (pl.adj_nt == 512)                                                                                     \
-        hipLaunchKernelGGL((tvam_adj_planar_kernel<ZZ, true, 512, PLL>), grid, dim3(512), lds, stream, k, pl, t,     \
-                           idxmap, gin, out);                                                                      \
-    else if (pf)                                                                                                   \
-        hipLaunchKernelGGL((tvam_adj_planar_kernel<ZZ, true, 256, PLL>), grid, dim3(256), lds, stream, k, pl, t,     \
-                           idxmap, gin, out);                                                                      \
-    else                                                                                                           \
-        hipLaunchKernelGGL((tvam_adj_planar_kernel<ZZ, false, 256, PLL>), grid, dim3(256), lds, stream, k, pl, t,    \
+    const bool w2 = k.vox_chord < TVAM_W2_MAX;
+    // Z = 8 (the list adjoint's fallback): 1024-thread workgroups, [z/4][voxel][4] planes; films
+    // under 8 slices: Z = 4, 512 threads
+    if (Z == 8 && pl.adj_nt == 1024 && w2)
+        hipLaunchKernelGGL((tvam_adj_planar_kernel<8, true, 1024, true, true>), grid, dim3(1024), lds, stream, k, pl, t,
                            idxmap, gin, out);
-#define TVAM_ADJ_LAUNCH(ZZ)                                                                                    \
-    if (pl.adj_planes && pl.adj_nt == 1024 && pl.adj_w2 && k.vox_chord < TVAM_W2_MAX)                         \
-        hipLaunchKernelGGL((tvam_adj_planar_kernel<ZZ, true, 1024, true, true>), grid, dim3(1024), lds, stream, k, \
-                           pl, t, idxmap, gin, out);                                                           \
-    else if (!pl.adj_planes && pl.adj_nt == 1024 && pl.adj_w2 && k.vox_chord < TVAM_W2_MAX)                   \
-        hipLaunchKernelGGL((tvam_adj_planar_kernel<ZZ, true, 1024, false, true>), grid, dim3(1024), lds, stream, k, \
-                           pl, t, idxmap, gin, out);                                                           \
-    else if (pl.adj_planes) {                                                                                  \
-        TVAM_ADJ_LAUNCH_PL(ZZ, true)                                                                           \
-    } else {                                                                                                   \
-        TVAM_ADJ_LAUNCH_PL(ZZ, false)                                                                          \
-    }
-    switch (Z) {
-        case 4: TVAM_ADJ_LAUNCH_PL(4, false) break;  // one 4-slice group: both layouts coincide
-        case 8: TVAM_ADJ_LAUNCH(8) break;
-        case 16: TVAM_ADJ_LAUNCH(16) break;
-        default: return hipErrorInvalidValue;
-    }
-#undef TVAM_ADJ_LAUNCH
-#undef TVAM_ADJ_LAUNCH_PL
+    else if (Z == 8 && pl.adj_nt == 1024)
+        hipLaunchKernelGGL((tvam_adj_planar_kernel<8, true, 1024, true, false>), grid, dim3(1024), lds, stream, k, pl, t,
+                           idxmap, gin, out);
+    else if (Z == 8)
+        hipLaunchKernelGGL((tvam_adj_planar_kernel<8, true, 512, true, false>), grid, dim3(512), lds, stream, k, pl, t,
+                           idxmap, gin, out);
+    else if (Z == 4)
+        hipLaunchKernelGGL((tvam_adj_planar_kernel<4, true, 512, false, false>), grid, dim3(512), lds, stream, k, pl, t,
+                           idxmap, gin, out);
+    else
+        return hipErrorInvalidValue;
     return hipGetLastError();
 }
 

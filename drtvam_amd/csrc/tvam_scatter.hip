@@ -1719,23 +1719,20 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
     const int nbricks = nbx * nby * nbz;
     // brick-march workgroup: 1024 threads double the waves per SIMD under the one 128 KB int64
     // tile per CU (forward) and the two 64 KB gradient tiles (adjoint); TVAM_BIN_NT=512 for A/B
-    static const int bin_nt = [] {
-        const char* v = getenv("TVAM_BIN_NT");
-        return v && atoi(v) == 512 ? 512 : 1024;
-    }();
+    static const int bin_nt = tvam_knob("TVAM_BIN_NT", 1024) == 512 ? 512 : 1024;
     int bits = 1;
     while ((1 << bits) < nbricks) ++bits;
     // length classes: 16, or 8 / 4 where that keeps the sort key within 16 bits (two radix passes
     // instead of three; config 4: 4225 bricks); TVAM_BIN_CBITS overrides (2..4)
     int cbits = bits <= 14 ? std::min(4, 16 - bits) : TVAM_BIN_CLASS_BITS;
-    if (const char* v = getenv("TVAM_BIN_CBITS")) cbits = std::min(4, std::max(2, atoi(v)));
+    if (const int cb = tvam_knob("TVAM_BIN_CBITS", 0)) cbits = std::min(4, std::max(2, cb));
     bits += cbits;
     const uint32_t kmask = bits >= 32 ? 0xffffffffu : ((1u << bits) - 1u);
     const int spp = (int)t.spp;
     const int64_t npaths = (int64_t)t.n_shard * k.crop_y * k.crop_x * spp;
     // chunk of paths: a whole number of pixels (the adjoint reduces a pixel's samples together)
     int64_t max_slots = (int64_t)1 << 27;  // 128M slots (TVAM_BIN_CHUNK_SLOTS: smaller, for tests)
-    if (const char* v = getenv("TVAM_BIN_CHUNK_SLOTS")) max_slots = std::max<int64_t>(1, atoll(v));
+    if (const int cs = tvam_knob("TVAM_BIN_CHUNK_SLOTS", 0)) max_slots = std::max<int64_t>(1, cs);
     int64_t chunk = std::max<int64_t>(1, max_slots / slots);
     chunk = std::max<int64_t>(spp, chunk / spp * spp);
     chunk = std::min(npaths, chunk);
@@ -1748,10 +1745,7 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
     // sorts' 8.4 ms per chunk go, but the fill's scattered 4-byte entry stores take 10.0 ms instead
     // of 5.6, and the brick marches lose the record-line sharing of the class-sorted fill order
     // (forward 18.8 -> 23.7 ms, adjoint 16.2 -> 20.1 ms per chunk): 0.2856 -> 0.2853 it/s.
-    static const bool bin_sort = [] {
-        const char* v = getenv("TVAM_BIN_SORT");
-        return !(v && atoi(v) == 0);
-    }();
+    static const bool bin_sort = tvam_knob("TVAM_BIN_SORT", 1) != 0;
     const bool csort = !bin_sort && !s.acc_float && bin_nt == 1024 && nbricks <= 16384 &&
                        nsl <= ((int64_t)1 << TVAM_ENT_SLOT_BITS);
     hipError_t e;
@@ -1774,8 +1768,7 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
     s.cap_bricks = (int32_t)capb;
     // forward bin cache: dense pattern sets only (a sparse set's streams follow the set), and not
     // with skip_zero (then the paths depend on the pattern); TVAM_BIN_CACHE=0 turns it off
-    const char* cache_env = getenv("TVAM_BIN_CACHE");
-    const bool cacheable = !adj && !idxmap && !k.skip_zero && !(cache_env && atoi(cache_env) == 0);
+    const bool cacheable = !adj && !idxmap && !k.skip_zero && tvam_knob("TVAM_BIN_CACHE", 1) != 0;
     if (cacheable) {
         const bool same = s.fc_key && s.fc_seed == t.seed && s.fc_spp == t.spp && s.fc_chunk == chunk &&
                           s.fc_npaths == npaths && std::memcmp(&s.fc_k, &k, sizeof(TvamConsts)) == 0;

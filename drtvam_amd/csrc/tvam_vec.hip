@@ -25,8 +25,7 @@
 
 // launch geometry knobs (read once): blocks of the history pass and of the direction pass
 static int vec_knob(const char* name, int def) {
-    const char* v = std::getenv(name);
-    const int x = v && *v ? std::atoi(v) : def;
+    const int x = tvam_knob(name, def);
     return x > 0 ? x : def;
 }
 static int hist_grid() {

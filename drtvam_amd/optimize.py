@@ -82,9 +82,11 @@ def angle_shard(n_angles: int, rank: int, world: int):
     return (n_angles * rank) // world, (n_angles * (rank + 1)) // world
 
 
-def _dist():
+def _dist(always=False):
+    """torch.distributed when a process group of more than one rank is up (or of any size with
+    `always`: config 'collectives': 'always' runs the sharded loop's collectives at world size 1)."""
     import torch.distributed as dist
-    if dist.is_available() and dist.is_initialized() and dist.get_world_size() > 1:
+    if dist.is_available() and dist.is_initialized() and (always or dist.get_world_size() > 1):
         return dist
     return None
 
@@ -372,7 +374,7 @@ class TvamProblem(ShardedLoop):
 
     def __init__(self, config, device=None, target=None, rank=None, world_size=None, filter_pixels=True):
         self.config = config
-        self.dist = _dist()
+        self.dist = _dist(always=config.get('collectives') == 'always')
         self.rank = rank if rank is not None else (self.dist.get_rank() if self.dist else 0)
         self.world = world_size if world_size is not None else (self.dist.get_world_size() if self.dist else 1)
         dev = torch.device(device) if device is not None else torch.device('cuda', torch.cuda.current_device())
