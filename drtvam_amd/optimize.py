@@ -430,6 +430,12 @@ class TvamProblem(ShardedLoop):
         self.crop_x, self.crop_y = p.crop[0], p.crop[1]
         full_desc = VolumeIntegrator(base).desc(self.scene, self.sensor)
         self.res_z = int(full_desc.film_res[2])
+        if 'flags' not in config and full_desc.albedo != 0.0:
+            # every path marched, as the reference marches every active pixel (projector.py:66-70,
+            # common.py:81-82): a scattering scene's paths then do not depend on the pattern, and
+            # the line-search forward is served from the forward bin cache (lbfgs.py:240-249)
+            from ._abi import FLAG_NO_ZERO_SKIP
+            base['flags'] = int(base['flags']) | FLAG_NO_ZERO_SKIP
         self.surface_aware = bool(self.sensor.film().surface_aware)
         # scattered paths leave their slice; surface-aware films run the per-path kernels
         planar = self.regular_sampling and full_desc.albedo == 0.0 and not self.surface_aware

@@ -78,8 +78,8 @@ def shard4(oracle):
 
 @pytest.fixture
 def full4(oracle):
-    """All 400 angles of config 4 (the bench's 1.02 G paths, 23 chunks), every 397th pixel checked."""
-    s = _make_shard(oracle, 0, N4, 397)
+    """All 400 angles of config 4 (the bench's 1.02 G paths, 23 chunks), every 50th pixel checked."""
+    s = _make_shard(oracle, 0, N4, 50)
     yield s
     s["proj"].close()
     torch.cuda.empty_cache()
@@ -135,7 +135,8 @@ def test_config4_shard_default_chunks(shard4):
 
 def test_config4_all_angles(full4):
     """The bench's whole config-4 pass: 400 angles in 23 default chunks, adjoint, forward and the
-    cached forward of the same seed."""
+    cached forward of the same seed; 1 pixel in 50 (25.6 K per angle's 160 K ... 1.28 M pixels,
+    20.5 M paths) traced by the oracle."""
     _default_chunks(full4, 23)
 
 
@@ -179,3 +180,46 @@ def test_config5_four_angle_shard(oracle):
     out = flip_protocol(oracle, proj, dfull, pat, G, spp, seed, active_pixels=pix, nthreads=THREADS)
     proj.close()
     assert out["pixels"] == n
+
+
+def test_config5_spread_angles(oracle):
+    """Config 5 (800^3, 800 angles, 4 spp, square vial + occluder) rendered whole on the GPU; the
+    oracle traces 32 angles spread over the 800 (every 25th), every 16th pixel of each, with the
+    whole set's sampler streams.  Forward: patterns nonzero on that subset only; adjoint: compared
+    on the subset.  Flip protocol as above (flipped pixels counted and zeroed)."""
+    N, spp, seed = 800, 4, 4
+    cfg = square_occluded(N=N, angles=N)
+    d = desc_from_config(cfg)
+    dfull = desc_from_config(cfg)
+    per = N * N
+    n = N * per
+    d.active_total = dfull.active_total = n
+    angles = np.arange(0, N, 25)
+    assert angles.size == 32
+    sub = np.concatenate([a * per + np.arange(0, per, 16, dtype=np.int64) for a in angles])
+    pix = sub.astype(np.uint32)
+    pos = sub.astype(np.uint64)
+    rng = np.random.default_rng(seed)
+    G = rng.uniform(-1, 1, (N, N, N)).astype(np.float32)
+    gref, _ = oracle.adjoint(dfull, G, active_pixels=pix, spp=spp, seed=seed, nthreads=THREADS, streams=pos)
+    gabs, _ = oracle.adjoint(dfull, np.abs(G), active_pixels=pix, spp=spp, seed=seed, nthreads=THREADS, streams=pos)
+    proj = Projection(d, DEV)
+    try:
+        g = proj.adjoint(torch.as_tensor(G, device=DEV), n, None, spp, seed).cpu().numpy()[sub]
+        flip = flipped_pixels(g, gref, gabs)
+        nflip = int(flip.sum())
+        keep = ~flip
+        ea = rel_l2(g[keep], gref[keep])
+        p = np.where(flip, 0.0, rng.uniform(0.0, 0.1, sub.size)).astype(np.float32)
+        ref, _ = oracle.forward(dfull, p, active_pixels=pix, spp=spp, seed=seed, nthreads=THREADS, streams=pos)
+        full = np.zeros(n, np.float32)
+        full[sub] = p
+        got = proj.forward(torch.as_tensor(full, device=DEV), None, spp, seed).cpu().numpy()[..., 0]
+        ef = rel_l2(got, ref)
+    finally:
+        proj.close()
+        torch.cuda.empty_cache()
+    print(f"config 5, 32 angles spread over 800, {sub.size} subset pixels ({sub.size * spp} paths): "
+          f"{nflip} flipped, adjoint rel-L2 {ea:.3e}, forward rel-L2 {ef:.3e}")
+    assert nflip <= max(2, 1e-4 * sub.size * spp)
+    assert ea < RTOL and ef < RTOL
