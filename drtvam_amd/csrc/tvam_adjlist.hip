@@ -170,7 +170,7 @@ __global__ __launch_bounds__(256) void tvam_adjl_fill_kernel(TvamConsts k, TvamP
 // the same +-1 and the lanes of a ds_read_b128 lane group keep the distinct chunks (mod 16) they
 // entered with: no bank conflicts.  Padding visits keep stepping in x through zeroed slack
 // (adjl_slack bytes) before, between and after the two planes.
-template <int Z, int NT, int MINW = 1>
+template <int Z, int NT, int MINW = 1, int PFD = 4>
 __global__ __launch_bounds__(NT, MINW) void tvam_adjl_kernel(TvamConsts k, TvamPlanar pl, TvamTiles tp, int nzc,
                                                        const int32_t* __restrict__ idxmap,
                                                        const float* __restrict__ gin, float* __restrict__ out) {
@@ -241,7 +241,7 @@ __global__ __launch_bounds__(NT, MINW) void tvam_adjl_kernel(TvamConsts k, TvamP
     int4 h;
     int n4;
     const float4* wp;
-    float4 w0, w1, w2, w3;
+    float4 w[PFD];  // weight rows PFD ahead, a register ring
     auto load_chunk = [&](int cc) {
         h = pl.adjl_hdr[(size_t)cc * 64 + lane];
         const int64_t r0 = pl.adjl_coff[cc];
@@ -252,10 +252,8 @@ __global__ __launch_bounds__(NT, MINW) void tvam_adjl_kernel(TvamConsts k, TvamP
         wp = pl.adjl_w + r0 * 64 + lane;
 #endif
         const int last = n4 - 1;
-        w0 = wp[0];
-        w1 = wp[(size_t)min(1, last) * 64];
-        w2 = wp[(size_t)min(2, last) * 64];
-        w3 = wp[(size_t)min(3, last) * 64];
+#pragma unroll
+        for (int j = 0; j < PFD; ++j) w[j] = wp[(size_t)min(j, last) * 64];
     };
     load_chunk(c);
     for (;;) {
@@ -282,27 +280,20 @@ __global__ __launch_bounds__(NT, MINW) void tvam_adjl_kernel(TvamConsts k, TvamP
                 pv += dx + ((__float_as_int(cw) & 1) ? ddy : 0);
             }
         };
-        // weight rows four ahead, in a ring of four registers
         const int last = n4 - 1;
         int q = 0;
 #pragma unroll 1
-        for (; q + 3 < n4; q += 4) {
-            float4 t = w0;
-            w0 = wp[(size_t)min(q + 4, last) * 64];
-            visits(t);
-            t = w1;
-            w1 = wp[(size_t)min(q + 5, last) * 64];
-            visits(t);
-            t = w2;
-            w2 = wp[(size_t)min(q + 6, last) * 64];
-            visits(t);
-            t = w3;
-            w3 = wp[(size_t)min(q + 7, last) * 64];
-            visits(t);
+        for (; q + PFD - 1 < n4; q += PFD) {
+#pragma unroll
+            for (int j = 0; j < PFD; ++j) {
+                const float4 t = w[j];
+                w[j] = wp[(size_t)min(q + PFD + j, last) * 64];
+                visits(t);
+            }
         }
-        if (q < n4) visits(w0);
-        if (q + 1 < n4) visits(w1);
-        if (q + 2 < n4) visits(w2);
+#pragma unroll
+        for (int j = 0; j < PFD - 1; ++j)
+            if (q + j < n4) visits(w[j]);
 #pragma unroll
         for (int z = 0; z < Z; ++z) acc[z] *= wsc;
         const int cn = c + NT / 64;
@@ -361,7 +352,10 @@ hipError_t tvam_launch_adj_lists(const TvamConsts& k, const TvamPlanar& pl, cons
     if (nb <= 0) return hipSuccess;
     if (nb > 0x7fffffff) return hipErrorInvalidValue;
     const size_t lds = tvam_adjl_lds(pl, t, ZL);
-    if (ZL == 16)
+    if (ZL == 16 && pl.adjl_pfd == 8)  // (one workgroup per CU: registers to spare for 8 rows in flight)
+        hipLaunchKernelGGL((tvam_adjl_kernel<16, 1024, 1, 8>), dim3((unsigned)nb), dim3(1024), lds, stream, k, q, t, nzc,
+                           idxmap, gin, out);
+    else if (ZL == 16)
         hipLaunchKernelGGL((tvam_adjl_kernel<16, 1024>), dim3((unsigned)nb), dim3(1024), lds, stream, k, q, t, nzc, idxmap,
                            gin, out);
     else if (pl.adjl_nt == 896)  // 14 waves, 2 workgroups (7 waves per SIMD) per CU at <= 72 VGPRs

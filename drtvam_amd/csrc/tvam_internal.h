@@ -106,6 +106,7 @@ struct TvamPlanar {
     int32_t adjl_slack;                // zeroed bytes around each plane (padding visits walk there)
     int32_t adjl_z;                    // slices per workgroup (8 or 16)
     int32_t adjl_nt;                   // threads per workgroup (1024, 896 or 768)
+    int32_t adjl_pfd;                  // weight rows loaded ahead (4 or 8)
 };
 
 // Device buffers of the visit lists (owned by the plan).

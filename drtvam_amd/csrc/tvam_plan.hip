@@ -391,11 +391,12 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     p->planar_fz = env_int("TVAM_PLANAR_FWD_Z", 0);  // 0: chosen from the slab depth (planar_fwd_setup)
     // adjoint slices per workgroup: 8 (one march gathers 8 slices: measured 5.2 -> 3.9 ms on
     // config 2 with 1024-thread workgroups and 45 x 45 tiles), 4 for films under 8 slices
-    p->planar_az = env_int("TVAM_PLANAR_ADJ_Z", k.nz >= 8 ? 8 : 4);
+    // (TVAM_PLANAR_ADJ_Z: 4 = the tile adjoint at 4 slices, 8 / 16 = the list adjoint's slices per workgroup)
+    const int az_knob = env_int("TVAM_PLANAR_ADJ_Z", 0);
+    p->planar_az = az_knob == 4 || k.nz < 8 ? 4 : 8;
     if (p->planar_fz != 8 && p->planar_fz != 16 && p->planar_fz != 24 && p->planar_fz != 28 && p->planar_fz != 32 &&
         p->planar_fz != 40 && p->planar_fz != 52)
         p->planar_fz = 0;
-    if (p->planar_az != 4 && p->planar_az != 8 && p->planar_az != 16) p->planar_az = 4;
     const int ns = (int)cs.size();
     int32_t mrc = 0;
     for (int z0 = 0; z0 < k.nz; z0 += p->planar_az)
@@ -503,10 +504,11 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     if (p->planar_az == 8 && ns > 0 && env_int("TVAM_ADJ_LISTS", 1)) {
         size_t fr = 0, tot = 0;
         if ((e = hipMemGetInfo(&fr, &tot)) != hipSuccess) return hip_fail(e, "hipMemGetInfo");
-        p->pl.adjl_z = env_int("TVAM_ADJL_Z", 16) == 8 ? 8 : 16;
+        p->pl.adjl_z = env_int("TVAM_ADJL_Z", az_knob == 8 ? 8 : 16) == 8 ? 8 : 16;
         const int64_t nwg4 = (int64_t)p->tiles.ntx * p->tiles.nty * 4 * ((k.nz + p->pl.adjl_z - 1) / p->pl.adjl_z);
         const int parts = (int)std::min<int64_t>(4, std::max<int64_t>(1, (4096 + nwg4 - 1) / std::max<int64_t>(nwg4, 1)));
         p->pl.adjl_nt = env_int("TVAM_ADJL_NT", 768);
+        p->pl.adjl_pfd = env_int("TVAM_ADJL_PFD", 8) == 4 ? 4 : 8;
         e = tvam_build_adj_lists(k, p->pl, p->tiles, parts, 0, fr / 4, p->adjl, nullptr);
         // 16 slices per workgroup where the tile's 4 planes fit in LDS (the weights are the same)
         if (e == hipSuccess && p->pl.adjl_z == 16 && tvam_adjl_lds(p->pl, p->tiles, 16) > 160 * 1024) p->pl.adjl_z = 8;

@@ -378,10 +378,16 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
         const float xa = X0 * g0.z, xb = X1 * g0.z, ya = Y0 * g0.w, yb = Y1 * g0.w;
         const float xn = fminf(xa, xb), xf = fmaxf(xa, xb), yn = fminf(ya, yb), yf = fmaxf(ya, yb);
         float wgt[NC];
+        // the candidates' ray records read together (each read's latency is paid once per angle),
+        // then pinned as 16-byte reads (ds_read_b128, not b96)
+        float4 qs[NC];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) qs[c] = sr[jj0 + c];
+#pragma unroll
+        for (int c = 0; c < NC; ++c) asm volatile("" : "+v"(qs[c].w));
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
-            float4 q = sr[jj0 + c];
-            asm volatile("" : "+v"(q.w));  // keep the 16-byte LDS read (ds_read_b128, not b96)
+            const float4 q = qs[c];
             float tnx = xn + q.x, tfx = xf + q.x, tny = yn + q.y, tfy = yf + q.y;
             if (!(fl & 1)) {  // |d.x| <= 1e-8: the DDA never steps x (q.x = its voxel index)
                 tnx = (float)ix == q.x ? -TVAM_INF : TVAM_INF;
