@@ -391,6 +391,8 @@ def main():
                "device_mem_used_bytes": (lambda fr_tot: fr_tot[1] - fr_tot[0])(torch.cuda.mem_get_info(dev))}
         if prob.proj.desc.albedo != 0.0:  # scattering: the brick-bin chunking and its device memory
             rec["bins"] = prob.proj.bin_stats()
+        if not prob.proj.desc.regular_sampling:
+            rec["tiles"] = prob.proj.tile_stats()
         if prob.shard == "angle" and ew > 1:
             # two ring all-reduces of the full dose per iteration (main forward + line-search forward):
             # each moves 2 (W - 1) / W of the film per rank at the RCCL bus bandwidth --ar-gbs.  When the
@@ -453,6 +455,7 @@ def main():
                             f"z-slab x{world} (film slabs + DMD row bands, scalar all-reduces only)"
                             if prob.shard == "slab" else
                             f"angle-shard x{world} + {'RCCL' if args.backend == 'nccl' else 'gloo'} dose all-reduce"),
+            "shard": prob.shard if world > 1 else None,
             "zero_skip": bool(args.zero_skip), "prewarm_forwards": n_pre, "tile": prob.proj.desc.tile,
             # slab bands of the pipelined iteration (TvamProblem._iteration_pipelined; 1: unbanded)
             "slab_bands": (len(prob.opt.pipeline.parts) if getattr(prob.opt, "pipeline", None) is not None else 1),
@@ -462,6 +465,8 @@ def main():
             "final_loss": prob.loss_hist[-1],
             # scattering: the last (line-search) forward's brick-bin chunks, how many the cache served
             "bins": prob.proj.bin_stats() if prob.proj.desc.albedo != 0.0 else None,
+            # jittered sampling: the per-ray tile kernels' stray rays and the row walks they cost
+            "tiles": prob.proj.tile_stats() if not prob.proj.desc.regular_sampling else None,
         },
         "roofline": roofline,
         "cpu_baseline": cpu,

@@ -444,7 +444,7 @@ __device__ __forceinline__ bool tvam_tile_slot(const TvamConsts& k, const TvamTi
 template <int MODE, bool W2>
 __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
     TvamConsts k, TvamTiles tp, const float* __restrict__ pat, const int32_t* __restrict__ idxmap,
-    const float* __restrict__ gin, float* __restrict__ out, unsigned long long* __restrict__ counter) {
+    const float* __restrict__ gin, float* __restrict__ out, unsigned long long* __restrict__ counter, int nzl) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     float* tile = reinterpret_cast<float*>(smem);
     const int tsx = tp.tsx, tsy = tp.tsy, ns = tp.n_shard;
@@ -456,7 +456,18 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
 #if TVAM_TILE_DIAG
     const unsigned long long dg_t0 = __builtin_amdgcn_s_memtime();
 #endif
-    const int tile_id = blockIdx.x, kz = (int)blockIdx.y + (MODE == TVAM_MODE_FWD ? tp.kz0 : 0);
+    // XCD-aware order: workgroup b runs on XCD b % 8; each XCD takes a contiguous run of slices,
+    // all tiles of a slice in turn, so the tiles re-reading one slice's ray records (every tile a
+    // ray crosses reads its record) share that XCD's L2 instead of fetching it into all eight
+    const int ntl = tp.ntx * tp.nty;
+#ifndef TVAM_TILE_XCD
+#define TVAM_TILE_XCD 1  // (0: workgroups in plain (slice, tile) order, for A/B builds)
+#endif
+    const int L = TVAM_TILE_XCD ? (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3)
+                                : (int)blockIdx.x;
+    if (L >= ntl * nzl) return;
+    const int zloc = L / ntl, tile_id = L - zloc * ntl;
+    const int kz = zloc + (MODE == TVAM_MODE_FWD ? tp.kz0 : 0);
     const int x0 = (tile_id % tp.ntx) * tsx, y0 = (tile_id / tp.ntx) * tsy;
     const int x1 = min(x0 + tsx, k.res[0]), y1 = min(y0 + tsy, k.res[1]);
     const int wx = x1 - x0, wy = y1 - y0;
@@ -667,7 +678,7 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
             }
         }
 #if TVAM_TILE_DIAG
-        if ((int)blockIdx.x == tvam_tile_dsel[0] && (int)blockIdx.y == tvam_tile_dsel[1] && f < (1 << 21))
+        if (tile_id == tvam_tile_dsel[0] && zloc == tvam_tile_dsel[1] && f < (1 << 21))
             tvam_tile_dslot[f] = why == 0 ? (unsigned)(nvis - vis_prev) : 0xffffffffu;
         dg[1] += 1;
         dg[2] += 1;
@@ -748,16 +759,17 @@ hipError_t tvam_launch_tiles(int mode, const TvamConsts& k, const TvamTiles& t, 
     const int nzl = mode == TVAM_MODE_FWD && t.kz1 > t.kz0 ? t.kz1 - t.kz0 : k.nz;
     TvamTiles tl = t;
     if (!(mode == TVAM_MODE_FWD && t.kz1 > t.kz0)) tl.kz0 = 0;
-    dim3 grid((unsigned)(t.ntx * t.nty), (unsigned)nzl);
+    const int64_t nwg = (int64_t)t.ntx * t.nty * nzl;
+    dim3 grid((unsigned)((nwg + 7) / 8 * 8));  // (a multiple of 8: the kernel's XCD-aware order)
     dim3 block(TVAM_BLOCK);
     const bool w2 = k.vox_chord < TVAM_W2_MAX;
 #define TVAM_TILE_LAUNCH(M)                                                                                      \
     if (w2)                                                                                                      \
         hipLaunchKernelGGL((tvam_tile_kernel<M, true>), grid, block, lds_bytes, stream, k, tl, pat, idxmap, gin, out, \
-                           counter);                                                                             \
+                           counter, nzl);                                                                        \
     else                                                                                                         \
         hipLaunchKernelGGL((tvam_tile_kernel<M, false>), grid, block, lds_bytes, stream, k, tl, pat, idxmap, gin, out, \
-                           counter);
+                           counter, nzl);
     switch (mode) {
         case TVAM_MODE_FWD:
             TVAM_TILE_LAUNCH(TVAM_MODE_FWD)

@@ -39,6 +39,9 @@ struct tvam_plan {
     int32_t ntiles;
     size_t lds_bytes;
     int32_t max_rows_per_slice;
+    int64_t n_slots_all = 0;  // (angle, column) slots over every tile (tvam_plan_tile_stats)
+    int64_t n_main_rows = 0;  // main-row list entries over every slice (0: no main-row lists)
+    int64_t n_rows_all = 0;   // row list entries over every slice
     bool empty;  // max_depth too small for any ray to reach the medium
     bool cyl;    // refracting (cylindrical / square) vial: per-ray directions and weights
     bool surface = false;    // surface-aware film (2 channels): per-path kernels cut at the target mesh
@@ -1274,6 +1277,9 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
     p->tiles.slots = p->d_slots;
     p->tiles.slot_off = p->d_slot_off;
     p->tiles.ang = p->d_ang;
+    p->n_slots_all = (int64_t)slots.size();
+    p->n_main_rows = main_rows ? (int64_t)slice_mrows.size() : 0;
+    p->n_rows_all = (int64_t)slice_rows.size();
     if (main_rows) {
         if (slice_mrows.empty()) slice_mrows.push_back(0);
         if ((rc = upload(&p->d_slice_moff, slice_moff)) || (rc = upload(&p->d_slice_mrows, slice_mrows)) ||
@@ -1867,6 +1873,37 @@ extern "C" int tvam_plan_bin_stats(tvam_plan* p, int64_t* stats) {
             return fail(TVAM_ERR_HIP, "tvam_plan_bin_stats: reading the count check");
         stats[7] = bad;
     }
+    return 0;
+}
+
+// The per-ray tile kernels' row walks for the plan's most recent ray records (jittered plans):
+// how many rays the ray setup listed as strays (rays outside their row's main slice) and what
+// the (tile, slice) workgroups walk because of them -- every workgroup of a slice walks that
+// slice's whole stray list, against its main rows' slots.
+extern "C" int tvam_plan_tile_stats(tvam_plan* p, int64_t* stats) {
+    if (!p || !stats) return fail(TVAM_ERR_INVALID, "null argument");
+    for (int i = 0; i < 8; ++i) stats[i] = 0;
+    stats[0] = -1;
+    const tvam_plan::RaySlot* r = nullptr;
+    for (const auto& s : p->rs)
+        if (s.valid && (!r || s.used > r->used)) r = &s;
+    if (!r) return 0;
+    unsigned long long ns = 0, nf = 0;
+    hipError_t e = hipSuccess;
+    if (r->stray_n && p->n_main_rows > 0) e = hipMemcpy(&ns, r->stray_n, sizeof(ns), hipMemcpyDeviceToHost);
+    if (e == hipSuccess && r->frozen_n) e = hipMemcpy(&nf, r->frozen_n, sizeof(nf), hipMemcpyDeviceToHost);
+    if (e != hipSuccess) return hip_fail(e, "hipMemcpy");
+    const bool lists = r->stray_n && p->n_main_rows > 0;
+    stats[0] = lists ? (int64_t)ns : -1;
+    stats[1] = lists ? (int64_t)TVAM_STRAY_CAP : 0;
+    // strays beyond the cap: the workgroups walk the full row lists instead (no stray walk)
+    const bool used = lists && ns <= (unsigned long long)TVAM_STRAY_CAP;
+    stats[2] = used ? (int64_t)ns * p->ntiles : 0;
+    stats[3] = (used ? p->n_main_rows : p->n_rows_all) * p->n_slots_all * (int64_t)r->spp;
+    stats[4] = (int64_t)nf;
+    stats[5] = (int64_t)r->spp;
+    stats[6] = p->ntiles;
+    stats[7] = p->n_slots_all;
     return 0;
 }
 

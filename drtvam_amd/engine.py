@@ -231,6 +231,19 @@ class Projection:
         return dict(zip(("chunks", "cached", "stored", "entries", "chunk_paths", "cache_bytes", "scratch_bytes",
                          "count_mismatch"), (int(x) for x in v)))
 
+    def tile_stats(self):
+        """Row walks of the per-ray tile kernels for the most recent ray records (jittered plans):
+        the rays listed as strays (-1: no stray lists), the list capacity, the (tile, slice)
+        workgroups' stray walk and main-row slot walk summed over a launch, the frozen-axis rays,
+        spp, tiles and slots (tvam_plan_tile_stats)."""
+        import numpy as np
+        v = np.zeros(8, dtype=np.int64)
+        with torch.cuda.device(self.device):
+            torch.cuda.synchronize(self.device)
+            _abi.check(self.lib.tvam_plan_tile_stats(self._plan, v.ctypes.data))
+        return dict(zip(("strays", "stray_cap", "stray_walk", "main_walk", "frozen", "spp", "tiles", "slots"),
+                        (int(x) for x in v)))
+
     def count_visits(self, spp: int = 1, seed: int = 0) -> int:
         v = ctypes.c_uint64(0)
         with torch.cuda.device(self.device):

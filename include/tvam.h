@@ -270,6 +270,17 @@ int tvam_plan_fwd_scale(tvam_plan* plan, float* scale);
    construction; host-synchronous read).  stats has 8 entries.  (ABI v10) */
 int tvam_plan_bin_stats(tvam_plan* plan, int64_t* stats);
 
+/* Diagnostics (host-synchronous): the per-ray tile kernels' row walks for the plan's most
+   recent ray records (jittered sampling).  stats[0] = rays the ray setup listed as strays
+   (outside their row's main slice; -1 when the plan keeps no stray lists: regular sampling,
+   rows whose interior jitters already change slice, or > 2^32 records), [1] = the stray-list
+   capacity (beyond it every workgroup walks its slice's full row list), [2] = the (tile, slice)
+   workgroups' stray walk summed over the launch (each walks its slice's whole stray list:
+   strays x tiles), [3] = their main-row slot walk (rows x slots x spp over all workgroups),
+   [4] = frozen-axis rays, [5] = spp of the records, [6] = tiles, [7] = (angle, column) slots
+   over all tiles.  stats has 8 entries.  (ABI v10, added in round 5) */
+int tvam_plan_tile_stats(tvam_plan* plan, int64_t* stats);
+
 /* Surface-aware plans: the per-channel voxel volumes the forward divides by and the
    adjoint multiplies the incoming gradient with (inv_vol = 1/volume, 0 where volume
    is 0: volume.py:41-42, :130).  Device pointer [z][y][x][2], caller-owned, kept by

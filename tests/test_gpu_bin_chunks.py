@@ -216,10 +216,16 @@ def test_config5_spread_angles(oracle):
         full[sub] = p
         got = proj.forward(torch.as_tensor(full, device=DEV), None, spp, seed).cpu().numpy()[..., 0]
         ef = rel_l2(got, ref)
+        ts = proj.tile_stats()  # the tile kernels' stray rays (tvam_plan_tile_stats)
     finally:
         proj.close()
         torch.cuda.empty_cache()
     print(f"config 5, 32 angles spread over 800, {sub.size} subset pixels ({sub.size * spp} paths): "
-          f"{nflip} flipped, adjoint rel-L2 {ea:.3e}, forward rel-L2 {ef:.3e}")
+          f"{nflip} flipped, adjoint rel-L2 {ea:.3e}, forward rel-L2 {ef:.3e}; tile stats {ts}")
+    # stray lists in use, each (tile, slice) workgroup walking its slice's strays: a tiny share of
+    # the main-row slots on config 5 (its rows meet slice boundaries only at the extreme jitters)
+    assert ts["spp"] == spp and 0 <= ts["strays"] <= ts["stray_cap"]
+    assert ts["stray_walk"] == ts["strays"] * ts["tiles"]
+    assert ts["main_walk"] > 0 and ts["stray_walk"] < 1e-3 * ts["main_walk"]
     assert nflip <= max(2, 1e-4 * sub.size * spp)
     assert ea < RTOL and ef < RTOL

@@ -11,7 +11,7 @@ for d in sys.argv[1:]:
             name = r["Kernel_Name"]
             if "tvam_" not in name:
                 continue
-            mode = name.split("(")[0]
+            mode = name.replace("(anonymous namespace)::", "").split("(")[0]
             agg[mode][r["Counter_Name"]].append(float(r["Counter_Value"]))
 for mode, cs in sorted(agg.items()):
     m = {c: sum(v) / len(v) for c, v in cs.items()}
