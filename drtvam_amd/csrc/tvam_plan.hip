@@ -943,7 +943,7 @@ static void cyl_slot_lists(const tvam_desc& d, const TvamConsts& k, const std::v
     std::vector<uint32_t> last((size_t)ntx * nty, 0xffffffffu);
     std::vector<size_t> angle_start((size_t)ntx * nty, 0);
     const int ns = (int)cs.size();
-    const int sort_mode = env_int("TVAM_SLOT_SORT", 2);
+    const int sort_mode = env_int("TVAM_SLOT_SORT", 3);
     const bool sort_len = sort_mode != 0;
     for (int i = 0; i < ns; ++i) {
         for (size_t t = 0; t < per_tile.size(); ++t) angle_start[t] = per_tile[t].size();
@@ -1007,18 +1007,24 @@ static void cyl_slot_lists(const tvam_desc& d, const TvamConsts& k, const std::v
             std::copy(lens.begin(), lens.end(), len_of[t].begin() + (std::ptrdiff_t)b);
         }
     }
-    // TVAM_SLOT_SORT=2 (default): length classes (eighths of the tile's longest chord) over all
-    // angles, longest class first; angle order and the within-angle order are kept inside a class,
-    // so a wave's lanes march similar lengths without mixing far-apart angles (config 4 first
-    // segments, 40-angle shard: forward 32.0 -> 28.7 ms, adjoint 35.4 -> 30.8 ms; config 5 unchanged)
-    if (sort_mode == 2 && !d.regular_sampling)  // (the planar adjoint keeps the per-angle order: 3.9 -> 8.2 ms)
+    // TVAM_SLOT_SORT=2: length classes (eighths of the tile's longest chord) over all angles,
+    // longest class first; angle order and the within-angle order are kept inside a class, so a
+    // wave's lanes march similar lengths without mixing far-apart angles (config 4 first segments,
+    // 40-angle shard: forward 32.0 -> 28.7 ms, adjoint 35.4 -> 30.8 ms; config 5 unchanged)
+    // TVAM_SLOT_SORT=3 (default): the same classes within blocks of 16 angles, so the tiles of a
+    // slice (one XCD's, tvam_tile_kernel) walk the angles in step and re-read each other's ray
+    // records from L2 (config 5, 200-angle shard: adjoint 211 -> 206 ms, forward -0.5 %; config 4
+    // unchanged; profiles/r05/ab_slot_blocks/)
+    const int ablk = sort_mode == 3 ? std::max(1, env_int("TVAM_SLOT_BLOCK", 16)) : (1 << 30);
+    if ((sort_mode == 2 || sort_mode == 3) && !d.regular_sampling)  // (the planar adjoint keeps the per-angle order: 3.9 -> 8.2 ms)
         for (size_t t = 0; t < per_tile.size(); ++t) {
             const size_t n = per_tile[t].size();
             if (n < 2) continue;
             const float lmax = *std::max_element(len_of[t].begin(), len_of[t].end());
             if (!(lmax > 0.0f)) continue;
             std::vector<int> cls(n);
-            for (size_t j = 0; j < n; ++j) cls[j] = std::min(7, (int)(8.0f * len_of[t][j] / lmax));
+            for (size_t j = 0; j < n; ++j)
+                cls[j] = std::min(7, (int)(8.0f * len_of[t][j] / lmax)) - 8 * (int)((per_tile[t][j] >> 16) / (uint32_t)ablk);
             std::vector<size_t> ord(n);
             for (size_t j = 0; j < n; ++j) ord[j] = j;
             std::stable_sort(ord.begin(), ord.end(), [&](size_t x, size_t y) { return cls[x] > cls[y]; });
