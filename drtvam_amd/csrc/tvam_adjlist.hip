@@ -7,8 +7,8 @@
 // crossing times, weight recurrence: 21 VALU per visit) once per (ray, tile, chunk of 8 slices),
 // i.e. 50 times per visit on a 400-slice film.  Here the plan marches every (ray, tile) once,
 // with the same fp32 expressions, and stores the weights; the adjoint then streams them:
-// per visit one weight (a quarter of a coalesced 16-byte load), two ds_read_b128 of the 8
-// slices' gradient and four v_pk_fma, about 10 VALU instead of 21.
+// per visit one weight (a quarter of a coalesced 16-byte load), four ds_read_b128 of the 16
+// slices' gradient (two of 8 where a 16-slice tile does not fit in LDS) and eight v_pk_fma.
 //
 // Layout (TvamPlanar::adjl_*):
 //   * group = (xy tile, part): the tile's crossing rays split into adj_split parts, as the
@@ -19,7 +19,7 @@
 //   * w[coff[chunk] + q][lane] = float4 of visits 4q .. 4q + 3 of the lane's ray, padded with 0 to
 //     the chunk's longest ray; the lowest mantissa bit of a weight says which axis the march
 //     steps after the visit (0: x, 1: y) -- a relative change of at most 2^-23 of that weight.
-// A workgroup = (group, 8-slice chunk); the workgroups of one group are dispatched to one XCD
+// A workgroup = (group, 16-slice chunk); the workgroups of one group are dispatched to one XCD
 // back to back (blockIdx -> (group, chunk) below), so the group's weights (~2 MB on config 2)
 // are read from HBM once and from that XCD's L2 by the other chunks.
 #include "tvam_internal.h"
@@ -246,11 +246,7 @@ __global__ __launch_bounds__(NT, MINW) void tvam_adjl_kernel(TvamConsts k, TvamP
         h = pl.adjl_hdr[(size_t)cc * 64 + lane];
         const int64_t r0 = pl.adjl_coff[cc];
         n4 = (int)(pl.adjl_coff[cc + 1] - r0);  // >= 1: chunks hold crossing rays only
-#if defined(TVAM_ADJL_PROBE) && TVAM_ADJL_PROBE == 1  // timing probe (wrong results): weights of chunk 0's rows only
-        wp = pl.adjl_w + lane;
-#else
         wp = pl.adjl_w + r0 * 64 + lane;
-#endif
         const int last = n4 - 1;
 #pragma unroll
         for (int j = 0; j < PFD; ++j) w[j] = wp[(size_t)min(j, last) * 64];
@@ -298,9 +294,6 @@ __global__ __launch_bounds__(NT, MINW) void tvam_adjl_kernel(TvamConsts k, TvamP
         for (int z = 0; z < Z; ++z) acc[z] *= wsc;
         const int cn = c + NT / 64;
         if (cn < c1) load_chunk(cn);  // before this chunk's atomics
-#if defined(TVAM_ADJL_PROBE) && TVAM_ADJL_PROBE == 2  // timing probe (wrong results): no gradient atomics
-        if (acc[0] == 1.2345e-30f)
-#endif
         if (e != 0xffffffffu) {  // (empty lanes add nothing)
             const int al = (int)(e >> 16), colc = (int)(e & 0xffffu);
             const int64_t base = (int64_t)(k.a0 + al) * k.crop_y * k.crop_x + colc - k.shard_base;
@@ -315,11 +308,7 @@ __global__ __launch_bounds__(NT, MINW) void tvam_adjl_kernel(TvamConsts k, TvamP
                         act = idxmap[act];
                         if (act < 0) continue;
                     }
-#if defined(TVAM_ADJL_PROBE) && TVAM_ADJL_PROBE == 3  // timing probe (wrong results): u32 atomics
-                    atomicAdd(reinterpret_cast<unsigned*>(out) + act, (unsigned)__float_as_int(acc[z]));
-#else
                     atomicAdd(&out[act], acc[z]);  // backward_from(Le * em_grad), volume.py:274-276
-#endif
                 }
             }
         }
@@ -352,20 +341,11 @@ hipError_t tvam_launch_adj_lists(const TvamConsts& k, const TvamPlanar& pl, cons
     if (nb <= 0) return hipSuccess;
     if (nb > 0x7fffffff) return hipErrorInvalidValue;
     const size_t lds = tvam_adjl_lds(pl, t, ZL);
-    if (ZL == 16 && pl.adjl_pfd == 8)  // (one workgroup per CU: registers to spare for 8 rows in flight)
+    if (ZL == 16)  // one workgroup per CU: registers to spare for 8 weight rows in flight
         hipLaunchKernelGGL((tvam_adjl_kernel<16, 1024, 1, 8>), dim3((unsigned)nb), dim3(1024), lds, stream, k, q, t, nzc,
                            idxmap, gin, out);
-    else if (ZL == 16)
-        hipLaunchKernelGGL((tvam_adjl_kernel<16, 1024>), dim3((unsigned)nb), dim3(1024), lds, stream, k, q, t, nzc, idxmap,
-                           gin, out);
-    else if (pl.adjl_nt == 896)  // 14 waves, 2 workgroups (7 waves per SIMD) per CU at <= 72 VGPRs
-        hipLaunchKernelGGL((tvam_adjl_kernel<8, 896, 7>), dim3((unsigned)nb), dim3(896), lds, stream, k, q, t, nzc, idxmap,
-                           gin, out);
-    else if (pl.adjl_nt == 768)
+    else  // two 768-thread workgroups (6 waves per SIMD) per CU at <= 80 VGPRs
         hipLaunchKernelGGL((tvam_adjl_kernel<8, 768, 6>), dim3((unsigned)nb), dim3(768), lds, stream, k, q, t, nzc, idxmap,
-                           gin, out);
-    else
-        hipLaunchKernelGGL((tvam_adjl_kernel<8, 1024>), dim3((unsigned)nb), dim3(1024), lds, stream, k, q, t, nzc, idxmap,
                            gin, out);
     return hipGetLastError();
 }
@@ -377,9 +357,8 @@ hipError_t tvam_launch_adj_lists(const TvamConsts& k, const TvamPlanar& pl, cons
 // The (tile, quadrant) chunk lists are split into `parts` groups.  Owned buffers come back in
 // `bufs` (freed with the plan); hipErrorOutOfMemory when the lists would exceed `max_bytes`
 // (the plan then keeps the tile adjoint).
-hipError_t tvam_build_adj_lists(const TvamConsts& k, TvamPlanar& pl, const TvamTiles& t, int parts, int order,
-                                size_t max_bytes, TvamAdjListBufs& bufs, hipStream_t stream) {
-    (void)order;
+hipError_t tvam_build_adj_lists(const TvamConsts& k, TvamPlanar& pl, const TvamTiles& t, int parts, size_t max_bytes,
+                                TvamAdjListBufs& bufs, hipStream_t stream) {
     const int ntiles = t.ntx * t.nty;
     const bool w2 = k.vox_chord < TVAM_W2_MAX;  // the tile adjoint's weight form (tvam_launch_adj_planar)
     const int w = t.tsx + 2;

@@ -81,6 +81,7 @@ struct TvamPlanar {
     int32_t rayfwd_nt;         // ray-driven forward: threads per workgroup (256 or 512)
     int32_t fwd_parts;         // forward: angle parts per (tile, slice chunk) (thin slabs; 1 = none)
     int32_t fwd_ab;            // forward: angles per barrier (1 or 2)
+    int32_t fwd_dma;           // forward: binned slabs staged by LDS-DMA (tvam_planar_fwd_dma_ok)
     float* fwd_part;           // forward: [fwd_parts][nz][res_y][res_x] partial doses when fwd_parts > 1
     float* fwd_bin;            // forward: [ns][crop_x + 2 bin_pad][bin_nz] slice-binned patterns (nullptr: staged
                                // from the [row][col] patterns directly)
@@ -105,8 +106,6 @@ struct TvamPlanar {
     int32_t adjl_tw0, adjl_tw1;        // row pitch (voxels) for equal / opposite step signs: 1 / 15 (mod 16)
     int32_t adjl_slack;                // zeroed bytes around each plane (padding visits walk there)
     int32_t adjl_z;                    // slices per workgroup (8 or 16)
-    int32_t adjl_nt;                   // threads per workgroup (1024, 896 or 768)
-    int32_t adjl_pfd;                  // weight rows loaded ahead (4 or 8)
 };
 
 // Device buffers of the visit lists (owned by the plan).
@@ -119,8 +118,8 @@ struct TvamAdjListBufs {
     int64_t visits_padded = 0;
 };
 size_t tvam_adjl_lds(const TvamPlanar& pl, const TvamTiles& t, int Z);
-hipError_t tvam_build_adj_lists(const TvamConsts& k, TvamPlanar& pl, const TvamTiles& t, int parts, int order,
-                                size_t max_bytes, TvamAdjListBufs& bufs, hipStream_t stream);
+hipError_t tvam_build_adj_lists(const TvamConsts& k, TvamPlanar& pl, const TvamTiles& t, int parts, size_t max_bytes,
+                                TvamAdjListBufs& bufs, hipStream_t stream);
 hipError_t tvam_launch_adj_lists(const TvamConsts& k, const TvamPlanar& pl, const TvamTiles& t, int Z,
                                  const int32_t* idxmap, const float* gin, float* out, hipStream_t stream);
 
@@ -132,6 +131,7 @@ hipError_t tvam_launch_refr_model(const TvamConsts& k, const TvamPlanar& pl, con
                                   int32_t* need, hipStream_t stream);
 size_t tvam_planar_fwd_lds(const TvamPlanar& pl, int Z);
 bool tvam_planar_fwd_fits(const TvamPlanar& pl, int Z);
+bool tvam_planar_fwd_dma_ok(const TvamPlanar& pl, int Z);
 hipError_t tvam_launch_fwd_planar(const TvamConsts& k, const TvamPlanar& pl, int Z, const float* pat, float* dose,
                                   hipStream_t stream);
 size_t tvam_planar_adj_lds(const TvamPlanar& pl, const TvamTiles& t, int Z);

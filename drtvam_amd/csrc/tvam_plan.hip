@@ -510,9 +510,7 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
         p->pl.adjl_z = env_int("TVAM_ADJL_Z", az_knob == 8 ? 8 : 16) == 8 ? 8 : 16;
         const int64_t nwg4 = (int64_t)p->tiles.ntx * p->tiles.nty * 4 * ((k.nz + p->pl.adjl_z - 1) / p->pl.adjl_z);
         const int parts = (int)std::min<int64_t>(4, std::max<int64_t>(1, (4096 + nwg4 - 1) / std::max<int64_t>(nwg4, 1)));
-        p->pl.adjl_nt = env_int("TVAM_ADJL_NT", 768);
-        p->pl.adjl_pfd = env_int("TVAM_ADJL_PFD", 8) == 4 ? 4 : 8;
-        e = tvam_build_adj_lists(k, p->pl, p->tiles, parts, 0, fr / 4, p->adjl, nullptr);
+        e = tvam_build_adj_lists(k, p->pl, p->tiles, parts, fr / 4, p->adjl, nullptr);
         // 16 slices per workgroup where the tile's 4 planes fit in LDS (the weights are the same)
         if (e == hipSuccess && p->pl.adjl_z == 16 && tvam_adjl_lds(p->pl, p->tiles, 16) > 160 * 1024) p->pl.adjl_z = 8;
         if (e == hipSuccess && tvam_adjl_lds(p->pl, p->tiles, p->pl.adjl_z) > 160 * 1024) e = hipErrorOutOfMemory;
@@ -566,6 +564,9 @@ static int fwd_buffers(tvam_plan* p) {
         p->pl.fwd_bin = p->d_pl_bin;
         p->pl.fwd_pf = nq;
     }
+    // binned slabs staged by LDS-DMA where the window fits (tvam_planar_fwd_dma_ok; TVAM_FWD_DMA=0
+    // builds keep the register staging)
+    p->pl.fwd_dma = tvam_planar_fwd_dma_ok(p->pl, Z) ? 1 : 0;
     return 0;
 }
 

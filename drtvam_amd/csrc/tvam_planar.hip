@@ -123,7 +123,21 @@ hipError_t tvam_launch_planar_rays(const TvamConsts& k, const TvamPlanar& pl, hi
 // slab row stride (words) of Z slices: an odd number of 16-byte groups, so 16
 // consecutive columns' ds_read_b128 hit 16 different bank groups
 __host__ __device__ constexpr int tvam_fwd_zs(int Z) { return ((Z + 4) / 4) % 2 ? Z + 4 : Z + 8; }
-#define TVAM_ACH 256  // angles per LDS chunk of per-angle constants
+
+// LDS-DMA staging of the binned slabs (TVAM_FWD_DMA, straight rays): global_load_lds writes a
+// wave's 64 lanes' 16-byte loads to 64 consecutive 16-byte LDS slots, so a buffer is laid out in
+// whole wave-instructions: the slab's ncm * ZS / 4 slots (a column's Z / 4 data slots and its pad
+// slots) rounded up to 64, and 64 record slots.  Each lane loads the global float4 its slot holds
+// (a pad or round-up slot re-loads a data slot; nothing reads it).
+#ifndef TVAM_FWD_DMA
+#define TVAM_FWD_DMA 1
+#endif
+__host__ __device__ constexpr int tvam_fwd_dma_np(int ncm, int Z) { return (ncm * (tvam_fwd_zs(Z) / 4) + 63) / 64 * 64; }
+// a staged column outside the crop: no chord ({q, t_end < 0}; refracted: the second record zero)
+__device__ float4 tvam_null_rec[2] = {{0.0f, 0.0f, -1.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
+#ifndef TVAM_ACH
+#define TVAM_ACH 128  // angles per LDS chunk of per-angle constants
+#endif
 
 // Z: slices per thread; NC: candidate DMD columns per (voxel, angle), a
 // bound the plan derives from the voxel's lateral width in columns; MULTI:
@@ -136,23 +150,29 @@ __host__ __device__ constexpr int tvam_fwd_zs(int Z) { return ((Z + 4) / 4) % 2 
 // per-angle constants are the (tile, angle) model of the chord index u (tvam_refr_model_kernel),
 // and each voxel visits a per-(tile, angle) number of candidates (the same for the whole
 // workgroup) from ceil(u - w).
-template <int Z, int NC, bool MULTI, int PF, int AB, bool BIN = false, bool REFR = false>
+template <int Z, int NC, bool MULTI, int PF, int AB, bool BIN = false, bool REFR = false, bool DMAP = false>
 __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, TvamPlanar pl,
                                                                   const float* __restrict__ pat,
                                                                   float* __restrict__ dose) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int ncm = pl.ncmax;
     constexpr int RW = REFR ? 2 : 1;  // records (float4) per staged column
+    constexpr bool DMA = BIN && DMAP && AB <= 2;  // LDS-DMA staging (pl.fwd_dma)
     // [2][AB][ncm * ZS + 4] (double buffer of AB angles per barrier), ZS = tvam_fwd_zs(Z);
-    // the 4 words past a buffer's slab take the BIN staging's idle slots
+    // the 4 words past a buffer's slab take the BIN staging's idle slots.  DMA: [2][AB][np] float4
+    // slab slots and [2][AB][64 RW] record slots (tvam_fwd_dma_np; refracted: record h of column j
+    // at 64 h + j)
     constexpr int ZS = tvam_fwd_zs(Z);
-    const int bstride = ncm * ZS + 4;
+    const int np = DMA ? tvam_fwd_dma_np(ncm, Z) : 0;
+    const int bstride = DMA ? 4 * np : ncm * ZS + 4;
+    const int rstride = DMA ? 64 * RW : ncm * RW;
+    const int rhalf = DMA ? 64 : ncm;  // refracted: the second records' offset
     float* s_p = reinterpret_cast<float*>(smem);
-    float4* s_r = reinterpret_cast<float4*>(s_p + 2 * AB * bstride);  // [2][AB][ncm * RW]
+    float4* s_r = reinterpret_cast<float4*>(s_p + 2 * AB * bstride);  // [2][AB][rstride]
     // per-angle constants of TVAM_ACH (+2 look-ahead) angles, copied to LDS so the
     // angle loop issues no scalar loads (an s_load's lgkmcnt wait would also
     // drain every outstanding LDS read)
-    float4* s_ang = reinterpret_cast<float4*>(s_r + 2 * AB * ncm * RW);  // [TVAM_ACH + 4][2]
+    float4* s_ang = reinterpret_cast<float4*>(s_r + 2 * AB * rstride);  // [TVAM_ACH + 4][2]
     int* s_cb = reinterpret_cast<int*>(s_ang + 2 * (TVAM_ACH + 4)); // [TVAM_ACH + 4]
     int* s_row = s_cb + (TVAM_ACH + 4);                            // [Z]: the slice's row, -1 none, -2 several
 
@@ -242,6 +262,43 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
             st_off[q] = jj * ZS + z;
         }
     }
+    // DMA: this lane's slab slots w * 64 + lane + q * 256 (w: its wave) -> source float4 offsets
+    // within an angle's binned window (angle-independent); a pad or round-up slot loads its
+    // column's last data slot / slot 0
+    const int dwave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
+    int dsrc[2] = {0, 0};
+    if constexpr (DMA) {
+        constexpr int GZ = ZS / 4, G = Z / 4;
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int P = (int)threadIdx.x + q * TVAM_PB;
+            const int jj = P / GZ, gq = min(P - (P / GZ) * GZ, G - 1);
+            dsrc[q] = P < ncm * GZ ? jj * (pl.bin_nz / 4) + gq : 0;
+        }
+    }
+    auto fetch_dma = [&](int al, int buf) __attribute__((always_inline)) {
+        const int cb = s_cb[al - tbase];
+        const pl_f4* src = reinterpret_cast<const pl_f4*>(pl.fwd_bin) +
+                           ((size_t)al * (k.crop_x + 2 * pl.bin_pad) + (cb + pl.bin_pad)) * (pl.bin_nz / 4) + z0 / 4;
+        float4* slab = reinterpret_cast<float4*>(s_p + buf * bstride);
+#pragma unroll
+        for (int q = 0; q < 2; ++q) {
+            const int wb = dwave * 64 + q * TVAM_PB;  // wave-uniform
+            if (wb < np)
+                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + dsrc[q]),
+                                                 (__attribute__((address_space(3))) void*)(slab + wb), 16, 0, 0);
+        }
+        if (dwave < RW) {  // the window's ray-table records (ncm <= 64, host-checked); refracted: wave 1
+                           // loads the columns' second records
+            const int lane = (int)threadIdx.x & 63, col = cb + lane;
+            const float4* tab = reinterpret_cast<const float4*>(REFR && dwave == 1 ? pl.vox2 : pl.vox);
+            const float4* rs = (lane < ncm && (unsigned)col < (unsigned)k.crop_x) ? tab + (size_t)al * k.crop_x + col
+                                                                                : &tvam_null_rec[dwave];
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)rs,
+                                             (__attribute__((address_space(3))) void*)(s_r + buf * rstride + 64 * dwave),
+                                             16, 0, 0);
+        }
+    };
     // global loads of angle al's slab (slice-binned pattern + ray table) into registers
     // (the ray-table entry travels in its own array: a 48-byte stage struct is left in scratch)
     struct StageDirect {
@@ -303,7 +360,7 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
             for (int q = 0; q < PF; ++q)
                 if (st_jj[q] >= 0) sp[st_off[q]] = S.pv[q];
         }
-        if ((int)threadIdx.x < ncm * RW) reinterpret_cast<pl_f4*>(s_r)[buf * ncm * RW + threadIdx.x] = rv;
+        if ((int)threadIdx.x < ncm * RW) reinterpret_cast<pl_f4*>(s_r)[buf * rstride + threadIdx.x] = rv;
     };
 
     float acc[Z];
@@ -313,7 +370,7 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
     auto compute_refr = [&](int al, int buf) {
         const int cb = s_cb[al - tbase];
         const float* sp = s_p + buf * bstride;
-        const float4* sr = s_r + buf * ncm * 2;
+        const float4* sr = s_r + buf * rstride;
         // u(lx, ly) = the chord index through the voxel centre (lattice coordinates from the tile corner)
         const float4 m0 = s_ang[2 * (al - tbase)], m1 = s_ang[2 * (al - tbase) + 1];
         // this wave's candidate count (uniform over the wave, >= 2)
@@ -325,7 +382,7 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
         jj0 = min(max(jj0, 0), ncm - nc);
         // candidate c's weight (exact slab intersection with its own chord; 0 when it misses the voxel)
         auto weight = [&](int jc) {
-            const float4 q = sr[jc], g = sr[ncm + jc];
+            const float4 q = sr[jc], g = sr[rhalf + jc];
             const int fl = __float_as_int(g.z);
             const float xa = fmaf(X0, g.x, q.x), xb = fmaf(X1, g.x, q.x);
             const float ya = fmaf(Y0, g.y, q.y), yb = fmaf(Y1, g.y, q.y);
@@ -365,7 +422,7 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
         }
         const int cb = s_cb[al - tbase];
         const float* sp = s_p + buf * bstride;
-        const float4* sr = s_r + buf * ncm;
+        const float4* sr = s_r + buf * rstride;
         // per-angle constants {s*du, -c*du, 1/d.x, 1/d.y}, {half width in columns, axis flags}
         const float4 g0 = s_ang[2 * (al - tbase)], g1 = s_ang[2 * (al - tbase) + 1];
         const int fl = __float_as_int(g1.y);
@@ -435,7 +492,32 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
 
     // Software pipeline over angles: angle a is computed from LDS buffer a & 1
     // while the loads of angle a + 1 are in flight in registers.
-    if (ab < ae && AB <= 2) {
+    if constexpr (DMA) {
+      if (ab < ae) {
+        // LDS-DMA: the next AB angles' slabs and records load straight into the other half while
+        // this half is computed (its last reads were before the previous barrier); the loads are
+        // drained (vmcnt) before the barrier that precedes their reads
+        fetch_dma(ab, 0);
+        if (AB > 1 && ab + 1 < ae) fetch_dma(ab + 1, 1);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        int half = 0;
+        for (int al = ab; al < ae; al += AB) {
+            if (al - tbase > TVAM_ACH + 4 - 2 * AB) {  // next chunk of per-angle constants
+                tbase = al;
+                load_table(al);
+                __syncthreads();
+            }
+            if (al + AB < ae) fetch_dma(al + AB, (half ^ 1) * AB);
+            if (AB > 1 && al + AB + 1 < ae) fetch_dma(al + AB + 1, (half ^ 1) * AB + 1);
+            compute(al, half * AB);
+            if (AB > 1 && al + 1 < ae) compute(al + 1, half * AB + 1);
+            half ^= 1;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+      }
+    } else if (ab < ae && AB <= 2) {
         // AB angles per barrier: the next group's global loads are in flight in
         // registers while this group is computed from LDS (named stages: an
         // array of them indexed by the angle in the group can end up in scratch)
@@ -613,9 +695,19 @@ __global__ __launch_bounds__(256) void tvam_slice_bin4_kernel(TvamConsts k, Tvam
                 make_float4(s_t[cc][4 * q], s_t[cc][4 * q + 1], s_t[cc][4 * q + 2], s_t[cc][4 * q + 3]);
 }
 
+// the binned slabs are staged by LDS-DMA (TVAM_FWD_DMA) where a window fits: <= 2 slab slots per
+// thread and one record wave per record kind (pl.fwd_dma; else register staging)
+bool tvam_planar_fwd_dma_ok(const TvamPlanar& pl, int Z) {
+    return TVAM_FWD_DMA && pl.fwd_bin && pl.ncmax <= 64 && tvam_fwd_dma_np(pl.ncmax, Z) <= 2 * TVAM_PB &&
+           (pl.fwd_ab == 1 || pl.fwd_ab == 2);
+}
+
 size_t tvam_planar_fwd_lds(const TvamPlanar& pl, int Z) {
     const int ab = pl.fwd_ab > 1 ? pl.fwd_ab : 1;
     const size_t rw = pl.fwd_refr ? 2 : 1;
+    if (pl.fwd_dma && pl.fwd_bin && ab <= 2)
+        return 2 * ab * ((size_t)tvam_fwd_dma_np(pl.ncmax, Z) + 64 * rw) * sizeof(float4) +
+               (size_t)(TVAM_ACH + 4) * (2 * sizeof(float4) + sizeof(int)) + (size_t)Z * sizeof(int);
     return 2 * ab * (((size_t)pl.ncmax * tvam_fwd_zs(Z) + 4) * sizeof(float) + rw * pl.ncmax * sizeof(float4)) +
            (size_t)(TVAM_ACH + 4) * (2 * sizeof(float4) + sizeof(int)) + (size_t)Z * sizeof(int);
 }
@@ -754,6 +846,18 @@ hipError_t tvam_launch_refr_model(const TvamConsts& k, const TvamPlanar& pl, con
 template <int Z, int NC>
 static void launch_fwd(dim3 grid, size_t lds, hipStream_t stream, const TvamConsts& k, const TvamPlanar& pl,
                        const float* pat, float* dose) {
+    if (pl.fwd_bin && pl.fwd_dma) {  // binned slabs staged by LDS-DMA
+        if (pl.fwd_refr)
+            hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, 2, false, 1, 2, true, true, true>), grid, dim3(TVAM_PB), lds,
+                               stream, k, pl, pat, dose);
+        else if (pl.fwd_ab == 1)
+            hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 1, 1, true, false, true>), grid, dim3(TVAM_PB), lds,
+                               stream, k, pl, pat, dose);
+        else
+            hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 1, 2, true, false, true>), grid, dim3(TVAM_PB), lds,
+                               stream, k, pl, pat, dose);
+        return;
+    }
     if (pl.fwd_refr) {  // refracted chords: binned staging, 2 angles per barrier, candidates per (tile, angle)
         if (pl.fwd_pf == 1)
             hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, 2, false, 1, 2, true, true>), grid, dim3(TVAM_PB), lds, stream,
