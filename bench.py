@@ -118,10 +118,11 @@ def cpu_baseline(config, N, seconds, threads):
 # Roofline of the dominant kernel, from the committed counter summary of the current build
 # (tools/pmc_bench.sh + tools/roofline_summary.py -> profiles/r03/roofline_config<K>.json): the
 # binding resource's bytes per launch (LDS-array cycles x 256 B, or HBM FETCH x 2 + WRITE) over
-# the launch duration of the counter run itself, against the 2.4 GHz spec peak (LDS 157.3 TB/s,
-# HBM 8 TB/s; MI355X_MICROARCH.md).  Every field can be recomputed from that one file; the bench's
-# own HIP-event time of the projection call that contains the kernel is reported beside it.
-ROOFLINE_DIR = os.path.join(ROOT, "profiles", "r04")
+# the kernel's average launch time measured live in the timed iterations (HIP events around each
+# launch on its stream, tvam_plan_kernel_time), against the 2.4 GHz spec peak (LDS 157.3 TB/s,
+# HBM 8 TB/s; MI355X_MICROARCH.md).  The counter run's own launch time and fraction stay beside
+# them, and every counter field can be recomputed from that one file.
+ROOFLINE_DIR = os.path.join(ROOT, "profiles", "r05")
 
 
 def csrc_digest():
@@ -144,7 +145,11 @@ DOMINANT = {2: "forward: voxel-driven planar forward (two per iteration)",
             5: "forward: per-ray tile kernel of the jittered first segments (two per iteration)"}
 
 
-def make_roofline(args, N, A, world, prob, visits, rays, fwd_s, adj_s):
+def make_roofline(args, N, A, world, prob, visits, rays, fwd_s, adj_s, kt=None):
+    """kt: (total ms, launches) of the dominant kernel over the timed iterations, from HIP events
+    on its launch stream (Projection.kernel_time): `achieved` / `frac` are the counters' resource
+    bytes (or instructions) per launch over that live average launch time; the counter run's own
+    figures stay beside them."""
     alg_bytes = 8.0 * visits + 4.0 * rays  # SURVEY.md 8(d): forward = 8 B per visit + 4 B per ray
     info = {"fwd_call_ms": fwd_s * 1e3, "adj_call_ms": adj_s * 1e3,
             "survey_8d_model": {"alg_bytes_per_forward": alg_bytes, "rate_gbs": alg_bytes / fwd_s / 1e9,
@@ -165,7 +170,15 @@ def make_roofline(args, N, A, world, prob, visits, rays, fwd_s, adj_s):
                 "counters": os.path.relpath(path, ROOT), "counters_build": summ["build"],
                 "counters_csrc_sha16": summ.get("csrc_sha16"), "csrc_sha16": here,
                 "stale_frac": r["frac"], **info}
-    return {"bound": r["bound"], "achieved": r["achieved"], "peak": r["peak"], "unit": r["unit"], "frac": r["frac"],
+    achieved, frac, live = r["achieved"], r["frac"], None
+    if kt is not None and kt[1] > 0:
+        live_ns = kt[0] * 1e6 / kt[1]
+        achieved = r["resource_bytes_per_launch"] / live_ns
+        frac = achieved / r["peak"]
+        live = {"launch_ns": live_ns, "launches": kt[1], "source": "HIP events around each launch on its stream "
+                                                                   "(tvam_plan_kernel_time), timed iterations"}
+    return {"bound": r["bound"], "achieved": achieved, "peak": r["peak"], "unit": r["unit"], "frac": frac,
+            "live": live, "achieved_counter_run": r["achieved"], "frac_counter_run": r["frac"],
             "traffic": r["traffic"], "traffic_over_min": r["traffic_over_min"], "min_bytes": r["min_bytes"],
             "kernel": summ["kernel"], "role": DOMINANT[args.config], "launch_ns_counter_run": summ["avg_ns"],
             "clock_ghz_counter_run": summ["clock_ghz_measured"],
@@ -356,6 +369,7 @@ def main():
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
+    prob.proj.kernel_time(True)  # (dominant-kernel launch events from here on; no GPU work)
     state["on"] = True
     t0 = time.perf_counter()
     for i in range(args.warmup, args.warmup + args.steps):
@@ -365,6 +379,7 @@ def main():
         dist.barrier()
     t1 = time.perf_counter()
     state["on"] = False
+    kt = prob.proj.kernel_time(False)
     elapsed = t1 - t0
     fwd = [s.elapsed_time(e) for s, e in fwd_ms]
     if fwd_slices:  # per forward: the sum of its slice ranges' times
@@ -420,7 +435,7 @@ def main():
             dist.destroy_process_group()
         return
 
-    roofline = make_roofline(args, N, A, world, prob, visits, rays, fwd_avg, adj_avg)
+    roofline = make_roofline(args, N, A, world, prob, visits, rays, fwd_avg, adj_avg, kt)
     cpu = None
     if args.cpu_baseline == "auto" and world == 1:
         threads = host_info()["threads"]

@@ -160,6 +160,8 @@ EXPORTS = {
     "tvam_plan_fwd_scale": (ctypes.c_int, [_P, _P]),
     "tvam_plan_bin_stats": (ctypes.c_int, [_P, _P]),
     "tvam_plan_tile_stats": (ctypes.c_int, [_P, _P]),
+    "tvam_plan_kernel_time": (ctypes.c_int, [_P, ctypes.c_int32, ctypes.POINTER(ctypes.c_double),
+                                              ctypes.POINTER(ctypes.c_int64)]),
     "tvam_loss_threshold": (
         ctypes.c_int,
         [_P, _P, ctypes.c_float, _P, ctypes.c_uint64, ctypes.c_int32, ctypes.c_float, ctypes.c_float,

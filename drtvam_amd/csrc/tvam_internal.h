@@ -16,6 +16,11 @@
 // A tuning knob: the environment variable `name` under TVAM_EXPERIMENTAL=1 (logged), else `def`
 // (tvam_plan.hip).
 int tvam_knob(const char* name, int def);
+// Launch timer of the dominant forward kernel (tvam_plan_kernel_time): while enabled, each launch
+// of the voxel-driven planar forward, the per-ray tile forward or the forward brick march is
+// bracketed by two HIP events on its stream.
+void tvam_kt_begin(hipStream_t stream);
+void tvam_kt_end(hipStream_t stream);
 
 // Device tables that drive one tile launch.
 struct TvamTiles {

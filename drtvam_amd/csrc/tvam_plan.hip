@@ -362,6 +362,27 @@ int tvam_knob(const char* name, int def) {
 }
 #define env_int tvam_knob
 
+// Launch timer of the dominant forward kernel (tvam_plan_kernel_time): event pairs recorded on the
+// launching stream around each launch while enabled (up to 1024 launches per measurement).
+namespace {
+struct KernelTimer {
+    bool on = false;
+    std::vector<hipEvent_t> ev;
+    size_t n = 0;
+};
+KernelTimer g_kt;
+}  // namespace
+
+void tvam_kt_begin(hipStream_t stream) {
+    if (g_kt.on && g_kt.n + 2 <= g_kt.ev.size()) (void)hipEventRecord(g_kt.ev[g_kt.n], stream);
+}
+
+void tvam_kt_end(hipStream_t stream) {
+    if (!g_kt.on || g_kt.n + 2 > g_kt.ev.size()) return;
+    (void)hipEventRecord(g_kt.ev[g_kt.n + 1], stream);
+    g_kt.n += 2;
+}
+
 // Planar fast path: regular sampling and rows whose vial entry offset is
 // row-independent (|z| <= 0.7 r < r / sqrt(2) <= max(|p_x|, |p_y|) on the
 // vial wall).  Builds the row -> slice CSR of valid rows and the per-(angle,
@@ -1589,7 +1610,9 @@ static int forward_impl(tvam_plan* p, const float* active_data, const uint32_t* 
                 return hip_fail(e, "hipMemsetAsync");
             stats = p->d_counter;
         }
+        tvam_kt_begin(stream);
         e = tvam_launch_tiles(TVAM_MODE_FWD, kc, t, p->lds_bytes, pat, idxmap, nullptr, dose, stats, stream);
+        tvam_kt_end(stream);
         if (e == hipSuccess) e = tvam_launch_frozen(TVAM_MODE_FWD, kc, t, pat, idxmap, nullptr, dose, nullptr, stream);
         if (e != hipSuccess) return hip_fail(e, "forward launch");
     }
@@ -1911,6 +1934,34 @@ extern "C" int tvam_plan_tile_stats(tvam_plan* p, int64_t* stats) {
     stats[5] = (int64_t)r->spp;
     stats[6] = p->ntiles;
     stats[7] = p->n_slots_all;
+    return 0;
+}
+
+extern "C" int tvam_plan_kernel_time(tvam_plan* p, int32_t enable, double* total_ms, int64_t* launches) {
+    if (!p || !total_ms || !launches) return fail(TVAM_ERR_INVALID, "null argument");
+    *total_ms = 0.0;
+    *launches = 0;
+    hipError_t e = hipSuccess;
+    if (g_kt.n > 0) {
+        e = hipEventSynchronize(g_kt.ev[g_kt.n - 1]);
+        for (size_t i = 0; e == hipSuccess && i < g_kt.n; i += 2) {
+            float ms = 0.0f;
+            e = hipEventElapsedTime(&ms, g_kt.ev[i], g_kt.ev[i + 1]);
+            *total_ms += ms;
+        }
+        *launches = (int64_t)(g_kt.n / 2);
+    }
+    if (e != hipSuccess) return hip_fail(e, "tvam_plan_kernel_time");
+    g_kt.n = 0;
+    g_kt.on = false;
+    if (enable) {
+        while (g_kt.ev.size() < 2048) {
+            hipEvent_t ev;
+            if ((e = hipEventCreate(&ev)) != hipSuccess) return hip_fail(e, "hipEventCreate");
+            g_kt.ev.push_back(ev);
+        }
+        g_kt.on = true;
+    }
     return 0;
 }
 

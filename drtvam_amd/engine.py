@@ -244,6 +244,16 @@ class Projection:
         return dict(zip(("strays", "stray_cap", "stray_walk", "main_walk", "frozen", "spp", "tiles", "slots"),
                         (int(x) for x in v)))
 
+    def kernel_time(self, enable: bool):
+        """Launch time of the dominant forward kernel from HIP events on its stream
+        (tvam_plan_kernel_time): (total ms, launches) recorded since the previous call; enable
+        starts a new measurement."""
+        t = ctypes.c_double(0.0)
+        n = ctypes.c_int64(0)
+        with torch.cuda.device(self.device):
+            _abi.check(self.lib.tvam_plan_kernel_time(self._plan, 1 if enable else 0, ctypes.byref(t), ctypes.byref(n)))
+        return float(t.value), int(n.value)
+
     def count_visits(self, spp: int = 1, seed: int = 0) -> int:
         v = ctypes.c_uint64(0)
         with torch.cuda.device(self.device):

@@ -281,6 +281,14 @@ int tvam_plan_bin_stats(tvam_plan* plan, int64_t* stats);
    over all tiles.  stats has 8 entries.  (ABI v10, added in round 5) */
 int tvam_plan_tile_stats(tvam_plan* plan, int64_t* stats);
 
+/* Measurement (host-synchronous): launch time of the dominant forward kernel -- the voxel-driven
+   planar forward, the per-ray tile forward, or the forward brick march of a scattering medium --
+   from HIP events recorded on its stream around each launch.  Returns the launches recorded since
+   the previous call and their summed time in ms (at most 1024 per measurement), then stops
+   recording, or (enable != 0) starts a new measurement.  Process-wide (one timer for every plan).
+   (ABI v10, added in round 5) */
+int tvam_plan_kernel_time(tvam_plan* plan, int32_t enable, double* total_ms, int64_t* launches);
+
 /* Surface-aware plans: the per-channel voxel volumes the forward divides by and the
    adjoint multiplies the incoming gradient with (inv_vol = 1/volume, 0 where volume
    is 0: volume.py:41-42, :130).  Device pointer [z][y][x][2], caller-owned, kept by

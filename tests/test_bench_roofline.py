@@ -1,5 +1,5 @@
 """The bench line's roofline (bench.make_roofline) from the committed counter summaries
-profiles/r04/roofline_config<K>.json: every number recomputes from that one file (bytes or
+profiles/r05/roofline_config<K>.json: every number recomputes from that one file (bytes or
 instructions per launch over the counter run's own launch time, against the spec peak), the kernel
 it names is the one the same command's rocprofv3 kernel stats list, and the bench copies it only
 while the summary's kernel-source digest is the tree's (otherwise the line says stale, no frac)."""
@@ -49,6 +49,11 @@ def test_roofline_summary_recomputes(config, n):
     assert line["stale"] == (s["csrc_sha16"] != bench.csrc_digest())
     if not line["stale"]:
         assert line["frac"] == r["frac"] and line["traffic"] == r["traffic"]
+        # with the live launch time of the timed iterations: the same bytes over that time
+        live = bench.make_roofline(args, n, n, 1, prob, 1e10, 1e7, 3e-3, 4e-3, kt=(40.0, 16))
+        assert live["live"]["launch_ns"] == pytest.approx(2.5e6)
+        assert live["achieved"] == pytest.approx(r["resource_bytes_per_launch"] / 2.5e6)
+        assert live["frac"] == pytest.approx(live["achieved"] / r["peak"]) and live["frac_counter_run"] == r["frac"]
     # other sizes carry no roofline
     assert bench.make_roofline(args, 64, 64, 1, prob, 1e6, 1e4, 1e-3, 1e-3)["frac"] is None
 
