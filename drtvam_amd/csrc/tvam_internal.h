@@ -17,10 +17,11 @@
 // (tvam_plan.hip).
 int tvam_knob(const char* name, int def);
 // Launch timer of the dominant forward kernel (tvam_plan_kernel_time): while enabled, each launch
-// of the voxel-driven planar forward, the per-ray tile forward or the forward brick march is
-// bracketed by two HIP events on its stream.
-void tvam_kt_begin(hipStream_t stream);
-void tvam_kt_end(hipStream_t stream);
+// of the measured plan's dominant kind -- the voxel-driven planar forward, the per-ray tile
+// forward or the forward brick march -- is bracketed by two HIP events on its stream.
+enum TvamKtKind { TVAM_KT_PLANAR = 0, TVAM_KT_TILE = 1, TVAM_KT_BRICK = 2 };
+void tvam_kt_begin(hipStream_t stream, int kind);
+void tvam_kt_end(hipStream_t stream, int kind);
 
 // Device tables that drive one tile launch.
 struct TvamTiles {

@@ -456,17 +456,25 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
 #if TVAM_TILE_DIAG
     const unsigned long long dg_t0 = __builtin_amdgcn_s_memtime();
 #endif
-    // XCD-aware order: workgroup b runs on XCD b % 8; each XCD takes a contiguous run of slices,
-    // all tiles of a slice in turn, so the tiles re-reading one slice's ray records (every tile a
-    // ray crosses reads its record) share that XCD's L2 instead of fetching it into all eight
+    // XCD-aware order: workgroup b runs on XCD b % 8; XCD x takes slices x, x + 8, x + 16, ..., all
+    // tiles of a slice in turn, so the tiles re-reading one slice's ray records (every tile a ray
+    // crosses reads its record) share that XCD's L2 instead of fetching it into all eight, and the
+    // XCDs' loads stay even where the work per slice is not (contiguous slice runs per XCD left the
+    // XCDs of a sparse active set's empty slices idle: config 5 with filter_radon 11 % slower)
     const int ntl = tp.ntx * tp.nty;
 #ifndef TVAM_TILE_XCD
 #define TVAM_TILE_XCD 1  // (0: workgroups in plain (slice, tile) order, for A/B builds)
 #endif
-    const int L = TVAM_TILE_XCD ? (int)(blockIdx.x & 7) * (int)(gridDim.x >> 3) + (int)(blockIdx.x >> 3)
-                                : (int)blockIdx.x;
-    if (L >= ntl * nzl) return;
-    const int zloc = L / ntl, tile_id = L - zloc * ntl;
+    int zloc, tile_id;
+    if (TVAM_TILE_XCD) {
+        const int i = (int)(blockIdx.x >> 3);
+        zloc = (i / ntl) * 8 + (int)(blockIdx.x & 7);
+        tile_id = i - (i / ntl) * ntl;
+    } else {
+        zloc = (int)blockIdx.x / ntl;
+        tile_id = (int)blockIdx.x - zloc * ntl;
+    }
+    if (zloc >= nzl) return;
     const int kz = zloc + (MODE == TVAM_MODE_FWD ? tp.kz0 : 0);
     const int x0 = (tile_id % tp.ntx) * tsx, y0 = (tile_id / tp.ntx) * tsy;
     const int x1 = min(x0 + tsx, k.res[0]), y1 = min(y0 + tsy, k.res[1]);
@@ -759,8 +767,8 @@ hipError_t tvam_launch_tiles(int mode, const TvamConsts& k, const TvamTiles& t, 
     const int nzl = mode == TVAM_MODE_FWD && t.kz1 > t.kz0 ? t.kz1 - t.kz0 : k.nz;
     TvamTiles tl = t;
     if (!(mode == TVAM_MODE_FWD && t.kz1 > t.kz0)) tl.kz0 = 0;
-    const int64_t nwg = (int64_t)t.ntx * t.nty * nzl;
-    dim3 grid((unsigned)((nwg + 7) / 8 * 8));  // (a multiple of 8: the kernel's XCD-aware order)
+    const int64_t nwg = (int64_t)t.ntx * t.nty * ((nzl + 7) / 8 * 8);
+    dim3 grid((unsigned)nwg);  // slices rounded up to a multiple of 8 (the kernel's XCD-aware order)
     dim3 block(TVAM_BLOCK);
     const bool w2 = k.vox_chord < TVAM_W2_MAX;
 #define TVAM_TILE_LAUNCH(M)                                                                                      \

@@ -367,18 +367,19 @@ int tvam_knob(const char* name, int def) {
 namespace {
 struct KernelTimer {
     bool on = false;
+    int kind = 0;  // TvamKtKind of the measured plan's dominant forward kernel
     std::vector<hipEvent_t> ev;
     size_t n = 0;
 };
 KernelTimer g_kt;
 }  // namespace
 
-void tvam_kt_begin(hipStream_t stream) {
-    if (g_kt.on && g_kt.n + 2 <= g_kt.ev.size()) (void)hipEventRecord(g_kt.ev[g_kt.n], stream);
+void tvam_kt_begin(hipStream_t stream, int kind) {
+    if (g_kt.on && kind == g_kt.kind && g_kt.n + 2 <= g_kt.ev.size()) (void)hipEventRecord(g_kt.ev[g_kt.n], stream);
 }
 
-void tvam_kt_end(hipStream_t stream) {
-    if (!g_kt.on || g_kt.n + 2 > g_kt.ev.size()) return;
+void tvam_kt_end(hipStream_t stream, int kind) {
+    if (!g_kt.on || kind != g_kt.kind || g_kt.n + 2 > g_kt.ev.size()) return;
     (void)hipEventRecord(g_kt.ev[g_kt.n + 1], stream);
     g_kt.n += 2;
 }
@@ -1610,9 +1611,9 @@ static int forward_impl(tvam_plan* p, const float* active_data, const uint32_t* 
                 return hip_fail(e, "hipMemsetAsync");
             stats = p->d_counter;
         }
-        tvam_kt_begin(stream);
+        tvam_kt_begin(stream, TVAM_KT_TILE);
         e = tvam_launch_tiles(TVAM_MODE_FWD, kc, t, p->lds_bytes, pat, idxmap, nullptr, dose, stats, stream);
-        tvam_kt_end(stream);
+        tvam_kt_end(stream, TVAM_KT_TILE);
         if (e == hipSuccess) e = tvam_launch_frozen(TVAM_MODE_FWD, kc, t, pat, idxmap, nullptr, dose, nullptr, stream);
         if (e != hipSuccess) return hip_fail(e, "forward launch");
     }
@@ -1960,6 +1961,9 @@ extern "C" int tvam_plan_kernel_time(tvam_plan* p, int32_t enable, double* total
             if ((e = hipEventCreate(&ev)) != hipSuccess) return hip_fail(e, "hipEventCreate");
             g_kt.ev.push_back(ev);
         }
+        // the plan's dominant forward kernel: the brick march of a scattering medium, else the
+        // voxel-driven planar forward where it serves, else the per-ray tile forward
+        g_kt.kind = p->desc.albedo != 0.0f ? TVAM_KT_BRICK : (p->planar_fwd ? TVAM_KT_PLANAR : TVAM_KT_TILE);
         g_kt.on = true;
     }
     return 0;

@@ -938,9 +938,9 @@ hipError_t tvam_launch_fwd_planar(const TvamConsts& k, const TvamPlanar& pl, int
         else
             hipLaunchKernelGGL(tvam_slice_bin_kernel, bg, dim3(256), 0, stream, k, pl, pat, b0);
     }
-    tvam_kt_begin(stream);
+    tvam_kt_begin(stream, TVAM_KT_PLANAR);
     hipError_t e = tvam_launch_fwd_planar_z(grid, lds, stream, k, pl, Z, pat, dose);
-    tvam_kt_end(stream);
+    tvam_kt_end(stream, TVAM_KT_PLANAR);
     if (e != hipSuccess || parts == 1) return e;
     // sum the angle parts of this launch's slices
     const int64_t plane = (int64_t)k.res[0] * k.res[1];

@@ -1793,7 +1793,7 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
     // forward brick march: int64 fixed point (default) or float LDS adds (TVAM_BIN_FLOAT)
     auto march_fwd = [&](const TvamSegBuf& sb, const uint32_t* vals, const uint32_t* bstart, bool ws) {
         const dim3 grid((unsigned)nbricks), blk(bin_nt);
-        tvam_kt_begin(stream);
+        tvam_kt_begin(stream, TVAM_KT_BRICK);
         if (ws)  // counting-sort entries (csort: int64 tiles, 1024 threads)
             hipLaunchKernelGGL((tvam_bin_march_kernel<0, 1024, true>), grid, dim3(1024), 0, stream, k, sb, vals,
                                bstart, out, nullptr, 0u, nullptr, nullptr);
@@ -1809,7 +1809,7 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
         else
             hipLaunchKernelGGL((tvam_bin_march_kernel<0, 512>), grid, blk, 0, stream, k, sb, vals, bstart, out,
                                nullptr, 0u, nullptr, nullptr);
-        tvam_kt_end(stream);
+        tvam_kt_end(stream, TVAM_KT_BRICK);
     };
     s.st[4] = chunk;
     for (int64_t p0 = 0; p0 < npaths; p0 += chunk) {

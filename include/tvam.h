@@ -281,11 +281,12 @@ int tvam_plan_bin_stats(tvam_plan* plan, int64_t* stats);
    over all tiles.  stats has 8 entries.  (ABI v10, added in round 5) */
 int tvam_plan_tile_stats(tvam_plan* plan, int64_t* stats);
 
-/* Measurement (host-synchronous): launch time of the dominant forward kernel -- the voxel-driven
-   planar forward, the per-ray tile forward, or the forward brick march of a scattering medium --
-   from HIP events recorded on its stream around each launch.  Returns the launches recorded since
-   the previous call and their summed time in ms (at most 1024 per measurement), then stops
-   recording, or (enable != 0) starts a new measurement.  Process-wide (one timer for every plan).
+/* Measurement (host-synchronous): launch time of the plan's dominant forward kernel -- the
+   forward brick march of a scattering medium, else the voxel-driven planar forward where it
+   serves, else the per-ray tile forward -- from HIP events recorded on its stream around each
+   launch.  Returns the launches recorded since the previous call and their summed time in ms (at
+   most 1024 per measurement), then stops recording, or (enable != 0) starts a new measurement of
+   the kernel kind of `plan`.  Process-wide (one timer).
    (ABI v10, added in round 5) */
 int tvam_plan_kernel_time(tvam_plan* plan, int32_t enable, double* total_ms, int64_t* launches);
 
