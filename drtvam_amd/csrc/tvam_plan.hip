@@ -529,7 +529,10 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     if (p->planar_az == 8 && ns > 0 && env_int("TVAM_ADJ_LISTS", 1)) {
         size_t fr = 0, tot = 0;
         if ((e = hipMemGetInfo(&fr, &tot)) != hipSuccess) return hip_fail(e, "hipMemGetInfo");
-        p->pl.adjl_z = env_int("TVAM_ADJL_Z", az_knob == 8 ? 8 : 16) == 8 ? 8 : 16;
+        // 16 slices per workgroup (one per CU) on deep films, 8 (two per CU) on thin ones: the
+        // 50-slice slabs of 8 ranks ran 0.68 ms at 16 (four chunks, the last 2 slices deep) and
+        // 0.47 ms at 8; 400 slices 3.20 ms at 16, 3.29 at 8 (profiles/r05/slab_adjoint_z/)
+        p->pl.adjl_z = env_int("TVAM_ADJL_Z", az_knob == 8 || k.nz < 256 ? 8 : 16) == 8 ? 8 : 16;
         const int64_t nwg4 = (int64_t)p->tiles.ntx * p->tiles.nty * 4 * ((k.nz + p->pl.adjl_z - 1) / p->pl.adjl_z);
         const int parts = (int)std::min<int64_t>(4, std::max<int64_t>(1, (4096 + nwg4 - 1) / std::max<int64_t>(nwg4, 1)));
         e = tvam_build_adj_lists(k, p->pl, p->tiles, parts, fr / 4, p->adjl, nullptr);
