@@ -138,6 +138,7 @@ hipError_t tvam_launch_refr_model(const TvamConsts& k, const TvamPlanar& pl, con
 size_t tvam_planar_fwd_lds(const TvamPlanar& pl, int Z);
 bool tvam_planar_fwd_fits(const TvamPlanar& pl, int Z);
 bool tvam_planar_fwd_dma_ok(const TvamPlanar& pl, int Z);
+bool tvam_planar_fwd_dma_window(const TvamPlanar& pl, int Z);
 hipError_t tvam_launch_fwd_planar(const TvamConsts& k, const TvamPlanar& pl, int Z, const float* pat, float* dose,
                                   hipStream_t stream);
 size_t tvam_planar_adj_lds(const TvamPlanar& pl, const TvamTiles& t, int Z);

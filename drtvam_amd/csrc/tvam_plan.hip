@@ -597,10 +597,11 @@ static int fwd_buffers(tvam_plan* p) {
 
 
 // Slices per workgroup of the voxel-driven forward: the fewest padded slice-passes
-// ceil(nz / Z) * (Z + 4) (the +4 prices the per-angle candidate geometry shared by the Z
-// slices; +10 % for the deep slabs' lower occupancy) among the depths whose staging fits:
-// Z = 32 on 400-slice films, 52 on the 50-slice slabs of 8 ranks (one chunk instead of two of
-// 28: forward 0.546 -> 0.477 ms per rank).  Returns false when none fits.
+// ceil(nz / Z) * (Z + 12) (the +12 prices the per-angle candidate geometry and staging shared by
+// the Z slices), register-staged depths (windows the LDS-DMA staging cannot take) priced 25 %
+// higher, among the depths whose staging fits.  With the DMA staging, Z = 52 on 400-slice films
+// (8 chunks: 2.68 ms against 2.72 at Z = 40 and 2.81 at 32, profiles/r05/fwd_depth/), and on the
+// 50-slice slabs of 8 ranks (one chunk).  Returns false when none fits.
 static int choose_fwd_z(tvam_plan* p) {
     const TvamConsts& k = p->k;
     if (p->planar_fz == 0) {
@@ -609,8 +610,8 @@ static int choose_fwd_z(tvam_plan* p) {
         const bool deep = env_int("TVAM_FWD_BIN", 1) != 0;
         for (int Z : {52, 40, 32, 28, 24, 16, 8}) {
             if ((Z > 32 && !deep) || !tvam_planar_fwd_fits(p->pl, Z)) continue;
-            // deep slabs (Z > 32: 4 instead of 5 waves per SIMD) measured ~4 % slower per slice at 400^3
-            const int64_t cost = (int64_t)((k.nz + Z - 1) / Z) * (Z + 4) * (Z > 32 ? 11 : 10);
+            const int64_t cost =
+                (int64_t)((k.nz + Z - 1) / Z) * (Z + 12) * (deep && tvam_planar_fwd_dma_window(p->pl, Z) ? 4 : 5);
             if (cost < bcost) bcost = cost, best = Z;
         }
         p->planar_fz = best;

@@ -697,9 +697,12 @@ __global__ __launch_bounds__(256) void tvam_slice_bin4_kernel(TvamConsts k, Tvam
 
 // the binned slabs are staged by LDS-DMA (TVAM_FWD_DMA) where a window fits: <= 2 slab slots per
 // thread and one record wave per record kind (pl.fwd_dma; else register staging)
+bool tvam_planar_fwd_dma_window(const TvamPlanar& pl, int Z) {
+    return TVAM_FWD_DMA && pl.ncmax <= 64 && tvam_fwd_dma_np(pl.ncmax, Z) <= 2 * TVAM_PB;
+}
+
 bool tvam_planar_fwd_dma_ok(const TvamPlanar& pl, int Z) {
-    return TVAM_FWD_DMA && pl.fwd_bin && pl.ncmax <= 64 && tvam_fwd_dma_np(pl.ncmax, Z) <= 2 * TVAM_PB &&
-           (pl.fwd_ab == 1 || pl.fwd_ab == 2);
+    return pl.fwd_bin && (pl.fwd_ab == 1 || pl.fwd_ab == 2) && tvam_planar_fwd_dma_window(pl, Z);
 }
 
 size_t tvam_planar_fwd_lds(const TvamPlanar& pl, int Z) {
