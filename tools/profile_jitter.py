@@ -31,7 +31,7 @@ def main():
             cfg["vial"]["medium"]["albedo"] = 0.0
     spp = cfg["spp"]
     a0 = N // 3
-    d = desc_from_config(cfg, angle_range=(a0, a0 + na))
+    d = desc_from_config(cfg, angle_range=(a0, a0 + na), tile=int(os.environ.get("PJ_TILE", "0")))
     d.flags |= _abi.FLAG_NO_ZERO_SKIP
     d.active_total = N * N * N
     n = na * N * N
