@@ -16,6 +16,17 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: long-running CPU test")
 
 
+def pytest_terminal_summary(terminalreporter, exitstatus, config):
+    """The parity numbers the tests recorded (tests/parity_report.py): flipped paths per test."""
+    from parity_report import RECORDS
+    if not RECORDS:
+        return
+    terminalreporter.section("parity report (flip protocol: flipped paths, errors outside them)")
+    for name, numbers in RECORDS:
+        terminalreporter.write_line(f"{name}: " + ", ".join(
+            f"{k} {v:.3e}" if isinstance(v, float) else f"{k} {v}" for k, v in numbers.items()))
+
+
 @pytest.fixture(scope="session")
 def oracle():
     from oracle import oracle as orc

@@ -11,6 +11,8 @@ agrees to fp32 rounding), counts them, and holds everything else to the north-st
 import numpy as np
 import torch
 
+from parity_report import report
+
 RTOL = 1e-4  # north star: 1e-4 relative L2
 
 
@@ -52,6 +54,7 @@ def flip_protocol(oracle, proj, desc, pat, G, spp, seed, active_pixels=None, gpu
     out = {"pixels": int(n), "flipped": nflip, "rel_l2_adjoint": e_adj, "rel_l2_forward": e_fwd,
            "rel_l2_adjoint_all": rel_l2(g, gref), "visits": int(visits)}
     print("flip protocol:", out)
+    report(flipped=nflip, of=int(n) * spp, rel_l2_adjoint=e_adj, rel_l2_forward=e_fwd)
     assert nflip <= max(2, max_flip_frac * n * spp), out  # flipped paths: at most 1e-4 of them
     assert e_adj < RTOL, out
     assert e_fwd < RTOL, out

@@ -22,6 +22,7 @@ from drtvam_amd import _abi
 from drtvam_amd.configs import (benchy_index_matched, cylindrical_refraction, cylindrical_scattering,
                                 desc_from_config, square_occluded)
 from drtvam_amd.engine import Projection
+from parity_report import report
 from parity_util import RTOL, flip_protocol, rel_l2
 
 DEV = "cuda:0"
@@ -39,6 +40,7 @@ def test_config2_every_angle(oracle):
     got = proj.forward(torch.as_tensor(pat, device=DEV), None, 1, 0).cpu().numpy()[..., 0]
     ref, visits = oracle.forward(d, pat, nthreads=THREADS)
     e = rel_l2(got, ref)
+    report(rel_l2_forward=e, visits=int(visits))
     print(f"config 2 forward rel-L2 {e:.3e}, visits {visits}")
     assert e < RTOL
     assert abs(proj.count_visits(1, 0) - visits) <= max(2, 1e-4 * visits)
@@ -47,6 +49,7 @@ def test_config2_every_angle(oracle):
     g = proj.adjoint(torch.as_tensor(G, device=DEV), n, None, 1, 0).cpu().numpy()
     gref, _ = oracle.adjoint(d, G, nthreads=THREADS)
     e = rel_l2(g, gref)
+    report(rel_l2_adjoint=e)
     print(f"config 2 adjoint rel-L2 {e:.3e}")
     assert e < RTOL
     proj.close()
@@ -105,6 +108,7 @@ def test_config3_adjoint_angle_shard(oracle):
     g = proj.adjoint(torch.as_tensor(G, device=DEV), n, None, 1, 0).cpu().numpy()
     gref, _ = oracle.adjoint(dfull, G, active_pixels=pix, nthreads=THREADS)
     e = rel_l2(g, gref)
+    report(rel_l2_adjoint=e)
     print(f"config 3 shard adjoint rel-L2 {e:.3e}")
     assert e < RTOL
     proj.close()

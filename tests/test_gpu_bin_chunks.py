@@ -29,6 +29,7 @@ pytestmark = pytest.mark.gpu
 from drtvam_amd import _abi
 from drtvam_amd.configs import cylindrical_scattering, desc_from_config, square_occluded
 from drtvam_amd.engine import Projection
+from parity_report import report
 from parity_util import RTOL, flip_protocol, flipped_pixels, rel_l2
 
 DEV = "cuda:0"
@@ -96,6 +97,7 @@ def _check_adjoint(s, g):
     nflip = int(s["flip"].sum())
     e = rel_l2(g[keep], s["gref"][keep])
     r99 = float(np.quantile(np.abs(g - s["gref"])[keep] / s["gabs"][keep], 0.99))
+    report(flipped=nflip, of=int(s["sub"].size) * SPP4, rel_l2_adjoint=e, p99=r99)
     print(f"adjoint: {s['sub'].size} subset pixels, {nflip} flipped, rel-L2 {e:.3e}, "
           f"99th percentile |g - ref| / sum|terms| {r99:.2e}")
     assert nflip <= max(2, 1e-4 * s["sub"].size * SPP4)
@@ -220,6 +222,7 @@ def test_config5_spread_angles(oracle):
     finally:
         proj.close()
         torch.cuda.empty_cache()
+    report(flipped=nflip, of=int(sub.size) * spp, rel_l2_adjoint=ea, rel_l2_forward=ef, strays=ts["strays"])
     print(f"config 5, 32 angles spread over 800, {sub.size} subset pixels ({sub.size * spp} paths): "
           f"{nflip} flipped, adjoint rel-L2 {ea:.3e}, forward rel-L2 {ef:.3e}; tile stats {ts}")
     # stray lists in use, each (tile, slice) workgroup walking its slice's strays: a tiny share of

@@ -19,6 +19,7 @@ pytestmark = pytest.mark.gpu
 
 from drtvam_amd.configs import BOX_HOLE_INDEX_MATCHED, benchy_index_matched, cylindrical_refraction, desc_from_config
 from drtvam_amd.engine import Projection
+from parity_report import report
 from drtvam_amd.optimize import optimize
 
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
@@ -163,6 +164,7 @@ def test_surface_scattering_matches_oracle(oracle, case):
     ref, visits = oracle.forward_surface(d, pat, vol, spp=spp, seed=9, nthreads=8)
     got = proj.forward(torch.as_tensor(pat, device="cuda:0"), None, spp, 9).cpu().numpy()
     e = rel_l2(got, ref)
+    report(flipped=nflip, of=int(n) * spp, rel_l2_forward=e)
     print(f"surface-aware scattering: {nflip} flipped pixels of {n}, forward rel-L2 {e:.2e}")
     assert e < 1e-4
     assert ref[..., 0].sum() > 0 and ref[..., 1].sum() > 0
@@ -219,6 +221,7 @@ def test_surface_estimators_match_oracle(oracle, sensor, albedo):
     ref, visits = oracle.forward_surface(d, pat, vol, spp=spp, seed=2, nthreads=8)
     got = proj.forward(torch.as_tensor(pat, device="cuda:0"), None, spp, 2).cpu().numpy()
     e = rel_l2(got, ref)
+    report(flipped=nflip, of=int(n) * spp, rel_l2_forward=e)
     print(f"surface-aware {sensor} (albedo {albedo}): {nflip} flipped pixels of {n}, forward rel-L2 {e:.2e}")
     assert e < 1e-4
     assert ref[..., 0].sum() > 0 and ref[..., 1].sum() > 0
