@@ -197,6 +197,10 @@ __global__ __launch_bounds__(NT, MINW) void tvam_adjl_kernel(TvamConsts k, TvamP
     const size_t plane = (size_t)k.res[0] * k.res[1];
     // gradient tile: a thread per voxel, its Z loads issued together (clamped addresses, no
     // branches), Z / 4 ds_write_b128
+#ifndef TVAM_ADJL_ZSKIP
+#define TVAM_ADJL_ZSKIP 1  // (0: march all-zero gradient tiles too, for A/B builds)
+#endif
+    int nonzero = 0;
     for (int li = threadIdx.x; li < nvox; li += NT) {
         const int ly = li / tw - 1, lx = li - (ly + 1) * tw - 1;
         const bool in = lx >= 0 && ly >= 0 && lx < wx && ly < wy;
@@ -207,6 +211,8 @@ __global__ __launch_bounds__(NT, MINW) void tvam_adjl_kernel(TvamConsts k, TvamP
         for (int z = 0; z < Z; ++z) v[z] = src[(size_t)min(z0 + z, k.nz - 1) * plane];
 #pragma unroll
         for (int z = 0; z < Z; ++z) v[z] = in && z0 + z < k.nz ? v[z] * k.inv_vol : 0.0f;
+#pragma unroll
+        for (int z = 0; z < Z; ++z) nonzero |= v[z] != 0.0f ? 1 : 0;
 #pragma unroll
         for (int q = 0; q < Z / 4; ++q)
             *reinterpret_cast<float4*>(tb + (size_t)q * P + (size_t)li * 16) =
@@ -226,8 +232,10 @@ __global__ __launch_bounds__(NT, MINW) void tvam_adjl_kernel(TvamConsts k, TvamP
         }
         s_roff[Z] = n;
     }
-    __syncthreads();
-    if (s_roff[Z] == 0) return;  // no DMD row lies in these slices
+    // an all-zero gradient tile (the thresholded loss is flat wherever the dose meets its bounds)
+    // makes every partial exactly 0, which adds nothing: no march
+    const int any = __syncthreads_or(nonzero);
+    if (s_roff[Z] == 0 || (TVAM_ADJL_ZSKIP && !any)) return;  // (or no DMD row lies in these slices)
 
     const int lane = (int)threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform chunk loop

@@ -481,18 +481,29 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
     const int wx = x1 - x0, wy = y1 - y0;
     const size_t slice_base = (size_t)kz * (size_t)k.res[0] * (size_t)k.res[1];
 
+    int nonzero = 0;
     for (int i = threadIdx.x; i < tile_words; i += TVAM_BLOCK) {
         float v = 0.0f;
         if (MODE == TVAM_MODE_ADJ) {
             int ly = i / tw - 1, lx = i - (ly + 1) * tw - 1;
             if (lx >= 0 && ly >= 0 && lx < wx && ly < wy)
                 v = gin[slice_base + (size_t)(y0 + ly) * k.res[0] + (x0 + lx)] * k.inv_vol;  // volume.py:130
+            nonzero |= v != 0.0f ? 1 : 0;
         }
         tile[i] = v;
     }
     if (MODE == TVAM_MODE_FWD)
         for (int i = threadIdx.x; i < ns; i += TVAM_BLOCK) s_amax[i] = 0u;
-    __syncthreads();
+#ifndef TVAM_TILE_ZSKIP
+#define TVAM_TILE_ZSKIP 1  // (0: march all-zero gradient tiles too, for A/B builds)
+#endif
+    if (MODE == TVAM_MODE_ADJ && TVAM_TILE_ZSKIP) {
+        // an all-zero gradient tile (the thresholded loss is flat wherever the dose meets its
+        // bounds) gathers exactly 0 on every ray, which adds nothing: no march
+        if (!__syncthreads_or(nonzero)) return;
+    } else {
+        __syncthreads();
+    }
 
     // this tile's (angle, column) slots, longest predicted in-tile march first
     const uint32_t* slots = tp.slots + tp.slot_off[tile_id];

@@ -1482,12 +1482,26 @@ __global__ __launch_bounds__(NT) void tvam_bin_march_kernel(TvamConsts k, TvamSe
         for (int i = threadIdx.x; i < NV; i += NT) ftile[i] = 0.0f;
         __syncthreads();
     } else {
+        int nonzero = 0;
         for (int i = threadIdx.x; i < wx * wy * wz; i += NT) {
             const int x = i % wx, y = (i / wx) % wy, z = i / (wx * wy);
             const size_t g = ((size_t)(lo[2] + z) * k.res[1] + (lo[1] + y)) * k.res[0] + (lo[0] + x);
-            ftile[z * sz + y * sy + x] = gin[g] * k.inv_vol;  // volume.py:130
+            const float v = gin[g] * k.inv_vol;  // volume.py:130
+            ftile[z * sz + y * sy + x] = v;
+            nonzero |= v != 0.0f ? 1 : 0;
         }
-        __syncthreads();
+#ifndef TVAM_BIN_ZSKIP
+#define TVAM_BIN_ZSKIP 1  // (0: march all-zero gradient bricks too, for A/B builds)
+#endif
+        if (!__syncthreads_or(nonzero) && !WS && TVAM_BIN_ZSKIP) {
+            // an all-zero gradient brick (the thresholded loss is flat wherever the dose meets its
+            // bounds): every entry's partial is exactly 0 -- written with its pixel for the sort
+            for (uint32_t e = e0 + threadIdx.x; e < e1; e += NT) {
+                part[e] = 0.0f;
+                ppix[e] = (vals[e] & ~TVAM_ENT_NULL) / pslots;
+            }
+            return;
+        }
     }
     // Load pipeline over this thread's entries e, e + S, e + 2S, ... (S = NT), unrolled by two with
     // two record register sets: while one entry marches, the records of the next are in flight and
