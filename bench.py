@@ -62,20 +62,25 @@ def host_info():
     except AttributeError:
         affinity = nproc
     omp = os.environ.get("OMP_NUM_THREADS")
-    threads = min(affinity, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else affinity
-    return {"cpu_model": model, "nproc": nproc, "affinity": affinity, "omp_num_threads": omp, "threads": threads}
+    omp_threads = min(affinity, int(omp)) if omp and omp.isdigit() and int(omp) > 0 else affinity
+    # the reported baseline runs on every CPU of the process's affinity; the OMP_NUM_THREADS share
+    # (16 per GPU on the box) is timed beside it
+    return {"cpu_model": model, "nproc": nproc, "affinity": affinity, "omp_num_threads": omp, "threads": affinity,
+            "omp_threads": omp_threads}
 
 
-def cpu_baseline(config, N, seconds, threads):
+def cpu_baseline(config, N, seconds, threads, alt_threads=None):
     """Oracle (C/OpenMP port of the reference march) on a bounded angle subset of the same workload,
-    plus the loss / L-BFGS vector work of an iteration (numpy, timed on one pass and scaled)."""
+    plus the loss / L-BFGS vector work of an iteration (numpy, timed on one pass and scaled).
+    `threads`: the OpenMP threads of the reported value (the process's affinity count); the same
+    sample is also timed at `alt_threads` (the OMP_NUM_THREADS share) when that differs."""
     import numpy as np
     from oracle import oracle
     from drtvam_amd.configs import desc_from_config
 
     oracle.build()
 
-    def run(na):
+    def run(na, nthreads=threads):
         cfg = scene_config(config, N, N)
         spp = cfg.get("spp", 1) if not cfg.get("regular_sampling") else 1
         d = desc_from_config(cfg)
@@ -84,9 +89,9 @@ def cpu_baseline(config, N, seconds, threads):
         pat = np.random.default_rng(0).uniform(0.0, 0.1, na * N * N).astype(np.float32)
         G = np.random.default_rng(1).uniform(-1.0, 1.0, (N, N, N)).astype(np.float32)
         t0 = time.perf_counter()
-        _, v = oracle.forward(d, pat, active_pixels=pix, spp=spp, nthreads=threads)
+        _, v = oracle.forward(d, pat, active_pixels=pix, spp=spp, nthreads=nthreads)
         t1 = time.perf_counter()
-        oracle.adjoint(d, G, active_pixels=pix, spp=spp, nthreads=threads)
+        oracle.adjoint(d, G, active_pixels=pix, spp=spp, nthreads=nthreads)
         t2 = time.perf_counter()
         return t1 - t0, t2 - t1, v
 
@@ -106,7 +111,13 @@ def cpu_baseline(config, N, seconds, threads):
     t_pass = time.perf_counter() - t0
     t_vec = 23 * t_pass
     t_iter = t_march + t_vec
+    alt = None
+    if alt_threads and alt_threads != threads:
+        tf2, ta2, _ = run(na, alt_threads)
+        alt = {"threads": alt_threads, "value": 1.0 / ((2 * tf2 + ta2) * (N / na) + t_vec), "unit": "it/s",
+               "sample": f"the same {na} angles: fwd {tf2:.2f}s + adj {ta2:.2f}s"}
     return {"value": 1.0 / t_iter, "unit": "it/s", "cores": threads, "kind": "port",
+            "at_omp_num_threads": alt,
             "impl": "oracle/tvam_oracle.c: scalar C restatement (gcc -O3 -fopenmp, no SIMD intrinsics), "
                     "slice-private accumulation -- not Dr.Jit's LLVM backend (mitsuba/drjit are not installed)",
             "host": host_info(),
@@ -372,8 +383,13 @@ def main():
     prob.proj.kernel_time(True)  # (dominant-kernel launch events from here on; no GPU work)
     state["on"] = True
     t0 = time.perf_counter()
+    # step boundaries as events on the stream every launch goes to (the median of the steps)
+    step_ev = [torch.cuda.Event(enable_timing=True)]
+    step_ev[0].record()
     for i in range(args.warmup, args.warmup + args.steps):
         prob.iteration(i)
+        step_ev.append(torch.cuda.Event(enable_timing=True))
+        step_ev[-1].record()
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -388,6 +404,9 @@ def main():
                 fwd.append(0.0)
             fwd[-1] += s.elapsed_time(e)
     adj = [s.elapsed_time(e) for s, e in adj_ms]
+    step_ms = sorted(a.elapsed_time(b) for a, b in zip(step_ev[:-1], step_ev[1:]))
+    step_med = step_ms[len(step_ms) // 2] if len(step_ms) % 2 else 0.5 * (step_ms[len(step_ms) // 2 - 1] +
+                                                                          step_ms[len(step_ms) // 2])
     fwd_avg = sum(fwd) / len(fwd) / 1e3
     adj_avg = sum(adj) / len(adj) / 1e3 if adj else float("nan")
     if dist:
@@ -401,7 +420,7 @@ def main():
         ew = int(args.emulate.split("/")[1])
         ms = elapsed / args.steps * 1e3
         rec = {"emulate": args.emulate, "shard": prob.shard, "config": args.config, "n": N,
-               "ms_per_step": ms, "fwd_ms": fwd_avg * 1e3, "adj_ms": adj_avg * 1e3, "visits_per_pass": visits,
+               "ms_per_step": ms, "ms_per_step_median": step_med, "fwd_ms": fwd_avg * 1e3, "adj_ms": adj_avg * 1e3, "visits_per_pass": visits,
                "slices": [prob.z0, prob.z1], "rows": [prob.r0, prob.r1], "angles": [prob.a0, prob.a1],
                "device_mem_used_bytes": (lambda fr_tot: fr_tot[1] - fr_tot[0])(torch.cuda.mem_get_info(dev))}
         if prob.proj.desc.albedo != 0.0:  # scattering: the brick-bin chunking and its device memory
@@ -435,12 +454,35 @@ def main():
             dist.destroy_process_group()
         return
 
+    # the adjoint on a dense gradient (U[-1, 1)): the timed iterations run near convergence,
+    # where the thresholded loss's gradient is exactly 0 on most of the film and the adjoint skips those
+    # partials and tiles (bit-identical); this is the same call with nothing to skip, untimed for `value`
+    dense = None
+    if world == 1 and adj:
+        gd = torch.empty(tuple(prob.proj.film_shape), device=dev).uniform_(
+            -1.0, 1.0, generator=torch.Generator(device=dev).manual_seed(1))
+        n_act = prob.x0.numel()
+        ga = orig_adj(gd, n_act, prob.active_pixels, prob.spp, 0)
+        ts = []
+        for _ in range(5):
+            s_, e_ = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s_.record()
+            orig_adj(gd, n_act, prob.active_pixels, prob.spp, 0, out=ga)
+            e_.record()
+            torch.cuda.synchronize()
+            ts.append(s_.elapsed_time(e_))
+        adj_dense = sorted(ts)[len(ts) // 2]
+        dense = {"adj_ms": adj_dense, "adj_ms_timed_iterations": adj_avg * 1e3,
+                 "ms_per_step_model": step_med - adj_avg * 1e3 + adj_dense,
+                 "note": "adjoint of a U[-1,1) gradient (no zero partials or tiles to skip), median of 5 calls; "
+                         "ms_per_step_model = the median step with its adjoint replaced by this one"}
+        del gd, ga
     roofline = make_roofline(args, N, A, world, prob, visits, rays, fwd_avg, adj_avg, kt)
     cpu = None
     if args.cpu_baseline == "auto" and world == 1:
-        threads = host_info()["threads"]
-        log(f"cpu baseline ({threads} threads, ~{args.cpu_seconds:.0f}s) ...")
-        cpu = cpu_baseline(args.config, N, args.cpu_seconds, threads)
+        hi = host_info()
+        log(f"cpu baseline ({hi['threads']} threads, and {hi['omp_threads']}; ~{args.cpu_seconds:.0f}s) ...")
+        cpu = cpu_baseline(args.config, N, args.cpu_seconds, hi["threads"], hi["omp_threads"])
     result = {
         "metric": f"optimizer iterations/sec (fwd+adjoint), {N}³ voxels × {A} angles",
         "value": args.steps / elapsed,
@@ -451,6 +493,11 @@ def main():
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": elapsed / args.steps * 1e3,
+        # the median of the timed steps (HIP events at the step boundaries) beside the mean
+        "ms_per_step_median": step_med,
+        "value_median": 1e3 / step_med,
+        "ms_per_step_min_max": [step_ms[0], step_ms[-1]],
+        "dense_gradient": dense,
         "higher_is_better": True,
         "scaling": "strong",
         "vs_baseline": None,

@@ -12,7 +12,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TVAM_LIB") or os.path.join(_HERE, "libtvam.so")  # TVAM_LIB: a variant build
 
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 TVAM_OK = 0
 TVAM_ERR_INVALID = -1
@@ -197,12 +197,20 @@ def load_library(path: str | None = None) -> ctypes.CDLL:
                 "or drtvam_amd/csrc/build.sh (there is no CPU fallback)"
             )
         lib = ctypes.CDLL(p)
+        # the version first: a library built before an export was added fails with this message,
+        # not an AttributeError from the binding loop
+        ver = getattr(lib, "tvam_abi_version", None)
+        if ver is None:
+            raise TvamError(f"{p} exports no tvam_abi_version; rebuild it")
+        ver.restype, ver.argtypes = ctypes.c_int, []
+        if ver() != ABI_VERSION:
+            raise TvamError(f"libtvam.so ABI version mismatch ({ver()} != {ABI_VERSION}); rebuild it")
         for name, (res, args) in EXPORTS.items():
-            fn = getattr(lib, name)
+            fn = getattr(lib, name, None)
+            if fn is None:
+                raise TvamError(f"libtvam.so lacks {name} (ABI {ABI_VERSION}); rebuild it")
             fn.restype = res
             fn.argtypes = args
-        if lib.tvam_abi_version() != ABI_VERSION:
-            raise TvamError("libtvam.so ABI version mismatch; rebuild it")
         if path is None:
             _lib = lib
         return lib

@@ -235,6 +235,12 @@ struct TvamBinScratch {
     // last call's chunking (tvam_plan_bin_stats): chunks, chunks served from the cache,
     // chunks stored into it, brick entries sorted, paths per chunk
     int64_t st[5] = {0, 0, 0, 0, 0};
+    // the bin-fill count check (sb.bad, cumulative since the scratch was allocated) is read lazily:
+    // each binned call ends with an async copy into pinned host memory and an event, and the next
+    // call checks the copy once its event has completed -- no stream synchronisation on the hot path
+    uint32_t* bad_host = nullptr;
+    hipEvent_t bad_ev = nullptr;
+    bool bad_pending = false;
     int64_t temp_cap() const { return (int64_t)temp_bytes; }
 };
 

@@ -11,6 +11,7 @@
 #include "tvam_internal.h"
 
 #include <algorithm>
+#include <mutex>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -203,11 +204,14 @@ static void plan_free(tvam_plan* p) {
     delete p;
 }
 
+static void kt_plan_gone(const tvam_plan* p);  // the kernel timer's events go with their owning plan
+
 extern "C" void tvam_plan_destroy(tvam_plan* p) {
     if (!p) return;
     int cur = 0;
     (void)hipGetDevice(&cur);
     (void)hipSetDevice(p->device);
+    kt_plan_gone(p);
     plan_free(p);
     (void)hipSetDevice(cur);
 }
@@ -363,23 +367,53 @@ int tvam_knob(const char* name, int def) {
 #define env_int tvam_knob
 
 // Launch timer of the dominant forward kernel (tvam_plan_kernel_time): event pairs recorded on the
-// launching stream around each launch while enabled (up to 1024 launches per measurement).
+// launching stream around each launch while enabled (up to 1024 launches per measurement).  One
+// timer per process, owned by the plan that enabled it: launches on another device are not
+// recorded, the state is guarded by a mutex (plans on other host threads may launch meanwhile),
+// and the events are destroyed with the owning plan.
 namespace {
 struct KernelTimer {
+    std::mutex mu;
     bool on = false;
     int kind = 0;  // TvamKtKind of the measured plan's dominant forward kernel
+    int device = -1;
+    const tvam_plan* owner = nullptr;
     std::vector<hipEvent_t> ev;
     size_t n = 0;
 };
 KernelTimer g_kt;
+
+bool kt_here(int kind) {
+    if (!g_kt.on || kind != g_kt.kind || g_kt.n + 2 > g_kt.ev.size()) return false;
+    int cur = -1;
+    return hipGetDevice(&cur) == hipSuccess && cur == g_kt.device;
+}
+
+// the owner's events (every recorded pair complete first); caller holds the mutex
+void kt_release() {
+    for (size_t i = 0; i < g_kt.n; ++i) (void)hipEventSynchronize(g_kt.ev[i]);
+    for (hipEvent_t e : g_kt.ev) (void)hipEventDestroy(e);
+    g_kt.ev.clear();
+    g_kt.n = 0;
+    g_kt.on = false;
+    g_kt.owner = nullptr;
+    g_kt.device = -1;
+}
 }  // namespace
 
+static void kt_plan_gone(const tvam_plan* p) {
+    std::lock_guard<std::mutex> lk(g_kt.mu);
+    if (g_kt.owner == p) kt_release();
+}
+
 void tvam_kt_begin(hipStream_t stream, int kind) {
-    if (g_kt.on && kind == g_kt.kind && g_kt.n + 2 <= g_kt.ev.size()) (void)hipEventRecord(g_kt.ev[g_kt.n], stream);
+    std::lock_guard<std::mutex> lk(g_kt.mu);
+    if (kt_here(kind)) (void)hipEventRecord(g_kt.ev[g_kt.n], stream);
 }
 
 void tvam_kt_end(hipStream_t stream, int kind) {
-    if (!g_kt.on || kind != g_kt.kind || g_kt.n + 2 > g_kt.ev.size()) return;
+    std::lock_guard<std::mutex> lk(g_kt.mu);
+    if (!kt_here(kind)) return;
     (void)hipEventRecord(g_kt.ev[g_kt.n + 1], stream);
     g_kt.n += 2;
 }
@@ -468,6 +502,10 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     hipError_t e;
     if ((rc = upload(&p->d_pl_slice_off, off)) || (rc = upload(&p->d_pl_slice_rows, rows))) return rc;
     if (p->planar_fwd) {
+        // the forward's scalar loads read two angles' constants at a time: pad both tables so the pair
+        // of the last angle stays inside its allocation
+        p->fwd_ang_h.resize(p->fwd_ang_h.size() + 4, make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+        p->fwd_cb_h.resize(p->fwd_cb_h.size() + 2, 0);
         if ((rc = upload(&p->d_pl_fwd_ang, p->fwd_ang_h)) || (rc = upload(&p->d_pl_fwd_cb, p->fwd_cb_h))) return rc;
         p->pl.fwd_ang = p->d_pl_fwd_ang;
         p->pl.fwd_cb = p->d_pl_fwd_cb;
@@ -1899,10 +1937,11 @@ extern "C" int tvam_plan_bin_stats(tvam_plan* p, int64_t* stats) {
     // the chunk scratch: records, brick counts and offsets, sort keys / values, adjoint partials
     stats[6] = b.cap_slots * (TVAM_REC_F4 * (int64_t)sizeof(float4) + 2 * (int64_t)sizeof(uint32_t)) +
                b.cap_entries * (int64_t)(4 * sizeof(uint32_t) + sizeof(float)) + b.cap_bricks * 4 + b.temp_cap();
-    // slots of the last call whose bin-fill walk disagreed with the record writer's closed-form
-    // brick count (sc_brick_count; 0 by construction, checked by the tests)
+    // slots whose bin-fill walk disagreed with the record writer's closed-form brick count
+    // (sc_brick_count; 0 by construction, checked by the tests), summed over the calls since the
+    // chunk scratch was allocated
     stats[7] = 0;
-    if (b.sb.bad && b.st[0] > 0) {
+    if (b.sb.bad) {
         uint32_t bad = 0;
         if (hipMemcpy(&bad, b.sb.bad, sizeof(uint32_t), hipMemcpyDeviceToHost) != hipSuccess)
             return fail(TVAM_ERR_HIP, "tvam_plan_bin_stats: reading the count check");
@@ -1946,20 +1985,26 @@ extern "C" int tvam_plan_kernel_time(tvam_plan* p, int32_t enable, double* total
     if (!p || !total_ms || !launches) return fail(TVAM_ERR_INVALID, "null argument");
     *total_ms = 0.0;
     *launches = 0;
+    std::lock_guard<std::mutex> lk(g_kt.mu);
+    if (g_kt.owner && g_kt.owner != p) return fail(TVAM_ERR_INVALID, "tvam_plan_kernel_time: another plan owns the timer");
     hipError_t e = hipSuccess;
-    if (g_kt.n > 0) {
-        e = hipEventSynchronize(g_kt.ev[g_kt.n - 1]);
-        for (size_t i = 0; e == hipSuccess && i < g_kt.n; i += 2) {
-            float ms = 0.0f;
-            e = hipEventElapsedTime(&ms, g_kt.ev[i], g_kt.ev[i + 1]);
-            *total_ms += ms;
-        }
-        *launches = (int64_t)(g_kt.n / 2);
+    for (size_t i = 0; e == hipSuccess && i < g_kt.n; i += 2) {  // each pair's end complete before it is read
+        float ms = 0.0f;
+        e = hipEventSynchronize(g_kt.ev[i + 1]);
+        if (e == hipSuccess) e = hipEventElapsedTime(&ms, g_kt.ev[i], g_kt.ev[i + 1]);
+        *total_ms += ms;
     }
+    *launches = (int64_t)(g_kt.n / 2);
     if (e != hipSuccess) return hip_fail(e, "tvam_plan_kernel_time");
     g_kt.n = 0;
     g_kt.on = false;
-    if (enable) {
+    if (!enable) {  // measurement read: the events go with it
+        kt_release();
+        return 0;
+    }
+    {
+        g_kt.owner = p;
+        g_kt.device = p->device;
         while (g_kt.ev.size() < 2048) {
             hipEvent_t ev;
             if ((e = hipEventCreate(&ev)) != hipSuccess) return hip_fail(e, "hipEventCreate");

@@ -132,11 +132,25 @@ __host__ __device__ constexpr int tvam_fwd_zs(int Z) { return ((Z + 4) / 4) % 2 
 #ifndef TVAM_FWD_DMA
 #define TVAM_FWD_DMA 1
 #endif
-__host__ __device__ constexpr int tvam_fwd_dma_np(int ncm, int Z) { return (ncm * (tvam_fwd_zs(Z) / 4) + 63) / 64 * 64; }
+// The DMA slab's column stride needs no pad when Z / 4 is odd (Z = 52: 13 float4 groups); slots are
+// exact (ncm columns x ZS / 4 groups, the last wave-instruction's surplus lanes masked), so 6
+// workgroups' LDS fits a CU at Z = 52 (4 with 64-slot rounding and a Z + 8 stride).
+__host__ __device__ constexpr int tvam_fwd_zs_dma(int Z) { return (Z / 4) % 2 ? Z : Z + 4; }
+__host__ __device__ constexpr int tvam_fwd_dma_np(int ncm, int Z) { return ncm * (tvam_fwd_zs_dma(Z) / 4); }
+// One wave-instruction of LDS-DMA: each active lane's 16 bytes at g land at LDS byte l + 16 * lane
+// (l wave-uniform, in M0).  Issued as inline asm so the compiler does not see an LDS write pending
+// on vmcnt: with __builtin_amdgcn_global_load_lds it waits vmcnt(0) before the next ds_read of any
+// LDS address, i.e. before computing the current buffer, which serialised the next angles' loads
+// with this angle's compute.  The kernel drains the loads itself (s_waitcnt vmcnt(0) before the
+// barrier that precedes their reads).
+__device__ __forceinline__ void tvam_lds_dma16(const void* g, void* l) {
+    const unsigned m = (unsigned)(uintptr_t)(__attribute__((address_space(3))) void*)l;
+    asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(g), "{m0}"(m) : "memory");
+}
 // a staged column outside the crop: no chord ({q, t_end < 0}; refracted: the second record zero)
 __device__ float4 tvam_null_rec[2] = {{0.0f, 0.0f, -1.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
 #ifndef TVAM_ACH
-#define TVAM_ACH 128  // angles per LDS chunk of per-angle constants
+#define TVAM_ACH 64  // angles per LDS chunk of per-angle constants
 #endif
 
 // Z: slices per thread; NC: candidate DMD columns per (voxel, angle), a
@@ -158,15 +172,16 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
     const int ncm = pl.ncmax;
     constexpr int RW = REFR ? 2 : 1;  // records (float4) per staged column
     constexpr bool DMA = BIN && DMAP && AB <= 2;  // LDS-DMA staging (pl.fwd_dma)
+    constexpr bool SCONST = DMA && !REFR && AB == 2;  // per-angle constants in SGPRs
     // [2][AB][ncm * ZS + 4] (double buffer of AB angles per barrier), ZS = tvam_fwd_zs(Z);
     // the 4 words past a buffer's slab take the BIN staging's idle slots.  DMA: [2][AB][np] float4
-    // slab slots and [2][AB][64 RW] record slots (tvam_fwd_dma_np; refracted: record h of column j
-    // at 64 h + j)
-    constexpr int ZS = tvam_fwd_zs(Z);
+    // slab slots (ZS = tvam_fwd_zs_dma(Z)) and [2][AB][RW ncm] record slots (refracted: record h of
+    // column j at ncm h + j)
+    constexpr int ZS = DMA ? tvam_fwd_zs_dma(Z) : tvam_fwd_zs(Z);
     const int np = DMA ? tvam_fwd_dma_np(ncm, Z) : 0;
     const int bstride = DMA ? 4 * np : ncm * ZS + 4;
-    const int rstride = DMA ? 64 * RW : ncm * RW;
-    const int rhalf = DMA ? 64 : ncm;  // refracted: the second records' offset
+    const int rstride = ncm * RW;
+    const int rhalf = ncm;  // refracted: the second records' offset
     float* s_p = reinterpret_cast<float*>(smem);
     float4* s_r = reinterpret_cast<float4*>(s_p + 2 * AB * bstride);  // [2][AB][rstride]
     // per-angle constants of TVAM_ACH (+2 look-ahead) angles, copied to LDS so the
@@ -263,8 +278,8 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
         }
     }
     // DMA: this lane's slab slots w * 64 + lane + q * 256 (w: its wave) -> source float4 offsets
-    // within an angle's binned window (angle-independent); a pad or round-up slot loads its
-    // column's last data slot / slot 0
+    // within an angle's binned window (angle-independent); a pad slot loads its column's last
+    // data slot, a lane past the slab (dsrc < 0) loads nothing
     const int dwave = __builtin_amdgcn_readfirstlane((int)threadIdx.x >> 6);
     int dsrc[2] = {0, 0};
     if constexpr (DMA) {
@@ -273,32 +288,32 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
         for (int q = 0; q < 2; ++q) {
             const int P = (int)threadIdx.x + q * TVAM_PB;
             const int jj = P / GZ, gq = min(P - (P / GZ) * GZ, G - 1);
-            dsrc[q] = P < ncm * GZ ? jj * (pl.bin_nz / 4) + gq : 0;
+            dsrc[q] = P < ncm * GZ ? jj * (pl.bin_nz / 4) + gq : -1;
         }
     }
-    auto fetch_dma = [&](int al, int buf) __attribute__((always_inline)) {
-        const int cb = s_cb[al - tbase];
+    auto fetch_dma_c = [&](int al, int buf, const int cb) __attribute__((always_inline)) {
         const pl_f4* src = reinterpret_cast<const pl_f4*>(pl.fwd_bin) +
                            ((size_t)al * (k.crop_x + 2 * pl.bin_pad) + (cb + pl.bin_pad)) * (pl.bin_nz / 4) + z0 / 4;
         float4* slab = reinterpret_cast<float4*>(s_p + buf * bstride);
 #pragma unroll
         for (int q = 0; q < 2; ++q) {
             const int wb = dwave * 64 + q * TVAM_PB;  // wave-uniform
-            if (wb < np)
-                __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src + dsrc[q]),
-                                                 (__attribute__((address_space(3))) void*)(slab + wb), 16, 0, 0);
+            // the LDS slot is M0 base + 16 * lane: the last wave-instruction's lanes past the slab are
+            // masked off (exec), so nothing is written past it
+            if (wb < np && dsrc[q] >= 0)
+                tvam_lds_dma16(src + dsrc[q], slab + wb);
         }
-        if (dwave < RW) {  // the window's ray-table records (ncm <= 64, host-checked); refracted: wave 1
-                           // loads the columns' second records
-            const int lane = (int)threadIdx.x & 63, col = cb + lane;
+        const int lane = (int)threadIdx.x & 63;
+        if (dwave < RW && lane < ncm) {  // the window's ray-table records (ncm <= 64, host-checked);
+                                         // refracted: wave 1 loads the columns' second records
+            const int col = cb + lane;
             const float4* tab = reinterpret_cast<const float4*>(REFR && dwave == 1 ? pl.vox2 : pl.vox);
-            const float4* rs = (lane < ncm && (unsigned)col < (unsigned)k.crop_x) ? tab + (size_t)al * k.crop_x + col
-                                                                                : &tvam_null_rec[dwave];
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)rs,
-                                             (__attribute__((address_space(3))) void*)(s_r + buf * rstride + 64 * dwave),
-                                             16, 0, 0);
+            const float4* rs = (unsigned)col < (unsigned)k.crop_x ? tab + (size_t)al * k.crop_x + col
+                                                                  : &tvam_null_rec[dwave];
+            tvam_lds_dma16(rs, s_r + buf * rstride + ncm * dwave);
         }
     };
+    auto fetch_dma = [&](int al, int buf) __attribute__((always_inline)) { fetch_dma_c(al, buf, s_cb[al - tbase]); };
     // global loads of angle al's slab (slice-binned pattern + ray table) into registers
     // (the ray-table entry travels in its own array: a 48-byte stage struct is left in scratch)
     struct StageDirect {
@@ -415,26 +430,23 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
         for (int c = 2; c < nc; ++c) accumulate(jj0 + c, weight(jj0 + c));
     };
 
-    auto compute = [&](int al, int buf) __attribute__((always_inline)) {
-        if constexpr (REFR) {
-            compute_refr(al, buf);
-            return;
-        }
-        const int cb = s_cb[al - tbase];
-        const float* sp = s_p + buf * bstride;
+    // the candidates of angle al (staged in buffer buf): the first window column jj0 and the
+    // candidates' weights (0 where the ray misses the voxel)
+    // per-angle constants {s*du, -c*du, 1/d.x, 1/d.y}, {half width in columns, axis flags}, and the
+    // window's first column: from LDS, or (TVAM_FWD_SCONST, straight-ray DMA path) from scalar registers
+    // loaded one angle pair ahead
+    auto geom_c = [&](const float4 g0, const float4 g1, const int cb, int buf, int& jj0, float (&wgt)[NC])
+        __attribute__((always_inline)) {
         const float4* sr = s_r + buf * rstride;
-        // per-angle constants {s*du, -c*du, 1/d.x, 1/d.y}, {half width in columns, axis flags}
-        const float4 g0 = s_ang[2 * (al - tbase)], g1 = s_ang[2 * (al - tbase) + 1];
         const int fl = __float_as_int(g1.y);
 
         // candidate columns: the rays whose lateral line meets the voxel's lateral extent
         const float u = fmaf(Xc, g0.x, fmaf(Yc, g0.y, u0));
-        int jj0 = (int)ceilf(u - g1.x) - cb;
+        jj0 = (int)ceilf(u - g1.x) - cb;
         jj0 = min(max(jj0, 0), ncm - NC);
         // crossing times of the voxel's x / y edges relative to the ray's o2 (+ q.x / q.y)
         const float xa = X0 * g0.z, xb = X1 * g0.z, ya = Y0 * g0.w, yb = Y1 * g0.w;
         const float xn = fminf(xa, xb), xf = fmaxf(xa, xb), yn = fminf(ya, yb), yf = fmaxf(ya, yb);
-        float wgt[NC];
         // the candidates' ray records read together (each read's latency is paid once per angle),
         // then pinned as 16-byte reads (ds_read_b128, not b96)
         float4 qs[NC];
@@ -461,6 +473,13 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
             const float e = pl_exp2(k.nsig2 * tin) - pl_exp2(k.nsig2 * tout);
             wgt[c] = tout > tin ? e : 0.0f;
         }
+    };
+    auto geom = [&](int al, int buf, int& jj0, float (&wgt)[NC]) __attribute__((always_inline)) {
+        geom_c(s_ang[2 * (al - tbase)], s_ang[2 * (al - tbase) + 1], s_cb[al - tbase], buf, jj0, wgt);
+    };
+    // dose += the candidates' weights x their staged slabs
+    auto fmas = [&](int buf, int jj0, const float (&wgt)[NC]) __attribute__((always_inline)) {
+        const float* sp = s_p + buf * bstride;
 #if TVAM_FWD_SKIPZERO
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
@@ -489,10 +508,78 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
             }
         }
     };
+    auto compute = [&](int al, int buf) __attribute__((always_inline)) {
+        if constexpr (REFR) {
+            compute_refr(al, buf);
+        } else {
+            int jj0;
+            float wgt[NC];
+            geom(al, buf, jj0, wgt);
+            fmas(buf, jj0, wgt);
+        }
+    };
+    // the AB angles of a barrier group, one after the other
+    auto compute2 = [&](int al, int buf, bool two) __attribute__((always_inline)) {
+        compute(al, buf);
+        if (two) compute(al + 1, buf + 1);
+    };
 
     // Software pipeline over angles: angle a is computed from LDS buffer a & 1
     // while the loads of angle a + 1 are in flight in registers.
-    if constexpr (DMA) {
+    if constexpr (DMA && SCONST) {
+      if (ab < ae) {
+        // as below, with the per-angle constants of the next pair in flight in scalar registers: no
+        // LDS table (its reads and reload barriers); the s_loads are waited for after the barrier,
+        // when the wave has no LDS read outstanding.  An angle pair is 16 dwords of fwd_ang and 2 of
+        // the tile's fwd_cb (both tables padded by the host past the last pair).
+        typedef unsigned su16 __attribute__((ext_vector_type(16)));
+        typedef unsigned su2 __attribute__((ext_vector_type(2)));
+        auto sload = [&](int al, su16& a, su2& c) __attribute__((always_inline)) {
+            const float4* ga = pl.fwd_ang + 2 * al;
+            const int32_t* gc = cbt + al;
+            asm volatile("s_load_dwordx16 %0, %1, 0x0" : "=s"(a) : "s"(ga));
+            asm volatile("s_load_dwordx2 %0, %1, 0x0" : "=s"(c) : "s"(gc));
+        };
+        auto sget = [](const su16& a, int j) {
+            return make_float4(__uint_as_float(a[4 * j]), __uint_as_float(a[4 * j + 1]), __uint_as_float(a[4 * j + 2]),
+                               __uint_as_float(a[4 * j + 3]));
+        };
+        su16 ca, na;
+        su2 cc, nc2;
+        sload(ab, ca, cc);
+        asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(ca), "+s"(cc)::"memory");  // cc feeds the first DMAs
+        fetch_dma_c(ab, 0, (int)cc[0]);
+        if (AB > 1 && ab + 1 < ae) fetch_dma_c(ab + 1, 1, (int)cc[1]);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+        int half = 0;
+        for (int al = ab; al < ae; al += AB) {
+            const bool more = al + AB < ae;
+            if (more) {
+                sload(al + AB, na, nc2);
+                asm volatile("s_waitcnt lgkmcnt(0)" : "+s"(na), "+s"(nc2)::"memory");
+                fetch_dma_c(al + AB, (half ^ 1) * AB, (int)nc2[0]);
+                if (AB > 1 && al + AB + 1 < ae) fetch_dma_c(al + AB + 1, (half ^ 1) * AB + 1, (int)nc2[1]);
+            }
+            const bool two = AB > 1 && al + 1 < ae;
+            int j0, j1 = 0;
+            float w0[NC], w1[NC];
+            // one angle's geometry and FMAs after the other (both angles' geometry first, then both
+            // angles' FMAs: 2.44 -> 2.52 ms on config 2, profiles/r06/ab_fwd/)
+            geom_c(sget(ca, 0), sget(ca, 1), (int)cc[0], half * AB, j0, w0);
+            fmas(half * AB, j0, w0);
+            if (two) {
+                geom_c(sget(ca, 2), sget(ca, 3), (int)cc[1], half * AB + 1, j1, w1);
+                fmas(half * AB + 1, j1, w1);
+            }
+            half ^= 1;
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            ca = na;
+            cc = nc2;
+        }
+      }
+    } else if constexpr (DMA) {
       if (ab < ae) {
         // LDS-DMA: the next AB angles' slabs and records load straight into the other half while
         // this half is computed (its last reads were before the previous barrier); the loads are
@@ -510,8 +597,7 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
             }
             if (al + AB < ae) fetch_dma(al + AB, (half ^ 1) * AB);
             if (AB > 1 && al + AB + 1 < ae) fetch_dma(al + AB + 1, (half ^ 1) * AB + 1);
-            compute(al, half * AB);
-            if (AB > 1 && al + 1 < ae) compute(al + 1, half * AB + 1);
+            compute2(al, half * AB, AB > 1 && al + 1 < ae);
             half ^= 1;
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
@@ -709,7 +795,7 @@ size_t tvam_planar_fwd_lds(const TvamPlanar& pl, int Z) {
     const int ab = pl.fwd_ab > 1 ? pl.fwd_ab : 1;
     const size_t rw = pl.fwd_refr ? 2 : 1;
     if (pl.fwd_dma && pl.fwd_bin && ab <= 2)
-        return 2 * ab * ((size_t)tvam_fwd_dma_np(pl.ncmax, Z) + 64 * rw) * sizeof(float4) +
+        return 2 * ab * ((size_t)tvam_fwd_dma_np(pl.ncmax, Z) + rw * pl.ncmax) * sizeof(float4) +
                (size_t)(TVAM_ACH + 4) * (2 * sizeof(float4) + sizeof(int)) + (size_t)Z * sizeof(int);
     return 2 * ab * (((size_t)pl.ncmax * tvam_fwd_zs(Z) + 4) * sizeof(float) + rw * pl.ncmax * sizeof(float4)) +
            (size_t)(TVAM_ACH + 4) * (2 * sizeof(float4) + sizeof(int)) + (size_t)Z * sizeof(int);

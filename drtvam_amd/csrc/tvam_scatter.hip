@@ -1716,6 +1716,9 @@ void tvam_bin_scratch_free(TvamBinScratch& s) {
         (void)hipFree(c.vals);
         (void)hipFree(c.bstart);
     }
+    if (s.bad_ev) (void)hipEventSynchronize(s.bad_ev);
+    (void)hipHostFree(s.bad_host);
+    if (s.bad_ev) (void)hipEventDestroy(s.bad_ev);
     s = TvamBinScratch{};
 }
 
@@ -1723,6 +1726,12 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
                                const int32_t* idxmap, const float* gin, float* out, TvamBinScratch& s,
                                hipStream_t stream) {
     for (int i = 0; i < 5; ++i) s.st[i] = 0;  // stats of this call, also when it bins nothing
+    // an earlier call's count check, if its copy has landed: a slot whose brick walk disagreed with
+    // the writer's closed-form count (never, by construction) may have dropped entries -- fail loudly
+    if (s.bad_pending && hipEventQuery(s.bad_ev) == hipSuccess) {
+        s.bad_pending = false;
+        if (*s.bad_host) return hipErrorIllegalState;
+    }
     const int nsurf = k.vial_type == 0 ? 1 : 2;
     const int slots = k.max_depth - nsurf - 1;  // later medium segments per path
     if (slots <= 0) return hipSuccess;
@@ -1771,12 +1780,16 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
             (e = hipMalloc((void**)&s.sb.m, (nsl + 1) * sizeof(uint32_t))) != hipSuccess ||
             (e = hipMalloc((void**)&s.off, (nsl + 1) * sizeof(uint32_t))) != hipSuccess ||
             (e = hipMalloc((void**)&s.sb.wmax, sizeof(uint32_t))) != hipSuccess ||
-            (e = hipMalloc((void**)&s.sb.bad, sizeof(uint32_t))) != hipSuccess)
+            (e = hipMalloc((void**)&s.sb.bad, sizeof(uint32_t))) != hipSuccess ||
+            (e = hipHostMalloc((void**)&s.bad_host, sizeof(uint32_t))) != hipSuccess ||
+            (e = hipEventCreateWithFlags(&s.bad_ev, hipEventDisableTiming)) != hipSuccess)
             return e;
+        *s.bad_host = 0;
+        // the fill walks that disagreed with the record writer's brick counts, summed over the calls
+        // (bin stats [7])
+        if ((e = hipMemsetAsync(s.sb.bad, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
         s.cap_slots = nsl;
     }
-    // this call's fill walks that disagreed with the record writer's brick counts (bin stats)
-    if ((e = hipMemsetAsync(s.sb.bad, 0, sizeof(uint32_t), stream)) != hipSuccess) return e;
     int64_t capb = s.cap_bricks;
     if ((e = grow(&s.bstart, capb, (int64_t)nbricks + 1)) != hipSuccess) return e;
     s.cap_bricks = (int32_t)capb;
@@ -2065,14 +2078,12 @@ hipError_t tvam_scatter_binned(int mode, const TvamConsts& k, const TvamTiles& t
         if ((e = hipGetLastError()) != hipSuccess) return e;
         if (keep) cc->valid = true;
     }
-    // a slot whose brick walk disagreed with the writer's closed-form count (never, by
-    // construction) may have dropped entries: fail loudly rather than return a short dose
-    if (s.sb.bad && s.st[0] > 0) {
-        uint32_t bad = 0;
-        if ((e = hipMemcpyAsync(&bad, s.sb.bad, sizeof(uint32_t), hipMemcpyDeviceToHost, stream)) != hipSuccess ||
-            (e = hipStreamSynchronize(stream)) != hipSuccess)
+    // the count check, read by a later call (above) or tvam_plan_bin_stats, without a sync here
+    if (s.sb.bad && s.st[0] > 0 && !s.bad_pending) {
+        if ((e = hipMemcpyAsync(s.bad_host, s.sb.bad, sizeof(uint32_t), hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+            (e = hipEventRecord(s.bad_ev, stream)) != hipSuccess)
             return e;
-        if (bad) return hipErrorIllegalState;
+        s.bad_pending = true;
     }
     return hipSuccess;
 }

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define TVAM_ABI_VERSION 10
+#define TVAM_ABI_VERSION 11
 
 /* error codes */
 #define TVAM_OK               0
@@ -265,9 +265,11 @@ int tvam_plan_fwd_scale(tvam_plan* plan, float* scale);
    chunks of paths, [1] = chunks served from the forward bin cache (weights rescaled to the
    new pattern, no replay / sort), [2] = chunks stored into the cache, [3] = brick entries
    marched, [4] = paths per chunk (all 0 when the plan's last call binned nothing), [5] = device
-   bytes the forward bin cache holds, [6] = device bytes of the chunk scratch, [7] = slots of the
-   last call whose bin-fill walk disagreed with the record writer's closed-form brick count (0 by
-   construction; host-synchronous read).  stats has 8 entries.  (ABI v10) */
+   bytes the forward bin cache holds, [6] = device bytes of the chunk scratch, [7] = slots whose
+   bin-fill walk disagreed with the record writer's closed-form brick count, summed over the calls
+   since the chunk scratch was allocated (0 by construction; host-synchronous read; a binned call
+   that finds an earlier call's count nonzero fails with TVAM_ERR_HIP).  stats has 8 entries.
+   (ABI v10) */
 int tvam_plan_bin_stats(tvam_plan* plan, int64_t* stats);
 
 /* Diagnostics (host-synchronous): the per-ray tile kernels' row walks for the plan's most
@@ -278,7 +280,7 @@ int tvam_plan_bin_stats(tvam_plan* plan, int64_t* stats);
    workgroups' stray walk summed over the launch (each walks its slice's whole stray list:
    strays x tiles), [3] = their main-row slot walk (rows x slots x spp over all workgroups),
    [4] = frozen-axis rays, [5] = spp of the records, [6] = tiles, [7] = (angle, column) slots
-   over all tiles.  stats has 8 entries.  (ABI v10, added in round 5) */
+   over all tiles.  stats has 8 entries.  (ABI v11) */
 int tvam_plan_tile_stats(tvam_plan* plan, int64_t* stats);
 
 /* Measurement (host-synchronous): launch time of the plan's dominant forward kernel -- the
@@ -286,8 +288,9 @@ int tvam_plan_tile_stats(tvam_plan* plan, int64_t* stats);
    serves, else the per-ray tile forward -- from HIP events recorded on its stream around each
    launch.  Returns the launches recorded since the previous call and their summed time in ms (at
    most 1024 per measurement), then stops recording, or (enable != 0) starts a new measurement of
-   the kernel kind of `plan`.  Process-wide (one timer).
-   (ABI v10, added in round 5) */
+   the kernel kind of `plan`.  One timer per process, owned by the plan that enabled it (another
+   plan's call fails while it runs; launches on other devices are not recorded); reading it
+   (enable == 0) releases it, and so does destroying the owning plan.  (ABI v11) */
 int tvam_plan_kernel_time(tvam_plan* plan, int32_t enable, double* total_ms, int64_t* launches);
 
 /* Surface-aware plans: the per-channel voxel volumes the forward divides by and the

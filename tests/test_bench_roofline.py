@@ -97,3 +97,14 @@ def test_csrc_digest_tracks_kernel_sources(tmp_path, monkeypatch):
         d1 = bench.csrc_digest()
         assert d1 != d0
         d0 = d1
+
+
+def test_host_info_threads_are_the_affinity(monkeypatch):
+    """The CPU baseline's reported value runs on every CPU of the process's affinity; the
+    OMP_NUM_THREADS share is the second timing."""
+    monkeypatch.setenv("OMP_NUM_THREADS", "1")
+    h = bench.host_info()
+    assert h["threads"] == h["affinity"] == len(os.sched_getaffinity(0))
+    assert h["omp_threads"] == 1
+    monkeypatch.delenv("OMP_NUM_THREADS")
+    assert bench.host_info()["omp_threads"] == h["affinity"]

@@ -31,6 +31,15 @@ def test_single_gpu_line():
     assert r["metric"] == "optimizer iterations/sec (fwd+adjoint), 64³ voxels × 64 angles"
     assert r["n_gpus"] == 1 and r["steps"] == 3 and r["value"] > 0
     assert r["cpu_baseline"]["kind"] == "port" and r["cpu_baseline"]["host"]["threads"] >= 1
+    # the baseline runs on the affinity's CPUs, the OMP share timed beside it
+    assert r["cpu_baseline"]["host"]["threads"] == len(os.sched_getaffinity(0)) == r["cpu_baseline"]["cores"]
+    if r["cpu_baseline"]["host"]["omp_threads"] != r["cpu_baseline"]["host"]["threads"]:
+        assert r["cpu_baseline"]["at_omp_num_threads"]["value"] > 0
+    # the median of the timed steps beside the mean, and the dense-gradient adjoint
+    steps = r["ms_per_step_min_max"]
+    assert steps[0] <= r["ms_per_step_median"] <= steps[1]
+    assert abs(r["value_median"] * r["ms_per_step_median"] - 1e3) < 1e-6 * r["value_median"] * r["ms_per_step_median"]
+    assert r["dense_gradient"]["adj_ms"] > 0 and r["dense_gradient"]["ms_per_step_model"] > 0
     # counter summaries are committed for the BASELINE sizes only (profiles/r03/roofline_config<K>.json)
     assert set(r["roofline"]) >= {"bound", "achieved", "peak", "unit", "frac", "traffic"}
     assert r["roofline"]["frac"] is None and r["roofline"]["fwd_call_ms"] > 0

@@ -38,3 +38,32 @@ def test_kernel_time_counts_forward_launches():
         assert p.kernel_time(False) == (0.0, 0)  # stopped
     finally:
         p.close()
+
+
+def test_kernel_timer_is_owned_by_its_plan():
+    """one timer per process, owned by the plan that enabled it: another plan cannot
+    take it while it runs; reading it or destroying the owner releases it (and its events)."""
+    from drtvam_amd._abi import TvamError
+    d = desc_from_config(benchy_index_matched(N=32, angles=8))
+    a, b = Projection(d, "cuda:0"), Projection(d, "cuda:0")
+    try:
+        n = int(d.crop_x) * int(d.crop_y) * 8
+        x = torch.rand(n, device="cuda:0")
+        a.kernel_time(True)
+        with pytest.raises((TvamError, RuntimeError, ValueError)):
+            b.kernel_time(True)
+        b.forward(x, None, 1, 0)  # the timer records its kernel kind on its device, whichever plan launches
+        a.forward(x, None, 1, 0)
+        ms, launches = a.kernel_time(False)  # read: released
+        assert launches == 2 and ms > 0.0
+        b.kernel_time(True)
+        b.forward(x, None, 1, 0)
+        b.close()  # the owner goes: the timer and its events with it
+        b = None
+        a.kernel_time(True)
+        a.forward(x, None, 1, 0)
+        assert a.kernel_time(False)[1] == 1
+    finally:
+        a.close()
+        if b is not None:
+            b.close()

@@ -2,6 +2,7 @@
 read at plan creation; "tile=T" sets desc.tile), HIP-event times of the forward and adjoint calls,
 and each variant's dose / gradient compared with the first variant's.
 usage: python tools/proj_ab.py [N] ["ENV=V ENV=V tile=T" ...]"""
+import hashlib
 import json
 import os
 import sys
@@ -50,7 +51,9 @@ def main():
         grad = proj.adjoint(G, x.numel())
         fmin, fmed = timed(lambda: proj.forward(x, out=dose))
         amin, amed = timed(lambda: proj.adjoint(G, x.numel(), out=grad))
-        rec = {"variant": v, "fwd_ms_min": fmin, "fwd_ms_med": fmed, "adj_ms_min": amin, "adj_ms_med": amed}
+        rec = {"variant": v, "fwd_ms_min": fmin, "fwd_ms_med": fmed, "adj_ms_min": amin, "adj_ms_med": amed,
+               "dose_sha": hashlib.sha256(dose.cpu().numpy().tobytes()).hexdigest()[:16],
+               "grad_sha": hashlib.sha256(grad.cpu().numpy().tobytes()).hexdigest()[:16]}
         if ref is None:
             ref = (dose.clone(), grad.clone())
         else:
