@@ -191,6 +191,7 @@ __global__ __launch_bounds__(NT, MINW) void tvam_adjl_kernel(TvamConsts k, TvamP
     char* tb = reinterpret_cast<char*>(smem) + S;  // plane 0
     int* s_roff = reinterpret_cast<int*>(tb + (size_t)P * (Z / 4));
     int* s_rows = s_roff + Z + 1;
+    int* s_next = s_rows + pl.max_rows_chunk * ((Z + 7) / 8);  // the group's next unclaimed chunk
     int x0, x1, y0, y1;
     adjl_tile_bounds(k, tp, tile_id, x0, x1, y0, y1);
     const int wx = x1 - x0, wy = y1 - y0;
@@ -224,6 +225,7 @@ __global__ __launch_bounds__(NT, MINW) void tvam_adjl_kernel(TvamConsts k, TvamP
         *reinterpret_cast<float4*>(tb + (size_t)q * P - S + (size_t)o * 16) = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     }
     if (threadIdx.x == 0) {
+        *s_next = c0 + NT / 64;  // wave w starts on chunk c0 + w
         int n = 0;
         for (int z = 0; z < Z; ++z) {
             s_roff[z] = n;
@@ -239,6 +241,9 @@ __global__ __launch_bounds__(NT, MINW) void tvam_adjl_kernel(TvamConsts k, TvamP
 
     const int lane = (int)threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform chunk loop
+    // A wave claims the group's chunks one at a time from an LDS counter (the chunks differ in
+    // length: a fixed round robin left a few waves marching while the workgroup held its CU; the
+    // builder orders each group's chunks longest first).
     // Pipelined over the wave's chunks: a chunk's header and its first four weight rows are loaded
     // before the previous chunk's gradient atomics are issued.  A load's data waits for every older
     // vector-memory operation of the wave (atomics included, ~3000 cycles each under load), so the
@@ -300,7 +305,7 @@ __global__ __launch_bounds__(NT, MINW) void tvam_adjl_kernel(TvamConsts k, TvamP
             if (q + j < n4) visits(w[j]);
 #pragma unroll
         for (int z = 0; z < Z; ++z) acc[z] *= wsc;
-        const int cn = c + NT / 64;
+        const int cn = __builtin_amdgcn_readfirstlane(lane == 0 ? atomicAdd(s_next, 1) : 0);
         if (cn < c1) load_chunk(cn);  // before this chunk's atomics
         if (e != 0xffffffffu) {  // (empty lanes add nothing)
             const int al = (int)(e >> 16), colc = (int)(e & 0xffffu);
@@ -328,7 +333,7 @@ __global__ __launch_bounds__(NT, MINW) void tvam_adjl_kernel(TvamConsts k, TvamP
 size_t tvam_adjl_lds(const TvamPlanar& pl, const TvamTiles& t, int Z) {
     const int tw = std::max(pl.adjl_tw0, pl.adjl_tw1);
     return (size_t)(Z / 4) * ((size_t)tw * (t.tsy + 2) * 16 + pl.adjl_slack) + pl.adjl_slack +
-           (size_t)(Z + 1 + pl.max_rows_chunk * ((Z + 7) / 8)) * sizeof(int);
+           (size_t)(Z + 2 + pl.max_rows_chunk * ((Z + 7) / 8)) * sizeof(int);
 }
 
 hipError_t tvam_launch_adj_lists(const TvamConsts& k, const TvamPlanar& pl, const TvamTiles& t, int Z,
@@ -418,6 +423,7 @@ hipError_t tvam_build_adj_lists(const TvamConsts& k, TvamPlanar& pl, const TvamT
             const int64_t nch = ((int64_t)v.size() + 63) / 64;
             for (int part = 0; part < parts; ++part) {
                 gchunk.push_back((int32_t)cgrp.size());
+                const size_t g0 = cgrp.size();
                 for (int64_t ch = nch * part / parts; ch < nch * (part + 1) / parts; ++ch) {
                     const size_t b0 = (size_t)ch * 64, b1 = std::min(v.size(), b0 + 64);
                     // lane group g takes rays 16 g .. 16 g + 15 of the chunk; in each group, longest first,
@@ -453,6 +459,21 @@ hipError_t tvam_build_adj_lists(const TvamConsts& k, TvamPlanar& pl, const TvamT
                     cgrp.push_back(tile * 4 + qd);
                     coff.push_back(coff.back() + (int64_t)((m + 3) / 4));
                     maxlen = std::max<int64_t>(maxlen, (m + 3) / 4 * 4);
+                }
+                // the group's chunks longest first (the kernel's waves claim them in this order)
+                const size_t nc = cgrp.size() - g0;
+                if (nc > 1) {
+                    std::vector<int64_t> len(nc);
+                    for (size_t i = 0; i < nc; ++i) len[i] = coff[g0 + i + 1] - coff[g0 + i];
+                    std::vector<size_t> ord(nc);
+                    std::iota(ord.begin(), ord.end(), (size_t)0);
+                    std::stable_sort(ord.begin(), ord.end(), [&](size_t a1, size_t a2) { return len[a1] > len[a2]; });
+                    std::vector<int32_t> cs2(nc * 64);
+                    for (size_t i = 0; i < nc; ++i)
+                        std::copy(cslot.begin() + (g0 + ord[i]) * 64, cslot.begin() + (g0 + ord[i] + 1) * 64,
+                                  cs2.begin() + i * 64);
+                    std::copy(cs2.begin(), cs2.end(), cslot.begin() + g0 * 64);
+                    for (size_t i = 0; i < nc; ++i) coff[g0 + i + 1] = coff[g0 + i] + len[ord[i]];
                 }
             }
         }

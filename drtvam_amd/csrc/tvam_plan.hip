@@ -454,7 +454,7 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     const int az_knob = env_int("TVAM_PLANAR_ADJ_Z", 0);
     p->planar_az = az_knob == 4 || k.nz < 8 ? 4 : 8;
     if (p->planar_fz != 8 && p->planar_fz != 16 && p->planar_fz != 24 && p->planar_fz != 28 && p->planar_fz != 32 &&
-        p->planar_fz != 40 && p->planar_fz != 52)
+        p->planar_fz != 40 && p->planar_fz != 52 && p->planar_fz != 60)
         p->planar_fz = 0;
     const int ns = (int)cs.size();
     int32_t mrc = 0;
@@ -637,16 +637,17 @@ static int fwd_buffers(tvam_plan* p) {
 // Slices per workgroup of the voxel-driven forward: the fewest padded slice-passes
 // ceil(nz / Z) * (Z + 12) (the +12 prices the per-angle candidate geometry and staging shared by
 // the Z slices), register-staged depths (windows the LDS-DMA staging cannot take) priced 25 %
-// higher, among the depths whose staging fits.  With the DMA staging, Z = 52 on 400-slice films
-// (8 chunks: 2.68 ms against 2.72 at Z = 40 and 2.81 at 32, profiles/r05/fwd_depth/), and on the
-// 50-slice slabs of 8 ranks (one chunk).  Returns false when none fits.
+// higher, among the depths whose staging fits.  With the DMA staging, Z = 60 on 400-slice films
+// (7 chunks, 504 slice-passes against 512 at Z = 52; measured 2.55-2.58 against 2.59-2.60 ms,
+// profiles/r06/ab_fwd/; round 5: Z = 52 2.68, 40 2.72, 32 2.81 ms, profiles/r05/fwd_depth/), and on
+// the <= 60-slice slabs of 8 ranks (one chunk).  Returns false when none fits.
 static int choose_fwd_z(tvam_plan* p) {
     const TvamConsts& k = p->k;
     if (p->planar_fz == 0) {
         int best = 8;
         int64_t bcost = INT64_MAX;
         const bool deep = env_int("TVAM_FWD_BIN", 1) != 0;
-        for (int Z : {52, 40, 32, 28, 24, 16, 8}) {
+        for (int Z : {60, 52, 40, 32, 28, 24, 16, 8}) {
             if ((Z > 32 && !deep) || !tvam_planar_fwd_fits(p->pl, Z)) continue;
             const int64_t cost =
                 (int64_t)((k.nz + Z - 1) / Z) * (Z + 12) * (deep && tvam_planar_fwd_dma_window(p->pl, Z) ? 4 : 5);
@@ -654,7 +655,7 @@ static int choose_fwd_z(tvam_plan* p) {
         }
         p->planar_fz = best;
     }
-    for (int Z : {52, 40, 32, 28, 24, 16, 8})  // the deepest instantiated depth <= the choice that fits
+    for (int Z : {60, 52, 40, 32, 28, 24, 16, 8})  // the deepest instantiated depth <= the choice that fits
         if (Z <= p->planar_fz && tvam_planar_fwd_fits(p->pl, Z)) {
             p->planar_fz = Z;
             break;

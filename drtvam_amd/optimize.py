@@ -82,6 +82,65 @@ def angle_shard(n_angles: int, rank: int, world: int):
     return (n_angles * rank) // world, (n_angles * (rank + 1)) // world
 
 
+# Relative cost of a film slice in a slab-sharded iteration: every slice costs its forward, vector
+# and base adjoint work (1), and the adjoint marches a (45 x 45 tile, slice chunk) only where the
+# thresholded loss's gradient is nonzero -- near convergence, the tiles that hold target voxels:
+# + SLAB_TARGET_COST x the slice's fraction of such tiles.  From the round-5 8-rank emulation of
+# config 2 (profiles/r05/final/emulate_slab.jsonl): slab 0 (10 of 50 slices in the box target) ran
+# its adjoint in 0.206 ms, slab 3 (50 of 50) in 0.458 ms, i.e. 0.0063 ms more per target slice on
+# a per-slice iteration cost of ~0.016 ms.
+SLAB_TARGET_COST = 0.4
+SLAB_TILE = 45
+
+
+def slab_costs(target, tile=SLAB_TILE, gamma=SLAB_TARGET_COST):
+    """Per-slice cost weights of a slab split from the target [Z, Y, X(, C)] (CPU tensor)."""
+    t = torch.as_tensor(target)
+    if t.dim() == 4:
+        t = t[..., 0]
+    occ = (t > 0).to(torch.float32)
+    Z, Y, X = occ.shape
+    py, px = (-Y) % tile, (-X) % tile
+    occ = torch.nn.functional.pad(occ, (0, px, 0, py))
+    tiles = occ.reshape(Z, (Y + py) // tile, tile, (X + px) // tile, tile).amax(dim=(2, 4))
+    frac = tiles.reshape(Z, -1).mean(dim=1)
+    return (1.0 + gamma * frac).double().numpy()
+
+
+def balanced_slabs(costs, world):
+    """Contiguous slabs [z0, z1) of the slices, one per rank, whose largest summed cost is least
+    (binary search on the bound, greedy fill; every slab keeps at least one slice)."""
+    n = len(costs)
+    if world >= n:
+        return [(min(k, n), min(k + 1, n)) for k in range(world)]
+    pre = np.concatenate([[0.0], np.cumsum(costs)])
+
+    def cut(bound):
+        edges, z = [0], 0
+        for k in range(world - 1):
+            left = world - 1 - k  # slabs after this one, each needing a slice
+            hi = n - left
+            j = z + 1
+            while j < hi and pre[j + 1] - pre[z] <= bound:
+                j += 1
+            edges.append(j)
+            z = j
+        edges.append(n)
+        return edges, max(pre[b] - pre[a] for a, b in zip(edges[:-1], edges[1:]))
+
+    lo, hi = float(max(costs)), float(pre[-1])
+    best = cut(hi)
+    for _ in range(60):
+        mid = 0.5 * (lo + hi)
+        e, m = cut(mid)
+        if m <= mid + 1e-12:
+            hi, best = mid, (e, m)
+        else:
+            lo = mid
+    e = best[0]
+    return [(e[k], e[k + 1]) for k in range(world)]
+
+
 def _dist(always=False):
     """torch.distributed when a process group of more than one rank is up (or of any size with
     `always`: config 'collectives': 'always' runs the sharded loop's collectives at world size 1)."""
@@ -437,6 +496,15 @@ class TvamProblem(ShardedLoop):
             from ._abi import FLAG_NO_ZERO_SKIP
             base['flags'] = int(base['flags']) | FLAG_NO_ZERO_SKIP
         self.surface_aware = bool(self.sensor.film().surface_aware)
+        if target is None:
+            if self.surface_aware:  # fractional inside / outside volumes (optimize.py:131-134)
+                target = self.sensor.compute_volume(self.scene).cpu()
+            elif 'filename' in config['target']:
+                target = discretize(self.scene, sensor=self.sensor)
+            else:
+                target = analytic_target(self.sensor.resolution(), self.sensor.bbox_min, self.sensor.bbox_max,
+                                         config['target'].get('analytic', 'box_hole'))
+        self.target_full = target.to(dtype=torch.float32)
         # scattered paths leave their slice; surface-aware films run the per-path kernels
         planar = self.regular_sampling and full_desc.albedo == 0.0 and not self.surface_aware
         if shard == 'slab' and not (planar and fusable):
@@ -447,7 +515,9 @@ class TvamProblem(ShardedLoop):
         self.n_vox = int(full_desc.film_res[0]) * int(full_desc.film_res[1]) * self.res_z
         if self.shard == 'slab':
             self.a0, self.a1 = 0, A
-            self.z0, self.z1 = angle_shard(self.res_z, self.rank, self.world)
+            # slabs of equal cost (slab_costs), the same on every rank
+            self.slabs = balanced_slabs(slab_costs(self.target_full.cpu()), self.world)
+            self.z0, self.z1 = self.slabs[self.rank]
             self.r0, self.r1 = self._row_band(full_desc)
             shard_props = {'angle_range': (0, A), 'row_band': (self.r0, self.r1), 'slab': (self.z0, self.z1)}
             self.dose_sharded = True
@@ -461,15 +531,6 @@ class TvamProblem(ShardedLoop):
         self.final_integrator = VolumeIntegrator(iprops | {'max_depth': config.get('max_depth_ref', 16),
                                                            'rr_depth': config.get('rr_depth_ref', 8)})
 
-        if target is None:
-            if self.surface_aware:  # fractional inside / outside volumes (optimize.py:131-134)
-                target = self.sensor.compute_volume(self.scene).cpu()
-            elif 'filename' in config['target']:
-                target = discretize(self.scene, sensor=self.sensor)
-            else:
-                target = analytic_target(self.sensor.resolution(), self.sensor.bbox_min, self.sensor.bbox_max,
-                                         config['target'].get('analytic', 'box_hole'))
-        self.target_full = target.to(dtype=torch.float32)
         self.target = self.target_full[self.z0:self.z1].to(device=dev).contiguous()
 
         # this rank's part of projector.active_data (dense crop order [angle][row][col])
@@ -545,7 +606,7 @@ class TvamProblem(ShardedLoop):
         _abi.check(_abi.load_library().tvam_row_slices(ctypes.byref(desc), m.ctypes.data_as(ctypes.c_void_p)))
         bands = []
         for k in range(self.world):
-            z0, z1 = angle_shard(self.res_z, k, self.world)
+            z0, z1 = self.slabs[k]
             rows = np.nonzero((m >= z0) & (m < z1))[0]
             bands.append((int(rows.min()), int(rows.max()) + 1) if rows.size else None)
             if rows.size and not np.all((m[rows.min():rows.max() + 1] >= z0) & (m[rows.min():rows.max() + 1] < z1)

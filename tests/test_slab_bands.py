@@ -48,3 +48,34 @@ def test_interleaved_rows_rejected():
     m = np.arange(R)
     m[10], m[100] = m[100], m[10]  # a row of the last range inside the first band
     assert slab_bands(m, nz, 2, 32, 8, R) is None
+
+
+def test_balanced_slabs_cover_and_balance():
+    """The slab split: contiguous slabs that tile the film, one per rank, whose
+    largest cost is the least any contiguous split reaches (brute force on small cases)."""
+    import itertools
+    import numpy as np
+    from drtvam_amd.optimize import balanced_slabs
+    rng = np.random.default_rng(0)
+    for n, w in [(10, 3), (12, 4), (9, 2), (7, 7), (16, 5)]:
+        c = rng.uniform(1.0, 1.5, n)
+        e = balanced_slabs(c, w)
+        assert e[0][0] == 0 and e[-1][1] == n and all(a < b for a, b in e)
+        assert all(e[i][1] == e[i + 1][0] for i in range(w - 1))
+        got = max(c[a:b].sum() for a, b in e)
+        best = min(max(c[a:b].sum() for a, b in zip((0,) + cut, cut + (n,)))
+                   for cut in itertools.combinations(range(1, n), w - 1))
+        assert got <= best + 1e-9
+
+
+def test_slab_costs_weigh_target_slices():
+    """Slices holding target voxels cost more (their adjoint tiles are marched); the box target's
+    8-rank split gives the two end slabs, which hold the empty slices, more slices."""
+    from drtvam_amd.optimize import balanced_slabs, slab_costs
+    from drtvam_amd.utils import analytic_target
+    t = analytic_target((400, 400, 400), (-5.0, -5.0, -5.0), (5.0, 5.0, 5.0))
+    c = slab_costs(t)
+    assert c[0] == 1.0 and c[200] > 1.2
+    e = balanced_slabs(c, 8)
+    sizes = [b - a for a, b in e]
+    assert sizes[0] > 50 and sizes[-1] > 50 and max(sizes[1:-1]) < 50
