@@ -175,12 +175,16 @@ __global__ __launch_bounds__(NT, MINW) void tvam_adjl_kernel(TvamConsts k, TvamP
                                                        const int32_t* __restrict__ idxmap,
                                                        const float* __restrict__ gin, float* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-    // blockIdx -> (group, slice chunk): workgroup b runs on XCD b % 8; XCD x takes groups x, x + 8,
-    // ..., each over all its slice chunks back to back (its weights stay in that XCD's L2)
+    // blockIdx -> (group, slice chunk): workgroup b runs on XCD b % 8; XCD x takes the listed
+    // groups x, x + 8, ..., each over all its slice chunks back to back (its weights stay in that
+    // XCD's L2).  Only groups that hold chunks are listed: an angle shard's rays fall in one or two
+    // step quadrants, and with every group in the grid the XCDs of the empty quadrants idled
+    // (groups 4 t + q land on XCDs q and q + 4).
     const int b = (int)blockIdx.x, xcd = b & 7, ib = b >> 3;
     const int gq = ib / nzc, zc = ib - gq * nzc;
-    const int grp = xcd + 8 * gq;
-    if (grp >= pl.adjl_ngroups) return;
+    const int gi = xcd + 8 * gq;
+    if (gi >= pl.adjl_nlist) return;
+    const int grp = pl.adjl_glist[gi];
     const int c0 = pl.adjl_gchunk[grp], c1 = pl.adjl_gchunk[grp + 1];
     if (c0 >= c1) return;
     const int tq = grp / pl.adjl_parts, tile_id = tq >> 2, qd = tq & 3;
@@ -349,7 +353,7 @@ hipError_t tvam_launch_adj_lists(const TvamConsts& k, const TvamPlanar& pl, cons
         q.adj_nzc = (z1 - z0 + ZL - 1) / ZL;
     }
     const int nzc = q.adj_nzc > 0 ? q.adj_nzc : (k.nz + ZL - 1) / ZL;
-    const int64_t gpad = ((int64_t)pl.adjl_ngroups + 7) / 8 * 8;
+    const int64_t gpad = ((int64_t)pl.adjl_nlist + 7) / 8 * 8;
     const int64_t nb = gpad * nzc;
     if (nb <= 0) return hipSuccess;
     if (nb > 0x7fffffff) return hipErrorInvalidValue;
@@ -479,6 +483,9 @@ hipError_t tvam_build_adj_lists(const TvamConsts& k, TvamPlanar& pl, const TvamT
         }
     }
     gchunk.push_back((int32_t)cgrp.size());
+    std::vector<int32_t> glist;  // the groups that hold chunks
+    for (size_t g = 0; g + 1 < gchunk.size(); ++g)
+        if (gchunk[g + 1] > gchunk[g]) glist.push_back((int32_t)g);
     const int64_t nchunks = (int64_t)cgrp.size();
     const size_t wbytes = (size_t)coff.back() * 64 * sizeof(float4);
     const size_t hbytes = (size_t)nchunks * 64 * sizeof(int4);
@@ -494,6 +501,7 @@ hipError_t tvam_build_adj_lists(const TvamConsts& k, TvamPlanar& pl, const TvamT
         return r;
     };
     if ((e = up((void**)&bufs.gchunk, gchunk.data(), gchunk.size() * sizeof(int32_t))) != hipSuccess ||
+        (e = up((void**)&bufs.glist, glist.data(), glist.size() * sizeof(int32_t))) != hipSuccess ||
         (e = up((void**)&bufs.coff, coff.data(), coff.size() * sizeof(int64_t))) != hipSuccess ||
         (e = up((void**)&d_cslot, cslot.data(), cslot.size() * sizeof(int32_t))) != hipSuccess ||
         (e = up((void**)&d_cgrp, cgrp.data(), cgrp.size() * sizeof(int32_t))) != hipSuccess ||
@@ -504,6 +512,8 @@ hipError_t tvam_build_adj_lists(const TvamConsts& k, TvamPlanar& pl, const TvamT
         return e;
     }
     pl.adjl_gchunk = bufs.gchunk;
+    pl.adjl_glist = bufs.glist;
+    pl.adjl_nlist = (int32_t)glist.size();
     pl.adjl_coff = bufs.coff;
     pl.adjl_hdr = bufs.hdr;
     pl.adjl_w = bufs.w;

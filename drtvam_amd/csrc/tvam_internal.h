@@ -108,7 +108,9 @@ struct TvamPlanar {
     const int64_t* adjl_coff;    // [nchunks + 1] first float4 row of each chunk's weights
     const int4* adjl_hdr;        // [nchunks][64] {entry LDS offset, slot, interface weight bits, x | y step << 16}
     const float4* adjl_w;        // [rows][64] weights, 4 visits per float4, LSB = y step after the visit
+    const int32_t* adjl_glist;   // [nlist] the groups that hold chunks, in group order (the grid's groups)
     int32_t adjl_ngroups, adjl_parts;  // groups = (tile, step quadrant, part)
+    int32_t adjl_nlist;                // groups that hold chunks
     int32_t adjl_tw0, adjl_tw1;        // row pitch (voxels) for equal / opposite step signs: 1 / 15 (mod 16)
     int32_t adjl_slack;                // zeroed bytes around each plane (padding visits walk there)
     int32_t adjl_z;                    // slices per workgroup (8 or 16)
@@ -117,6 +119,7 @@ struct TvamPlanar {
 // Device buffers of the visit lists (owned by the plan).
 struct TvamAdjListBufs {
     int32_t* gchunk = nullptr;
+    int32_t* glist = nullptr;
     int64_t* coff = nullptr;
     int4* hdr = nullptr;
     float4* w = nullptr;

@@ -152,6 +152,7 @@ extern "C" int tvam_abi_version(void) { return TVAM_ABI_VERSION; }
 
 static void adjl_free(TvamAdjListBufs& b) {
     (void)hipFree(b.gchunk);
+    (void)hipFree(b.glist);
     (void)hipFree(b.coff);
     (void)hipFree(b.hdr);
     (void)hipFree(b.w);

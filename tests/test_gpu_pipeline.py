@@ -71,8 +71,13 @@ def test_direction_rows_equal_full_direction():
     assert torch.equal(full, banded)
 
 
-def test_adjoint_slices_assemble_the_adjoint():
-    """tvam_adjoint_slices over slab bands (rows from tvam_row_slices) == tvam_adjoint."""
+@pytest.mark.parametrize("adjl_z", [None, "16"])
+def test_adjoint_slices_assemble_the_adjoint(adjl_z, monkeypatch):
+    """tvam_adjoint_slices over slab bands (rows from tvam_row_slices) == tvam_adjoint; also with the
+    list adjoint's 16-slice workgroups on a film whose slab chunks are counted in 8-slice chunks
+    (tvam_launch_adj_lists converts them)."""
+    if adjl_z is not None:
+        monkeypatch.setenv("TVAM_ADJL_Z", adjl_z)
     cfg = benchy_index_matched(N=128, angles=12)
     cfg["direction_parts"] = 2
     prob = TvamProblem(cfg, device=torch.device("cuda", 0))
@@ -84,3 +89,28 @@ def test_adjoint_slices_assemble_the_adjoint():
     for r0, r1, z0, z1 in pipe.parts:
         prob.proj.adjoint_slices(gv, prob.n_local, z0, z1, r0, r1, banded)
     torch.testing.assert_close(banded, full, rtol=1e-6, atol=1e-6 * float(full.abs().max()))
+
+
+def test_list_adjoint_matches_the_tile_adjoint(monkeypatch):
+    """The list adjoint (visit lists built at plan creation, chunks claimed from an LDS counter,
+    only groups holding chunks launched) against the per-ray tile adjoint on one plan's geometry
+    (TVAM_ADJ_LISTS=0): the same weights in the same per-(ray, tile, slice) order, so equal to
+    float-atomic ordering; on a full film and on an angle shard whose rays fill one step quadrant."""
+    from drtvam_amd.configs import desc_from_config
+    from drtvam_amd.engine import Projection
+    N = 96
+    for a0, a1 in [(0, N), (0, N // 8)]:
+        d = desc_from_config(benchy_index_matched(N=N, angles=N))
+        d.angle_begin, d.angle_end = a0, a1
+        n = (a1 - a0) * int(d.crop_x) * int(d.crop_y)
+        g = torch.rand((N, N, N), device="cuda", generator=torch.Generator(device="cuda").manual_seed(3)) - 0.5
+        out = []
+        for lists in ("1", "0"):
+            monkeypatch.setenv("TVAM_ADJ_LISTS", lists)
+            p = Projection(d, "cuda:0")
+            try:
+                assert p.planar
+                out.append(p.adjoint(g, n, None, 1, 0))
+            finally:
+                p.close()
+        torch.testing.assert_close(out[0], out[1], rtol=1e-5, atol=1e-6 * float(out[1].abs().max()))
