@@ -202,9 +202,6 @@ __global__ __launch_bounds__(NT, MINW) void tvam_adjl_kernel(TvamConsts k, TvamP
     const size_t plane = (size_t)k.res[0] * k.res[1];
     // gradient tile: a thread per voxel, its Z loads issued together (clamped addresses, no
     // branches), Z / 4 ds_write_b128
-#ifndef TVAM_ADJL_ZSKIP
-#define TVAM_ADJL_ZSKIP 1  // (0: march all-zero gradient tiles too, for A/B builds)
-#endif
     int nonzero = 0;
     for (int li = threadIdx.x; li < nvox; li += NT) {
         const int ly = li / tw - 1, lx = li - (ly + 1) * tw - 1;
@@ -241,7 +238,7 @@ __global__ __launch_bounds__(NT, MINW) void tvam_adjl_kernel(TvamConsts k, TvamP
     // an all-zero gradient tile (the thresholded loss is flat wherever the dose meets its bounds)
     // makes every partial exactly 0, which adds nothing: no march
     const int any = __syncthreads_or(nonzero);
-    if (s_roff[Z] == 0 || (TVAM_ADJL_ZSKIP && !any)) return;  // (or no DMD row lies in these slices)
+    if (s_roff[Z] == 0 || !any) return;  // (or no DMD row lies in these slices)
 
     const int lane = (int)threadIdx.x & 63;
     const int wv = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));  // wave-uniform chunk loop

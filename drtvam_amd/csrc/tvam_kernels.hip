@@ -21,48 +21,7 @@
 
 #define TVAM_BLOCK 256
 #define TVAM_WAVES (TVAM_BLOCK / 64)
-#ifndef TVAM_FWD_ACC64
-#define TVAM_FWD_ACC64 0  // 1: forward accumulates 64-bit fixed point (8 B per voxel of LDS)
-#endif
-#ifndef TVAM_TILE_DIAG
-#define TVAM_TILE_DIAG 0  // 1 (diagnostic builds only): per-wave slot / visit / cycle counters
-#endif
 
-#if TVAM_TILE_DIAG
-// [0] waves, [1] loop iterations, [2] lane slots, [3] zero-pattern skips, [4] inactive pixels,
-// [5] other slice / no segment, [6] misses the tile window, [7] marched lanes, [8] visits,
-// [9] sum over iterations of the wave's largest visit count, [10] cycles before the loop,
-// [11] setup cycles, [12] march cycles, [13] / [14] loop end / start times, [16 + b] marched lanes
-// whose visits are in [b/8, (b+1)/8) of their wave's largest count (b = 0..7)
-__device__ unsigned long long tvam_tile_diag[24];
-extern "C" int tvam_tile_diag_read(unsigned long long* host, int reset) {
-    if (hipMemcpyFromSymbol(host, HIP_SYMBOL(tvam_tile_diag), sizeof(tvam_tile_diag)) != hipSuccess) return -1;
-    if (reset) {
-        static const unsigned long long zero[24] = {};
-        if (hipMemcpyToSymbol(HIP_SYMBOL(tvam_tile_diag), zero, sizeof(zero)) != hipSuccess) return -1;
-    }
-    return 0;
-}
-// per-slot visit counts of one (tile, slice) workgroup (0xffffffff: nothing marched)
-__device__ unsigned tvam_tile_dslot[1 << 21];
-__device__ int tvam_tile_dsel[2] = {-1, -1};
-extern "C" int tvam_tile_diag_slots(int tile, int slice, unsigned* host, int n) {
-    const int sel[2] = {tile, slice};
-    if (hipMemcpyToSymbol(HIP_SYMBOL(tvam_tile_dsel), sel, sizeof(sel)) != hipSuccess) return -1;
-    if (host && n > 0 &&
-        hipMemcpyFromSymbol(host, HIP_SYMBOL(tvam_tile_dslot), sizeof(unsigned) * (size_t)min(n, 1 << 21)) != hipSuccess)
-        return -1;
-    return 0;
-}
-__device__ __forceinline__ unsigned tvam_wave_umax(unsigned v) {
-    for (int off = 32; off > 0; off >>= 1) v = max(v, (unsigned)__shfl_xor((int)v, off, 64));
-    return v;
-}
-__device__ __forceinline__ unsigned long long tvam_wave_usum(unsigned long long v) {
-    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
-    return v;
-}
-#endif
 
 __device__ __forceinline__ float tvam_exp2(float x) { return __builtin_amdgcn_exp2f(x); }
 
@@ -74,15 +33,8 @@ __device__ __forceinline__ int tvam_rint(float x) {
 }
 
 // How the in-tile march consumes one visit.
-enum TvamAcc { ACC_FLOAT = 0, ACC_FIXED = 1, ACC_GATHER = 2, ACC_COUNT = 3, ACC_FIXED64 = 4 };
+enum TvamAcc { ACC_FLOAT = 0, ACC_FIXED = 1, ACC_GATHER = 2, ACC_COUNT = 3 };
 
-// Exact split of a rounded fixed-point value q = rint(c) (|q| < 2^62) into a 64-bit integer.
-__device__ __forceinline__ unsigned long long tvam_f2i64(float c) {
-    const float q = rintf(c);
-    const float hi = floorf(q * 2.3283064365386963e-10f);          // q / 2^32, exact power-of-two scale
-    const float lo = fmaf(-hi, 4294967296.0f, q);                   // exact: low bits of q, in [0, 2^32)
-    return ((unsigned long long)(unsigned)(int)hi << 32) + (unsigned long long)(unsigned)lo;
-}
 
 
 // March state of one ray inside one tile (times measured from the tile entry).
@@ -116,7 +68,7 @@ __device__ __forceinline__ void tvam_march(TvamMarchRay a, const float tsx, cons
                                            const int syb, const float sig, float& acc,
                                            unsigned long long& nvis, const char* tile = nullptr, const int tw = 0,
                                            const int wx = 0, const int wy = 0) {
-    constexpr int ESZ = ACC == ACC_FIXED64 ? 8 : 4;
+    constexpr int ESZ = 4;
     const float mhs = -0.5f * sig, msig = -sig;
     float tp = 0.0f;
     for (;;) {
@@ -127,13 +79,11 @@ __device__ __forceinline__ void tvam_march(TvamMarchRay a, const float tsx, cons
         const float e1 = W2 ? fmaf(msig, c, a.e0) : a.e0 - c;
         if (ACC == ACC_FLOAT) atomicAdd(reinterpret_cast<float*>(a.pv), c);
         else if (ACC == ACC_FIXED) atomicAdd(reinterpret_cast<int*>(a.pv), tvam_rint(c));
-        else if (ACC == ACC_FIXED64) atomicAdd(reinterpret_cast<unsigned long long*>(a.pv), tvam_f2i64(c));
         else if (ACC == ACC_GATHER) acc = fmaf(c, *reinterpret_cast<const float*>(a.pv), acc);
         else {  // interior visits of nonzero length (guard-band visits carry rounding-level dt)
             const int li = (int)(a.pv - tile) / ESZ, ly = li / tw, lx = li - ly * tw;
             nvis += (tn > tp && lx >= 1 && lx <= wx && ly >= 1 && ly <= wy) ? 1 : 0;
         }
-        if (TVAM_TILE_DIAG && ACC != ACC_COUNT) ++nvis;  // diagnostic builds: every visit
         tp = tn;
         const bool mx = a.Tx <= a.Ty;
         a.Tx = mx ? a.Tx + tsx : a.Tx;
@@ -449,31 +399,19 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
     float* tile = reinterpret_cast<float*>(smem);
     const int tsx = tp.tsx, tsy = tp.tsy, ns = tp.n_shard;
     const int tw = TVAM_TILE_PITCH(tsx), th = tsy + 2;  // tile + 1-voxel guard band, odd row pitch
-    const int tile_words = (MODE == TVAM_MODE_FWD && TVAM_FWD_ACC64) ? 2 * tw * th : tw * th;
+    const int tile_words = tw * th;
     float* s_red = tile + tile_words;
     unsigned* s_amax = reinterpret_cast<unsigned*>(s_red + 16);  // forward: per-angle max |p|
 
-#if TVAM_TILE_DIAG
-    const unsigned long long dg_t0 = __builtin_amdgcn_s_memtime();
-#endif
     // XCD-aware order: workgroup b runs on XCD b % 8; XCD x takes slices x, x + 8, x + 16, ..., all
     // tiles of a slice in turn, so the tiles re-reading one slice's ray records (every tile a ray
     // crosses reads its record) share that XCD's L2 instead of fetching it into all eight, and the
     // XCDs' loads stay even where the work per slice is not (contiguous slice runs per XCD left the
     // XCDs of a sparse active set's empty slices idle: config 5 with filter_radon 11 % slower)
     const int ntl = tp.ntx * tp.nty;
-#ifndef TVAM_TILE_XCD
-#define TVAM_TILE_XCD 1  // (0: workgroups in plain (slice, tile) order, for A/B builds)
-#endif
-    int zloc, tile_id;
-    if (TVAM_TILE_XCD) {
-        const int i = (int)(blockIdx.x >> 3);
-        zloc = (i / ntl) * 8 + (int)(blockIdx.x & 7);
-        tile_id = i - (i / ntl) * ntl;
-    } else {
-        zloc = (int)blockIdx.x / ntl;
-        tile_id = (int)blockIdx.x - zloc * ntl;
-    }
+    const int bi = (int)(blockIdx.x >> 3);
+    const int zloc = (bi / ntl) * 8 + (int)(blockIdx.x & 7);
+    const int tile_id = bi - (bi / ntl) * ntl;
     if (zloc >= nzl) return;
     const int kz = zloc + (MODE == TVAM_MODE_FWD ? tp.kz0 : 0);
     const int x0 = (tile_id % tp.ntx) * tsx, y0 = (tile_id / tp.ntx) * tsy;
@@ -494,10 +432,7 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
     }
     if (MODE == TVAM_MODE_FWD)
         for (int i = threadIdx.x; i < ns; i += TVAM_BLOCK) s_amax[i] = 0u;
-#ifndef TVAM_TILE_ZSKIP
-#define TVAM_TILE_ZSKIP 1  // (0: march all-zero gradient tiles too, for A/B builds)
-#endif
-    if (MODE == TVAM_MODE_ADJ && TVAM_TILE_ZSKIP) {
+    if (MODE == TVAM_MODE_ADJ) {
         // an all-zero gradient tile (the thresholded loss is flat wherever the dose meets its
         // bounds) gathers exactly 0 on every ray, which adds nothing: no march
         if (!__syncthreads_or(nonzero)) return;
@@ -576,7 +511,7 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
         const float pcnt = tvam_block_sum(nz, s_red);
         // outlier test: how many rays are within 2^10 of the largest |value|
         float nbig = 0.0f;
-        if (!TVAM_FWD_ACC64 && pmax > 0.0f && isfinite(pmax)) {
+        if (pmax > 0.0f && isfinite(pmax)) {
             const float thr = pmax * (1.0f / 1024.0f);
             tvam_slot_init(sl, threadIdx.x, max(per_row, 1));
             for (int f = threadIdx.x; f < first; f += TVAM_BLOCK, tvam_slot_next(sl, per_row)) {
@@ -598,16 +533,16 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
         }
         const float per_angle = k.rays_per_voxel / (float)ns;
         const float bound = amax_sum * fabsf(k.wscale) * k.vox_chord * per_angle * (float)(nrows_all * spp);
-        const int headroom = TVAM_FWD_ACC64 ? 62 : 30;
+        const int headroom = 30;
         if (!(amax_sum > 0.0f)) {
-            acc_mode = TVAM_FWD_ACC64 ? ACC_FIXED64 : ACC_FIXED;  // all-zero tile: every contribution is 0
-        } else if ((TVAM_FWD_ACC64 || 64.0f * nbig >= pcnt) && isfinite(bound)) {
+            acc_mode = ACC_FIXED;  // all-zero tile: every contribution is 0
+        } else if (64.0f * nbig >= pcnt && isfinite(bound)) {
             int e;
             frexpf(bound, &e);  // bound < 2^e
             e = headroom - e;
             e = e > 126 ? 126 : (e < -126 ? -126 : e);
             fscale = ldexpf(1.0f, e);
-            acc_mode = TVAM_FWD_ACC64 ? ACC_FIXED64 : ACC_FIXED;
+            acc_mode = ACC_FIXED;
         } else {
             acc_mode = ACC_FLOAT;
             if (counter && threadIdx.x == 0) atomicAdd(counter, 1ull);  // fallback statistics
@@ -615,15 +550,13 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
         __syncthreads();
     }
 
-    constexpr int ESZ = (MODE == TVAM_MODE_FWD && TVAM_FWD_ACC64) ? 8 : 4;
+    constexpr int ESZ = 4;
     unsigned long long nvis = 0;
     // one march from a resumed state, into the tile (forward / count) or gathering from it (adjoint)
     auto march = [&](TvamMarchRay& m, float rtsx, float rtsy, int sxb, int syb) -> float {
         float acc = 0.0f;
         if (MODE == TVAM_MODE_FWD) {
-            if (TVAM_FWD_ACC64 && acc_mode == ACC_FIXED64)
-                tvam_march<ACC_FIXED64, W2>(m, rtsx, rtsy, sxb, syb, k.sig_t, acc, nvis);
-            else if (!TVAM_FWD_ACC64 && acc_mode == ACC_FIXED)
+            if (acc_mode == ACC_FIXED)
                 tvam_march<ACC_FIXED, W2>(m, rtsx, rtsy, sxb, syb, k.sig_t, acc, nvis);
             else
                 tvam_march<ACC_FLOAT, W2>(m, rtsx, rtsy, sxb, syb, k.sig_t, acc, nvis);
@@ -635,22 +568,6 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
         }
         return acc;
     };
-#if TVAM_TILE_DIAG
-    unsigned long long dg[16] = {};
-    unsigned hist[8] = {};
-    const unsigned long long tk0 = __builtin_amdgcn_s_memtime();
-    dg[10] = tk0 - dg_t0;
-    unsigned long long vis_prev = 0;
-    // per march round: visits of this lane, the wave's largest count, the lanes' histogram
-    auto diag_round = [&]() {
-        const unsigned v = (unsigned)(nvis - vis_prev);
-        vis_prev = nvis;
-        dg[8] += v;
-        const unsigned vm = tvam_wave_umax(v);
-        dg[9] += vm;
-        if (v > 0) ++hist[min(7, (int)(8u * v / vm))];
-    };
-#endif
 
     // Adjoint with spp a power of two <= 64: the sample FASTEST instead (lanes of a group of spp march
     // one pixel's jittered rays), so the group sums its partials with shuffles and adds them to the
@@ -696,18 +613,6 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
                 if (act >= 0) atomicAdd(&out[act], part);
             }
         }
-#if TVAM_TILE_DIAG
-        if (tile_id == tvam_tile_dsel[0] && zloc == tvam_tile_dsel[1] && f < (1 << 21))
-            tvam_tile_dslot[f] = why == 0 ? (unsigned)(nvis - vis_prev) : 0xffffffffu;
-        dg[1] += 1;
-        dg[2] += 1;
-        dg[3] += why == 4;
-        dg[4] += why == 1;
-        dg[5] += why == 2;
-        dg[6] += why == 3;
-        dg[7] += why == 0;
-        diag_round();
-#endif
     }
     for (int f = sbeg + (int)threadIdx.x; f < send; f += TVAM_BLOCK) {  // the slice's stray rays
         int al, rowc, colc, smp;
@@ -728,41 +633,15 @@ __global__ __launch_bounds__(TVAM_BLOCK) void tvam_tile_kernel(
             if (MODE == TVAM_MODE_ADJ) atomicAdd(&out[r.act], acc * (k.wscale * r.weight));
         }
     }
-#if TVAM_TILE_DIAG
-    {
-        const unsigned long long tk1 = __builtin_amdgcn_s_memtime();
-        // per-lane counts summed over the wave; iteration / cycle / max counts are wave-uniform (lane 0's)
-        unsigned long long sums[7];
-        for (int i = 2; i <= 8; ++i) sums[i - 2] = tvam_wave_usum(dg[i]);
-        if ((threadIdx.x & 63) == 0) {
-            atomicAdd(&tvam_tile_diag[0], 1ull);
-            atomicAdd(&tvam_tile_diag[1], dg[1]);
-            for (int i = 2; i <= 8; ++i) atomicAdd(&tvam_tile_diag[i], sums[i - 2]);
-            atomicAdd(&tvam_tile_diag[9], dg[9]);
-            atomicAdd(&tvam_tile_diag[10], dg[10]);
-            atomicAdd(&tvam_tile_diag[11], dg[11]);
-            atomicAdd(&tvam_tile_diag[12], dg[12]);
-            atomicAdd(&tvam_tile_diag[13], tk1);  // minus tk0 below
-            atomicAdd(&tvam_tile_diag[14], tk0);
-        }
-        for (int b = 0; b < 8; ++b) {
-            const unsigned long long hb = tvam_wave_usum((unsigned long long)hist[b]);
-            if ((threadIdx.x & 63) == 0) atomicAdd(&tvam_tile_diag[16 + b], hb);
-        }
-    }
-#endif
 
     if (MODE == TVAM_MODE_FWD) {
         __syncthreads();
         const float outscale = k.inv_vol / fscale;
         const int* itile = reinterpret_cast<const int*>(tile);
-        const long long* ltile = reinterpret_cast<const long long*>(tile);
         for (int i = threadIdx.x; i < wx * wy; i += TVAM_BLOCK) {
             int ly = i / wx, lx = i - ly * wx;
             const int li = (ly + 1) * tw + (lx + 1);
-            float v = acc_mode == ACC_FIXED64 ? (float)ltile[li] * outscale
-                      : acc_mode == ACC_FIXED ? (float)itile[li] * outscale
-                                              : tile[li] * k.inv_vol;
+            float v = acc_mode == ACC_FIXED ? (float)itile[li] * outscale : tile[li] * k.inv_vol;
             out[slice_base + (size_t)(y0 + ly) * k.res[0] + (x0 + lx)] = v;
         }
     } else if (MODE == TVAM_MODE_COUNT) {

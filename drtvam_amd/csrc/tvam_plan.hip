@@ -354,11 +354,8 @@ static int upload(T** dst, const std::vector<T>& v) {
 // A/B runs and the tests that force a code path (work splits, slab depths, chunk sizes) -- and
 // each honoured one is logged; production plans take the defaults whatever the environment holds.
 int tvam_knob(const char* name, int def) {
-    static const bool on = [] {
-        const char* v = std::getenv("TVAM_EXPERIMENTAL");
-        return v && std::atoi(v) == 1;
-    }();
-    if (!on) return def;
+    const char* x = std::getenv("TVAM_EXPERIMENTAL");  // read per call: a test process sets it per test
+    if (!(x && std::atoi(x) == 1)) return def;
     const char* v = std::getenv(name);
     if (!(v && *v)) return def;
     const int r = std::atoi(v);
@@ -628,8 +625,8 @@ static int fwd_buffers(tvam_plan* p) {
         p->pl.fwd_bin = p->d_pl_bin;
         p->pl.fwd_pf = nq;
     }
-    // binned slabs staged by LDS-DMA where the window fits (tvam_planar_fwd_dma_ok; TVAM_FWD_DMA=0
-    // builds keep the register staging)
+    // binned slabs staged by LDS-DMA where the window fits (tvam_planar_fwd_dma_ok; wider windows
+    // keep the register staging)
     p->pl.fwd_dma = tvam_planar_fwd_dma_ok(p->pl, Z) ? 1 : 0;
     return 0;
 }
@@ -1170,10 +1167,7 @@ extern "C" int tvam_plan_create(const tvam_desc* desc, int device, tvam_plan** o
     int ntx = (k.res[0] + tsx - 1) / tsx, nty = (k.res[1] + tsy - 1) / tsy;
     p->ntiles = ntx * nty;
     // tile (+ guard band) + reduction scratch + per-angle max |p|
-#ifndef TVAM_FWD_ACC64
-#define TVAM_FWD_ACC64 0
-#endif
-    p->lds_bytes = (size_t)TVAM_TILE_PITCH(tsx) * (tsy + 2) * sizeof(float) * (TVAM_FWD_ACC64 ? 2 : 1) +
+    p->lds_bytes = (size_t)TVAM_TILE_PITCH(tsx) * (tsy + 2) * sizeof(float) +
                    16 * sizeof(float) + (size_t)ns * sizeof(float);
     if (p->lds_bytes > 160 * 1024) {
         plan_free(p);

@@ -114,24 +114,16 @@ hipError_t tvam_launch_planar_rays(const TvamConsts& k, const TvamPlanar& pl, hi
 // in exact arithmetic), so the dose is the same sum of telescoped weights
 // the DDA forms, up to fp32 rounding of the crossing times.
 // ---------------------------------------------------------------------------
-// a lane reads (and FMAs) only the slabs of candidates that meet its voxel: the LDS array serves
-// the active lanes only (config 2 forward, 200-angle shard: 1.8 -> 1.7 ms)
-#ifndef TVAM_FWD_SKIPZERO
-#define TVAM_FWD_SKIPZERO 1
-#endif
 #define TVAM_PF 4     // most staged pattern values per thread and angle (host: ncmax * Z <= TVAM_PF * TVAM_PB)
 // slab row stride (words) of Z slices: an odd number of 16-byte groups, so 16
 // consecutive columns' ds_read_b128 hit 16 different bank groups
 __host__ __device__ constexpr int tvam_fwd_zs(int Z) { return ((Z + 4) / 4) % 2 ? Z + 4 : Z + 8; }
 
-// LDS-DMA staging of the binned slabs (TVAM_FWD_DMA, straight rays): global_load_lds writes a
+// LDS-DMA staging of the binned slabs (straight rays): global_load_lds writes a
 // wave's 64 lanes' 16-byte loads to 64 consecutive 16-byte LDS slots, so a buffer is laid out in
 // whole wave-instructions: the slab's ncm * ZS / 4 slots (a column's Z / 4 data slots and its pad
 // slots) rounded up to 64, and 64 record slots.  Each lane loads the global float4 its slot holds
 // (a pad or round-up slot re-loads a data slot; nothing reads it).
-#ifndef TVAM_FWD_DMA
-#define TVAM_FWD_DMA 1
-#endif
 // The DMA slab's column stride needs no pad when Z / 4 is odd (Z = 52: 13 float4 groups); slots are
 // exact (ncm columns x ZS / 4 groups, the last wave-instruction's surplus lanes masked), so 6
 // workgroups' LDS fits a CU at Z = 52 (4 with 64-slot rounding and a Z + 8 stride).
@@ -149,9 +141,7 @@ __device__ __forceinline__ void tvam_lds_dma16(const void* g, void* l) {
 }
 // a staged column outside the crop: no chord ({q, t_end < 0}; refracted: the second record zero)
 __device__ float4 tvam_null_rec[2] = {{0.0f, 0.0f, -1.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
-#ifndef TVAM_ACH
-#define TVAM_ACH 64  // angles per LDS chunk of per-angle constants
-#endif
+#define TVAM_ACH 64  // angles per LDS chunk of per-angle constants (paths without the SGPR constants)
 
 // Z: slices per thread; NC: candidate DMD columns per (voxel, angle), a
 // bound the plan derives from the voxel's lateral width in columns; MULTI:
@@ -412,7 +402,7 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
             return tout > tin ? e * g.w : 0.0f;  // x the interfaces' transmission (sensor.py:404)
         };
         auto accumulate = [&](int jc, float wgt) {
-            if (TVAM_FWD_SKIPZERO && wgt == 0.0f) return;
+            if (wgt == 0.0f) return;
 #pragma unroll
             for (int z4 = 0; z4 < Z / 4; ++z4) {
                 const float4 p4 = reinterpret_cast<const float4*>(sp + jc * ZS)[z4];
@@ -480,7 +470,9 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
     // dose += the candidates' weights x their staged slabs
     auto fmas = [&](int buf, int jj0, const float (&wgt)[NC]) __attribute__((always_inline)) {
         const float* sp = s_p + buf * bstride;
-#if TVAM_FWD_SKIPZERO
+        // a lane reads (and FMAs) only the slabs of candidates that meet its voxel, and a wave skips a
+        // candidate none of its lanes meets (with the zero weights FMAed instead: 2.44 -> 2.54 ms,
+        // profiles/r06/ab_fwd/)
 #pragma unroll
         for (int c = 0; c < NC; ++c) {
             if (wgt[c] != 0.0f) {
@@ -492,19 +484,6 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
                     acc[4 * z4 + 2] = fmaf(wgt[c], p4.z, acc[4 * z4 + 2]);
                     acc[4 * z4 + 3] = fmaf(wgt[c], p4.w, acc[4 * z4 + 3]);
                 }
-            }
-        }
-        if (false)
-#endif
-#pragma unroll
-        for (int z4 = 0; z4 < Z / 4; ++z4) {
-#pragma unroll
-            for (int c = 0; c < NC; ++c) {
-                const float4 p4 = reinterpret_cast<const float4*>(sp + (jj0 + c) * ZS)[z4];
-                acc[4 * z4 + 0] = fmaf(wgt[c], p4.x, acc[4 * z4 + 0]);
-                acc[4 * z4 + 1] = fmaf(wgt[c], p4.y, acc[4 * z4 + 1]);
-                acc[4 * z4 + 2] = fmaf(wgt[c], p4.z, acc[4 * z4 + 2]);
-                acc[4 * z4 + 3] = fmaf(wgt[c], p4.w, acc[4 * z4 + 3]);
             }
         }
     };
@@ -781,10 +760,10 @@ __global__ __launch_bounds__(256) void tvam_slice_bin4_kernel(TvamConsts k, Tvam
                 make_float4(s_t[cc][4 * q], s_t[cc][4 * q + 1], s_t[cc][4 * q + 2], s_t[cc][4 * q + 3]);
 }
 
-// the binned slabs are staged by LDS-DMA (TVAM_FWD_DMA) where a window fits: <= 2 slab slots per
+// the binned slabs are staged by LDS-DMA where a window fits: <= 2 slab slots per
 // thread and one record wave per record kind (pl.fwd_dma; else register staging)
 bool tvam_planar_fwd_dma_window(const TvamPlanar& pl, int Z) {
-    return TVAM_FWD_DMA && pl.ncmax <= 64 && tvam_fwd_dma_np(pl.ncmax, Z) <= 2 * TVAM_PB;
+    return pl.ncmax <= 64 && tvam_fwd_dma_np(pl.ncmax, Z) <= 2 * TVAM_PB;
 }
 
 bool tvam_planar_fwd_dma_ok(const TvamPlanar& pl, int Z) {

@@ -1490,10 +1490,7 @@ __global__ __launch_bounds__(NT) void tvam_bin_march_kernel(TvamConsts k, TvamSe
             ftile[z * sz + y * sy + x] = v;
             nonzero |= v != 0.0f ? 1 : 0;
         }
-#ifndef TVAM_BIN_ZSKIP
-#define TVAM_BIN_ZSKIP 1  // (0: march all-zero gradient bricks too, for A/B builds)
-#endif
-        if (!__syncthreads_or(nonzero) && !WS && TVAM_BIN_ZSKIP) {
+        if (!__syncthreads_or(nonzero) && !WS) {
             // an all-zero gradient brick (the thresholded loss is flat wherever the dose meets its
             // bounds): every entry's partial is exactly 0 -- written with its pixel for the sort
             for (uint32_t e = e0 + threadIdx.x; e < e1; e += NT) {

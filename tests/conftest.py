@@ -4,9 +4,10 @@ import sys
 import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-# the tests that force a code path (work splits, slab depths, bin chunk sizes) do so through the
-# library's TVAM_* tuning knobs, which it honours only under TVAM_EXPERIMENTAL=1 (tvam_knob)
-os.environ.setdefault("TVAM_EXPERIMENTAL", "1")
+# The tests that force a code path (work splits, slab depths, bin chunk sizes) do so through the
+# library's TVAM_* tuning knobs, which it honours only under TVAM_EXPERIMENTAL=1 (tvam_knob, read at
+# plan creation): each such test sets both with monkeypatch (the `knobs` fixture); every other test
+# runs the production defaults.
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
@@ -32,3 +33,13 @@ def oracle():
     from oracle import oracle as orc
     orc.build()
     return orc
+
+
+@pytest.fixture
+def knobs(monkeypatch):
+    """knobs(NAME=value, ...): set tuning knobs for this test, with TVAM_EXPERIMENTAL=1."""
+    def set_(**kv):
+        monkeypatch.setenv("TVAM_EXPERIMENTAL", "1")
+        for k, v in kv.items():
+            monkeypatch.setenv(k, str(v))
+    return set_

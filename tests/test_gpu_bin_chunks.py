@@ -145,6 +145,7 @@ def test_config4_all_angles(full4):
 def test_config4_shard_many_chunks(shard4, monkeypatch):
     """(ii): the same shard in >= 8 chunks (forward, cached forward and adjoint)."""
     s, proj = shard4, shard4["proj"]
+    monkeypatch.setenv("TVAM_EXPERIMENTAL", "1")
     monkeypatch.setenv("TVAM_BIN_CHUNK_SLOTS", str(1 << 24))
     (p1, ref1), (p2, ref2) = s["pats"]
     got = proj.forward(_dense(s, p1), None, SPP4, SEED4).cpu().numpy()[..., 0]

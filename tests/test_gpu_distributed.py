@@ -66,6 +66,7 @@ def _run(rank, world, steps, shard):
 
 def _worker(rank, world, port, steps, shard, q):
     if shard == "angle_scatter":
+        os.environ["TVAM_EXPERIMENTAL"] = "1"
         os.environ["TVAM_BIN_CHUNK_SLOTS"] = str(SCATTER_CHUNK_SLOTS)
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)

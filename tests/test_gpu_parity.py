@@ -113,6 +113,7 @@ def test_work_splits_match_oracle(oracle, monkeypatch, parts, split, fz, az, nt)
     ray-list splits of the planar adjoint, every forward slab depth Z, the adjoint's
     slices per workgroup and its workgroup size give the oracle's results (the plan
     picks them from the slab depth; forced here)."""
+    monkeypatch.setenv("TVAM_EXPERIMENTAL", "1")
     monkeypatch.setenv("TVAM_FWD_PARTS", str(parts))
     monkeypatch.setenv("TVAM_ADJ_SPLIT", str(split))
     monkeypatch.setenv("TVAM_PLANAR_FWD_Z", str(fz))
@@ -137,6 +138,7 @@ def test_work_splits_match_oracle(oracle, monkeypatch, parts, split, fz, az, nt)
 def test_forward_direct_staging_matches_oracle(oracle, monkeypatch, case):
     """The voxel-driven forward staging its windows from the [row][col] patterns directly
     (TVAM_FWD_BIN=0) instead of the slice-binned copy: same results."""
+    monkeypatch.setenv("TVAM_EXPERIMENTAL", "1")
     monkeypatch.setenv("TVAM_FWD_BIN", "0")
     d = make(**case)
     n = d.n_patterns * d.crop_y * d.crop_x
@@ -294,6 +296,7 @@ def test_deep_slab_forward(oracle, monkeypatch, Z):
     """The deep-slab voxel-driven forward (Z = 40 / 52 slices per workgroup, binned staging; the
     plan picks 52 for the 50-slice slabs of 8 z-slab ranks) against the oracle, including a
     partial last chunk (60 slices)."""
+    monkeypatch.setenv("TVAM_EXPERIMENTAL", "1")
     monkeypatch.setenv("TVAM_PLANAR_FWD_Z", str(Z))
     d = make(N=60, A=30)
     n = d.n_patterns * d.crop_y * d.crop_x

@@ -31,7 +31,7 @@ def _run(parts, N, steps=5, scene=benchy_index_matched):
 def test_pipelined_direction_matches(N, parts, scene, monkeypatch):
     # band edges fall on multiples of the forward's and the adjoint's slice chunks: the default
     # 52-slice forward chunks leave these small films no common multiple, so the bands run at 32
-    # (TVAM_EXPERIMENTAL is on for the tests, tests/conftest.py)
+    monkeypatch.setenv("TVAM_EXPERIMENTAL", "1")
     monkeypatch.setenv("TVAM_PLANAR_FWD_Z", "32")
     ref, loss0, x0 = _run(1, N, scene=scene)
     assert ref.opt.pipeline is None  # (the default: off)
@@ -77,6 +77,7 @@ def test_adjoint_slices_assemble_the_adjoint(adjl_z, monkeypatch):
     list adjoint's 16-slice workgroups on a film whose slab chunks are counted in 8-slice chunks
     (tvam_launch_adj_lists converts them)."""
     if adjl_z is not None:
+        monkeypatch.setenv("TVAM_EXPERIMENTAL", "1")
         monkeypatch.setenv("TVAM_ADJL_Z", adjl_z)
     cfg = benchy_index_matched(N=128, angles=12)
     cfg["direction_parts"] = 2
@@ -106,6 +107,7 @@ def test_list_adjoint_matches_the_tile_adjoint(monkeypatch):
         g = torch.rand((N, N, N), device="cuda", generator=torch.Generator(device="cuda").manual_seed(3)) - 0.5
         out = []
         for lists in ("1", "0"):
+            monkeypatch.setenv("TVAM_EXPERIMENTAL", "1")
             monkeypatch.setenv("TVAM_ADJ_LISTS", lists)
             p = Projection(d, "cuda:0")
             try:

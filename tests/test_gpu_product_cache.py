@@ -15,7 +15,9 @@ def test_scattering_line_search_forward_served_from_the_bin_cache(monkeypatch):
     from drtvam_amd.configs import cylindrical_scattering
     from drtvam_amd.optimize import TvamProblem
 
-    monkeypatch.setenv("TVAM_BIN_CHUNK_SLOTS", "12000")  # several chunks (tests run under TVAM_EXPERIMENTAL=1)
+    monkeypatch.setenv("TVAM_EXPERIMENTAL", "1")
+
+    monkeypatch.setenv("TVAM_BIN_CHUNK_SLOTS", "12000")  # several chunks
     cfg = cylindrical_scattering(N=24, angles=12, spp=4)
     assert "flags" not in cfg
     prob = TvamProblem(cfg, device=torch.device("cuda", 0))

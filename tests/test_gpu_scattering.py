@@ -155,6 +155,7 @@ def test_forward_bin_cache(monkeypatch, chunk_slots):
     """A second forward of the same seed reuses the cached brick bins (records rescaled to the new
     pattern): bit-identical to an uncached plan, for the cached seed, a new pattern and a new seed."""
     if chunk_slots:
+        monkeypatch.setenv("TVAM_EXPERIMENTAL", "1")
         monkeypatch.setenv("TVAM_BIN_CHUNK_SLOTS", chunk_slots)
     import gc
     gc.collect()  # plans of earlier tests (their bin caches) and torch's cached blocks: the cache
@@ -175,6 +176,7 @@ def test_forward_bin_cache(monkeypatch, chunk_slots):
     st = cached.bin_stats()
     assert st["cached"] == st["chunks"] >= 1, st
     print("bin stats", st)
+    monkeypatch.setenv("TVAM_EXPERIMENTAL", "1")
     monkeypatch.setenv("TVAM_BIN_CACHE", "0")
     plain = Projection(d, "cuda:0")
     want = [plain.forward(p1, None, 2, 3), plain.forward(p2, None, 2, 3), plain.forward(p1, None, 2, 3),

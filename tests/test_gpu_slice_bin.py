@@ -36,7 +36,7 @@ def test_vec4_binning_bit_identical(tmp_path, scene, N, rows):
     outs = []
     for knob in ("0", "1"):
         f = str(tmp_path / f"f{knob}.npy")
-        env = dict(os.environ, TVAM_SLICE_BIN1=knob)
+        env = dict(os.environ, TVAM_SLICE_BIN1=knob, TVAM_EXPERIMENTAL="1")
         r = subprocess.run([sys.executable, "-c", CHILD, ROOT, scene, str(N), str(rows), f], env=env,
                            capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-2000:]
