@@ -635,10 +635,11 @@ static int fwd_buffers(tvam_plan* p) {
 // Slices per workgroup of the voxel-driven forward: the fewest padded slice-passes
 // ceil(nz / Z) * (Z + 12) (the +12 prices the per-angle candidate geometry and staging shared by
 // the Z slices), register-staged depths (windows the LDS-DMA staging cannot take) priced 25 %
-// higher, among the depths whose staging fits.  With the DMA staging, Z = 60 on 400-slice films
-// (7 chunks, 504 slice-passes against 512 at Z = 52; measured 2.55-2.58 against 2.59-2.60 ms,
-// profiles/r06/ab_fwd/; round 5: Z = 52 2.68, 40 2.72, 32 2.81 ms, profiles/r05/fwd_depth/), and on
-// the <= 60-slice slabs of 8 ranks (one chunk).  Returns false when none fits.
+// higher, among the depths whose staging fits.  With the DMA staging, Z = 52 on 400-slice films
+// (8 chunks; Z = 60, 7 chunks, measured a tie: kernel 2294 against 2306 us, its 420-slice binning
+// 110 against 93 us, profiles/r06/; round 5: Z = 52 2.68, 40 2.72, 32 2.81 ms, profiles/r05/fwd_depth/),
+// and Z = 60 only on films of <= 60 slices (the slabs of 8 ranks: one chunk).  Returns false when
+// none fits.
 static int choose_fwd_z(tvam_plan* p) {
     const TvamConsts& k = p->k;
     if (p->planar_fz == 0) {
@@ -647,6 +648,7 @@ static int choose_fwd_z(tvam_plan* p) {
         const bool deep = env_int("TVAM_FWD_BIN", 1) != 0;
         for (int Z : {60, 52, 40, 32, 28, 24, 16, 8}) {
             if ((Z > 32 && !deep) || !tvam_planar_fwd_fits(p->pl, Z)) continue;
+            if (Z == 60 && k.nz > 60) continue;  // one-chunk slabs only (400 slices: a tie with 52, binning +15 %)
             const int64_t cost =
                 (int64_t)((k.nz + Z - 1) / Z) * (Z + 12) * (deep && tvam_planar_fwd_dma_window(p->pl, Z) ? 4 : 5);
             if (cost < bcost) bcost = cost, best = Z;
