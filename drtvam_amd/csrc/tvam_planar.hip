@@ -141,6 +141,9 @@ __device__ __forceinline__ void tvam_lds_dma16(const void* g, void* l) {
 }
 // a staged column outside the crop: no chord ({q, t_end < 0}; refracted: the second record zero)
 __device__ float4 tvam_null_rec[2] = {{0.0f, 0.0f, -1.0f, 0.0f}, {0.0f, 0.0f, 0.0f, 0.0f}};
+// super-block edge (tiles) of the forward's workgroup order: 5 x 5 (2.39-2.42 -> 2.36 ms on config 2;
+// 8 x 8 2.36-2.43, 12 x 12 2.43-2.45; profiles/r06/ab_fwd/)
+#define TVAM_FWD_SB 5
 #define TVAM_ACH 64  // angles per LDS chunk of per-angle constants (paths without the SGPR constants)
 
 // Z: slices per thread; NC: candidate DMD columns per (voxel, angle), a
@@ -197,8 +200,26 @@ __global__ __launch_bounds__(TVAM_PB) void tvam_fwd_planar_kernel(TvamConsts k, 
     const int part = L / nwg1;
     L -= part * nwg1;
     const int ab = (int)(((int64_t)pl.ns * part) / parts), ae = (int)(((int64_t)pl.ns * (part + 1)) / parts);
-    const int tile = L % ntiles;
-    const int bx = tile % ntx, by = tile / ntx;
+    // tiles in super-blocks of SB x SB (row-major blocks, row-major inside): the ~128 workgroups of a
+    // z-chunk resident on one XCD cover a square of tiles, which rays of every angle cross several
+    // tiles deep, so a staged column's slab is re-read from that XCD's L2 (a band of tile rows
+    // shares it only along rays near the x axis)
+    int bx, by;
+    {
+        const int t = L % ntiles;
+        constexpr int SB = TVAM_FWD_SB;
+        if (SB > 1) {
+            const int sr = t / (ntx * SB), h = min(SB, nty - sr * SB);
+            const int r2 = t - sr * ntx * SB, bc = r2 / (SB * h), w = min(SB, ntx - bc * SB);
+            const int r3 = r2 - bc * SB * h;
+            by = sr * SB + r3 / w;
+            bx = bc * SB + r3 % w;
+        } else {
+            bx = t % ntx;
+            by = t / ntx;
+        }
+    }
+    const int tile = by * ntx + bx;
     const int ix = bx * 16 + (threadIdx.x & 15), iy = by * 16 + (threadIdx.x >> 4);
     const int z0 = ((pl.fwd_nzc > 0 ? pl.fwd_zc0 : 0) + L / ntiles) * Z;
     const float hx = k.h[0], hy = k.h[1];
