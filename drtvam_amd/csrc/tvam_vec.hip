@@ -19,6 +19,7 @@
 #define TVAM_VB 256       // threads per block
 #define TVAM_VGRID_MAX 2048  // most blocks of the reduction kernels (work[] holds grid * ndots doubles)
 #define TVAM_HMAX 8
+#define TVAM_VU 1  // grid-stride elements per loop trip (2 and 4: no faster, profiles/r06/vec/)
 
 #include <algorithm>
 #include <cstdlib>
@@ -35,6 +36,14 @@ static int hist_grid() {
 static int dir_grid() {
     static const int g = vec_knob("TVAM_VEC_DGRID", 1024);
     return g;
+}
+
+// a streamed float4, loaded non-temporal: every pass reads a history vector once, gigabytes before the
+// next pass reads it again (direction pass 0.75 -> 0.65 ms at config 2's size, profiles/r06/vec/)
+__device__ __forceinline__ float4 vld(const float* p, uint64_t i) {
+    typedef float vf4 __attribute__((ext_vector_type(4)));
+    const vf4 v = __builtin_nontemporal_load(reinterpret_cast<const vf4*>(p) + i);
+    return make_float4(v.x, v.y, v.z, v.w);
 }
 
 struct VecPtrs {
@@ -126,34 +135,51 @@ __global__ __launch_bounds__(TVAM_VB) void tvam_lbfgs_hist_kernel(uint64_t n, co
 
     const uint64_t n4 = n / 4, stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (uint64_t t = tid; t < n4; t += stride) {
-        const uint64_t i = SEG ? vec_seg_index(sg, t) : t;
-        const float4 g4 = reinterpret_cast<const float4*>(g)[i];
-        float4 p4 = make_float4(0, 0, 0, 0), po4 = p4, go4 = p4;
-        if (NEW) {
-            p4 = reinterpret_cast<const float4*>(p)[i];
-            po4 = reinterpret_cast<const float4*>(p_old)[i];
-            go4 = reinterpret_cast<const float4*>(g_old)[i];
-        }
-        float4 s4[TVAM_HMAX], y4[TVAM_HMAX];
+    // VU grid-stride elements per trip, all their loads issued before the first is summed (more bytes
+    // in flight per wave); each thread still sums its elements in grid-stride order (the same dots)
+    struct El {
+        float4 g4, p4, po4, go4, s4[H > 0 ? H : 1], y4[H > 0 ? H : 1];
+    };
+    for (uint64_t t0 = tid; t0 < n4; t0 += (uint64_t)TVAM_VU * stride) {
+        El el[TVAM_VU];
 #pragma unroll
-        for (int j = 0; j < H; ++j) {
-            s4[j] = reinterpret_cast<const float4*>(hv.s[j])[i];
-            y4[j] = reinterpret_cast<const float4*>(hv.y[j])[i];
+        for (int u = 0; u < TVAM_VU; ++u) {
+            const uint64_t t = t0 + (uint64_t)u * stride;
+            if (t >= n4) break;
+            const uint64_t i = SEG ? vec_seg_index(sg, t) : t;
+            el[u].g4 = vld(g, i);
+            el[u].p4 = el[u].po4 = el[u].go4 = make_float4(0, 0, 0, 0);
+            if (NEW) {
+                el[u].p4 = vld(p, i);
+                el[u].po4 = vld(p_old, i);
+                el[u].go4 = vld(g_old, i);
+            }
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                el[u].s4[j] = vld(hv.s[j], i);
+                el[u].y4[j] = vld(hv.y[j], i);
+            }
         }
-        float sv[TVAM_HMAX], yv[TVAM_HMAX];
-        float4 sn4, yn4;
+#pragma unroll
+        for (int u = 0; u < TVAM_VU; ++u) {
+            const uint64_t t = t0 + (uint64_t)u * stride;
+            if (t >= n4) break;
+            const uint64_t i = SEG ? vec_seg_index(sg, t) : t;
+            const El& e = el[u];
+            float sv[TVAM_HMAX], yv[TVAM_HMAX];
+            float4 sn4, yn4;
 #define TVAM_LANE(c)                                                    \
-        _Pragma("unroll") for (int j = 0; j < H; ++j) {                 \
-            sv[j] = s4[j].c;                                            \
-            yv[j] = y4[j].c;                                            \
-        }                                                               \
-        visit(p4.c, po4.c, g4.c, go4.c, sv, yv, sn4.c, yn4.c);
-        TVAM_LANE(x) TVAM_LANE(y) TVAM_LANE(z) TVAM_LANE(w)
+            _Pragma("unroll") for (int j = 0; j < H; ++j) {             \
+                sv[j] = e.s4[j].c;                                      \
+                yv[j] = e.y4[j].c;                                      \
+            }                                                           \
+            visit(e.p4.c, e.po4.c, e.g4.c, e.go4.c, sv, yv, sn4.c, yn4.c);
+            TVAM_LANE(x) TVAM_LANE(y) TVAM_LANE(z) TVAM_LANE(w)
 #undef TVAM_LANE
-        if (NEW) {
-            reinterpret_cast<float4*>(s_new)[i] = sn4;
-            reinterpret_cast<float4*>(y_new)[i] = yn4;
+            if (NEW) {
+                reinterpret_cast<float4*>(s_new)[i] = sn4;
+                reinterpret_cast<float4*>(y_new)[i] = yn4;
+            }
         }
     }
     for (uint64_t i = 4 * n4 + tid; !SEG && i < n; i += stride) {  // tail
@@ -263,20 +289,35 @@ __global__ __launch_bounds__(TVAM_VB) void tvam_lbfgs_dir_kernel(uint64_t n, con
     }
     const uint64_t n4 = n / 4, stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    for (uint64_t t = tid; t < n4; t += stride) {
-        const uint64_t i = SEG ? vec_seg_index(sg, t) : t;
-        const float4 g4 = reinterpret_cast<const float4*>(g)[i];
-        float4 r = make_float4(c.cg * g4.x, c.cg * g4.y, c.cg * g4.z, c.cg * g4.w);
+    for (uint64_t t0 = tid; t0 < n4; t0 += (uint64_t)TVAM_VU * stride) {
+        float4 g4[TVAM_VU], s4[TVAM_VU][H > 0 ? H : 1], y4[TVAM_VU][H > 0 ? H : 1];
 #pragma unroll
-        for (int j = 0; j < H; ++j) {
-            const float4 s4 = reinterpret_cast<const float4*>(hv.s[j])[i];
-            const float4 y4 = reinterpret_cast<const float4*>(hv.y[j])[i];
-            r.x = fmaf(c.cs[j], s4.x, fmaf(c.cy[j], y4.x, r.x));
-            r.y = fmaf(c.cs[j], s4.y, fmaf(c.cy[j], y4.y, r.y));
-            r.z = fmaf(c.cs[j], s4.z, fmaf(c.cy[j], y4.z, r.z));
-            r.w = fmaf(c.cs[j], s4.w, fmaf(c.cy[j], y4.w, r.w));
+        for (int u = 0; u < TVAM_VU; ++u) {  // every load of the trip first (bytes in flight)
+            const uint64_t t = t0 + (uint64_t)u * stride;
+            if (t >= n4) break;
+            const uint64_t i = SEG ? vec_seg_index(sg, t) : t;
+            g4[u] = vld(g, i);
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                s4[u][j] = vld(hv.s[j], i);
+                y4[u][j] = vld(hv.y[j], i);
+            }
         }
-        reinterpret_cast<float4*>(d)[i] = r;
+#pragma unroll
+        for (int u = 0; u < TVAM_VU; ++u) {
+            const uint64_t t = t0 + (uint64_t)u * stride;
+            if (t >= n4) break;
+            const uint64_t i = SEG ? vec_seg_index(sg, t) : t;
+            float4 r = make_float4(c.cg * g4[u].x, c.cg * g4[u].y, c.cg * g4[u].z, c.cg * g4[u].w);
+#pragma unroll
+            for (int j = 0; j < H; ++j) {
+                r.x = fmaf(c.cs[j], s4[u][j].x, fmaf(c.cy[j], y4[u][j].x, r.x));
+                r.y = fmaf(c.cs[j], s4[u][j].y, fmaf(c.cy[j], y4[u][j].y, r.y));
+                r.z = fmaf(c.cs[j], s4[u][j].z, fmaf(c.cy[j], y4[u][j].z, r.z));
+                r.w = fmaf(c.cs[j], s4[u][j].w, fmaf(c.cy[j], y4[u][j].w, r.w));
+            }
+            reinterpret_cast<float4*>(d)[i] = r;
+        }
     }
     for (uint64_t i = 4 * n4 + tid; !SEG && i < n; i += stride) {
         float r = c.cg * g[i];

@@ -58,7 +58,13 @@ def main():
         ms = e0.elapsed_time(e1) / reps
         res[name] = {"ms": round(ms, 4), "GB/s": round(nbytes / ms / 1e6, 1)}
     env = {k: v for k, v in os.environ.items() if k.startswith("TVAM_VEC")}
-    print(json.dumps({"env": env, **res}))
+    import hashlib
+    hist()
+    direction()
+    torch.cuda.synchronize()
+    res["dots_sha"] = hashlib.sha256(dots.cpu().numpy().tobytes()).hexdigest()[:16]
+    res["d_sha"] = hashlib.sha256(d.cpu().numpy().tobytes()).hexdigest()[:16]
+    print(json.dumps({"env": env, "lib": os.environ.get("TVAM_LIB", ""), **res}))
 
 
 if __name__ == "__main__":
