@@ -127,13 +127,13 @@ def cpu_baseline(config, N, seconds, threads, alt_threads=None):
 
 
 # Roofline of the dominant kernel, from the committed counter summary of the current build
-# (tools/pmc_bench.sh + tools/roofline_summary.py -> profiles/r03/roofline_config<K>.json): the
+# (tools/pmc_final.sh: tools/pmc_bench.sh + tools/roofline_summary.py -> profiles/r06/roofline_config<K>.json): the
 # binding resource's bytes per launch (LDS-array cycles x 256 B, or HBM FETCH x 2 + WRITE) over
 # the kernel's average launch time measured live in the timed iterations (HIP events around each
 # launch on its stream, tvam_plan_kernel_time), against the 2.4 GHz spec peak (LDS 157.3 TB/s,
 # HBM 8 TB/s; MI355X_MICROARCH.md).  The counter run's own launch time and fraction stay beside
 # them, and every counter field can be recomputed from that one file.
-ROOFLINE_DIR = os.path.join(ROOT, "profiles", "r05")
+ROOFLINE_DIR = os.path.join(ROOT, "profiles", "r06")
 
 
 def csrc_digest():

@@ -1,6 +1,6 @@
 #!/usr/bin/env bash
 # Counters of one BASELINE config's bench iteration for the committed roofline summaries
-# (tools/roofline_summary.py -> profiles/r05/roofline_config<K>.json, read by bench.py):
+# (tools/roofline_summary.py -> profiles/r06/roofline_config<K>.json, read by bench.py; tools/pmc_final.sh):
 # one rocprofv3 --pmc pass per counter set (never combined with tracing, each within the
 # per-block limits), then a --kernel-trace --stats pass of the same command.
 # usage (GPU box, repo root): tools/pmc_bench.sh OUT CONFIG [N]
