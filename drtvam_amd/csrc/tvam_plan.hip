@@ -105,6 +105,8 @@ struct tvam_plan {
     float* d_fscale = nullptr;
     int32_t planar_rz = 4;
     TvamAdjListBufs adjl;  // planar adjoint: slice-invariant visit lists (tvam_adjlist.hip)
+    bool adjl_pending = false;  // the lists are to be built by the first adjoint call
+    int adjl_parts = 1;
     TvamBinScratch bins;  // scattering media: brick-binned forward scratch
     std::vector<float4> fwd_ang_h;  // host staging of the forward tables (plan creation only)
     std::vector<int32_t> fwd_cb_h;
@@ -452,7 +454,7 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     const int az_knob = env_int("TVAM_PLANAR_ADJ_Z", 0);
     p->planar_az = az_knob == 4 || k.nz < 8 ? 4 : 8;
     if (p->planar_fz != 8 && p->planar_fz != 16 && p->planar_fz != 24 && p->planar_fz != 28 && p->planar_fz != 32 &&
-        p->planar_fz != 40 && p->planar_fz != 52 && p->planar_fz != 60)
+        p->planar_fz != 40 && p->planar_fz != 48 && p->planar_fz != 52 && p->planar_fz != 60)
         p->planar_fz = 0;
     const int ns = (int)cs.size();
     int32_t mrc = 0;
@@ -563,24 +565,15 @@ static int planar_setup(tvam_plan* p, const std::vector<float2>& cs) {
     // Groups = (tile, step quadrant, part), parts until the grid holds >= 8K workgroups.
     p->pl.adjl_ngroups = 0;
     if (p->planar_az == 8 && ns > 0 && env_int("TVAM_ADJ_LISTS", 1)) {
-        size_t fr = 0, tot = 0;
-        if ((e = hipMemGetInfo(&fr, &tot)) != hipSuccess) return hip_fail(e, "hipMemGetInfo");
         // 16 slices per workgroup (one per CU) on deep films, 8 (two per CU) on thin ones: the
         // 50-slice slabs of 8 ranks ran 0.68 ms at 16 (four chunks, the last 2 slices deep) and
         // 0.47 ms at 8; 400 slices 3.20 ms at 16, 3.29 at 8 (profiles/r05/slab_adjoint_z/)
         p->pl.adjl_z = env_int("TVAM_ADJL_Z", az_knob == 8 || k.nz < 256 ? 8 : 16) == 8 ? 8 : 16;
         const int64_t nwg4 = (int64_t)p->tiles.ntx * p->tiles.nty * 4 * ((k.nz + p->pl.adjl_z - 1) / p->pl.adjl_z);
-        const int parts = (int)std::min<int64_t>(4, std::max<int64_t>(1, (4096 + nwg4 - 1) / std::max<int64_t>(nwg4, 1)));
-        e = tvam_build_adj_lists(k, p->pl, p->tiles, parts, fr / 4, p->adjl, nullptr);
-        // 16 slices per workgroup where the tile's 4 planes fit in LDS (the weights are the same)
-        if (e == hipSuccess && p->pl.adjl_z == 16 && tvam_adjl_lds(p->pl, p->tiles, 16) > 160 * 1024) p->pl.adjl_z = 8;
-        if (e == hipSuccess && tvam_adjl_lds(p->pl, p->tiles, p->pl.adjl_z) > 160 * 1024) e = hipErrorOutOfMemory;
-        if (e != hipSuccess) {
-            adjl_free(p->adjl);
-            p->pl.adjl_ngroups = 0;
-            if (e != hipErrorOutOfMemory) return hip_fail(e, "adjoint visit lists");
-            (void)hipGetLastError();
-        }
+        // built by the first adjoint call (ensure_adj_lists): a forward-only plan (final_render) never
+        // pays for them
+        p->adjl_parts = (int)std::min<int64_t>(4, std::max<int64_t>(1, (4096 + nwg4 - 1) / std::max<int64_t>(nwg4, 1)));
+        p->adjl_pending = true;
     }
     p->planar = true;
     return 0;
@@ -638,15 +631,15 @@ static int fwd_buffers(tvam_plan* p) {
 // higher, among the depths whose staging fits.  With the DMA staging, Z = 52 on 400-slice films
 // (8 chunks; Z = 60, 7 chunks, measured a tie: kernel 2294 against 2306 us, its 420-slice binning
 // 110 against 93 us, profiles/r06/; round 5: Z = 52 2.68, 40 2.72, 32 2.81 ms, profiles/r05/fwd_depth/),
-// and Z = 60 only on films of <= 60 slices (the slabs of 8 ranks: one chunk).  Returns false when
-// none fits.
+// and Z = 60 / 48 on films of <= 60 / 48 slices (the slabs of 8 ranks, 48-57 slices: one chunk).
+// Returns false when none fits.
 static int choose_fwd_z(tvam_plan* p) {
     const TvamConsts& k = p->k;
     if (p->planar_fz == 0) {
         int best = 8;
         int64_t bcost = INT64_MAX;
         const bool deep = env_int("TVAM_FWD_BIN", 1) != 0;
-        for (int Z : {60, 52, 40, 32, 28, 24, 16, 8}) {
+        for (int Z : {60, 52, 48, 40, 32, 28, 24, 16, 8}) {
             if ((Z > 32 && !deep) || !tvam_planar_fwd_fits(p->pl, Z)) continue;
             if (Z == 60 && k.nz > 60) continue;  // one-chunk slabs only (400 slices: a tie with 52, binning +15 %)
             const int64_t cost =
@@ -655,7 +648,7 @@ static int choose_fwd_z(tvam_plan* p) {
         }
         p->planar_fz = best;
     }
-    for (int Z : {60, 52, 40, 32, 28, 24, 16, 8})  // the deepest instantiated depth <= the choice that fits
+    for (int Z : {60, 52, 48, 40, 32, 28, 24, 16, 8})  // the deepest instantiated depth <= the choice that fits
         if (Z <= p->planar_fz && tvam_planar_fwd_fits(p->pl, Z)) {
             p->planar_fz = Z;
             break;
@@ -1679,6 +1672,28 @@ static int forward_impl(tvam_plan* p, const float* active_data, const uint32_t* 
 // angle of grad_active (dense crop order; those rows zeroed first, the others untouched): the caller's rows
 // are exactly the rows whose rays lie in those slices (tvam_row_slices), so the rows hold their whole
 // gradient.  Regular-sampling planar plans of a dense set; slices on the adjoint's Z-slice chunks.
+// The planar adjoint's visit lists, built at the plan's first adjoint call when they fit in a
+// quarter of the free device memory (else the tile adjoint serves).  16 slices per workgroup where
+// the tile's 4 planes fit in LDS, else 8 (the weights are the same; the adjoint's chunk reported
+// before the build, max(8, adjl_z), stays a multiple of the one the kernel then runs).
+static int ensure_adj_lists(tvam_plan* p) {
+    if (!p->adjl_pending) return 0;
+    p->adjl_pending = false;
+    size_t fr = 0, tot = 0;
+    hipError_t e = hipMemGetInfo(&fr, &tot);
+    if (e != hipSuccess) return hip_fail(e, "hipMemGetInfo");
+    e = tvam_build_adj_lists(p->k, p->pl, p->tiles, p->adjl_parts, fr / 4, p->adjl, nullptr);
+    if (e == hipSuccess && p->pl.adjl_z == 16 && tvam_adjl_lds(p->pl, p->tiles, 16) > 160 * 1024) p->pl.adjl_z = 8;
+    if (e == hipSuccess && tvam_adjl_lds(p->pl, p->tiles, p->pl.adjl_z) > 160 * 1024) e = hipErrorOutOfMemory;
+    if (e != hipSuccess) {
+        adjl_free(p->adjl);
+        p->pl.adjl_ngroups = 0;
+        if (e != hipErrorOutOfMemory) return hip_fail(e, "adjoint visit lists");
+        (void)hipGetLastError();
+    }
+    return 0;
+}
+
 extern "C" int tvam_adjoint_slices(tvam_plan* p, const float* grad_dose, uint64_t n_active, int32_t z_begin,
                                    int32_t z_end, int32_t row_begin, int32_t row_end, float* grad_active,
                                    void* stream_) {
@@ -1690,7 +1705,9 @@ extern "C" int tvam_adjoint_slices(tvam_plan* p, const float* grad_dose, uint64_
     uint32_t spp = 1;
     int rc = call_setup(p, n_active, nullptr, spp, k);
     if (rc) return rc;
-    const int Z = p->pl.adjl_ngroups > 0 ? std::max(p->planar_az, p->pl.adjl_z) : p->planar_az, nz = k.nz;
+    const int Z = p->pl.adjl_ngroups > 0 || p->adjl_pending ? std::max(p->planar_az, p->pl.adjl_z) : p->planar_az,
+              nz = k.nz;
+    if ((rc = ensure_adj_lists(p))) return rc;
     const int64_t R = k.crop_y, C = k.crop_x, A = (int64_t)p->tiles.n_shard;
     if (z_begin < 0 || z_end > nz || z_begin >= z_end || z_begin % Z != 0 || (z_end % Z != 0 && z_end != nz) ||
         row_begin < 0 || row_end > R || row_begin > row_end || (int64_t)n_active != A * R * C)
@@ -1709,7 +1726,7 @@ extern "C" int tvam_adjoint_slices(tvam_plan* p, const float* grad_dose, uint64_
 
 extern "C" int tvam_plan_adj_chunk(const tvam_plan* p) {
     if (!p || !p->planar || p->general || p->surface || p->desc.albedo != 0.0f) return 0;
-    return p->pl.adjl_ngroups > 0 ? std::max(p->planar_az, p->pl.adjl_z) : p->planar_az;
+    return p->pl.adjl_ngroups > 0 || p->adjl_pending ? std::max(p->planar_az, p->pl.adjl_z) : p->planar_az;
 }
 
 extern "C" int tvam_adjoint(tvam_plan* p, const float* grad_dose, const uint32_t* active_pixels, uint64_t n_active,
@@ -1733,6 +1750,7 @@ extern "C" int tvam_adjoint(tvam_plan* p, const float* grad_dose, const uint32_t
             return hip_fail(e, "scatter launch");
         idxmap = p->d_idxmap;
     }
+    if ((rc = ensure_adj_lists(p))) return rc;
     if ((e = hipMemsetAsync(grad_active, 0, n_active * sizeof(float), stream)) != hipSuccess)
         return hip_fail(e, "hipMemsetAsync");
     if (p->general) {

@@ -1051,6 +1051,7 @@ static hipError_t tvam_launch_fwd_planar_z(dim3 grid, size_t lds, hipStream_t st
         case 28: return launch_fwd_z<28>(grid, lds, stream, k, pl, pat, dose);
         case 32: return launch_fwd_z<32>(grid, lds, stream, k, pl, pat, dose);
         case 40: return pl.fwd_bin ? launch_fwd_z<40>(grid, lds, stream, k, pl, pat, dose) : hipErrorInvalidValue;
+        case 48: return pl.fwd_bin ? launch_fwd_z<48>(grid, lds, stream, k, pl, pat, dose) : hipErrorInvalidValue;
         case 52: return pl.fwd_bin ? launch_fwd_z<52>(grid, lds, stream, k, pl, pat, dose) : hipErrorInvalidValue;
         case 60: return pl.fwd_bin ? launch_fwd_z<60>(grid, lds, stream, k, pl, pat, dose) : hipErrorInvalidValue;
         default: return hipErrorInvalidValue;

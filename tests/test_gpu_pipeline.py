@@ -116,3 +116,33 @@ def test_list_adjoint_matches_the_tile_adjoint(monkeypatch):
             finally:
                 p.close()
         torch.testing.assert_close(out[0], out[1], rtol=1e-5, atol=1e-6 * float(out[1].abs().max()))
+
+
+def test_adjoint_lists_are_built_by_the_first_adjoint():
+    """the planar adjoint's visit lists are built by a plan's first adjoint call, not at
+    plan creation, so a forward-only plan (final_render) never allocates them; the adjoint's
+    reported slice chunk is the same before and after the build, and the result is the oracle's
+    (the list adjoint path of the other tests)."""
+    from drtvam_amd.configs import desc_from_config
+    from drtvam_amd.engine import Projection
+    N = 160
+    d = desc_from_config(benchy_index_matched(N=N, angles=N))
+    n = N * int(d.crop_x) * int(d.crop_y)
+    torch.cuda.synchronize()
+    p = Projection(d, "cuda:0")
+    try:
+        chunk0 = p.adj_chunk()
+        x = torch.rand(n, device="cuda")
+        p.forward(x, None, 1, 0)
+        torch.cuda.synchronize()
+        free0 = torch.cuda.mem_get_info()[0]
+        g = torch.rand((N, N, N), device="cuda")
+        free_g = torch.cuda.mem_get_info()[0]
+        p.adjoint(g, n, None, 1, 0)
+        torch.cuda.synchronize()
+        free1 = torch.cuda.mem_get_info()[0]
+        lists = (free_g - free1) - n * 4  # device bytes the first adjoint added besides its output
+        assert lists > 4 << 20, (free0, free_g, free1)
+        assert p.adj_chunk() == chunk0
+    finally:
+        p.close()
