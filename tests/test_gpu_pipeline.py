@@ -131,7 +131,7 @@ def test_adjoint_lists_are_built_by_the_first_adjoint():
     torch.cuda.synchronize()
     p = Projection(d, "cuda:0")
     try:
-        chunk0 = p.adj_chunk()
+        chunk0 = p.adj_chunk
         x = torch.rand(n, device="cuda")
         p.forward(x, None, 1, 0)
         torch.cuda.synchronize()
@@ -143,6 +143,6 @@ def test_adjoint_lists_are_built_by_the_first_adjoint():
         free1 = torch.cuda.mem_get_info()[0]
         lists = (free_g - free1) - n * 4  # device bytes the first adjoint added besides its output
         assert lists > 4 << 20, (free0, free_g, free1)
-        assert p.adj_chunk() == chunk0
+        assert p.adj_chunk == chunk0
     finally:
         p.close()
