@@ -12,7 +12,7 @@ import threading
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("TVAM_LIB") or os.path.join(_HERE, "libtvam.so")  # TVAM_LIB: a variant build
 
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 TVAM_OK = 0
 TVAM_ERR_INVALID = -1
@@ -145,6 +145,9 @@ EXPORTS = {
     "tvam_lbfgs_direction_rows": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _P,
                                                  ctypes.c_int32, _P, _P, _P, _P, _P]),
     "tvam_axpy_clamp": (ctypes.c_int, [ctypes.c_uint64, _P, ctypes.c_float, _P, ctypes.c_float, _P, _P]),
+    "tvam_axpy_clamp_dev": (ctypes.c_int, [ctypes.c_uint64, _P, _P, _P, ctypes.c_float, _P, _P]),
+    "tvam_lbfgs_armijo": (ctypes.c_int, [ctypes.c_int32, ctypes.c_double, _P, _P, ctypes.c_double, ctypes.c_double,
+                                         _P, ctypes.c_double, _P, _P, _P]),
     "tvam_row_slices": (ctypes.c_int, [ctypes.POINTER(TvamDesc), _P]),
     "tvam_plan_path": (ctypes.c_int, [_P]),
     "tvam_adjoint_slices": (ctypes.c_int, [_P, _P, ctypes.c_uint64, ctypes.c_int32, ctypes.c_int32, ctypes.c_int32,
@@ -171,6 +174,17 @@ EXPORTS = {
         ctypes.c_int,
         [_P, _P, _P, ctypes.c_int32, _P, ctypes.c_uint64, ctypes.c_int32, ctypes.c_float, ctypes.c_float,
          ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, _P],
+    ),
+    "tvam_target_mask": (ctypes.c_int, [_P, ctypes.c_uint64, _P, _P]),
+    "tvam_loss_threshold_mask": (
+        ctypes.c_int,
+        [_P, _P, ctypes.c_float, _P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int32, ctypes.c_float, ctypes.c_float,
+         ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, _P, _P],
+    ),
+    "tvam_loss_threshold_probes_mask": (
+        ctypes.c_int,
+        [_P, _P, _P, ctypes.c_int32, _P, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_int32, ctypes.c_float,
+         ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, ctypes.c_float, _P, _P],
     ),
     "tvam_last_error": (ctypes.c_char_p, []),
     "tvam_abi_version": (ctypes.c_int, []),

@@ -293,13 +293,16 @@ hipError_t tvam_launch_gather(const TvamConsts& k, const float* dense, const uin
                               uint64_t n, float* out, hipStream_t stream);
 
 #define TVAM_MAX_PROBES 8
+// target: f32 (> 0 = object), or mask != nullptr: its bit mask (tvam_launch_target_mask) read from bit mbit0
 hipError_t tvam_launch_loss_probes(const float* dose, const float* ddose, const float* alphas, int na,
-                                   const float* target, uint64_t n, int K, float tl, float tu, float w_object,
-                                   float w_void, float w_limit, float scale, double* out, hipStream_t stream);
-hipError_t tvam_launch_loss_threshold(const float* dose, const float* ddose, float alpha,
-                                      const float* target, uint64_t n, int K, float tl, float tu,
-                                      float w_object, float w_void, float w_limit, float scale,
-                                      double* out, float* grad, hipStream_t stream);
+                                   const float* target, const uint32_t* mask, uint64_t mbit0, uint64_t n, int K,
+                                   float tl, float tu, float w_object, float w_void, float w_limit, float scale,
+                                   double* out, hipStream_t stream);
+hipError_t tvam_launch_loss_threshold(const float* dose, const float* ddose, float alpha, const float* target,
+                                      const uint32_t* mask, uint64_t mbit0, uint64_t n, int K, float tl, float tu,
+                                      float w_object, float w_void, float w_limit, float scale, double* out,
+                                      float* grad, hipStream_t stream);
+hipError_t tvam_launch_target_mask(const float* target, uint64_t n, uint32_t* mask, hipStream_t stream);
 
 // Fused L-BFGS vector kernels (tvam_vec.hip).
 hipError_t tvam_launch_lbfgs_history(uint64_t n, const float* p, const float* p_old, const float* g,
@@ -317,4 +320,7 @@ hipError_t tvam_launch_lbfgs_direction_dev(uint64_t n, const float* g, int h, co
                                            uint64_t nseg = 0, uint64_t seg_len = 0, uint64_t seg_stride = 0,
                                            uint64_t seg_off = 0);
 hipError_t tvam_launch_axpy_clamp(uint64_t n, const float* p, float alpha, const float* d, float lo, float* out,
-                                  hipStream_t stream);
+                                  hipStream_t stream, const float* alpha_dev = nullptr);
+hipError_t tvam_launch_armijo(int nprobe, double a0, const double* probes, const double* loss_dev, double loss_host,
+                              double loss_div, const double* gdz, double c1, float* alpha, double* report,
+                              hipStream_t stream);

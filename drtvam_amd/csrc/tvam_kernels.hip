@@ -741,30 +741,100 @@ __device__ __forceinline__ float tvam_powi(float x, int K) {
     return r;
 }
 
+// The object test of a voxel: target > 0 (loss.py:119), from the f32 target or from its bit mask
+// (tvam_target_mask: bit i of word i / 32 = target[i] > 0, read at bit offset mbit0 + i): the same
+// predicate from 1/32 of the bytes.
+template <bool MASK>
+__device__ __forceinline__ bool tvam_is_obj(const float* __restrict__ target, const uint32_t* __restrict__ mask,
+                                            uint64_t mbit0, uint64_t i) {
+    if (MASK) {
+        const uint64_t b = mbit0 + i;
+        return (mask[b >> 5] >> (b & 31)) & 1u;
+    }
+    return target[i] > 0.0f;
+}
+
+// four consecutive voxels' object bits (bit j = voxel i + j); i = 4 t, mbit0 % 4 == 0 on the float4 path of a mask
+template <bool MASK>
+__device__ __forceinline__ uint32_t tvam_obj4(const float* __restrict__ target, const uint32_t* __restrict__ mask,
+                                              uint64_t mbit0, uint64_t t) {
+    if (MASK) {
+        const uint64_t b = mbit0 + 4 * t;
+        return (mask[b >> 5] >> (b & 31)) & 15u;
+    }
+    const float4 tg = reinterpret_cast<const float4*>(target)[t];
+    return (tg.x > 0.0f ? 1u : 0u) | (tg.y > 0.0f ? 2u : 0u) | (tg.z > 0.0f ? 4u : 0u) | (tg.w > 0.0f ? 8u : 0u);
+}
+
+__global__ __launch_bounds__(256) void tvam_target_mask_kernel(const float* __restrict__ target, uint64_t n,
+                                                               uint32_t* __restrict__ mask) {
+    // one word per thread: 32 voxels, the last word's bits past n are 0
+    const uint64_t nw = (n + 31) / 32, stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t w = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; w < nw; w += stride) {
+        uint32_t m = 0;
+        for (int j = 0; j < 32; ++j) {
+            const uint64_t i = 32 * w + j;
+            if (i < n && target[i] > 0.0f) m |= 1u << j;
+        }
+        mask[w] = m;
+    }
+}
+
+hipError_t tvam_launch_target_mask(const float* target, uint64_t n, uint32_t* mask, hipStream_t stream) {
+    const uint64_t nw = (n + 31) / 32;
+    unsigned g = (unsigned)((nw + 255) / 256);
+    if (g > 4096) g = 4096;
+    if (g == 0) g = 1;
+    hipLaunchKernelGGL(tvam_target_mask_kernel, dim3(g), dim3(256), 0, stream, target, n, mask);
+    return hipGetLastError();
+}
+
+__device__ __forceinline__ float tvam_loss_grad_elem(float x, bool obj, int K, float tl, float tu, float w_object,
+                                                     float w_void, float w_limit, float& gr) {
+    if (obj) {
+        const float zo = tu - x, zl = x - 1.0f;
+        const float ro = zo > 0.0f ? zo : 0.0f, rl = zl > 0.0f ? zl : 0.0f;
+        gr = (zo > 0.0f ? -w_object * (float)K * tvam_powi(ro, K - 1) : 0.0f) +
+             (zl > 0.0f ? w_limit * (float)K * tvam_powi(rl, K - 1) : 0.0f);
+        return w_object * tvam_powi(ro, K) + w_limit * tvam_powi(rl, K);
+    }
+    const float zv = x - tl;
+    const float rv = zv > 0.0f ? zv : 0.0f;
+    gr = zv > 0.0f ? w_void * (float)K * tvam_powi(rv, K - 1) : 0.0f;
+    return w_void * tvam_powi(rv, K);
+}
+
+// n4: elements / 4 when dose, ddose, grad (and the f32 target, or a mask offset % 4 == 0) allow
+// float4 accesses, else 0
+template <bool MASK>
 __global__ __launch_bounds__(256) void tvam_loss_threshold_kernel(
     const float* __restrict__ dose, const float* __restrict__ ddose, float alpha, const float* __restrict__ target,
-    uint64_t n, int K, float tl, float tu, float w_object, float w_void, float w_limit, float scale,
-    double* __restrict__ out, float* __restrict__ grad) {
+    const uint32_t* __restrict__ mask, uint64_t mbit0, uint64_t n, uint64_t n4, int K, float tl, float tu,
+    float w_object, float w_void, float w_limit, float scale, double* __restrict__ out, float* __restrict__ grad) {
     __shared__ double red[256 / 64];
     double acc = 0.0;
-    const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
-    for (uint64_t i = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-        float x = dose[i];
-        if (ddose) x = fmaf(alpha, ddose[i], x);  // vol + alpha * dvol (lbfgs.py:258)
-        float l, gr;
-        if (target[i] > 0.0f) {
-            float zo = tu - x, zl = x - 1.0f;
-            float ro = zo > 0.0f ? zo : 0.0f, rl = zl > 0.0f ? zl : 0.0f;
-            l = w_object * tvam_powi(ro, K) + w_limit * tvam_powi(rl, K);
-            gr = (zo > 0.0f ? -w_object * (float)K * tvam_powi(ro, K - 1) : 0.0f) +
-                 (zl > 0.0f ? w_limit * (float)K * tvam_powi(rl, K - 1) : 0.0f);
-        } else {
-            float zv = x - tl;
-            float rv = zv > 0.0f ? zv : 0.0f;
-            l = w_void * tvam_powi(rv, K);
-            gr = zv > 0.0f ? w_void * (float)K * tvam_powi(rv, K - 1) : 0.0f;
+    const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
+    for (uint64_t t = tid; t < n4; t += stride) {
+        float4 x = reinterpret_cast<const float4*>(dose)[t];
+        if (ddose) {  // vol + alpha * dvol (lbfgs.py:258)
+            const float4 dx = reinterpret_cast<const float4*>(ddose)[t];
+            x = make_float4(fmaf(alpha, dx.x, x.x), fmaf(alpha, dx.y, x.y), fmaf(alpha, dx.z, x.z), fmaf(alpha, dx.w, x.w));
         }
-        acc += (double)l;
+        const uint32_t ob = tvam_obj4<MASK>(target, mask, mbit0, t);
+        float4 g;
+        acc += (double)tvam_loss_grad_elem(x.x, ob & 1u, K, tl, tu, w_object, w_void, w_limit, g.x);
+        acc += (double)tvam_loss_grad_elem(x.y, ob & 2u, K, tl, tu, w_object, w_void, w_limit, g.y);
+        acc += (double)tvam_loss_grad_elem(x.z, ob & 4u, K, tl, tu, w_object, w_void, w_limit, g.z);
+        acc += (double)tvam_loss_grad_elem(x.w, ob & 8u, K, tl, tu, w_object, w_void, w_limit, g.w);
+        if (grad)
+            reinterpret_cast<float4*>(grad)[t] = make_float4(g.x * scale, g.y * scale, g.z * scale, g.w * scale);
+    }
+    for (uint64_t i = 4 * n4 + tid; i < n; i += stride) {
+        float x = dose[i];
+        if (ddose) x = fmaf(alpha, ddose[i], x);
+        float gr;
+        acc += (double)tvam_loss_grad_elem(x, tvam_is_obj<MASK>(target, mask, mbit0, i), K, tl, tu, w_object, w_void,
+                                           w_limit, gr);
         if (grad) grad[i] = gr * scale;
     }
     for (int off = 32; off > 0; off >>= 1) acc += __shfl_down(acc, off, 64);
@@ -796,33 +866,33 @@ __device__ __forceinline__ float tvam_loss_elem(float x, bool obj, int K, float 
     return w_void * tvam_powi(rv, K);
 }
 
+template <bool MASK>
 __global__ __launch_bounds__(256) void tvam_loss_probes_kernel(
     const float* __restrict__ dose, const float* __restrict__ ddose, TvamProbeAlphas al, int na,
-    const float* __restrict__ target, uint64_t n, uint64_t n4, int K, float tl, float tu, float w_object,
-    float w_void, float w_limit, float scale, double* __restrict__ out) {
+    const float* __restrict__ target, const uint32_t* __restrict__ mask, uint64_t mbit0, uint64_t n, uint64_t n4, int K,
+    float tl, float tu, float w_object, float w_void, float w_limit, float scale, double* __restrict__ out) {
     __shared__ double red[TVAM_MAX_PROBES][256 / 64];
     double acc[TVAM_MAX_PROBES];
 #pragma unroll
     for (int j = 0; j < TVAM_MAX_PROBES; ++j) acc[j] = 0.0;
-    auto elem = [&](float x0, float dx, float tg) {
-        const bool obj = tg > 0.0f;
+    auto elem = [&](float x0, float dx, bool obj) {
 #pragma unroll
         for (int j = 0; j < TVAM_MAX_PROBES; ++j)
             if (j < na) acc[j] += (double)tvam_loss_elem(fmaf(al.a[j], dx, x0), obj, K, tl, tu, w_object, w_void, w_limit);
     };
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
-    // n4: elements / 4 when all three arrays are 16-byte aligned (float4 loads), else 0
+    // n4: elements / 4 when the arrays allow float4 loads, else 0
     const float4* d4 = reinterpret_cast<const float4*>(dose);
     const float4* dd4 = reinterpret_cast<const float4*>(ddose);
-    const float4* t4 = reinterpret_cast<const float4*>(target);
     for (uint64_t i = tid; i < n4; i += stride) {
-        const float4 x = d4[i], dx = dd4[i], tg = t4[i];
-        elem(x.x, dx.x, tg.x);
-        elem(x.y, dx.y, tg.y);
-        elem(x.z, dx.z, tg.z);
-        elem(x.w, dx.w, tg.w);
+        const float4 x = d4[i], dx = dd4[i];
+        const uint32_t ob = tvam_obj4<MASK>(target, mask, mbit0, i);
+        elem(x.x, dx.x, ob & 1u);
+        elem(x.y, dx.y, ob & 2u);
+        elem(x.z, dx.z, ob & 4u);
+        elem(x.w, dx.w, ob & 8u);
     }
-    for (uint64_t i = 4 * n4 + tid; i < n; i += stride) elem(dose[i], ddose[i], target[i]);
+    for (uint64_t i = 4 * n4 + tid; i < n; i += stride) elem(dose[i], ddose[i], tvam_is_obj<MASK>(target, mask, mbit0, i));
 #pragma unroll
     for (int j = 0; j < TVAM_MAX_PROBES; ++j) {
         double v = acc[j];
@@ -837,29 +907,45 @@ __global__ __launch_bounds__(256) void tvam_loss_probes_kernel(
     }
 }
 
+static bool tvam_al16(const void* a, const void* b, const void* c) {
+    return ((reinterpret_cast<uintptr_t>(a) | reinterpret_cast<uintptr_t>(b) | reinterpret_cast<uintptr_t>(c)) & 15) == 0;
+}
+
 hipError_t tvam_launch_loss_probes(const float* dose, const float* ddose, const float* alphas, int na,
-                                   const float* target, uint64_t n, int K, float tl, float tu, float w_object,
-                                   float w_void, float w_limit, float scale, double* out, hipStream_t stream) {
+                                   const float* target, const uint32_t* mask, uint64_t mbit0, uint64_t n, int K,
+                                   float tl, float tu, float w_object, float w_void, float w_limit, float scale,
+                                   double* out, hipStream_t stream) {
     TvamProbeAlphas al{};
     for (int j = 0; j < na; ++j) al.a[j] = alphas[j];
-    const bool al16 = ((reinterpret_cast<uintptr_t>(dose) | reinterpret_cast<uintptr_t>(ddose) |
-                        reinterpret_cast<uintptr_t>(target)) & 15) == 0;
-    const uint64_t n4 = al16 ? n / 4 : 0;
-    unsigned g = (unsigned)(((al16 ? n4 : n) + 255) / 256);
+    const bool v4 = tvam_al16(dose, ddose, mask ? nullptr : target) && (!mask || mbit0 % 4 == 0);
+    const uint64_t n4 = v4 ? n / 4 : 0;
+    unsigned g = (unsigned)(((v4 ? n4 : n) + 255) / 256);
     if (g > 2048) g = 2048;
     if (g == 0) g = 1;
-    hipLaunchKernelGGL(tvam_loss_probes_kernel, dim3(g), dim3(256), 0, stream, dose, ddose, al, na, target, n, n4, K,
-                       tl, tu, w_object, w_void, w_limit, scale, out);
+    if (mask)
+        hipLaunchKernelGGL(tvam_loss_probes_kernel<true>, dim3(g), dim3(256), 0, stream, dose, ddose, al, na, target,
+                           mask, mbit0, n, n4, K, tl, tu, w_object, w_void, w_limit, scale, out);
+    else
+        hipLaunchKernelGGL(tvam_loss_probes_kernel<false>, dim3(g), dim3(256), 0, stream, dose, ddose, al, na, target,
+                           mask, mbit0, n, n4, K, tl, tu, w_object, w_void, w_limit, scale, out);
     return hipGetLastError();
 }
 
 hipError_t tvam_launch_loss_threshold(const float* dose, const float* ddose, float alpha, const float* target,
-                                      uint64_t n, int K, float tl, float tu, float w_object, float w_void,
-                                      float w_limit, float scale, double* out, float* grad, hipStream_t stream) {
-    unsigned g = (unsigned)((n + 255) / 256);
+                                      const uint32_t* mask, uint64_t mbit0, uint64_t n, int K, float tl, float tu,
+                                      float w_object, float w_void, float w_limit, float scale, double* out,
+                                      float* grad, hipStream_t stream) {
+    const bool v4 = tvam_al16(dose, ddose, grad) && tvam_al16(mask ? nullptr : target, nullptr, nullptr) &&
+                    (!mask || mbit0 % 4 == 0);
+    const uint64_t n4 = v4 ? n / 4 : 0;
+    unsigned g = (unsigned)(((v4 ? n4 : n) + 255) / 256);
     if (g > 2048) g = 2048;
     if (g == 0) g = 1;
-    hipLaunchKernelGGL(tvam_loss_threshold_kernel, dim3(g), dim3(256), 0, stream, dose, ddose, alpha, target, n, K, tl,
-                       tu, w_object, w_void, w_limit, scale, out, grad);
+    if (mask)
+        hipLaunchKernelGGL(tvam_loss_threshold_kernel<true>, dim3(g), dim3(256), 0, stream, dose, ddose, alpha, target,
+                           mask, mbit0, n, n4, K, tl, tu, w_object, w_void, w_limit, scale, out, grad);
+    else
+        hipLaunchKernelGGL(tvam_loss_threshold_kernel<false>, dim3(g), dim3(256), 0, stream, dose, ddose, alpha, target,
+                           mask, mbit0, n, n4, K, tl, tu, w_object, w_void, w_limit, scale, out, grad);
     return hipGetLastError();
 }

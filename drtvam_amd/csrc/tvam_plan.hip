@@ -2039,9 +2039,39 @@ extern "C" int tvam_loss_threshold(const float* dose, const float* ddose, float 
                                    float scale, double* out, float* grad, void* stream) {
     if (!dose || !target || !out) return fail(TVAM_ERR_INVALID, "null argument");
     if (K < 1 || K > 16) return fail(TVAM_ERR_UNSUPPORTED, "ThresholdedLoss: integer K in [1, 16] required on the GPU path");
-    hipError_t e = tvam_launch_loss_threshold(dose, ddose, alpha, target, n, K, tl, tu, w_object, w_void, w_limit, scale,
-                                              out, grad, (hipStream_t)stream);
+    hipError_t e = tvam_launch_loss_threshold(dose, ddose, alpha, target, nullptr, 0, n, K, tl, tu, w_object, w_void,
+                                              w_limit, scale, out, grad, (hipStream_t)stream);
     return e == hipSuccess ? 0 : hip_fail(e, "loss launch");
+}
+
+extern "C" int tvam_target_mask(const float* target, uint64_t n, uint32_t* mask, void* stream) {
+    if (!target || !mask) return fail(TVAM_ERR_INVALID, "null argument");
+    hipError_t e = tvam_launch_target_mask(target, n, mask, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "target mask launch");
+}
+
+extern "C" int tvam_loss_threshold_mask(const float* dose, const float* ddose, float alpha, const uint32_t* mask,
+                                        uint64_t mask_bit0, uint64_t n, int32_t K, float tl, float tu, float w_object,
+                                        float w_void, float w_limit, float scale, double* out, float* grad,
+                                        void* stream) {
+    if (!dose || !mask || !out) return fail(TVAM_ERR_INVALID, "null argument");
+    if (K < 1 || K > 16) return fail(TVAM_ERR_UNSUPPORTED, "ThresholdedLoss: integer K in [1, 16] required on the GPU path");
+    hipError_t e = tvam_launch_loss_threshold(dose, ddose, alpha, nullptr, mask, mask_bit0, n, K, tl, tu, w_object,
+                                              w_void, w_limit, scale, out, grad, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "loss launch");
+}
+
+extern "C" int tvam_loss_threshold_probes_mask(const float* dose, const float* ddose, const float* alphas,
+                                               int32_t n_alpha, const uint32_t* mask, uint64_t mask_bit0, uint64_t n,
+                                               int32_t K, float tl, float tu, float w_object, float w_void,
+                                               float w_limit, float scale, double* out, void* stream) {
+    if (!dose || !ddose || !alphas || !mask || !out) return fail(TVAM_ERR_INVALID, "null argument");
+    if (n_alpha < 1 || n_alpha > TVAM_MAX_PROBES)
+        return fail(TVAM_ERR_INVALID, "tvam_loss_threshold_probes_mask: 1 <= n_alpha <= 8");
+    if (K < 1 || K > 16) return fail(TVAM_ERR_UNSUPPORTED, "ThresholdedLoss: integer K in [1, 16] required on the GPU path");
+    hipError_t e = tvam_launch_loss_probes(dose, ddose, alphas, n_alpha, nullptr, mask, mask_bit0, n, K, tl, tu,
+                                           w_object, w_void, w_limit, scale, out, (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "loss probes launch");
 }
 
 extern "C" int tvam_loss_threshold_probes(const float* dose, const float* ddose, const float* alphas, int32_t n_alpha,
@@ -2051,8 +2081,8 @@ extern "C" int tvam_loss_threshold_probes(const float* dose, const float* ddose,
     if (!dose || !ddose || !alphas || !target || !out) return fail(TVAM_ERR_INVALID, "null argument");
     if (n_alpha < 1 || n_alpha > TVAM_MAX_PROBES) return fail(TVAM_ERR_INVALID, "tvam_loss_threshold_probes: 1 <= n_alpha <= 8");
     if (K < 1 || K > 16) return fail(TVAM_ERR_UNSUPPORTED, "ThresholdedLoss: integer K in [1, 16] required on the GPU path");
-    hipError_t e = tvam_launch_loss_probes(dose, ddose, alphas, n_alpha, target, n, K, tl, tu, w_object, w_void,
-                                           w_limit, scale, out, (hipStream_t)stream);
+    hipError_t e = tvam_launch_loss_probes(dose, ddose, alphas, n_alpha, target, nullptr, 0, n, K, tl, tu, w_object,
+                                           w_void, w_limit, scale, out, (hipStream_t)stream);
     return e == hipSuccess ? 0 : hip_fail(e, "loss probes launch");
 }
 
@@ -2150,6 +2180,27 @@ extern "C" int tvam_axpy_clamp(uint64_t n, const float* p, float alpha, const fl
         return fail(TVAM_ERR_INVALID, "tvam_axpy_clamp: vectors must be 16-byte aligned");
     hipError_t e = tvam_launch_axpy_clamp(n, p, alpha, d, lo, out, (hipStream_t)stream);
     return e == hipSuccess ? 0 : hip_fail(e, "axpy launch");
+}
+
+extern "C" int tvam_axpy_clamp_dev(uint64_t n, const float* p, const float* alpha, const float* d, float lo,
+                                   float* out, void* stream) {
+    if (!p || !alpha || !d || !out) return fail(TVAM_ERR_INVALID, "null argument");
+    if (!aligned16(p) || !aligned16(d) || !aligned16(out))
+        return fail(TVAM_ERR_INVALID, "tvam_axpy_clamp_dev: vectors must be 16-byte aligned");
+    hipError_t e = tvam_launch_axpy_clamp(n, p, 0.0f, d, lo, out, (hipStream_t)stream, alpha);
+    return e == hipSuccess ? 0 : hip_fail(e, "axpy launch");
+}
+
+extern "C" int tvam_lbfgs_armijo(int32_t nprobe, double alpha0, const double* probes, const double* loss_dev,
+                                 double loss_host, double loss_div, const double* gdz, double c1, float* alpha,
+                                 double* report, void* stream) {
+    if (!probes || !gdz || !alpha) return fail(TVAM_ERR_INVALID, "null argument");
+    if (nprobe < 1 || nprobe > 64) return fail(TVAM_ERR_INVALID, "tvam_lbfgs_armijo: 1 <= nprobe <= 64");
+    if (!(alpha0 > 0.0) || !(loss_div > 0.0))
+        return fail(TVAM_ERR_INVALID, "tvam_lbfgs_armijo: alpha0 and loss_div must be positive");
+    hipError_t e = tvam_launch_armijo(nprobe, alpha0, probes, loss_dev, loss_host, loss_div, gdz, c1, alpha, report,
+                                      (hipStream_t)stream);
+    return e == hipSuccess ? 0 : hip_fail(e, "armijo launch");
 }
 
 extern "C" int tvam_row_slices(const tvam_desc* desc, int32_t* slice_of_row) {

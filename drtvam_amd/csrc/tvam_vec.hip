@@ -462,9 +462,12 @@ hipError_t tvam_launch_lbfgs_direction_dev(uint64_t n, const float* g, int h, co
 }
 
 // ---------------------------------------------------------------------------
+// alpha_dev (tvam_axpy_clamp_dev): the step size read from device memory, tvam_armijo_kernel's pick
 __global__ __launch_bounds__(TVAM_VB) void tvam_axpy_clamp_kernel(uint64_t n, const float* __restrict__ p, float alpha,
                                                                   const float* __restrict__ d, float lo,
-                                                                  float* __restrict__ out) {
+                                                                  float* __restrict__ out,
+                                                                  const float* __restrict__ alpha_dev) {
+    if (alpha_dev) alpha = alpha_dev[0];
     const uint64_t n4 = n / 4, stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (uint64_t i = tid; i < n4; i += stride) {
@@ -477,7 +480,51 @@ __global__ __launch_bounds__(TVAM_VB) void tvam_axpy_clamp_kernel(uint64_t n, co
 }
 
 hipError_t tvam_launch_axpy_clamp(uint64_t n, const float* p, float alpha, const float* d, float lo, float* out,
-                                  hipStream_t stream) {
-    hipLaunchKernelGGL(tvam_axpy_clamp_kernel, dim3(2048), dim3(TVAM_VB), 0, stream, n, p, alpha, d, lo, out);
+                                  hipStream_t stream, const float* alpha_dev) {
+    hipLaunchKernelGGL(tvam_axpy_clamp_kernel, dim3(2048), dim3(TVAM_VB), 0, stream, n, p, alpha, d, lo, out,
+                       alpha_dev);
+    return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// The first batch of Armijo probes decided on the device (FusedLinearLBFGS.step), so that the
+// update p + alpha d can follow the probes on the stream while the host reads them: alpha[0] =
+// a_j for the first probe j with f_j <= loss + c1 a_j g.d, a_j = a0 / 2^j (lbfgs.py:256-266), in
+// the host loop's fp64 operations and order (no contraction); 0 when no probe passes (the host
+// then discards the update launched behind it).  loss = loss_dev[0] / loss_div, or loss_host.
+// report (optional, e.g. pinned host memory the host reads once the kernel is done, no copy kernel):
+// the undivided loss, g.d, the probes and the chosen alpha, as f64.
+__global__ void tvam_armijo_kernel(int nprobe, double a0, const double* __restrict__ probes,
+                                   const double* __restrict__ loss_dev, double loss_host, double loss_div,
+                                   const double* __restrict__ gdz, double c1, float* __restrict__ alpha,
+                                   double* __restrict__ report) {
+#pragma clang fp contract(off)
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    const double l0 = loss_dev ? loss_dev[0] : loss_host;
+    const double lv = loss_dev ? l0 / loss_div : loss_host;
+    const double gd = 0.0 + gdz[0];
+    float r = 0.0f;
+    for (int j = 0; j < nprobe; ++j) {
+        const double a = a0 * ldexp(1.0, -j);
+        if (probes[j] <= lv + c1 * a * gd) {
+            r = (float)a;
+            break;
+        }
+    }
+    alpha[0] = r;
+    if (report) {
+        report[0] = l0;
+        report[1] = gdz[0];
+        for (int j = 0; j < nprobe; ++j) report[2 + j] = probes[j];
+        report[2 + nprobe] = (double)r;
+        __threadfence_system();
+    }
+}
+
+hipError_t tvam_launch_armijo(int nprobe, double a0, const double* probes, const double* loss_dev, double loss_host,
+                              double loss_div, const double* gdz, double c1, float* alpha, double* report,
+                              hipStream_t stream) {
+    hipLaunchKernelGGL(tvam_armijo_kernel, dim3(1), dim3(64), 0, stream, nprobe, a0, probes, loss_dev, loss_host,
+                       loss_div, gdz, c1, alpha, report);
     return hipGetLastError();
 }

@@ -288,9 +288,32 @@ def render(proj: Projection, active_data: torch.Tensor, active_pixels: Optional[
     return TvamRender.apply(active_data, proj, active_pixels, spp, spp_grad, seed, seed_grad)
 
 
+def target_mask(target: torch.Tensor) -> torch.Tensor:
+    """Bit mask of a contiguous f32 target (tvam_target_mask): int32 words, bit j of word w =
+    target[32 w + j] > 0, the loss kernels' object test from 1/32 of the bytes."""
+    if target.dtype != torch.float32 or not target.is_contiguous() or not target.is_cuda:
+        raise ValueError("target_mask: a contiguous float32 CUDA tensor")
+    n = target.numel()
+    mask = torch.empty((n + 31) // 32, dtype=torch.int32, device=target.device)
+    with torch.cuda.device(target.device):
+        _abi.check(_abi.load_library().tvam_target_mask(target.data_ptr(), n, mask.data_ptr(),
+                                                        _stream_ptr(target.device)))
+    return mask
+
+
+def _check_mask(mask, mask_bit0, n, dev):
+    if mask.dtype != torch.int32 or not mask.is_contiguous() or mask.device != dev:
+        raise ValueError(f"mask must be a contiguous int32 tensor on {dev}")
+    if mask_bit0 < 0 or mask_bit0 + n > 32 * mask.numel():
+        raise ValueError("mask: bits [mask_bit0, mask_bit0 + n) out of range")
+
+
 def loss_threshold_probes(dose: torch.Tensor, ddose: torch.Tensor, alphas, target: torch.Tensor, K: int, tl: float,
-                          tu: float, w_object: float, w_void: float, w_limit: float, scale: float) -> torch.Tensor:
-    """Fused ThresholdedLoss of dose + a * ddose for each a in alphas (<= 8): f64 device vector, one pass."""
+                          tu: float, w_object: float, w_void: float, w_limit: float, scale: float,
+                          mask: Optional[torch.Tensor] = None, mask_bit0: int = 0) -> torch.Tensor:
+    """Fused ThresholdedLoss of dose + a * ddose for each a in alphas (<= 8): f64 device vector, one pass.
+    ``mask``: target_mask() of a tensor whose elements [mask_bit0, mask_bit0 + n) are this target
+    (the object test read from it instead of the f32 target)."""
     lib = _abi.load_library()
     na = len(alphas)
     if not 1 <= na <= 8:
@@ -304,16 +327,25 @@ def loss_threshold_probes(dose: torch.Tensor, ddose: torch.Tensor, alphas, targe
     out = torch.zeros(na, dtype=torch.float64, device=dose.device)
     a = (ctypes.c_float * na)(*[float(v) for v in alphas])
     with torch.cuda.device(dose.device):
-        _abi.check(lib.tvam_loss_threshold_probes(
-            dose.data_ptr(), ddose.data_ptr(), a, na, target.data_ptr(), n, int(K), float(tl), float(tu),
-            float(w_object), float(w_void), float(w_limit), float(scale), out.data_ptr(), _stream_ptr(dose.device)))
+        if mask is not None:
+            _check_mask(mask, mask_bit0, n, dose.device)
+            _abi.check(lib.tvam_loss_threshold_probes_mask(
+                dose.data_ptr(), ddose.data_ptr(), a, na, mask.data_ptr(), int(mask_bit0), n, int(K), float(tl),
+                float(tu), float(w_object), float(w_void), float(w_limit), float(scale), out.data_ptr(),
+                _stream_ptr(dose.device)))
+        else:
+            _abi.check(lib.tvam_loss_threshold_probes(
+                dose.data_ptr(), ddose.data_ptr(), a, na, target.data_ptr(), n, int(K), float(tl), float(tu),
+                float(w_object), float(w_void), float(w_limit), float(scale), out.data_ptr(), _stream_ptr(dose.device)))
     return out
 
 
 def loss_threshold(dose: torch.Tensor, target: torch.Tensor, K: int, tl: float, tu: float, w_object: float,
                    w_void: float, w_limit: float, scale: float, ddose: Optional[torch.Tensor] = None,
-                   alpha: float = 0.0, grad: Optional[torch.Tensor] = None) -> torch.Tensor:
-    """Fused ThresholdedLoss value (f64 device scalar) and optional dL/dx (HIP kernel)."""
+                   alpha: float = 0.0, grad: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None,
+                   mask_bit0: int = 0) -> torch.Tensor:
+    """Fused ThresholdedLoss value (f64 device scalar) and optional dL/dx (HIP kernel); ``mask`` as in
+    loss_threshold_probes."""
     lib = _abi.load_library()
     out = torch.zeros(1, dtype=torch.float64, device=dose.device)
     for name, t in (("dose", dose), ("target", target), ("ddose", ddose), ("grad", grad)):
@@ -323,8 +355,15 @@ def loss_threshold(dose: torch.Tensor, target: torch.Tensor, K: int, tl: float, 
     if target.numel() != n or (ddose is not None and ddose.numel() != n) or (grad is not None and grad.numel() != n):
         raise ValueError("loss_threshold: size mismatch")
     with torch.cuda.device(dose.device):
-        _abi.check(lib.tvam_loss_threshold(
-            dose.data_ptr(), None if ddose is None else ddose.data_ptr(), float(alpha), target.data_ptr(), n, int(K),
-            float(tl), float(tu), float(w_object), float(w_void), float(w_limit), float(scale), out.data_ptr(),
-            None if grad is None else grad.data_ptr(), _stream_ptr(dose.device)))
+        if mask is not None:
+            _check_mask(mask, mask_bit0, n, dose.device)
+            _abi.check(lib.tvam_loss_threshold_mask(
+                dose.data_ptr(), None if ddose is None else ddose.data_ptr(), float(alpha), mask.data_ptr(),
+                int(mask_bit0), n, int(K), float(tl), float(tu), float(w_object), float(w_void), float(w_limit),
+                float(scale), out.data_ptr(), None if grad is None else grad.data_ptr(), _stream_ptr(dose.device)))
+        else:
+            _abi.check(lib.tvam_loss_threshold(
+                dose.data_ptr(), None if ddose is None else ddose.data_ptr(), float(alpha), target.data_ptr(), n,
+                int(K), float(tl), float(tu), float(w_object), float(w_void), float(w_limit), float(scale),
+                out.data_ptr(), None if grad is None else grad.data_ptr(), _stream_ptr(dose.device)))
     return out[0]

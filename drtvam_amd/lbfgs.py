@@ -352,6 +352,49 @@ class FusedLinearLBFGS(LinearLBFGS):
         self.variables[k] = out.reshape(p.shape).requires_grad_(True)
         return loss_v
 
+    speculate = True  # decide the first probe batch on the device and launch the update behind it
+
+    def _speculative_update(self, fd, nb, c1, loss, loss_cell, gdz, loss_summed, search, lo):
+        """The first probe batch decided on the device (tvam_lbfgs_armijo) and the update p + alpha d
+        with that alpha (tvam_axpy_clamp_dev) launched behind it, the host reading the decision's
+        report (loss, g.d, probes, alpha) from pinned memory as soon as the decision kernel is done:
+        the update runs while the host decides and launches the next iteration, where the GPU
+        idled through the read before.  Returns ((update, device alpha), loss, g.d, probes) with
+        the loss and g.d formed as host_scalars forms them; the caller keeps the update only when
+        its own decision took the same alpha from this batch."""
+        from . import _abi
+        lib = self._lib()
+        (k, p), = self.variables.items()
+        pf = _aligned(p.detach().reshape(-1))
+        dev = pf.device
+        main = torch.cuda.current_stream(dev)
+        div = 1.0
+        divided = loss_cell is not None and self.allreduce is not None and not loss_summed
+        if divided:
+            import torch.distributed as _d
+            div = float(_d.get_world_size())
+        rep = getattr(self, '_report', None)
+        if rep is None or rep.numel() < 3 + nb:
+            rep = self._report = torch.zeros(3 + self.probe_batch, dtype=torch.float64, pin_memory=True)
+            self._alpha_dev = torch.empty(1, dtype=torch.float32, device=dev)
+        alpha_dev = self._alpha_dev
+        if alpha_dev.device != dev:
+            alpha_dev = self._alpha_dev = torch.empty(1, dtype=torch.float32, device=dev)
+        loss_host = float(loss) if loss_cell is None else 0.0
+        fdc = fd.contiguous()
+        _abi.check(lib.tvam_lbfgs_armijo(nb, 1.0, fdc.data_ptr(), loss_cell.data_ptr() if loss_cell is not None else None,
+                                         loss_host, div, gdz.data_ptr(), c1, alpha_dev.data_ptr(), rep.data_ptr(),
+                                         main.cuda_stream))
+        ev = torch.cuda.Event()
+        ev.record(main)
+        out = torch.empty_like(pf)
+        _abi.check(lib.tvam_axpy_clamp_dev(pf.numel(), pf.data_ptr(), alpha_dev.data_ptr(), search[k].data_ptr(), lo,
+                                           out.data_ptr(), main.cuda_stream))
+        ev.synchronize()
+        v = rep.tolist()
+        lv = v[0] / div if divided else (v[0] if loss_cell is not None else loss_host)
+        return (out, v[2 + nb]), float(lv), 0.0 + v[1], v[2:2 + nb]
+
     @staticmethod
     def _stream(dev):
         return torch.cuda.current_stream(dev).cuda_stream if dev.type == 'cuda' else None
@@ -461,6 +504,8 @@ class FusedLinearLBFGS(LinearLBFGS):
         key = 'projector.active_data' if 'projector.active_data' in params else next(iter(params))
         alpha = 1.0
         steps = 0
+        lo = -float('inf') if self.clamp_min is None else float(self.clamp_min)
+        spec = None  # (update, its step size on the device) launched behind the first probes
         if self.loss_steps is not None and self.search_it > 0:
             # the same backtracking sequence (alpha = 1, 1/2, ...; first Armijo pass wins), its
             # probes evaluated probe_batch at a time: one loss pass and one host read per batch
@@ -472,7 +517,11 @@ class FusedLinearLBFGS(LinearLBFGS):
                 alphas = [alpha * 0.5 ** j for j in range(nb)]
                 fd = self.loss_steps(vol, dvol, alphas, params[key])
                 if first:
-                    loss_v, gdz_total, fv = host_scalars(fd)
+                    if self.speculate and len(self.variables) == 1 and fd.is_cuda and fd.dtype == torch.float64:
+                        spec, loss_v, gdz_total, fv = self._speculative_update(fd, nb, c1, loss, loss_cell, gdz_dev[0],
+                                                                               loss_summed, search, lo)
+                    else:
+                        loss_v, gdz_total, fv = host_scalars(fd)
                     first = False
                     if loss_cell is not None and loss_v == 0.0:  # converged (optimize.py:305-307): no update
                         return loss_v
@@ -502,7 +551,11 @@ class FusedLinearLBFGS(LinearLBFGS):
         self.last_alpha = alpha
         self.last_search_steps = steps
 
-        lo = -float('inf') if self.clamp_min is None else float(self.clamp_min)
+        if spec is not None and steps <= self.probe_batch and alpha == spec[1]:
+            # the device picked the same step size in the same f64 arithmetic: its update stands
+            (k, p), = self.variables.items()
+            self.variables[k] = spec[0].reshape(p.shape).requires_grad_(True)
+            return loss_v
         for k, p in self.variables.items():
             pf = _aligned(p.detach().reshape(-1))
             out = torch.empty_like(pf)

@@ -129,15 +129,33 @@ class ThresholdedLoss(Loss):
         p = patterns.detach()
         return self.reduction(torch.abs(p) ** self.M * self.weight_sparsity).to(torch.float64)
 
+    def _target_mask(self, target):
+        """(bit mask, bit offset) of target's object test (engine.target_mask), built once per target:
+        the mask covers the contiguous base tensor a view (a slab of the film) comes from, and is
+        rebuilt when that tensor is written in place (its version counter moves).  None: use the f32
+        target."""
+        base = target if target._base is None else target._base
+        if not (base.is_contiguous() and base.dtype == torch.float32 and base.is_cuda):
+            return None
+        key = (base.data_ptr(), base.numel(), base._version)
+        c = getattr(self, '_mask_cache', None)
+        if c is None or c[0] != key:
+            from .engine import target_mask
+            c = (key, base, target_mask(base))
+            self._mask_cache = c
+        return c[2], (target.data_ptr() - base.data_ptr()) // 4
+
     def fused_value(self, x, target, patterns, dx=None, alpha=0.0, count=None):
         """Loss of x (+ alpha*dx) as an f64 device scalar, one kernel pass.  ``patterns=None``
         leaves out the sparsity term; ``count`` is the element count of a 'mean' reduction
         when x is one slab of the film."""
         from .engine import loss_threshold
         scale = 1.0 / (count or x.numel()) if self.reduction_name == 'mean' else 1.0
+        m = self._target_mask(target)
         v = loss_threshold(x.reshape(-1), target.reshape(-1), int(self.K), self.tl, self.tu, self.weight_object,
                            self.weight_void, self.weight_limit, scale,
-                           None if dx is None else dx.reshape(-1), alpha)
+                           None if dx is None else dx.reshape(-1), alpha, mask=m[0] if m else None,
+                           mask_bit0=m[1] if m else 0)
         s = self._sparsity_value(patterns)
         return v if s is None else v + s
 
@@ -146,8 +164,10 @@ class ThresholdedLoss(Loss):
         pass (the Armijo probes of the line search; ``patterns`` / ``count`` as in fused_value)."""
         from .engine import loss_threshold_probes
         scale = 1.0 / (count or x.numel()) if self.reduction_name == 'mean' else 1.0
+        m = self._target_mask(target)
         v = loss_threshold_probes(x.reshape(-1), dx.reshape(-1), alphas, target.reshape(-1), int(self.K), self.tl,
-                                  self.tu, self.weight_object, self.weight_void, self.weight_limit, scale)
+                                  self.tu, self.weight_object, self.weight_void, self.weight_limit, scale,
+                                  mask=m[0] if m else None, mask_bit0=m[1] if m else 0)
         s = self._sparsity_value(patterns)
         return v if s is None else v + s
 
@@ -156,8 +176,10 @@ class ThresholdedLoss(Loss):
         (``patterns`` / ``count`` as in fused_value)."""
         from .engine import loss_threshold
         scale = 1.0 / (count or x.numel()) if self.reduction_name == 'mean' else 1.0
+        m = self._target_mask(target)
         v = loss_threshold(x.reshape(-1), target.reshape(-1), int(self.K), self.tl, self.tu, self.weight_object,
-                           self.weight_void, self.weight_limit, scale, grad=grad_out.reshape(-1))
+                           self.weight_void, self.weight_limit, scale, grad=grad_out.reshape(-1),
+                           mask=m[0] if m else None, mask_bit0=m[1] if m else 0)
         s = self._sparsity_value(patterns)
         return v if s is None else v + s
 

@@ -45,7 +45,7 @@
 extern "C" {
 #endif
 
-#define TVAM_ABI_VERSION 11
+#define TVAM_ABI_VERSION 12
 
 /* error codes */
 #define TVAM_OK               0
@@ -334,6 +334,16 @@ int tvam_plan_path(const tvam_plan* plan);
  *   [0, seg_len) of every a < nseg only (a band of DMD rows of every angle:
  *   seg_stride = rows * columns), so that the forward of one band's slices can
  *   start while the next band's direction is formed (all multiples of 4).
+ * tvam_lbfgs_armijo: the first batch of backtracking Armijo probes (lbfgs.py:256-266)
+ *   decided on the device, one lane: alpha[0] (device f32) = a_j = alpha0 / 2^j
+ *   for the first j < nprobe with probes[j] <= loss + c1 a_j gdz[0] (device f64
+ *   probes and g.d; loss = loss_dev[0] / loss_div, or loss_host when loss_dev is
+ *   NULL), evaluated as the host loop evaluates it in f64; 0 when none passes.
+ *   report (may be NULL; device-visible, e.g. pinned host memory read after the
+ *   kernel): loss_dev[0] (or loss_host) | gdz[0] | probes[0..nprobe) | alpha, f64.
+ * tvam_axpy_clamp_dev: tvam_axpy_clamp with alpha read from device memory
+ *   (tvam_lbfgs_armijo's output), so the update follows the probes on the stream
+ *   without a host round trip.  (Both ABI v12.)
  */
 #define TVAM_LBFGS_WORK_DOUBLES (2048 * 64)
 int tvam_lbfgs_history(uint64_t n, const float* p, const float* p_old, const float* g, const float* g_old,
@@ -354,6 +364,11 @@ int tvam_lbfgs_direction_rows(uint64_t nseg, uint64_t seg_len, uint64_t seg_stri
                               const float* coef, float* d, void* hip_stream);
 int tvam_axpy_clamp(uint64_t n, const float* p, float alpha, const float* d, float lo, float* out,
                     void* hip_stream);
+int tvam_axpy_clamp_dev(uint64_t n, const float* p, const float* alpha, const float* d, float lo, float* out,
+                        void* hip_stream);
+int tvam_lbfgs_armijo(int32_t nprobe, double alpha0, const double* probes, const double* loss_dev, double loss_host,
+                      double loss_div, const double* gdz, double c1, float* alpha, double* report,
+                      void* hip_stream);
 
 /* Global film z-slice of every crop row's rays under regular sampling
    (slice_of_row[crop_y]; -1 when the row's rays miss the grid or the vial),
@@ -402,6 +417,28 @@ int tvam_loss_threshold_probes(const float* dose, const float* ddose,
                                float tl, float tu, float w_object, float w_void,
                                float w_limit, float scale, double* out,
                                void* hip_stream);
+
+/*
+ * The object test of both loss kernels (target > 0, loss.py:119) from a bit mask
+ * of the target, 1/32 of its bytes (ABI v12):
+ *   tvam_target_mask: mask[(n + 31) / 32] (device u32), bit j of word w =
+ *   target[32 w + j] > 0 (0 past n).
+ *   tvam_loss_threshold_mask / tvam_loss_threshold_probes_mask: tvam_loss_threshold /
+ *   tvam_loss_threshold_probes with voxel i's object bit read at bit mask_bit0 + i
+ *   of mask (a slab of the film: mask_bit0 = its first voxel's index).
+ */
+int tvam_target_mask(const float* target, uint64_t n, uint32_t* mask, void* hip_stream);
+int tvam_loss_threshold_mask(const float* dose, const float* ddose, float alpha,
+                             const uint32_t* mask, uint64_t mask_bit0, uint64_t n, int32_t K,
+                             float tl, float tu, float w_object, float w_void,
+                             float w_limit, float scale, double* out, float* grad,
+                             void* hip_stream);
+int tvam_loss_threshold_probes_mask(const float* dose, const float* ddose,
+                                    const float* alphas, int32_t n_alpha,
+                                    const uint32_t* mask, uint64_t mask_bit0, uint64_t n,
+                                    int32_t K, float tl, float tu, float w_object,
+                                    float w_void, float w_limit, float scale,
+                                    double* out, void* hip_stream);
 
 /* Thread-local message describing the last error ("" if none). */
 const char* tvam_last_error(void);

@@ -176,3 +176,126 @@ def test_device_recursion_matches_host(is_new):
     assert torch.equal(d_dev, d_val)
     # and g.d of the direction itself
     np.testing.assert_allclose(gdz.item(), float(torch.dot(G[1].double(), d_dev.double())), rtol=1e-4)
+
+
+def test_armijo_kernel_matches_host_decision():
+    """tvam_lbfgs_armijo (the first probe batch decided on one device lane) against the host loop of
+    FusedLinearLBFGS.step (lbfgs.py:256-266): the same step size, bit for bit, on probes placed at
+    and around the Armijo bound (ties included), with a device loss (divided over ranks) and a host
+    loss; 0 when no probe passes."""
+    import ctypes
+    from drtvam_amd import _abi
+    lib = _abi.load_library()
+    stream = torch.cuda.current_stream().cuda_stream
+    c1 = 1e-4
+    rng = np.random.default_rng(7)
+    alpha = torch.empty(1, dtype=torch.float32, device='cuda')
+    for case in range(200):
+        nb = int(rng.integers(1, 5))
+        loss = float(rng.uniform(0.1, 10.0)) * (1.0 if case % 5 else 0.0)
+        gdz = -float(rng.uniform(0.0, 5.0))
+        div = float(rng.choice([1.0, 2.0, 8.0]))
+        lv = (loss * div) / div
+        bound = [lv + c1 * (0.5 ** j) * gdz for j in range(nb)]
+        kind = rng.integers(0, 3, size=nb)  # above / at / below the bound
+        probes = [b + (1.0 if k == 0 else (0.0 if k == 1 else -1e-3)) * (abs(b) + 1.0) for b, k in zip(bound, kind)]
+        host = 0.0
+        for j, f in enumerate(probes):
+            if f <= lv + c1 * (1.0 * 0.5 ** j) * (0.0 + gdz):
+                host = 0.5 ** j
+                break
+        pr = torch.tensor(probes, dtype=torch.float64, device='cuda')
+        gd = torch.tensor([gdz], dtype=torch.float64, device='cuda')
+        if case % 2:
+            ld = torch.tensor([loss * div], dtype=torch.float64, device='cuda')
+            _abi.check(lib.tvam_lbfgs_armijo(nb, 1.0, pr.data_ptr(), ld.data_ptr(), 0.0, div, gd.data_ptr(), c1,
+                                             alpha.data_ptr(), None, stream))
+        else:
+            _abi.check(lib.tvam_lbfgs_armijo(nb, 1.0, pr.data_ptr(), None, lv, 1.0, gd.data_ptr(), c1,
+                                             alpha.data_ptr(), None, stream))
+        assert float(alpha.item()) == host, (case, probes, bound)
+    with pytest.raises(ValueError):
+        _abi.check(lib.tvam_lbfgs_armijo(0, 1.0, pr.data_ptr(), None, 1.0, 1.0, gd.data_ptr(), c1,
+                                         alpha.data_ptr(), None, stream))
+
+
+@pytest.mark.parametrize("scale", [1.0, 30.0])
+def test_speculative_update_is_the_host_update(scale):
+    """FusedLinearLBFGS.step with the update launched behind the first probes (tvam_lbfgs_armijo +
+    tvam_axpy_clamp_dev, the host reading the probes on a side stream) against the host-decided
+    update: identical step sizes, probe counts and patterns, bit for bit; scale 30 overshoots, so
+    searches outlast the first batch and the speculative update is discarded."""
+    A, b = _problem(8192, 256, seed=9)
+    A = A * scale
+    key = 'projector.active_data'
+
+    def render(vars_):
+        return A @ vars_[key]
+
+    def loss_steps(vol, dvol, alphas, p):
+        return torch.stack([((vol + a * dvol - b) ** 2).sum().to(torch.float64) for a in alphas])
+
+    x0 = torch.rand(8192, device='cuda') * 0.1
+    runs = {}
+    for spec in (False, True):
+        opt = FusedLinearLBFGS(render_fn=render, clamp_min=0.0, loss_steps=loss_steps)
+        opt.speculate = spec
+        opt[key] = x0
+        trace, xs = [], []
+        for _ in range(10):
+            x = opt[key]
+            vol = A @ x.detach()
+            r = vol - b
+            x.grad = 2.0 * (A.t() @ r)
+            opt.step(vol, None, loss_dev=(r * r).sum().to(torch.float64))
+            trace.append((opt.last_alpha, opt.last_search_steps))
+            xs.append(opt[key].detach().clone())
+        runs[spec] = (trace, xs)
+    assert runs[True][0] == runs[False][0]
+    for a, c in zip(runs[True][1], runs[False][1]):
+        assert torch.equal(a, c)
+    if scale > 1.0:
+        assert max(t[1] for t in runs[True][0]) > FusedLinearLBFGS.probe_batch
+
+
+def test_target_mask_loss_is_the_f32_target_loss():
+    """tvam_loss_threshold(_probes)_mask (the object test read from the target's bit mask) against the
+    f32-target kernels: values to 1e-12 (the blocks' f64 partials meet in atomics, in any order)
+    and the same gradient bit for bit, on the whole film and on slabs at
+    bit offsets that are and are not multiples of 4 and 32 (scalar and float4 paths); greyscale
+    targets (> 0 = object); and ThresholdedLoss rebuilds its cached mask when the target is written."""
+    from drtvam_amd.engine import loss_threshold, loss_threshold_probes, target_mask
+    from drtvam_amd.loss import ThresholdedLoss
+    g = torch.Generator().manual_seed(4)
+    n = 64 * 1000 + 13
+    dose = (torch.rand(n, generator=g) * 1.3).cuda()
+    ddose = (torch.randn(n, generator=g) * 0.2).cuda()
+    tgt = torch.rand(n, generator=g)
+    tgt = torch.where(tgt > 0.55, tgt, torch.where(tgt > 0.5, -tgt, torch.zeros_like(tgt))).cuda()
+    mask = target_mask(tgt)
+    bits = torch.tensor([(int(w) & 0xffffffff) >> j & 1 for w in mask.cpu().tolist() for j in range(32)][:n])
+    assert torch.equal(bits.bool(), (tgt > 0).cpu())
+    args = (2, 0.85, 0.95, 1.0, 1.3, 0.7, 1.0 / n)
+    alphas = [1.0, 0.5, 0.25, 0.125]
+    for z0, z1 in ((0, n), (32 * 500, 32 * 1500), (4 * 301, n - 7), (5, 64 * 999)):
+        d, dd, t = dose[z0:z1], ddose[z0:z1], tgt[z0:z1]
+        g0, g1 = torch.empty_like(d), torch.empty_like(d)
+        v0 = loss_threshold(d, t, *args, grad=g0)
+        v1 = loss_threshold(d, t, *args, grad=g1, mask=mask, mask_bit0=z0)
+        assert float(v0) == pytest.approx(float(v1), rel=1e-12)
+        assert torch.equal(g0, g1)
+        p0 = loss_threshold_probes(d, dd, alphas, t, *args)
+        p1 = loss_threshold_probes(d, dd, alphas, t, *args, mask=mask, mask_bit0=z0)
+        torch.testing.assert_close(p0, p1, rtol=1e-12, atol=0)
+        s0 = loss_threshold(d, t, *args, ddose=dd, alpha=0.3)
+        s1 = loss_threshold(d, t, *args, ddose=dd, alpha=0.3, mask=mask, mask_bit0=z0)
+        assert float(s0) == pytest.approx(float(s1), rel=1e-12)
+    with pytest.raises(ValueError):
+        loss_threshold(dose, tgt, *args, mask=mask, mask_bit0=32)
+    lf = ThresholdedLoss({"K": 2, "tl": 0.85, "tu": 0.95})
+    grad = torch.empty_like(dose)
+    a = float(lf.fused_value_grad(dose, tgt, None, grad))
+    tgt[: n // 2] = 1.0  # in place: the cached mask is rebuilt
+    b = float(lf.fused_value_grad(dose, tgt, None, grad))
+    ref = float(loss_threshold(dose, tgt, 2, lf.tl, lf.tu, 1.0, 1.0, 1.0, 1.0))  # sum reduction
+    assert b == pytest.approx(ref, rel=1e-12) and abs(a - b) > 1e-6 * abs(b)
