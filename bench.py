@@ -236,6 +236,8 @@ def main():
     ap.add_argument("--tile", type=int, default=0)
     ap.add_argument("--zero-skip", action="store_true", help="skip rays whose pattern value is 0 (exact)")
     ap.add_argument("--stats", action="store_true", help="report float-fallback tiles per forward (syncs)")
+    ap.add_argument("--breakdown", type=int, default=3,
+                    help="iterations after the timed ones whose forward / adjoint calls are timed (fwd_ms, adj_ms)")
     ap.add_argument("--cpu-baseline", choices=["auto", "off"], default="auto")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--shard", choices=["auto", "angle", "slab"], default="auto",
@@ -381,7 +383,6 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     prob.proj.kernel_time(True)  # (dominant-kernel launch events from here on; no GPU work)
-    state["on"] = True
     t0 = time.perf_counter()
     # step boundaries as events on the stream every launch goes to (the median of the steps)
     step_ev = [torch.cuda.Event(enable_timing=True)]
@@ -394,9 +395,17 @@ def main():
     if dist:
         dist.barrier()
     t1 = time.perf_counter()
-    state["on"] = False
     kt = prob.proj.kernel_time(False)
     elapsed = t1 - t0
+    # the forward / adjoint call times of the line (fwd_ms / adj_ms): events around each call, taken in
+    # --breakdown iterations after the timed ones (an event record between two kernels idles the GPU
+    # for a few microseconds: none in the timed steps beyond the step boundaries and the dominant
+    # kernel's launch events)
+    state["on"] = True
+    for i in range(args.warmup + args.steps, args.warmup + args.steps + args.breakdown):
+        prob.iteration(i)
+    torch.cuda.synchronize()
+    state["on"] = False
     fwd = [s.elapsed_time(e) for s, e in fwd_ms]
     if fwd_slices:  # per forward: the sum of its slice ranges' times
         for z0, s, e in fwd_slices:
@@ -407,7 +416,7 @@ def main():
     step_ms = sorted(a.elapsed_time(b) for a, b in zip(step_ev[:-1], step_ev[1:]))
     step_med = step_ms[len(step_ms) // 2] if len(step_ms) % 2 else 0.5 * (step_ms[len(step_ms) // 2 - 1] +
                                                                           step_ms[len(step_ms) // 2])
-    fwd_avg = sum(fwd) / len(fwd) / 1e3
+    fwd_avg = sum(fwd) / len(fwd) / 1e3 if fwd else float("nan")
     adj_avg = sum(adj) / len(adj) / 1e3 if adj else float("nan")
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)

@@ -789,8 +789,12 @@ hipError_t tvam_launch_target_mask(const float* target, uint64_t n, uint32_t* ma
     return hipGetLastError();
 }
 
-__device__ __forceinline__ float tvam_loss_grad_elem(float x, bool obj, int K, float tl, float tu, float w_object,
+// KC: the exponent K as a compile-time constant (1..4: tvam_powi unrolled, the same products in the same
+// order), or 0: K at run time
+template <int KC>
+__device__ __forceinline__ float tvam_loss_grad_elem(float x, bool obj, int Kr, float tl, float tu, float w_object,
                                                      float w_void, float w_limit, float& gr) {
+    const int K = KC ? KC : Kr;
     if (obj) {
         const float zo = tu - x, zl = x - 1.0f;
         const float ro = zo > 0.0f ? zo : 0.0f, rl = zl > 0.0f ? zl : 0.0f;
@@ -806,7 +810,7 @@ __device__ __forceinline__ float tvam_loss_grad_elem(float x, bool obj, int K, f
 
 // n4: elements / 4 when dose, ddose, grad (and the f32 target, or a mask offset % 4 == 0) allow
 // float4 accesses, else 0
-template <bool MASK>
+template <bool MASK, int KC>
 __global__ __launch_bounds__(256) void tvam_loss_threshold_kernel(
     const float* __restrict__ dose, const float* __restrict__ ddose, float alpha, const float* __restrict__ target,
     const uint32_t* __restrict__ mask, uint64_t mbit0, uint64_t n, uint64_t n4, int K, float tl, float tu,
@@ -822,10 +826,10 @@ __global__ __launch_bounds__(256) void tvam_loss_threshold_kernel(
         }
         const uint32_t ob = tvam_obj4<MASK>(target, mask, mbit0, t);
         float4 g;
-        acc += (double)tvam_loss_grad_elem(x.x, ob & 1u, K, tl, tu, w_object, w_void, w_limit, g.x);
-        acc += (double)tvam_loss_grad_elem(x.y, ob & 2u, K, tl, tu, w_object, w_void, w_limit, g.y);
-        acc += (double)tvam_loss_grad_elem(x.z, ob & 4u, K, tl, tu, w_object, w_void, w_limit, g.z);
-        acc += (double)tvam_loss_grad_elem(x.w, ob & 8u, K, tl, tu, w_object, w_void, w_limit, g.w);
+        acc += (double)tvam_loss_grad_elem<KC>(x.x, ob & 1u, K, tl, tu, w_object, w_void, w_limit, g.x);
+        acc += (double)tvam_loss_grad_elem<KC>(x.y, ob & 2u, K, tl, tu, w_object, w_void, w_limit, g.y);
+        acc += (double)tvam_loss_grad_elem<KC>(x.z, ob & 4u, K, tl, tu, w_object, w_void, w_limit, g.z);
+        acc += (double)tvam_loss_grad_elem<KC>(x.w, ob & 8u, K, tl, tu, w_object, w_void, w_limit, g.w);
         if (grad)
             reinterpret_cast<float4*>(grad)[t] = make_float4(g.x * scale, g.y * scale, g.z * scale, g.w * scale);
     }
@@ -833,7 +837,7 @@ __global__ __launch_bounds__(256) void tvam_loss_threshold_kernel(
         float x = dose[i];
         if (ddose) x = fmaf(alpha, ddose[i], x);
         float gr;
-        acc += (double)tvam_loss_grad_elem(x, tvam_is_obj<MASK>(target, mask, mbit0, i), K, tl, tu, w_object, w_void,
+        acc += (double)tvam_loss_grad_elem<KC>(x, tvam_is_obj<MASK>(target, mask, mbit0, i), K, tl, tu, w_object, w_void,
                                            w_limit, gr);
         if (grad) grad[i] = gr * scale;
     }
@@ -854,8 +858,10 @@ struct TvamProbeAlphas {
     float a[TVAM_MAX_PROBES];
 };
 
-__device__ __forceinline__ float tvam_loss_elem(float x, bool obj, int K, float tl, float tu, float w_object,
+template <int KC>
+__device__ __forceinline__ float tvam_loss_elem(float x, bool obj, int Kr, float tl, float tu, float w_object,
                                                 float w_void, float w_limit) {
+    const int K = KC ? KC : Kr;
     if (obj) {
         const float zo = tu - x, zl = x - 1.0f;
         const float ro = zo > 0.0f ? zo : 0.0f, rl = zl > 0.0f ? zl : 0.0f;
@@ -866,7 +872,7 @@ __device__ __forceinline__ float tvam_loss_elem(float x, bool obj, int K, float 
     return w_void * tvam_powi(rv, K);
 }
 
-template <bool MASK>
+template <bool MASK, int KC>
 __global__ __launch_bounds__(256) void tvam_loss_probes_kernel(
     const float* __restrict__ dose, const float* __restrict__ ddose, TvamProbeAlphas al, int na,
     const float* __restrict__ target, const uint32_t* __restrict__ mask, uint64_t mbit0, uint64_t n, uint64_t n4, int K,
@@ -878,7 +884,7 @@ __global__ __launch_bounds__(256) void tvam_loss_probes_kernel(
     auto elem = [&](float x0, float dx, bool obj) {
 #pragma unroll
         for (int j = 0; j < TVAM_MAX_PROBES; ++j)
-            if (j < na) acc[j] += (double)tvam_loss_elem(fmaf(al.a[j], dx, x0), obj, K, tl, tu, w_object, w_void, w_limit);
+            if (j < na) acc[j] += (double)tvam_loss_elem<KC>(fmaf(al.a[j], dx, x0), obj, K, tl, tu, w_object, w_void, w_limit);
     };
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x, stride = (uint64_t)gridDim.x * blockDim.x;
     // n4: elements / 4 when the arrays allow float4 loads, else 0
@@ -922,12 +928,24 @@ hipError_t tvam_launch_loss_probes(const float* dose, const float* ddose, const 
     unsigned g = (unsigned)(((v4 ? n4 : n) + 255) / 256);
     if (g > 2048) g = 2048;
     if (g == 0) g = 1;
-    if (mask)
-        hipLaunchKernelGGL(tvam_loss_probes_kernel<true>, dim3(g), dim3(256), 0, stream, dose, ddose, al, na, target,
-                           mask, mbit0, n, n4, K, tl, tu, w_object, w_void, w_limit, scale, out);
-    else
-        hipLaunchKernelGGL(tvam_loss_probes_kernel<false>, dim3(g), dim3(256), 0, stream, dose, ddose, al, na, target,
-                           mask, mbit0, n, n4, K, tl, tu, w_object, w_void, w_limit, scale, out);
+#define TVAM_PROBES(M, KC)                                                                                    \
+    hipLaunchKernelGGL((tvam_loss_probes_kernel<M, KC>), dim3(g), dim3(256), 0, stream, dose, ddose, al, na, target, \
+                       mask, mbit0, n, n4, K, tl, tu, w_object, w_void, w_limit, scale, out)
+#define TVAM_PROBES_K(M)                     \
+    switch (K) {                             \
+        case 1: TVAM_PROBES(M, 1); break;    \
+        case 2: TVAM_PROBES(M, 2); break;    \
+        case 3: TVAM_PROBES(M, 3); break;    \
+        case 4: TVAM_PROBES(M, 4); break;    \
+        default: TVAM_PROBES(M, 0); break;   \
+    }
+    if (mask) {
+        TVAM_PROBES_K(true)
+    } else {
+        TVAM_PROBES_K(false)
+    }
+#undef TVAM_PROBES_K
+#undef TVAM_PROBES
     return hipGetLastError();
 }
 
@@ -941,11 +959,23 @@ hipError_t tvam_launch_loss_threshold(const float* dose, const float* ddose, flo
     unsigned g = (unsigned)(((v4 ? n4 : n) + 255) / 256);
     if (g > 2048) g = 2048;
     if (g == 0) g = 1;
-    if (mask)
-        hipLaunchKernelGGL(tvam_loss_threshold_kernel<true>, dim3(g), dim3(256), 0, stream, dose, ddose, alpha, target,
-                           mask, mbit0, n, n4, K, tl, tu, w_object, w_void, w_limit, scale, out, grad);
-    else
-        hipLaunchKernelGGL(tvam_loss_threshold_kernel<false>, dim3(g), dim3(256), 0, stream, dose, ddose, alpha, target,
-                           mask, mbit0, n, n4, K, tl, tu, w_object, w_void, w_limit, scale, out, grad);
+#define TVAM_LOSS(M, KC)                                                                                           \
+    hipLaunchKernelGGL((tvam_loss_threshold_kernel<M, KC>), dim3(g), dim3(256), 0, stream, dose, ddose, alpha, target, \
+                       mask, mbit0, n, n4, K, tl, tu, w_object, w_void, w_limit, scale, out, grad)
+#define TVAM_LOSS_K(M)                     \
+    switch (K) {                           \
+        case 1: TVAM_LOSS(M, 1); break;    \
+        case 2: TVAM_LOSS(M, 2); break;    \
+        case 3: TVAM_LOSS(M, 3); break;    \
+        case 4: TVAM_LOSS(M, 4); break;    \
+        default: TVAM_LOSS(M, 0); break;   \
+    }
+    if (mask) {
+        TVAM_LOSS_K(true)
+    } else {
+        TVAM_LOSS_K(false)
+    }
+#undef TVAM_LOSS_K
+#undef TVAM_LOSS
     return hipGetLastError();
 }

@@ -492,8 +492,8 @@ hipError_t tvam_launch_axpy_clamp(uint64_t n, const float* p, float alpha, const
 // a_j for the first probe j with f_j <= loss + c1 a_j g.d, a_j = a0 / 2^j (lbfgs.py:256-266), in
 // the host loop's fp64 operations and order (no contraction); 0 when no probe passes (the host
 // then discards the update launched behind it).  loss = loss_dev[0] / loss_div, or loss_host.
-// report (optional, e.g. pinned host memory the host reads once the kernel is done, no copy kernel):
-// the undivided loss, g.d, the probes and the chosen alpha, as f64.
+// report (optional, e.g. pinned host memory the host polls, no copy kernel and no event): the undivided
+// loss, g.d, the probes and the chosen alpha, as f64, then 1.0 once they are visible system-wide.
 __global__ void tvam_armijo_kernel(int nprobe, double a0, const double* __restrict__ probes,
                                    const double* __restrict__ loss_dev, double loss_host, double loss_div,
                                    const double* __restrict__ gdz, double c1, float* __restrict__ alpha,
@@ -517,6 +517,8 @@ __global__ void tvam_armijo_kernel(int nprobe, double a0, const double* __restri
         report[1] = gdz[0];
         for (int j = 0; j < nprobe; ++j) report[2 + j] = probes[j];
         report[2 + nprobe] = (double)r;
+        __threadfence_system();
+        report[3 + nprobe] = 1.0;
         __threadfence_system();
     }
 }

@@ -12,6 +12,7 @@ only host syncs are the Armijo decisions (as in the reference, lbfgs.py:263).
 from __future__ import annotations
 
 import ctypes
+import time
 
 import torch
 
@@ -374,9 +375,12 @@ class FusedLinearLBFGS(LinearLBFGS):
             import torch.distributed as _d
             div = float(_d.get_world_size())
         rep = getattr(self, '_report', None)
-        if rep is None or rep.numel() < 3 + nb:
-            rep = self._report = torch.zeros(3 + self.probe_batch, dtype=torch.float64, pin_memory=True)
+        if rep is None or rep.numel() < 4 + nb:
+            rep = self._report = torch.zeros(4 + max(nb, self.probe_batch), dtype=torch.float64, pin_memory=True)
+            self._report_np = rep.numpy()
             self._alpha_dev = torch.empty(1, dtype=torch.float32, device=dev)
+        rnp = self._report_np
+        rnp[3 + nb] = 0.0  # the kernel's done flag
         alpha_dev = self._alpha_dev
         if alpha_dev.device != dev:
             alpha_dev = self._alpha_dev = torch.empty(1, dtype=torch.float32, device=dev)
@@ -385,13 +389,20 @@ class FusedLinearLBFGS(LinearLBFGS):
         _abi.check(lib.tvam_lbfgs_armijo(nb, 1.0, fdc.data_ptr(), loss_cell.data_ptr() if loss_cell is not None else None,
                                          loss_host, div, gdz.data_ptr(), c1, alpha_dev.data_ptr(), rep.data_ptr(),
                                          main.cuda_stream))
-        ev = torch.cuda.Event()
-        ev.record(main)
         out = torch.empty_like(pf)
         _abi.check(lib.tvam_axpy_clamp_dev(pf.numel(), pf.data_ptr(), alpha_dev.data_ptr(), search[k].data_ptr(), lo,
                                            out.data_ptr(), main.cuda_stream))
-        ev.synchronize()
-        v = rep.tolist()
+        # poll the done flag (an event recorded between the decision and the update would idle the GPU
+        # for a few microseconds at that boundary)
+        polls, t_end = 0, None
+        while rnp[3 + nb] == 0.0:
+            polls += 1
+            if polls % 4096 == 0:
+                now = time.perf_counter()
+                t_end = t_end or now + 60.0
+                if now > t_end:
+                    raise RuntimeError("tvam_lbfgs_armijo: no report after 60 s")
+        v = [float(x) for x in rnp[:3 + nb]]
         lv = v[0] / div if divided else (v[0] if loss_cell is not None else loss_host)
         return (out, v[2 + nb]), float(lv), 0.0 + v[1], v[2:2 + nb]
 

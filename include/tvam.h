@@ -339,8 +339,9 @@ int tvam_plan_path(const tvam_plan* plan);
  *   for the first j < nprobe with probes[j] <= loss + c1 a_j gdz[0] (device f64
  *   probes and g.d; loss = loss_dev[0] / loss_div, or loss_host when loss_dev is
  *   NULL), evaluated as the host loop evaluates it in f64; 0 when none passes.
- *   report (may be NULL; device-visible, e.g. pinned host memory read after the
- *   kernel): loss_dev[0] (or loss_host) | gdz[0] | probes[0..nprobe) | alpha, f64.
+ *   report (may be NULL; device-visible, e.g. pinned host memory the host polls):
+ *   loss_dev[0] (or loss_host) | gdz[0] | probes[0..nprobe) | alpha | 1.0, f64, the
+ *   final 1.0 written after the others are visible system-wide.
  * tvam_axpy_clamp_dev: tvam_axpy_clamp with alpha read from device memory
  *   (tvam_lbfgs_armijo's output), so the update follows the probes on the stream
  *   without a host round trip.  (Both ABI v12.)
