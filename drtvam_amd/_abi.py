@@ -145,7 +145,7 @@ EXPORTS = {
     "tvam_lbfgs_direction_rows": (ctypes.c_int, [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64, _P,
                                                  ctypes.c_int32, _P, _P, _P, _P, _P]),
     "tvam_axpy_clamp": (ctypes.c_int, [ctypes.c_uint64, _P, ctypes.c_float, _P, ctypes.c_float, _P, _P]),
-    "tvam_axpy_clamp_dev": (ctypes.c_int, [ctypes.c_uint64, _P, _P, _P, ctypes.c_float, _P, _P]),
+    "tvam_axpy_clamp_dev": (ctypes.c_int, [ctypes.c_uint64, _P, _P, _P, ctypes.c_float, _P, _P, _P]),
     "tvam_lbfgs_armijo": (ctypes.c_int, [ctypes.c_int32, ctypes.c_double, _P, _P, ctypes.c_double, ctypes.c_double,
                                          _P, ctypes.c_double, _P, _P, _P]),
     "tvam_row_slices": (ctypes.c_int, [ctypes.POINTER(TvamDesc), _P]),

@@ -320,7 +320,7 @@ hipError_t tvam_launch_lbfgs_direction_dev(uint64_t n, const float* g, int h, co
                                            uint64_t nseg = 0, uint64_t seg_len = 0, uint64_t seg_stride = 0,
                                            uint64_t seg_off = 0);
 hipError_t tvam_launch_axpy_clamp(uint64_t n, const float* p, float alpha, const float* d, float lo, float* out,
-                                  hipStream_t stream, const float* alpha_dev = nullptr);
+                                  hipStream_t stream, const float* alpha_dev = nullptr, float* s_out = nullptr);
 hipError_t tvam_launch_armijo(int nprobe, double a0, const double* probes, const double* loss_dev, double loss_host,
                               double loss_div, const double* gdz, double c1, float* alpha, double* report,
                               hipStream_t stream);

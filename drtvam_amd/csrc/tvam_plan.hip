@@ -2094,8 +2094,12 @@ extern "C" int tvam_lbfgs_history(uint64_t n, const float* p, const float* p_old
     if (!g || !work || !dots || (h > 0 && (!S || !Y))) return fail(TVAM_ERR_INVALID, "null argument");
     if (h < 0 || h > 7) return fail(TVAM_ERR_INVALID, "tvam_lbfgs_history: 0 <= h <= 7 retained pairs");
     if (p_old && (!p || !g_old || !s_new || !y_new)) return fail(TVAM_ERR_INVALID, "null argument");
+    // p_old NULL with g_old given: a new pair whose s_new already holds p - p_old (read, not written)
+    const bool spre = !p_old && g_old;
+    if (spre && (!s_new || !y_new)) return fail(TVAM_ERR_INVALID, "tvam_lbfgs_history: precomputed s_new needs s_new, y_new");
     bool ok = aligned16(g) && (!p_old || (aligned16(p) && aligned16(p_old) && aligned16(g_old) &&
-                                          aligned16(s_new) && aligned16(y_new)));
+                                          aligned16(s_new) && aligned16(y_new))) &&
+              (!spre || (aligned16(g_old) && aligned16(s_new) && aligned16(y_new)));
     for (int j = 0; j < h; ++j) ok = ok && S[j] && Y[j] && aligned16(S[j]) && aligned16(Y[j]);
     if (!ok) return fail(TVAM_ERR_INVALID, "tvam_lbfgs_history: vectors must be 16-byte aligned");
     hipError_t e = tvam_launch_lbfgs_history(n, p, p_old, g, g_old, h, S, Y, s_new, y_new, work, dots,
@@ -2110,6 +2114,7 @@ extern "C" int tvam_lbfgs_history_rows(uint64_t nseg, uint64_t seg_len, uint64_t
     if (!g || !work || !dots || (h > 0 && (!S || !Y))) return fail(TVAM_ERR_INVALID, "null argument");
     if (h < 0 || h > 7) return fail(TVAM_ERR_INVALID, "tvam_lbfgs_history_rows: 0 <= h <= 7 retained pairs");
     if (p_old && (!p || !g_old || !s_new || !y_new)) return fail(TVAM_ERR_INVALID, "null argument");
+    if (!p_old && g_old) return fail(TVAM_ERR_INVALID, "tvam_lbfgs_history_rows: g_old without p_old");
     if (nseg == 0 || seg_len == 0 || seg_len % 4 || seg_stride % 4 || seg_off % 4 || seg_len > seg_stride ||
         seg_len / 4 > 0xffffffffull)
         return fail(TVAM_ERR_INVALID, "tvam_lbfgs_history_rows: segments of a multiple of 4 entries, 4-aligned");
@@ -2183,11 +2188,13 @@ extern "C" int tvam_axpy_clamp(uint64_t n, const float* p, float alpha, const fl
 }
 
 extern "C" int tvam_axpy_clamp_dev(uint64_t n, const float* p, const float* alpha, const float* d, float lo,
-                                   float* out, void* stream) {
+                                   float* out, float* s_out, void* stream) {
     if (!p || !alpha || !d || !out) return fail(TVAM_ERR_INVALID, "null argument");
-    if (!aligned16(p) || !aligned16(d) || !aligned16(out))
+    if (!aligned16(p) || !aligned16(d) || !aligned16(out) || (s_out && !aligned16(s_out)))
         return fail(TVAM_ERR_INVALID, "tvam_axpy_clamp_dev: vectors must be 16-byte aligned");
-    hipError_t e = tvam_launch_axpy_clamp(n, p, 0.0f, d, lo, out, (hipStream_t)stream, alpha);
+    if (s_out && (s_out == p || s_out == out || s_out == d))
+        return fail(TVAM_ERR_INVALID, "tvam_axpy_clamp_dev: s_out must not alias p, d or out");
+    hipError_t e = tvam_launch_axpy_clamp(n, p, 0.0f, d, lo, out, (hipStream_t)stream, alpha, s_out);
     return e == hipSuccess ? 0 : hip_fail(e, "axpy launch");
 }
 

@@ -101,7 +101,9 @@ struct HistLayout {
     static constexpr int ND = (NEW ? 5 * HT : 2 * HT) + 1;
 };
 
-template <int H, bool NEW, bool SEG = false>
+// SPRE: s_new already holds p - p_old (written by the previous step's update, tvam_axpy_clamp_dev's
+// s_out): read instead of formed from p and p_old (two vector reads and a write fewer)
+template <int H, bool NEW, bool SEG = false, bool SPRE = false>
 __global__ __launch_bounds__(TVAM_VB) void tvam_lbfgs_hist_kernel(uint64_t n, const float* __restrict__ p,
                                                                    const float* __restrict__ p_old,
                                                                    const float* __restrict__ g,
@@ -150,8 +152,12 @@ __global__ __launch_bounds__(TVAM_VB) void tvam_lbfgs_hist_kernel(uint64_t n, co
             el[u].g4 = vld(g, i);
             el[u].p4 = el[u].po4 = el[u].go4 = make_float4(0, 0, 0, 0);
             if (NEW) {
-                el[u].p4 = vld(p, i);
-                el[u].po4 = vld(p_old, i);
+                if (SPRE) {
+                    el[u].p4 = vld(s_new, i);  // s_new = p - p_old, with p_old = 0 below
+                } else {
+                    el[u].p4 = vld(p, i);
+                    el[u].po4 = vld(p_old, i);
+                }
                 el[u].go4 = vld(g_old, i);
             }
 #pragma unroll
@@ -177,7 +183,7 @@ __global__ __launch_bounds__(TVAM_VB) void tvam_lbfgs_hist_kernel(uint64_t n, co
             TVAM_LANE(x) TVAM_LANE(y) TVAM_LANE(z) TVAM_LANE(w)
 #undef TVAM_LANE
             if (NEW) {
-                reinterpret_cast<float4*>(s_new)[i] = sn4;
+                if (!SPRE) reinterpret_cast<float4*>(s_new)[i] = sn4;
                 reinterpret_cast<float4*>(y_new)[i] = yn4;
             }
         }
@@ -190,9 +196,10 @@ __global__ __launch_bounds__(TVAM_VB) void tvam_lbfgs_hist_kernel(uint64_t n, co
             yv[j] = hv.y[j][i];
         }
         float sn, yn;
-        visit(NEW ? p[i] : 0.0f, NEW ? p_old[i] : 0.0f, g[i], NEW ? g_old[i] : 0.0f, sv, yv, sn, yn);
+        visit(NEW ? (SPRE ? s_new[i] : p[i]) : 0.0f, NEW && !SPRE ? p_old[i] : 0.0f, g[i], NEW ? g_old[i] : 0.0f, sv,
+              yv, sn, yn);
         if (NEW) {
-            s_new[i] = sn;
+            if (!SPRE) s_new[i] = sn;
             y_new[i] = yn;
         }
     }
@@ -226,6 +233,9 @@ static hipError_t launch_hist(uint64_t n, const float* p, const float* p_old, co
     if (sg.len4)
         hipLaunchKernelGGL((tvam_lbfgs_hist_kernel<H, NEW, true>), dim3(nb), dim3(TVAM_VB), 0, stream, n, p, p_old, g,
                            g_old, hv, s_new, y_new, work, sg);
+    else if (NEW && !p_old)  // s_new precomputed (tvam_lbfgs_history: g_old given, p_old NULL)
+        hipLaunchKernelGGL((tvam_lbfgs_hist_kernel<H, NEW, false, true>), dim3(nb), dim3(TVAM_VB), 0, stream, n, p,
+                           p_old, g, g_old, hv, s_new, y_new, work, sg);
     else
         hipLaunchKernelGGL((tvam_lbfgs_hist_kernel<H, NEW>), dim3(nb), dim3(TVAM_VB), 0, stream, n, p, p_old, g,
                            g_old, hv, s_new, y_new, work, sg);
@@ -263,7 +273,7 @@ hipError_t tvam_launch_lbfgs_history(uint64_t n, const float* p, const float* p_
         sg.stride4 = seg_stride / 4;
         sg.off4 = seg_off / 4;
     }
-    if (p_old) return dispatch_hist<true>(h, n, p, p_old, g, g_old, hv, s_new, y_new, work, dots, stream, sg);
+    if (p_old || g_old) return dispatch_hist<true>(h, n, p, p_old, g, g_old, hv, s_new, y_new, work, dots, stream, sg);
     return dispatch_hist<false>(h, n, p, p_old, g, g_old, hv, s_new, y_new, work, dots, stream, sg);
 }
 
@@ -463,26 +473,35 @@ hipError_t tvam_launch_lbfgs_direction_dev(uint64_t n, const float* g, int h, co
 
 // ---------------------------------------------------------------------------
 // alpha_dev (tvam_axpy_clamp_dev): the step size read from device memory, tvam_armijo_kernel's pick
+// s_out (optional): the next history pair's s = out - p (the fp32 difference tvam_lbfgs_history forms
+// from p_new and p_old, so that pass reads it instead of both vectors)
 __global__ __launch_bounds__(TVAM_VB) void tvam_axpy_clamp_kernel(uint64_t n, const float* __restrict__ p, float alpha,
                                                                   const float* __restrict__ d, float lo,
                                                                   float* __restrict__ out,
-                                                                  const float* __restrict__ alpha_dev) {
+                                                                  const float* __restrict__ alpha_dev,
+                                                                  float* __restrict__ s_out) {
     if (alpha_dev) alpha = alpha_dev[0];
     const uint64_t n4 = n / 4, stride = (uint64_t)gridDim.x * blockDim.x;
     const uint64_t tid = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x;
     for (uint64_t i = tid; i < n4; i += stride) {
         const float4 p4 = reinterpret_cast<const float4*>(p)[i];
         const float4 d4 = reinterpret_cast<const float4*>(d)[i];
-        reinterpret_cast<float4*>(out)[i] = make_float4(fmaxf(fmaf(alpha, d4.x, p4.x), lo), fmaxf(fmaf(alpha, d4.y, p4.y), lo),
-                                                        fmaxf(fmaf(alpha, d4.z, p4.z), lo), fmaxf(fmaf(alpha, d4.w, p4.w), lo));
+        const float4 o = make_float4(fmaxf(fmaf(alpha, d4.x, p4.x), lo), fmaxf(fmaf(alpha, d4.y, p4.y), lo),
+                                     fmaxf(fmaf(alpha, d4.z, p4.z), lo), fmaxf(fmaf(alpha, d4.w, p4.w), lo));
+        reinterpret_cast<float4*>(out)[i] = o;
+        if (s_out) reinterpret_cast<float4*>(s_out)[i] = make_float4(o.x - p4.x, o.y - p4.y, o.z - p4.z, o.w - p4.w);
     }
-    for (uint64_t i = 4 * n4 + tid; i < n; i += stride) out[i] = fmaxf(fmaf(alpha, d[i], p[i]), lo);
+    for (uint64_t i = 4 * n4 + tid; i < n; i += stride) {
+        const float o = fmaxf(fmaf(alpha, d[i], p[i]), lo);
+        out[i] = o;
+        if (s_out) s_out[i] = o - p[i];
+    }
 }
 
 hipError_t tvam_launch_axpy_clamp(uint64_t n, const float* p, float alpha, const float* d, float lo, float* out,
-                                  hipStream_t stream, const float* alpha_dev) {
+                                  hipStream_t stream, const float* alpha_dev, float* s_out) {
     hipLaunchKernelGGL(tvam_axpy_clamp_kernel, dim3(2048), dim3(TVAM_VB), 0, stream, n, p, alpha, d, lo, out,
-                       alpha_dev);
+                       alpha_dev, s_out);
     return hipGetLastError();
 }
 

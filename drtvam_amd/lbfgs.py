@@ -390,8 +390,16 @@ class FusedLinearLBFGS(LinearLBFGS):
                                          loss_host, div, gdz.data_ptr(), c1, alpha_dev.data_ptr(), rep.data_ptr(),
                                          main.cuda_stream))
         out = torch.empty_like(pf)
+        # the next step's new pair goes to the first free ring slot, or evicts the oldest: its s = out - p
+        # is written there now (the slot's old pair, if any, is past its last read: this step's direction)
+        st = self.state[k]
+        nxt = st['free'][0] if st['free'] else st['slots'][0]
+        pre = None
+        if st['p_old'] is not None and st['p_old'].data_ptr() == pf.data_ptr():
+            pre = {'slot': nxt, 'out': out, 'out_v': out._version, 'p': st['p_old'], 'p_v': st['p_old']._version}
         _abi.check(lib.tvam_axpy_clamp_dev(pf.numel(), pf.data_ptr(), alpha_dev.data_ptr(), search[k].data_ptr(), lo,
-                                           out.data_ptr(), main.cuda_stream))
+                                           out.data_ptr(), st['S_ptr'][nxt] if pre is not None else None,
+                                           main.cuda_stream))
         # poll the done flag (an event recorded between the decision and the update would idle the GPU
         # for a few microseconds at that boundary)
         polls, t_end = 0, None
@@ -404,7 +412,7 @@ class FusedLinearLBFGS(LinearLBFGS):
                     raise RuntimeError("tvam_lbfgs_armijo: no report after 60 s")
         v = [float(x) for x in rnp[:3 + nb]]
         lv = v[0] / div if divided else (v[0] if loss_cell is not None else loss_host)
-        return (out, v[2 + nb]), float(lv), 0.0 + v[1], v[2:2 + nb]
+        return (out, v[2 + nb], pre), float(lv), 0.0 + v[1], v[2:2 + nb]
 
     @staticmethod
     def _stream(dev):
@@ -460,8 +468,15 @@ class FusedLinearLBFGS(LinearLBFGS):
             S_ptrs = (ctypes.c_void_p * max(h, 1))(*[st['S_ptr'][j] for j in kept])
             Y_ptrs = (ctypes.c_void_p * max(h, 1))(*[st['Y_ptr'][j] for j in kept])
             slot = st['free'][0] if new else None
+            # the last update already wrote this pair's s = p - p_old into its slot (s_out of
+            # tvam_axpy_clamp_dev) when p is still that update's output and p_old its input, unchanged
+            sp, st['s_pre'] = st.get('s_pre'), None
+            spre = (new and sp is not None and sp['slot'] == slot and sp['out'].data_ptr() == pf.data_ptr()
+                    and sp['out']._version == sp['out_v'] and pf._version == sp['out_v']
+                    and sp['p'] is st['p_old'] and st['p_old']._version == sp['p_v'])
             _abi.check(lib.tvam_lbfgs_history(
-                n, pf.data_ptr() if new else None, st['p_old'].data_ptr() if new else None, g.data_ptr(),
+                n, pf.data_ptr() if new and not spre else None,
+                st['p_old'].data_ptr() if new and not spre else None, g.data_ptr(),
                 st['g_old'].data_ptr() if new else None, h, S_ptrs, Y_ptrs,
                 st['S_ptr'][slot] if new else None, st['Y_ptr'][slot] if new else None,
                 st['work'].data_ptr(), st['dots'].data_ptr(), stream))
@@ -563,9 +578,12 @@ class FusedLinearLBFGS(LinearLBFGS):
         self.last_search_steps = steps
 
         if spec is not None and steps <= self.probe_batch and alpha == spec[1]:
-            # the device picked the same step size in the same f64 arithmetic: its update stands
+            # the device picked the same step size in the same f64 arithmetic: its update stands (and
+            # the s = p_new - p it wrote into the next pair's slot)
             (k, p), = self.variables.items()
             self.variables[k] = spec[0].reshape(p.shape).requires_grad_(True)
+            if spec[2] is not None:
+                self.state[k]['s_pre'] = spec[2]
             return loss_v
         for k, p in self.variables.items():
             pf = _aligned(p.detach().reshape(-1))

@@ -314,7 +314,10 @@ int tvam_plan_path(const tvam_plan* plan);
  *   pairs S[j], Y[j] (oldest first, 0 <= h <= 7) followed by the new pair,
  *   writes to dots (f64): s_j.g | y_j.g | s_new.y_j | s_j.y_new | y_new.y_j
  *   (h + 1 entries each) | g.g.  With p_old == NULL only s_j.g | y_j.g | g.g
- *   (h entries each).  work: >= TVAM_LBFGS_WORK_DOUBLES f64 of scratch.
+ *   (h entries each).  With p_old == NULL and g_old != NULL (ABI v12): the new
+ *   pair's s_new already holds p - p_old (tvam_axpy_clamp_dev's s_out) and is
+ *   read, y_new formed; the same dots as the p_old path.  work: >=
+ *   TVAM_LBFGS_WORK_DOUBLES f64 of scratch.
  * tvam_lbfgs_direction: d = cg g + sum_j (cs[j] S[j] + cy[j] Y[j]), h <= 8.
  * tvam_axpy_clamp: out = max(p + alpha d, lo) (out may alias p).
  * tvam_lbfgs_coef: the two-loop recursion (lbfgs.py:221-243) on the device, in
@@ -344,7 +347,8 @@ int tvam_plan_path(const tvam_plan* plan);
  *   final 1.0 written after the others are visible system-wide.
  * tvam_axpy_clamp_dev: tvam_axpy_clamp with alpha read from device memory
  *   (tvam_lbfgs_armijo's output), so the update follows the probes on the stream
- *   without a host round trip.  (Both ABI v12.)
+ *   without a host round trip; s_out (may be NULL, no alias of p / d / out) =
+ *   out - p, the next step's s_new.  (Both ABI v12.)
  */
 #define TVAM_LBFGS_WORK_DOUBLES (2048 * 64)
 int tvam_lbfgs_history(uint64_t n, const float* p, const float* p_old, const float* g, const float* g_old,
@@ -366,7 +370,7 @@ int tvam_lbfgs_direction_rows(uint64_t nseg, uint64_t seg_len, uint64_t seg_stri
 int tvam_axpy_clamp(uint64_t n, const float* p, float alpha, const float* d, float lo, float* out,
                     void* hip_stream);
 int tvam_axpy_clamp_dev(uint64_t n, const float* p, const float* alpha, const float* d, float lo, float* out,
-                        void* hip_stream);
+                        float* s_out, void* hip_stream);
 int tvam_lbfgs_armijo(int32_t nprobe, double alpha0, const double* probes, const double* loss_dev, double loss_host,
                       double loss_div, const double* gdz, double c1, float* alpha, double* report,
                       void* hip_stream);

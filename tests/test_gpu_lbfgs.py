@@ -299,3 +299,45 @@ def test_target_mask_loss_is_the_f32_target_loss():
     b = float(lf.fused_value_grad(dose, tgt, None, grad))
     ref = float(loss_threshold(dose, tgt, 2, lf.tl, lf.tu, 1.0, 1.0, 1.0, 1.0))  # sum reduction
     assert b == pytest.approx(ref, rel=1e-12) and abs(a - b) > 1e-6 * abs(b)
+
+
+def test_history_with_precomputed_s():
+    """tvam_lbfgs_history with the new pair's s already in its slot (p_old NULL, g_old given: written by
+    tvam_axpy_clamp_dev's s_out) against the pass that forms s = p - p_old: the same dots and y, bit for
+    bit, and the update's s_out equal to out - p."""
+    import ctypes
+    from drtvam_amd import _abi
+    lib = _abi.load_library()
+    n, m = (1 << 16) + 12, 7
+    gen = torch.Generator().manual_seed(21)
+    P0 = torch.rand(n, generator=gen).cuda()
+    D = torch.randn(n, generator=gen).cuda()
+    G = torch.randn(2, n, generator=gen).cuda()
+    S = torch.randn(m, n, generator=gen).cuda() * 0.1
+    Y = S * 0.5 + torch.randn(m, n, generator=gen).cuda() * 0.05
+    ptr = lambda t: ctypes.c_void_p(t.data_ptr())
+    stream = torch.cuda.current_stream().cuda_stream
+    alpha = torch.tensor([0.25], dtype=torch.float32, device='cuda')
+    P1 = torch.empty_like(P0)
+    s_pre = torch.empty_like(P0)
+    _abi.check(lib.tvam_axpy_clamp_dev(n, ptr(P0), ptr(alpha), ptr(D), 0.0, ptr(P1), ptr(s_pre), stream))
+    assert torch.equal(s_pre, P1 - P0)
+    assert torch.equal(P1, torch.clamp_min(P0 + 0.25 * D, 0.0))
+    h = 4
+    Sp = (ctypes.c_void_p * m)(*[S[j].data_ptr() for j in range(h)])
+    Yp = (ctypes.c_void_p * m)(*[Y[j].data_ptr() for j in range(h)])
+    work = torch.empty(_abi.LBFGS_WORK_DOUBLES, dtype=torch.float64, device='cuda')
+    res = []
+    for pre in (False, True):
+        s_new = s_pre.clone() if pre else torch.empty_like(P0)
+        y_new = torch.empty_like(P0)
+        dots = torch.zeros(5 * (m + 1) + 1, dtype=torch.float64, device='cuda')
+        _abi.check(lib.tvam_lbfgs_history(n, None if pre else ptr(P1), None if pre else ptr(P0), ptr(G[1]), ptr(G[0]),
+                                          h, Sp, Yp, ptr(s_new), ptr(y_new), ptr(work), ptr(dots), stream))
+        res.append((s_new, y_new, dots))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
+    assert torch.equal(res[0][2], res[1][2])
+    with pytest.raises(ValueError):  # g_old without p_old in the row-band variant
+        _abi.check(lib.tvam_lbfgs_history_rows(1, 64, 64, 0, None, None, ptr(G[1]), ptr(G[0]), h, Sp, Yp,
+                                               ptr(s_pre), ptr(P1), ptr(work), ptr(res[0][2]), stream))
