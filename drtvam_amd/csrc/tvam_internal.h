@@ -22,6 +22,8 @@ int tvam_knob(const char* name, int def);
 enum TvamKtKind { TVAM_KT_PLANAR = 0, TVAM_KT_TILE = 1, TVAM_KT_BRICK = 2 };
 void tvam_kt_begin(hipStream_t stream, int kind);
 void tvam_kt_end(hipStream_t stream, int kind);
+// the next timer event pair for a launch that records them itself (hipExtLaunchKernelGGL); false: untimed
+bool tvam_kt_take(int kind, hipEvent_t* start, hipEvent_t* stop);
 
 // Device tables that drive one tile launch.
 struct TvamTiles {

@@ -411,6 +411,15 @@ void tvam_kt_begin(hipStream_t stream, int kind) {
     if (kt_here(kind)) (void)hipEventRecord(g_kt.ev[g_kt.n], stream);
 }
 
+bool tvam_kt_take(int kind, hipEvent_t* start, hipEvent_t* stop) {
+    std::lock_guard<std::mutex> lk(g_kt.mu);
+    if (!kt_here(kind)) return false;
+    *start = g_kt.ev[g_kt.n];
+    *stop = g_kt.ev[g_kt.n + 1];
+    g_kt.n += 2;
+    return true;
+}
+
 void tvam_kt_end(hipStream_t stream, int kind) {
     std::lock_guard<std::mutex> lk(g_kt.mu);
     if (!kt_here(kind)) return;

@@ -29,6 +29,8 @@
 // slice's.
 #include "tvam_internal.h"
 
+#include <hip/hip_ext.h>
+
 #include <algorithm>
 
 #define TVAM_PB 256
@@ -932,57 +934,61 @@ hipError_t tvam_launch_refr_model(const TvamConsts& k, const TvamPlanar& pl, con
     return hipGetLastError();
 }
 
+// the kernel timer's start / stop events of the next forward launch (tvam_kt_take), recorded by the
+// launch itself (hipExtLaunchKernelGGL: no event packets between the kernels); null: untimed
+static thread_local hipEvent_t g_fwd_ev[2] = {nullptr, nullptr};
+
 template <int Z, int NC>
 static void launch_fwd(dim3 grid, size_t lds, hipStream_t stream, const TvamConsts& k, const TvamPlanar& pl,
                        const float* pat, float* dose) {
     if (pl.fwd_bin && pl.fwd_dma) {  // binned slabs staged by LDS-DMA
         if (pl.fwd_refr)
-            hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, 2, false, 1, 2, true, true, true>), grid, dim3(TVAM_PB), lds,
-                               stream, k, pl, pat, dose);
+            hipExtLaunchKernelGGL((tvam_fwd_planar_kernel<Z, 2, false, 1, 2, true, true, true>), grid, dim3(TVAM_PB), lds,
+                               stream, g_fwd_ev[0], g_fwd_ev[1], 0, k, pl, pat, dose);
         else if (pl.fwd_ab == 1)
-            hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 1, 1, true, false, true>), grid, dim3(TVAM_PB), lds,
-                               stream, k, pl, pat, dose);
+            hipExtLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 1, 1, true, false, true>), grid, dim3(TVAM_PB), lds,
+                               stream, g_fwd_ev[0], g_fwd_ev[1], 0, k, pl, pat, dose);
         else
-            hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 1, 2, true, false, true>), grid, dim3(TVAM_PB), lds,
-                               stream, k, pl, pat, dose);
+            hipExtLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 1, 2, true, false, true>), grid, dim3(TVAM_PB), lds,
+                               stream, g_fwd_ev[0], g_fwd_ev[1], 0, k, pl, pat, dose);
         return;
     }
     if (pl.fwd_refr) {  // refracted chords: binned staging, 2 angles per barrier, candidates per (tile, angle)
         if (pl.fwd_pf == 1)
-            hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, 2, false, 1, 2, true, true>), grid, dim3(TVAM_PB), lds, stream,
+            hipExtLaunchKernelGGL((tvam_fwd_planar_kernel<Z, 2, false, 1, 2, true, true>), grid, dim3(TVAM_PB), lds, stream, g_fwd_ev[0], g_fwd_ev[1], 0,
                                k, pl, pat, dose);
         else
-            hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, 2, false, 2, 2, true, true>), grid, dim3(TVAM_PB), lds, stream,
+            hipExtLaunchKernelGGL((tvam_fwd_planar_kernel<Z, 2, false, 2, 2, true, true>), grid, dim3(TVAM_PB), lds, stream, g_fwd_ev[0], g_fwd_ev[1], 0,
                                k, pl, pat, dose);
         return;
     }
     if constexpr (Z > 32) {  // deep slabs (thin-slab shards, 400-slice films in 10 chunks): binned staging only
         if (pl.fwd_pf == 1)
-            hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 1, 2, true>), grid, dim3(TVAM_PB), lds, stream, k, pl,
+            hipExtLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 1, 2, true>), grid, dim3(TVAM_PB), lds, stream, g_fwd_ev[0], g_fwd_ev[1], 0, k, pl,
                                pat, dose);
         else
-            hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 2, 2, true>), grid, dim3(TVAM_PB), lds, stream, k, pl,
+            hipExtLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 2, 2, true>), grid, dim3(TVAM_PB), lds, stream, g_fwd_ev[0], g_fwd_ev[1], 0, k, pl,
                                pat, dose);
         return;
     }
     if (pl.fwd_bin && pl.fwd_pf == 1 && pl.fwd_ab == 1)
-        hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 1, 1, true>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
+        hipExtLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 1, 1, true>), grid, dim3(TVAM_PB), lds, stream, g_fwd_ev[0], g_fwd_ev[1], 0, k, pl, pat, dose);
     else if (pl.fwd_bin && pl.fwd_pf == 1)
-        hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 1, 2, true>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
+        hipExtLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 1, 2, true>), grid, dim3(TVAM_PB), lds, stream, g_fwd_ev[0], g_fwd_ev[1], 0, k, pl, pat, dose);
     else if (pl.fwd_bin)
-        hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 2, 2, true>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
+        hipExtLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 2, 2, true>), grid, dim3(TVAM_PB), lds, stream, g_fwd_ev[0], g_fwd_ev[1], 0, k, pl, pat, dose);
     else if (pl.fwd_multi)
-        hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, true, 4, 1>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
+        hipExtLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, true, 4, 1>), grid, dim3(TVAM_PB), lds, stream, g_fwd_ev[0], g_fwd_ev[1], 0, k, pl, pat, dose);
     else if (pl.fwd_pf == 2)
-        hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 2, 1>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
+        hipExtLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 2, 1>), grid, dim3(TVAM_PB), lds, stream, g_fwd_ev[0], g_fwd_ev[1], 0, k, pl, pat, dose);
     else if (NC == 2 && pl.fwd_ab == 4)
-        hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 4, 4>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
+        hipExtLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 4, 4>), grid, dim3(TVAM_PB), lds, stream, g_fwd_ev[0], g_fwd_ev[1], 0, k, pl, pat, dose);
     else if (NC == 2 && pl.fwd_ab == 3)
-        hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 4, 3>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
+        hipExtLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 4, 3>), grid, dim3(TVAM_PB), lds, stream, g_fwd_ev[0], g_fwd_ev[1], 0, k, pl, pat, dose);
     else if (NC == 2 && pl.fwd_ab == 2)
-        hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 4, 2>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
+        hipExtLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 4, 2>), grid, dim3(TVAM_PB), lds, stream, g_fwd_ev[0], g_fwd_ev[1], 0, k, pl, pat, dose);
     else
-        hipLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 4, 1>), grid, dim3(TVAM_PB), lds, stream, k, pl, pat, dose);
+        hipExtLaunchKernelGGL((tvam_fwd_planar_kernel<Z, NC, false, 4, 1>), grid, dim3(TVAM_PB), lds, stream, g_fwd_ev[0], g_fwd_ev[1], 0, k, pl, pat, dose);
 }
 
 template <int Z>
@@ -1027,9 +1033,9 @@ hipError_t tvam_launch_fwd_planar(const TvamConsts& k, const TvamPlanar& pl, int
         else
             hipLaunchKernelGGL(tvam_slice_bin_kernel, bg, dim3(256), 0, stream, k, pl, pat, b0);
     }
-    tvam_kt_begin(stream, TVAM_KT_PLANAR);
+    if (!tvam_kt_take(TVAM_KT_PLANAR, &g_fwd_ev[0], &g_fwd_ev[1])) g_fwd_ev[0] = g_fwd_ev[1] = nullptr;
     hipError_t e = tvam_launch_fwd_planar_z(grid, lds, stream, k, pl, Z, pat, dose);
-    tvam_kt_end(stream, TVAM_KT_PLANAR);
+    g_fwd_ev[0] = g_fwd_ev[1] = nullptr;
     if (e != hipSuccess || parts == 1) return e;
     // sum the angle parts of this launch's slices
     const int64_t plane = (int64_t)k.res[0] * k.res[1];
