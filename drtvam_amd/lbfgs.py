@@ -407,9 +407,9 @@ class FusedLinearLBFGS(LinearLBFGS):
             polls += 1
             if polls % 4096 == 0:
                 now = time.perf_counter()
-                t_end = t_end or now + 60.0
+                t_end = t_end or now + 600.0  # the queue ahead of the decision: a forward and the probes
                 if now > t_end:
-                    raise RuntimeError("tvam_lbfgs_armijo: no report after 60 s")
+                    raise RuntimeError("tvam_lbfgs_armijo: no report after 600 s")
         v = [float(x) for x in rnp[:3 + nb]]
         lv = v[0] / div if divided else (v[0] if loss_cell is not None else loss_host)
         return (out, v[2 + nb], pre), float(lv), 0.0 + v[1], v[2:2 + nb]
